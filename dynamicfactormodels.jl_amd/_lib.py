@@ -1,0 +1,99 @@
+"""ctypes binding of libdfm.so (the C ABI declared in include/dfm.h).
+
+The library is built in-tree (``__graft_entry__.build()`` or ``make -C
+dynamicfactormodels.jl_amd/csrc``).  There is no fallback: if the shared
+object is missing or no GPU is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfm.so")
+
+c_double_p = C.POINTER(C.c_double)
+c_int32_p = C.POINTER(C.c_int32)
+c_int64_p = C.POINTER(C.c_int64)
+c_uint8_p = C.POINTER(C.c_uint8)
+
+
+class dfm_stat(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("arg0", C.c_int32), ("arg1", C.c_int32), ("pad", C.c_int32)]
+
+
+# (name, restype, argtypes) — one row per symbol of include/dfm.h
+SIGNATURES = [
+    ("dfm_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("dfm_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("dfm_last_error", C.c_char_p, [C.c_void_p]),
+    ("dfm_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("dfm_ctx_synchronize", C.c_int, [C.c_void_p]),
+    ("dfm_ctx_set_eig_params", C.c_int, [C.c_void_p, C.c_double, C.c_int, C.c_int]),
+    ("dfm_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("dfm_ctx_read_timing", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int]),
+    ("dfm_ctx_reset_timing", C.c_int, [C.c_void_p]),
+    ("dfm_kernel_class_name", C.c_char_p, [C.c_int]),
+    ("dfm_pca", C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                          c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("dfm_full_spectrum_max", C.c_int, []),
+    ("dfm_gram_spectrum", C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.c_int64, C.c_int64,
+                                    c_double_p, c_double_p]),
+    ("dfm_ic_sweep", C.c_int, [c_double_p, C.c_int, C.c_int, C.c_double, C.c_int64, C.c_int64,
+                               C.c_double, c_double_p]),
+    ("dfm_model_fit", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
+                                c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                C.c_int, C.POINTER(C.c_void_p)]),
+    ("dfm_model_destroy", C.c_int, [C.c_void_p]),
+    ("dfm_model_scalars", C.c_int, [C.c_void_p, c_int64_p, c_double_p, c_double_p, c_double_p]),
+    ("dfm_model_read", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                 c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("dfm_bootstrap", C.c_int, [C.c_void_p, C.c_int, C.c_int64, c_int32_p, c_double_p,
+                                C.POINTER(dfm_stat), C.c_int, c_double_p]),
+    ("dfm_bootstrap_dev", C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.POINTER(dfm_stat), C.c_int, C.c_void_p]),
+    ("dfm_stats_width", C.c_int64, [C.c_void_p, C.POINTER(dfm_stat), C.c_int]),
+    ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
+    ("dfm_chow_all", C.c_int, [C.c_void_p, C.c_int64, c_double_p, c_double_p, c_double_p]),
+    ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
+                                    c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                                    C.c_double, c_double_p, c_uint8_p]),
+]
+
+_lock = threading.Lock()
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load libdfm.so (once).  Raises LibraryMissing — never falls back."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
+        lib = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return [s[0] for s in SIGNATURES]
+
+
+def ptr(a):
+    """double* of a C-contiguous float64 numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(c_double_p)

@@ -1,0 +1,485 @@
+"""Python mirror of the DynamicFactorModels.jl export surface
+(``src/DynamicFactorModels.jl:16-20``) for the hot path, dispatching to
+libdfm through its C ABI.  Names, argument meaning and error behaviour follow
+the reference:
+
+* ``DynamicFactorModel(y, w, x, number_of_factors, criterion)`` — the
+  workhorse constructor (``src/DynamicFactorModel.jl:28-51``);
+  ``DynamicFactorModel(y, w, x, "ICp2")`` — the IC-sweep constructor
+  (``:53-66``);
+* ``calculate_factors`` (``:71-121``), ``calculate_criterion`` (``:135-141``),
+  ``factor_residual_variance`` and ``criterion_*`` (``src/criteria.jl``);
+* ``wild_bootstrap`` / ``residual_bootstrap`` (``src/bootstrap.jl:21-51``) with
+  a device stat menu in place of the Julia closure;
+* ``LR_test`` / ``LM_test`` / ``Wald_test`` (``src/chowtest.jl``) —
+  ``variable_index`` is 1-based, as in the reference;
+* ``targeted_predictors`` (``src/targeted_predictors.jl``, hard thresholding).
+
+Every numeric result comes from the GPU; this module only marshals arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+from .host import draw_residual, draw_wild, t_quantile
+
+CRITERIA = ("PCp1", "PCp2", "PCp3", "ICp1", "ICp2", "ICp3", "BIC")
+_CRIT_CODE = {n: i for i, n in enumerate(CRITERIA)}
+
+
+class DFMError(RuntimeError):
+    """A non-zero return code of libdfm (the message is dfm_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libdfm error {code}: {msg}")
+        self.code = code
+
+
+# ------------------------------------------------------------------ context
+class Context:
+    """One libdfm context per GPU (``dfm_ctx``)."""
+
+    def __init__(self, device: Optional[int] = None):
+        self.lib = _lib.load()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        h = C.c_void_p()
+        rc = self.lib.dfm_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise DFMError(rc, f"dfm_ctx_create(device={device}) failed — no usable GPU?")
+        self.h = h
+        self.device = device
+
+    def check(self, rc: int):
+        if rc != 0:
+            raise DFMError(rc, self.lib.dfm_last_error(self.h).decode(errors="replace"))
+
+    def set_stream(self, stream_handle: Optional[int]):
+        self.check(self.lib.dfm_ctx_set_stream(self.h, C.c_void_p(stream_handle or 0)))
+
+    def synchronize(self):
+        self.check(self.lib.dfm_ctx_synchronize(self.h))
+
+    def set_eig_params(self, tol: float = -1.0, max_iter: int = -1, block: int = -1):
+        self.check(self.lib.dfm_ctx_set_eig_params(self.h, tol, max_iter, block))
+
+    def enable_timing(self, on: bool = True):
+        self.check(self.lib.dfm_ctx_enable_timing(self.h, int(on)))
+
+    def read_timing(self):
+        ms = (C.c_double * 16)()
+        n = (C.c_int64 * 16)()
+        k = self.lib.dfm_ctx_read_timing(self.h, ms, n, 16)
+        return {self.lib.dfm_kernel_class_name(i).decode(): (ms[i], n[i]) for i in range(k)}
+
+    def reset_timing(self):
+        self.check(self.lib.dfm_ctx_reset_timing(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dfm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx
+
+
+def _f64(a, ndim=None) -> np.ndarray:
+    a = np.asarray(a, dtype=np.float64)
+    if ndim == 2 and a.ndim == 1:
+        a = a.reshape(-1, 1)
+    return a
+
+
+def _colmajor(a: np.ndarray) -> np.ndarray:
+    return np.asfortranarray(a, dtype=np.float64)
+
+
+# --------------------------------------------------------------- stat menu
+@dataclass(frozen=True)
+class Stat:
+    """Replicate statistic (the device replacement of ``stat::Function``)."""
+    kind: int
+    arg0: int = 0
+    arg1: int = 0
+
+    @staticmethod
+    def V():                      # factor_residual_variance, src/criteria.jl:5
+        return Stat(0)
+
+    @staticmethod
+    def criterion(name: Optional[str] = None):
+        return Stat(1, _CRIT_CODE[name] if name else -1)
+
+    @staticmethod
+    def eigenvalue(j: int):       # 1-based, descending
+        return Stat(2, j - 1)
+
+    @staticmethod
+    def coefficient(j: int):      # 1-based into [w F_r]
+        return Stat(3, j - 1)
+
+    @staticmethod
+    def t_stat(j: int):
+        return Stat(4, j - 1)
+
+    @staticmethod
+    def trace():
+        return Stat(5)
+
+    @staticmethod
+    def LR(break_period: int, variable_index: int):
+        return Stat(6, break_period, variable_index - 1)
+
+    @staticmethod
+    def LM(break_period: int, variable_index: int):
+        return Stat(7, break_period, variable_index - 1)
+
+    @staticmethod
+    def Wald(break_period: int, variable_index: int):
+        return Stat(8, break_period, variable_index - 1)
+
+    @staticmethod
+    def LR_all(break_period: int):
+        return Stat(9, break_period)
+
+    @staticmethod
+    def LM_all(break_period: int):
+        return Stat(10, break_period)
+
+    @staticmethod
+    def Wald_all(break_period: int):
+        return Stat(11, break_period)
+
+
+def _stat_array(stats: Sequence[Stat]):
+    arr = (_lib.dfm_stat * max(len(stats), 1))()
+    for i, s in enumerate(stats):
+        arr[i].kind, arr[i].arg0, arr[i].arg1, arr[i].pad = s.kind, s.arg0, s.arg1, 0
+    return arr
+
+
+# --------------------------------------------------------------- the record
+class DynamicFactorModelResult:
+    """The ``DynamicFactorModel`` record (``src/DynamicFactorModel.jl:6-25``).
+    The fitted model stays resident in HBM (``dfm_model``) for the bootstrap
+    and Chow entry points; host copies are fetched lazily.  ``factors`` and
+    ``loadings`` hold the r consumed columns (the reference keeps full-width
+    matrices but only ever reads ``[:, 1:r]``, ``:33``, ``:131``)."""
+
+    def __init__(self, ctx: Context, handle: C.c_void_p, y, w, x, criterion: str,
+                 break_indices=(), kmax: int = 0):
+        self._ctx, self._h = ctx, handle
+        self.y, self.w, self.x = y, w, x
+        self.number_of_factors_criterion = criterion
+        self.break_indices = list(break_indices)
+        self.factor_type = "principal components"
+        self.number_of_factor_lags = 0
+        T, N = x.shape
+        r = C.c_int64()
+        V, cv, tr = C.c_double(), C.c_double(), C.c_double()
+        ctx.check(ctx.lib.dfm_model_scalars(handle, C.byref(r), C.byref(V), C.byref(cv), C.byref(tr)))
+        self.number_of_factors = int(r.value)
+        self.V = float(V.value)
+        self.number_of_factors_criterion_value = float(cv.value) if criterion else float("nan")  # D3
+        self.trace_G = float(tr.value)
+        self.kmax = kmax
+        q, rr = w.shape[1], self.number_of_factors
+        d = q + rr
+        ne = max(kmax, rr)
+        self.eigenvalues = np.zeros(ne)
+        self.coefficients = np.zeros(d)
+        self.t_stats = np.zeros(d)
+        self.coefficient_covariance = np.zeros((d, d), order="F")
+        self.residuals = np.zeros(T)
+        F = np.zeros((T, rr), order="F")
+        L = np.zeros((N, rr), order="F")
+        self.ic_values = np.zeros((7, kmax)) if (kmax and criterion) else None
+        ctx.check(ctx.lib.dfm_model_read(
+            handle, _lib.ptr(self.eigenvalues), _lib.ptr(self.coefficients), _lib.ptr(self.t_stats),
+            self.coefficient_covariance.ctypes.data_as(_lib.c_double_p), _lib.ptr(self.residuals),
+            F.ctypes.data_as(_lib.c_double_p), L.ctypes.data_as(_lib.c_double_p), None,
+            _lib.ptr(self.ic_values) if self.ic_values is not None else None))
+        self.factors = [np.ascontiguousarray(F)]
+        self.loadings = [np.ascontiguousarray(L)]
+        self._E = None
+
+    @property
+    def factor_residuals(self) -> np.ndarray:
+        if self._E is None:
+            T, N = self.x.shape
+            E = np.zeros((T, N), order="F")
+            self._ctx.check(self._ctx.lib.dfm_model_read(
+                self._h, None, None, None, None, None, None, None,
+                E.ctypes.data_as(_lib.c_double_p), None))
+            self._E = np.ascontiguousarray(E)
+        return self._E
+
+    @property
+    def design_matrix(self) -> np.ndarray:           # :130-133
+        return np.hstack([self.w, self.factors[0]])
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_batch(self, batch: int):
+        self._ctx.check(self._ctx.lib.dfm_model_set_batch(self._h, int(batch)))
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._ctx.lib.dfm_model_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def __repr__(self):                               # Base.show, :143-149
+        T, N = self.x.shape
+        return (f"Dynamic Factor Model\nDimensions of X: ({T}, {N})\n"
+                f"Number of factors used: {self.number_of_factors}\n"
+                f"Factors calculated by: {self.factor_type}\n"
+                f"Factor model residual variance: {self.V}\n")
+
+
+# ------------------------------------------------------------- constructors
+def DynamicFactorModel(y, w, x, number_of_factors: Union[int, str, None] = None,
+                       number_of_factors_criterion: str = "",
+                       factor_type: str = "principal components", targeted_predictors=None,
+                       number_of_factor_lags: int = 0, break_indices: Sequence[int] = (),
+                       *, kmax: Optional[int] = None, ctx: Optional[Context] = None
+                       ) -> DynamicFactorModelResult:
+    """Both constructors of ``src/DynamicFactorModel.jl``: an int (or None →
+    ceil(min(T,N)/2), defect D2) fits at fixed r (``:28-51``); a criterion name
+    as the 4th argument runs the IC sweep k = 1..kmax (``:53-66``, kmax default
+    ceil(m/2), defect D11)."""
+    ctx = ctx or default_context()
+    if factor_type != "principal components":
+        raise NotImplementedError(f"factor_type {factor_type!r}: the reference branch is broken "
+                                  "(defect D6) and out of scope")
+    if len(break_indices):
+        raise NotImplementedError("break-aware PCA (SURVEY §8(f) next #3) is not built yet")
+    if number_of_factor_lags:
+        raise NotImplementedError("factor lags are unfinished in the reference (:35-37)")
+    y = _f64(y).ravel()
+    w = _f64(w, 2)
+    x = _f64(x, 2)
+    T, N = x.shape
+    if len(y) != T or w.shape[0] != T:
+        raise ValueError("y, w and x must have the same number of rows")
+    if isinstance(number_of_factors, str):
+        crit = number_of_factors
+        r = 0
+    else:
+        crit = number_of_factors_criterion
+        r = int(math.ceil(min(T, N) / 2)) if number_of_factors is None else int(number_of_factors)
+        if r < 1:
+            raise ValueError("number_of_factors must be >= 1")
+    code = _CRIT_CODE[crit] if crit else -1
+    if crit and crit not in _CRIT_CODE:
+        raise KeyError(f"criterion_{crit} is not defined")
+    km = int(kmax) if kmax else 0
+    xc, wc = _colmajor(x), _colmajor(w)
+    h = C.c_void_p()
+    ctx.check(ctx.lib.dfm_model_fit(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p),
+                                    w.shape[1], T, xc.ctypes.data_as(_lib.c_double_p), T, N, T,
+                                    r, code, km, C.byref(h)))
+    mfn = int(math.ceil(min(T, N) / 2))
+    kk = min(km if km > 0 else mfn, mfn) if r == 0 else 0
+    res = DynamicFactorModelResult(ctx, h, y, w, x, crit, break_indices, kk)
+    res.targeted_predictors = (np.ones(N, dtype=bool) if targeted_predictors is None
+                               else np.asarray(targeted_predictors, dtype=bool))
+    return res
+
+
+def calculate_factors(x, factor_type: str = "principal components", targeted_predictors=None,
+                      number_of_factors: Optional[int] = None, break_indices: Sequence[int] = (),
+                      *, ctx: Optional[Context] = None):
+    """``src/DynamicFactorModel.jl:71-121``: returns ([F], [L], r) with the r
+    consumed columns (r clamped to ceil(m/2), ``:116-119``)."""
+    ctx = ctx or default_context()
+    if factor_type != "principal components":
+        raise NotImplementedError("only the principal-components branch exists (defect D6)")
+    if len(break_indices):
+        raise NotImplementedError("break-aware PCA is not built yet")
+    x = _f64(x, 2)
+    T, N = x.shape
+    mfn = int(math.ceil(min(T, N) / 2))
+    r = mfn if number_of_factors is None else min(int(number_of_factors), mfn)
+    ev, F, L, tr = principal_components(x, r, ctx=ctx)
+    return [F], [L], r
+
+
+def principal_components(x, k: int, *, ctx: Optional[Context] = None):
+    """Top-k of ``principal_components`` (``:75-95``): (eigvals, F, L, trace)."""
+    ctx = ctx or default_context()
+    x = _f64(x, 2)
+    T, N = x.shape
+    xc = _colmajor(x)
+    ev = np.zeros(k)
+    F = np.zeros((T, k), order="F")
+    L = np.zeros((N, k), order="F")
+    tr = C.c_double()
+    ctx.check(ctx.lib.dfm_pca(ctx.h, xc.ctypes.data_as(_lib.c_double_p), T, N, T, k, _lib.ptr(ev),
+                              F.ctypes.data_as(_lib.c_double_p), L.ctypes.data_as(_lib.c_double_p),
+                              C.byref(tr)))
+    return ev, np.ascontiguousarray(F), np.ascontiguousarray(L), float(tr.value)
+
+
+def gram_spectrum(x, *, ctx: Optional[Context] = None):
+    """All eigenvalues (descending) of the smaller Gram, min(T,N) <= 140."""
+    ctx = ctx or default_context()
+    x = _f64(x, 2)
+    T, N = x.shape
+    xc = _colmajor(x)
+    ev = np.zeros(min(T, N))
+    tr = C.c_double()
+    ctx.check(ctx.lib.dfm_gram_spectrum(ctx.h, xc.ctypes.data_as(_lib.c_double_p), T, N, T,
+                                        _lib.ptr(ev), C.byref(tr)))
+    return ev, float(tr.value)
+
+
+def factor_residual_variance(dfm: DynamicFactorModelResult) -> float:
+    """``src/criteria.jl:5``."""
+    return dfm.V
+
+
+def calculate_criterion(dfm: DynamicFactorModelResult) -> DynamicFactorModelResult:
+    """``src/DynamicFactorModel.jl:135-141`` (already evaluated on the device)."""
+    return dfm
+
+
+def criterion_value(name: str, dfm: DynamicFactorModelResult) -> float:
+    """``criterion_<name>`` (``src/criteria.jl:17-53``) for the fitted r."""
+    if name == dfm.number_of_factors_criterion:
+        return dfm.number_of_factors_criterion_value
+    T, N = dfm.x.shape
+    k, V = dfm.number_of_factors, dfm.V
+    c, m = (N + T) / (N * T), min(T, N)
+    if name in ("PCp1", "PCp2", "PCp3"):
+        ev, tr = gram_spectrum(dfm.x, ctx=dfm._ctx)
+        s2 = (tr - ev[:int(math.ceil(m / 2))].sum()) / (N * T)
+        g = {"PCp1": c * math.log(1 / c), "PCp2": c * math.log(m), "PCp3": math.log(m) / m}[name]
+        return V + k * s2 * g
+    return {"ICp1": math.log(V) + k * c * math.log(1 / c), "ICp2": math.log(V) + k * c * math.log(m),
+            "ICp3": math.log(V) + k * math.log(m) / m, "BIC": V + k * math.log(T) / T}[name]
+
+
+for _n in CRITERIA:
+    globals()[f"criterion_{_n}"] = (lambda name: lambda dfm: criterion_value(name, dfm))(_n)
+
+
+# ---------------------------------------------------------------- bootstrap
+def _run_bootstrap(dfm, kind, B, stat, idx, eta):
+    ctx = dfm._ctx
+    stats = list(stat) if isinstance(stat, (list, tuple)) else [stat]
+    arr = _stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(dfm.handle, arr, len(stats)))
+    T = dfm.x.shape[0]
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    if idx.shape != (B, T):
+        raise ValueError(f"idx must be (B, T) = ({B}, {T})")
+    etap = None
+    if eta is not None:
+        eta = np.ascontiguousarray(eta, dtype=np.float64)
+        if eta.shape != (B, T):
+            raise ValueError("eta must be (B, T)")
+        etap = _lib.ptr(eta)
+    out = np.zeros((B, max(width, 1)))
+    ctx.check(ctx.lib.dfm_bootstrap(dfm.handle, kind, B, idx.ctypes.data_as(_lib.c_int32_p), etap,
+                                    arr, len(stats), _lib.ptr(out)))
+    if len(stats) == 1 and width == 1:
+        return out[:, 0]
+    return out
+
+
+def wild_bootstrap(dfm: DynamicFactorModelResult, B: int, stat, *, idx=None, eta=None,
+                   rng: Optional[np.random.Generator] = None):
+    """``src/bootstrap.jl:41-51``.  ``idx`` (B×T, 0-based) and ``eta`` (B×T)
+    are the host draws of ``:44-45``; drawn from ``rng`` when omitted."""
+    if idx is None or eta is None:
+        idx, eta = draw_wild(rng or np.random.default_rng(), B, dfm.x.shape[0])
+    return _run_bootstrap(dfm, 0, B, stat, idx, eta)
+
+
+def residual_bootstrap(dfm: DynamicFactorModelResult, B: int, stat, *, idx=None,
+                       rng: Optional[np.random.Generator] = None):
+    """``src/bootstrap.jl:21-39``."""
+    if idx is None:
+        idx = draw_residual(rng or np.random.default_rng(), B, dfm.x.shape[0], dfm.break_indices)
+    return _run_bootstrap(dfm, 1, B, stat, idx, None)
+
+
+# --------------------------------------------------------------- Chow tests
+def chow_all(dfm: DynamicFactorModelResult, break_period: int):
+    """LR, LM, Wald for every variable (N-vectors)."""
+    ctx = dfm._ctx
+    N = dfm.x.shape[1]
+    LR, LM, W = np.zeros(N), np.zeros(N), np.zeros(N)
+    ctx.check(ctx.lib.dfm_chow_all(dfm.handle, int(break_period), _lib.ptr(LR), _lib.ptr(LM),
+                                   _lib.ptr(W)))
+    return LR, LM, W
+
+
+def LR_test(dfm, break_period: int, variable_index: int) -> float:
+    """``src/chowtest.jl:19-23`` (variable_index 1-based)."""
+    return float(chow_all(dfm, break_period)[0][variable_index - 1])
+
+
+def LM_test(dfm, break_period: int, variable_index: int) -> float:
+    """``src/chowtest.jl:35-42``."""
+    return float(chow_all(dfm, break_period)[1][variable_index - 1])
+
+
+def Wald_test(dfm, break_period: int, variable_index: int) -> float:
+    """``src/chowtest.jl:25-33``."""
+    return float(chow_all(dfm, break_period)[2][variable_index - 1])
+
+
+# ------------------------------------------------------- targeted predictors
+def targeted_predictors(y, w, x, thresholding: str = "hard", mode: str = "joint",
+                        *, return_tstats: bool = False, ctx: Optional[Context] = None):
+    """``src/targeted_predictors.jl:1-37``: boolean mask of the x columns whose
+    |t| exceeds t_{0.975}.  mode="joint" is the reference (needs q + N < T);
+    mode="per_candidate" is the Bai–Ng (2008) extension (defect D8)."""
+    if thresholding == "soft":
+        raise NotImplementedError("soft thresholding (glmnet lasso-CV) is SURVEY §8(f) next #2; "
+                                  "the reference's GLMNet call is not even imported (defect D5)")
+    if thresholding != "hard":
+        raise ValueError(thresholding)
+    ctx = ctx or default_context()
+    y = _f64(y).ravel()
+    w = _f64(w, 2)
+    x = _f64(x, 2)
+    T, N = x.shape
+    q = w.shape[1]
+    m = {"joint": 0, "per_candidate": 1}[mode]
+    df = (T - q - N) if m == 0 else (T - q - 1)
+    cv = t_quantile(0.975, df) if df > 0 else float("nan")
+    ts = np.zeros(N)
+    mask = np.zeros(N, dtype=np.uint8)
+    xc, wc = _colmajor(x), _colmajor(w)
+    ctx.check(ctx.lib.dfm_targeted_hard(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T,
+                                        xc.ctypes.data_as(_lib.c_double_p), T, N, T, m, cv,
+                                        _lib.ptr(ts), mask.ctypes.data_as(_lib.c_uint8_p)))
+    return (mask.astype(bool), ts) if return_tstats else mask.astype(bool)

@@ -1,0 +1,902 @@
+// dfm_api.hip — the C ABI of include/dfm.h: context, model fit, bootstrap.
+// Host-side orchestration only; all arithmetic runs in the kernels of
+// dfm_gram.hip (K1), dfm_eig.hip (K2), dfm_model.hip / dfm_chow.hip (K3).
+#include "dfm_common.h"
+#include "../../include/dfm.h"
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace dfm {
+hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
+                       int64_t strideG, int nrep, hipStream_t st);
+typedef void (*timer_fn)(void *ctx, int cls, int begin);
+int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
+            const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
+            double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
+            timer_fn tf, void *tctx);
+size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
+int eig_block_p(int m, int k, int req);
+int spectrum_max();
+hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+                           hipStream_t st);
+// dfm_model.hip
+__global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
+__global__ void colmajor_from_rows_kernel(const double *, int64_t, int, int, double *);
+int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb, const double *Uk,
+                   double *F, double *L, double *colssr, hipStream_t st);
+__global__ void colssr_cols_kernel(const double *, int64_t, int64_t, int, int, const double *,
+                                   const double *, double *);
+__global__ void common_residual_kernel(const double *, int64_t, int, int, int, const double *,
+                                       const double *, double *, double *);
+__global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, double *,
+                               double *, double *, double *, int *);
+struct StatDesc { int kind, arg0, arg1, off; };
+__global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *,
+                             const double *, const double *, const StatDesc *, int, double *, int64_t);
+// dfm_chow.hip
+hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
+                       const double *F, const double *Lm, double *LR, double *LM, double *Wald,
+                       int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st);
+size_t chow_workspace_bytes(int T, int N, int r, int nb);
+hipError_t launch_targeted(int mode, const double *y, const double *w, int q, const double *Xp,
+                           int64_t ld, int T, int N, double cv, double *tstat, uint8_t *mask,
+                           char *ws, size_t ws_bytes, hipStream_t st, int *bad);
+size_t targeted_workspace_bytes(int mode, int T, int N, int q);
+}  // namespace dfm
+
+using namespace dfm;
+
+static const char *kclass_names[DFM_KC_COUNT] = {"gram", "eig_gq", "eig_small", "eig_apply",
+                                                 "eig_other", "factors", "ols", "stats", "chow",
+                                                 "misc"};
+
+struct dfm_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::string err;
+  double tol = 1e-12;
+  int maxit = 400, block = 0, poll = 4;
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  struct Pend { int cls; hipEvent_t a, b; };
+  std::vector<Pend> pend;
+  hipEvent_t cur_a[DFM_KC_COUNT] = {};
+  double ms[DFM_KC_COUNT] = {};
+  int64_t launches[DFM_KC_COUNT] = {};
+};
+
+struct dfm_model {
+  dfm_ctx *ctx = nullptr;
+  int T = 0, N = 0, q = 0, r = 0, crit = -1, kmax = 0, m = 0, orient = 0, k_eig = 0;
+  int64_t ld = 0;
+  double *Xp = nullptr, *Cp = nullptr, *Ep = nullptr, *y = nullptr, *w = nullptr;
+  double *F = nullptr, *L = nullptr, *Ub = nullptr, *colssr = nullptr;
+  std::vector<double> lam, coef, tstat, cov, resid, ic;
+  double trace = 0, V = 0, critval = NAN, sigma2 = NAN;
+  int64_t batch = 0;
+  char *ws = nullptr;
+  size_t ws_bytes = 0;
+  StatDesc *sd_dev = nullptr;
+  int sd_cap = 0;
+  int *flag_dev = nullptr;
+};
+
+static int fail(dfm_ctx *ctx, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+#define HIPCHK(ctx, x)                                                                            \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess)                                                                         \
+      return fail(ctx, 1000 + (int)e_, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                                      \
+  } while (0)
+
+static void timer_cb(void *p, int cls, int begin) {
+  dfm_ctx *ctx = (dfm_ctx *)p;
+  if (!ctx->timing) return;
+  auto get = [&]() {
+    hipEvent_t e;
+    if (!ctx->pool.empty()) { e = ctx->pool.back(); ctx->pool.pop_back(); }
+    else hipEventCreate(&e);
+    return e;
+  };
+  if (begin) {
+    ctx->cur_a[cls] = get();
+    hipEventRecord(ctx->cur_a[cls], ctx->stream);
+  } else {
+    hipEvent_t b = get();
+    hipEventRecord(b, ctx->stream);
+    ctx->pend.push_back({cls, ctx->cur_a[cls], b});
+    ctx->launches[cls]++;
+  }
+}
+static void harvest(dfm_ctx *ctx) {
+  if (ctx->pend.empty()) return;
+  hipEventSynchronize(ctx->pend.back().b);
+  for (auto &p : ctx->pend) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    ctx->ms[p.cls] += ms;
+    ctx->pool.push_back(p.a);
+    ctx->pool.push_back(p.b);
+  }
+  ctx->pend.clear();
+}
+struct Scope {
+  dfm_ctx *c; int cls;
+  Scope(dfm_ctx *c_, int k) : c(c_), cls(k) { timer_cb(c, cls, 1); }
+  ~Scope() { timer_cb(c, cls, 0); }
+};
+
+static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+static int ceil_half(int m) { return (m + 1) / 2; }
+
+template <class T>
+static hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
+
+extern "C" {
+
+int dfm_ctx_create(int device, dfm_ctx **out) {
+  if (!out) return -1;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return -2;
+  dfm_ctx *c = new dfm_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) { delete c; return -3; }
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return -4; }
+  c->stream = c->own;
+  *out = c;
+  return 0;
+}
+
+int dfm_ctx_destroy(dfm_ctx *ctx) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  harvest(ctx);
+  for (auto e : ctx->pool) hipEventDestroy(e);
+  if (ctx->own) hipStreamDestroy(ctx->own);
+  delete ctx;
+  return 0;
+}
+
+const char *dfm_last_error(const dfm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dfm_ctx_set_stream(dfm_ctx *ctx, void *s) {
+  if (!ctx) return -1;
+  ctx->stream = s ? (hipStream_t)s : ctx->own;
+  return 0;
+}
+int dfm_ctx_synchronize(dfm_ctx *ctx) {
+  if (!ctx) return -1;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+int dfm_ctx_set_eig_params(dfm_ctx *ctx, double tol, int max_iter, int block) {
+  if (!ctx) return -1;
+  if (tol > 0) ctx->tol = tol;
+  if (max_iter > 0) ctx->maxit = max_iter;
+  if (block >= 0) ctx->block = block;
+  return 0;
+}
+int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable) {
+  if (!ctx) return -1;
+  ctx->timing = enable != 0;
+  return 0;
+}
+int dfm_ctx_read_timing(dfm_ctx *ctx, double *ms_out, int64_t *launches_out, int cap) {
+  if (!ctx) return -1;
+  harvest(ctx);
+  const int n = std::min(cap, (int)DFM_KC_COUNT);
+  for (int i = 0; i < n; ++i) {
+    if (ms_out) ms_out[i] = ctx->ms[i];
+    if (launches_out) launches_out[i] = ctx->launches[i];
+  }
+  return n;
+}
+int dfm_ctx_reset_timing(dfm_ctx *ctx) {
+  if (!ctx) return -1;
+  harvest(ctx);
+  for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
+  return 0;
+}
+const char *dfm_kernel_class_name(int cls) {
+  return (cls >= 0 && cls < DFM_KC_COUNT) ? kclass_names[cls] : "?";
+}
+int dfm_full_spectrum_max(void) { return spectrum_max(); }
+
+int dfm_ic_sweep(const double *eig, int n_eig, int kmax, double trace, int64_t T, int64_t N,
+                 double sigma2, double *out) {
+  if (!eig || !out || kmax < 1 || n_eig < kmax || T < 1 || N < 1) return -1;
+  const int m = (int)std::min(T, N);
+  if (sigma2 < 0) {
+    const int kh = ceil_half(m);
+    if (n_eig < kh) return -2;
+    double s = trace;
+    for (int j = 0; j < kh; ++j) s -= eig[j];
+    sigma2 = s / ((double)N * (double)T);
+  }
+  const double c = (double)(N + T) / ((double)N * (double)T);
+  double cum = trace;
+  for (int k = 1; k <= kmax; ++k) {
+    cum -= eig[k - 1];
+    const double V = cum / ((double)N * (double)T);
+    out[0 * kmax + k - 1] = V + k * sigma2 * c * std::log(1.0 / c);
+    out[1 * kmax + k - 1] = V + k * sigma2 * c * std::log((double)m);
+    out[2 * kmax + k - 1] = V + k * sigma2 * std::log((double)m) / m;
+    out[3 * kmax + k - 1] = std::log(V) + k * c * std::log(1.0 / c);
+    out[4 * kmax + k - 1] = std::log(V) + k * c * std::log((double)m);
+    out[5 * kmax + k - 1] = std::log(V) + k * std::log((double)m) / m;
+    out[6 * kmax + k - 1] = V + k * std::log((double)T) / T;
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- internals
+// Top-k eigen-decomposition of nb Grams + trace; G workspace provided.
+static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const double *warm, int kw,
+                   double *lam, double *Uk, double *trace, int *status_dev) {
+  const int p = eig_block_p(m, k, ctx->block);
+  if (p > 32 || p < k) return fail(ctx, -20, "eigensolver block %d unsupported for k=%d m=%d", p, k, m);
+  const int P = p <= 16 ? 16 : 32;
+  const size_t bytes = eig_workspace_bytes_padded(m, nb, P, ctx->maxit);
+  char *ws = nullptr;
+  HIPCHK(ctx, hipMalloc(&ws, bytes));
+  int rc = eig_run(G, m, (int64_t)m * m, m, nb, k, p, warm, kw, ctx->tol, ctx->maxit, ctx->poll, ws,
+                   lam, Uk, trace, status_dev, nullptr, ctx->stream, timer_cb, ctx);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(ws);
+  if (rc != 0) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+  return 0;
+}
+
+extern "C" {
+
+int dfm_model_destroy(dfm_model *m) {
+  if (!m) return -1;
+  hipSetDevice(m->ctx->device);
+  hipStreamSynchronize(m->ctx->stream);
+  for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->L, m->Ub, m->colssr}) hipFree(p);
+  hipFree(m->ws);
+  hipFree(m->sd_dev);
+  hipFree(m->flag_dev);
+  delete m;
+  return 0;
+}
+
+int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                  const double *X, int64_t T64, int64_t N64, int64_t ldx, int r, int crit, int kmax,
+                  dfm_model **out) {
+  if (!ctx || !out) return -1;
+  *out = nullptr;
+  if (!y || !X || T64 < 2 || N64 < 1 || ldx < T64 || q < 0 || (q > 0 && (!w || ldw < T64)))
+    return fail(ctx, -2, "dfm_model_fit: bad arguments");
+  if (T64 > (1 << 24) || N64 > (1 << 24)) return fail(ctx, -2, "panel too large");
+  if (crit < -1 || crit > 6) return fail(ctx, -3, "unknown criterion %d", crit);
+  if (r <= 0 && crit < 0) return fail(ctx, -3, "IC sweep needs a criterion");
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  const int T = (int)T64, N = (int)N64, m = std::min(T, N);
+  const int mfn = ceil_half(m);  // max_factor_number, src/DynamicFactorModel.jl:101
+  dfm_model *M = new dfm_model();
+  M->ctx = ctx; M->T = T; M->N = N; M->q = q; M->crit = crit; M->m = m;
+  M->orient = (N > T) ? 0 : 1;  // src/DynamicFactorModel.jl:77 (T >= N) vs :86 (N > T)
+  M->ld = round_up(N, 16);
+  auto bail = [&](int code) { dfm_model_destroy(M); return code; };
+  int rc = 0;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return bail(fail(ctx, 1000 + (int)e_, "HIP %s line %d", hipGetErrorString(e_), __LINE__)); } while (0)
+  const size_t panel = (size_t)T * M->ld;
+  CK(dalloc(&M->Xp, panel));
+  CK(dalloc(&M->Cp, panel));
+  CK(dalloc(&M->Ep, panel));
+  CK(dalloc(&M->y, T));
+  CK(dalloc(&M->w, (size_t)T * std::max(q, 1)));
+  double *Xraw = nullptr, *G = nullptr;
+  CK(dalloc(&Xraw, (size_t)T * N));
+  CK(hipMemcpy2DAsync(Xraw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(M->y, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
+  if (q > 0) CK(hipMemcpy2DAsync(M->w, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  {
+    Scope sc(ctx, DFM_KC_MISC);
+    hipLaunchKernelGGL(panel_from_colmajor_kernel, dim3((unsigned)((M->ld + 31) / 32), (T + 31) / 32),
+                       dim3(256), 0, st, Xraw, (int64_t)T, T, N, M->Xp, M->ld);
+  }
+  CK(hipGetLastError());
+  CK(dalloc(&G, (size_t)m * m));
+  PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld};
+  {
+    Scope sc(ctx, DFM_KC_GRAM);
+    CK(launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
+  }
+  // --- how many eigenvalues: the IC sweep needs kmax, PCp needs sigma^2 = V(ceil(m/2))
+  const bool pcp = crit >= 0 && crit <= 2;
+  if (kmax <= 0) kmax = mfn;  // src/DynamicFactorModel.jl:54 (D11)
+  kmax = std::min(kmax, mfn);
+  M->kmax = kmax;
+  std::vector<double> spec;
+  double trace = 0.0;
+  // the sweep reports all 7 criteria: PCp rows need sigma^2 (NaN when the full
+  // spectrum is out of reach and the chosen criterion is not a PCp one)
+  const bool need_spec = pcp || (r <= 0 && kmax > 24) || (r <= 0 && m <= spectrum_max());
+  if (need_spec) {
+    if (m > spectrum_max()) {
+      hipFree(Xraw); hipFree(G);
+      return bail(fail(ctx, -30, "PCp criteria / kmax > 24 need the full spectrum; supported for "
+                                 "min(T,N) <= %d (got %d)", spectrum_max(), m));
+    }
+    double *ev = nullptr;
+    CK(dalloc(&ev, m));
+    {
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      CK(launch_spectrum(G, m, (int64_t)m * m, m, 1, ev, st));
+    }
+    spec.resize(m);
+    CK(hipMemcpyAsync(spec.data(), ev, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    hipFree(ev);
+    for (double v : spec) trace += v;  // replaced below by the Gram trace
+  }
+  // --- top-k eigenpairs
+  const int k_eig = (r <= 0) ? (need_spec ? 1 : kmax) : std::min(r, mfn);
+  int kk = std::max(k_eig, 1);
+  double *lam_d = nullptr, *Uk = nullptr, *tr_d = nullptr;
+  int *st_d = nullptr;
+  CK(dalloc(&lam_d, kk)); CK(dalloc(&Uk, (size_t)m * kk)); CK(dalloc(&tr_d, 1)); CK(dalloc(&st_d, 1));
+  rc = run_eig(ctx, G, m, 1, kk, nullptr, 0, lam_d, Uk, tr_d, st_d);
+  if (rc) { hipFree(Xraw); hipFree(G); return bail(rc); }
+  std::vector<double> lam(kk);
+  int est = 0;
+  CK(hipMemcpyAsync(lam.data(), lam_d, (size_t)kk * 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(&trace, tr_d, 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(&est, st_d, 4, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  if (est) { hipFree(Xraw); hipFree(G); return bail(fail(ctx, 2, "eigensolver did not converge")); }
+  const double NT = (double)N * (double)T;
+  // eigenvalues used by the sweep: full spectrum when computed, else the top-k
+  const std::vector<double> &ev = need_spec ? spec : lam;
+  if (need_spec) {
+    double s = trace;
+    for (int j = 0; j < mfn; ++j) s -= spec[j];
+    M->sigma2 = s / NT;   // V of DynamicFactorModel(y, w, x), src/criteria.jl:18
+  }
+  if (r <= 0) {
+    M->ic.assign(7 * kmax, 0.0);
+    dfm_ic_sweep(ev.data(), (int)ev.size(), kmax, trace, T, N, need_spec ? M->sigma2 : NAN, M->ic.data());
+    int best = 0;
+    for (int k = 1; k < kmax; ++k)   // first argmin, indmin (src/DynamicFactorModel.jl:65)
+      if (M->ic[crit * kmax + k] < M->ic[crit * kmax + best]) best = k;
+    r = best + 1;
+  }
+  r = std::min(r, mfn);   // src/DynamicFactorModel.jl:116-119
+  M->r = r;
+  if (r > kk) {   // the sweep used the full spectrum: now the r eigenvectors
+    hipFree(lam_d); hipFree(Uk);
+    kk = r;
+    CK(dalloc(&lam_d, kk)); CK(dalloc(&Uk, (size_t)m * kk));
+    rc = run_eig(ctx, G, m, 1, kk, nullptr, 0, lam_d, Uk, tr_d, st_d);
+    if (rc) { hipFree(Xraw); hipFree(G); return bail(rc); }
+    lam.resize(kk);
+    CK(hipMemcpyAsync(lam.data(), lam_d, (size_t)kk * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(&est, st_d, 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    if (est) { hipFree(Xraw); hipFree(G); return bail(fail(ctx, 2, "eigensolver did not converge")); }
+  }
+  M->lam.assign(ev.begin(), ev.begin() + std::max<size_t>(std::min<size_t>(ev.size(), std::max(kmax, r)), 0));
+  if (M->lam.size() < (size_t)r) M->lam = lam;
+  M->k_eig = kk;
+  // --- factors, loadings for r (first r canonical eigenvectors)
+  CK(dalloc(&M->Ub, (size_t)m * r));
+  CK(dalloc(&M->F, (size_t)T * r));
+  CK(dalloc(&M->L, (size_t)N * r));
+  CK(dalloc(&M->colssr, N));
+  CK(hipMemcpy2DAsync(M->Ub, (size_t)r * 8, Uk, (size_t)kk * 8, (size_t)r * 8, m, hipMemcpyDeviceToDevice, st));
+  {
+    Scope sc(ctx, DFM_KC_FACTORS);
+    if (launch_factors(M->orient, src, T, N, r, 1, M->Ub, M->F, M->L, M->colssr, st))
+      return bail(fail(ctx, -4, "r=%d too large", r));
+    if (M->orient == 1) {
+      double *lr = nullptr;
+      CK(dalloc(&lr, r));
+      CK(hipMemcpyAsync(lr, lam_d, (size_t)r * 8, hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(colssr_cols_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, st, G, m,
+                         (int64_t)m * m, N, r, lr, M->Ub, M->colssr);
+      CK(hipStreamSynchronize(st));
+      hipFree(lr);
+    }
+  }
+  {
+    Scope sc(ctx, DFM_KC_MISC);
+    hipLaunchKernelGGL(common_residual_kernel, dim3((unsigned)((M->ld + 255) / 256), T), dim3(256), 0,
+                       st, M->Xp, M->ld, T, N, r, M->F, M->L, M->Cp, M->Ep);
+  }
+  CK(hipGetLastError());
+  // --- OLS + HC2 on [w F_r]
+  const int d = q + r;
+  if (d > 32) return bail(fail(ctx, -5, "q + r = %d > 32 unsupported", d));
+  double *coef = nullptr, *tst = nullptr, *cov = nullptr, *res = nullptr;
+  int *ost = nullptr;
+  CK(dalloc(&coef, d)); CK(dalloc(&tst, d)); CK(dalloc(&cov, (size_t)d * d)); CK(dalloc(&res, T));
+  CK(dalloc(&ost, 1));
+  {
+    Scope sc(ctx, DFM_KC_OLS);
+    hipLaunchKernelGGL(ols_hc2_kernel, dim3(1), dim3(256), 0, st, M->y, M->w, q, M->F, T, r, coef,
+                       tst, cov, res, ost);
+  }
+  CK(hipGetLastError());
+  M->coef.resize(d); M->tstat.resize(d); M->cov.resize((size_t)d * d); M->resid.resize(T);
+  int ols_bad = 0;
+  CK(hipMemcpyAsync(M->coef.data(), coef, (size_t)d * 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(M->tstat.data(), tst, (size_t)d * 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(M->cov.data(), cov, (size_t)d * d * 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(M->resid.data(), res, (size_t)T * 8, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(&ols_bad, ost, 4, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  for (double *p : {Xraw, G, lam_d, Uk, tr_d, coef, tst, cov, res}) hipFree(p);
+  hipFree(st_d); hipFree(ost);
+  if (ols_bad) return bail(fail(ctx, 3, "singular design matrix D'D"));
+  M->trace = trace;
+  double s = trace;
+  for (int j = 0; j < r; ++j) s -= lam[j];
+  M->V = s / NT;
+  if (crit >= 0) {
+    const double c = (double)(N + T) / NT;
+    switch (crit) {
+      case 0: M->critval = M->V + r * M->sigma2 * c * std::log(1.0 / c); break;
+      case 1: M->critval = M->V + r * M->sigma2 * c * std::log((double)m); break;
+      case 2: M->critval = M->V + r * M->sigma2 * std::log((double)m) / m; break;
+      case 3: M->critval = std::log(M->V) + r * c * std::log(1.0 / c); break;
+      case 4: M->critval = std::log(M->V) + r * c * std::log((double)m); break;
+      case 5: M->critval = std::log(M->V) + r * std::log((double)m) / m; break;
+      case 6: M->critval = M->V + r * std::log((double)T) / T; break;
+    }
+  }
+  M->lam.resize(std::max<size_t>(M->lam.size(), (size_t)r));
+  for (int j = 0; j < r; ++j) M->lam[j] = lam[j];
+  CK(dalloc(&M->flag_dev, 4));
+  *out = M;
+  return 0;
+#undef CK
+}
+
+int dfm_model_scalars(const dfm_model *m, int64_t *r, double *V, double *cv, double *tr) {
+  if (!m) return -1;
+  if (r) *r = m->r;
+  if (V) *V = m->V;
+  if (cv) *cv = m->critval;
+  if (tr) *tr = m->trace;
+  return 0;
+}
+
+int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *tstat, double *coef_cov,
+                   double *ols_resid, double *F, double *L, double *E, double *ic_values) {
+  if (!m) return -1;
+  dfm_ctx *ctx = m->ctx;
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  const int d = m->q + m->r;
+  if (eigvals) std::copy(m->lam.begin(), m->lam.begin() + std::min<size_t>(m->lam.size(), std::max(m->kmax, m->r)), eigvals);
+  if (coef) std::copy(m->coef.begin(), m->coef.end(), coef);
+  if (tstat) std::copy(m->tstat.begin(), m->tstat.end(), tstat);
+  if (coef_cov) std::copy(m->cov.begin(), m->cov.end(), coef_cov);
+  if (ols_resid) std::copy(m->resid.begin(), m->resid.end(), ols_resid);
+  if (ic_values && !m->ic.empty()) std::copy(m->ic.begin(), m->ic.end(), ic_values);
+  (void)d;
+  std::vector<double> tmp;
+  auto rows_to_colmajor = [&](const double *src, int rows, int cols, double *dst) -> int {
+    tmp.resize((size_t)rows * cols);
+    if (hipMemcpyAsync(tmp.data(), src, tmp.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess) return 1;
+    if (hipStreamSynchronize(st) != hipSuccess) return 1;
+    for (int i = 0; i < rows; ++i)
+      for (int j = 0; j < cols; ++j) dst[(size_t)j * rows + i] = tmp[(size_t)i * cols + j];
+    return 0;
+  };
+  if (F && rows_to_colmajor(m->F, m->T, m->r, F)) return fail(ctx, 1001, "copy F");
+  if (L && rows_to_colmajor(m->L, m->N, m->r, L)) return fail(ctx, 1001, "copy L");
+  if (E) {
+    double *d_out = nullptr;
+    HIPCHK(ctx, dalloc(&d_out, (size_t)m->T * m->N));
+    hipLaunchKernelGGL(colmajor_from_rows_kernel, dim3((m->N + 31) / 32, (m->T + 31) / 32), dim3(256), 0,
+                       st, m->Ep, m->ld, m->T, m->N, d_out);
+    HIPCHK(ctx, hipMemcpyAsync(E, d_out, (size_t)m->T * m->N * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    hipFree(d_out);
+  }
+  return 0;
+}
+
+int dfm_model_set_batch(dfm_model *m, int64_t batch) {
+  if (!m || batch < 0) return -1;
+  m->batch = batch;
+  return 0;
+}
+
+int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
+  if (!m || (!stats && nstats)) return -1;
+  int64_t w = 0;
+  for (int i = 0; i < nstats; ++i) w += (stats[i].kind >= DFM_STAT_LR_ALL) ? m->N : 1;
+  return w;
+}
+
+// Per-batch device workspace layout for the bootstrap.
+struct BootWs {
+  double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat;
+  int *status, *ost;
+  char *eig, *chow;
+  size_t eig_bytes, chow_bytes;
+};
+static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool chow, BootWs *o, char *base) {
+  const int m = M->m, r = M->r, T = M->T, N = M->N, d = M->q + M->r;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char *p = base ? base + off : nullptr; off += (bytes + 255) & ~size_t(255); return p; };
+  BootWs w{};
+  w.G = (double *)take((size_t)nb * m * m * 8);
+  w.lam = (double *)take((size_t)nb * r * 8);
+  w.Uk = (double *)take((size_t)nb * m * r * 8);
+  w.trace = (double *)take((size_t)nb * 8);
+  w.F = (double *)take((size_t)nb * T * r * 8);
+  w.L = (double *)take((size_t)nb * N * r * 8);
+  w.colssr = (double *)take((size_t)nb * N * 8);
+  w.coef = (double *)take((size_t)nb * d * 8);
+  w.tstat = (double *)take((size_t)nb * d * 8);
+  w.status = (int *)take((size_t)nb * 4);
+  w.ost = (int *)take((size_t)nb * 4);
+  w.eig_bytes = eig_workspace_bytes_padded(m, nb, P, maxit);
+  w.eig = take(w.eig_bytes);
+  w.chow_bytes = chow ? chow_workspace_bytes(T, N, r, nb) : 0;
+  w.chow = take(w.chow_bytes);
+  if (o) *o = w;
+  return off;
+}
+
+__global__ void or_status_kernel(const int *s1, const int *s2, int nb, int *flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb) {
+    if (s1[i]) atomicOr(flag, 1);
+    if (s2[i]) atomicOr(flag, 2);
+  }
+}
+
+int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+                      const dfm_stat *stats, int ns, double *out) {
+  if (!M) return -1;
+  dfm_ctx *ctx = M->ctx;
+  if (B < 0 || !idx || (kind == DFM_BOOT_WILD && !eta) || (ns > 0 && (!stats || !out)) || ns < 0)
+    return fail(ctx, -2, "dfm_bootstrap: bad arguments");
+  if (kind != DFM_BOOT_WILD && kind != DFM_BOOT_RESIDUAL) return fail(ctx, -2, "bad bootstrap kind");
+  if (B == 0) return 0;
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  const int m = M->m, r = M->r, T = M->T, N = M->N, q = M->q, d = q + r;
+  // stat descriptors
+  std::vector<StatDesc> sd(ns);
+  int64_t width = 0;
+  bool chow = false;
+  int chow_bp = -1;
+  for (int i = 0; i < ns; ++i) {
+    const dfm_stat s = stats[i];
+    if (s.kind < 0 || s.kind > DFM_STAT_WALD_ALL) return fail(ctx, -6, "unknown stat kind %d", s.kind);
+    if (s.kind == DFM_STAT_CRIT) {
+      const int c = s.arg0 >= 0 ? s.arg0 : M->crit;
+      if (c < 0 || c > 6) return fail(ctx, -6, "criterion stat without a criterion");
+      if (c <= 2) return fail(ctx, -31, "PCp criteria inside the bootstrap need a per-replicate "
+                                        "unrestricted fit (not supported yet)");
+    }
+    if (s.kind >= DFM_STAT_LR) {
+      if (s.arg0 < r || s.arg0 > T - r) return fail(ctx, -7, "break period %d out of range", s.arg0);
+      if (chow && s.arg0 != chow_bp) return fail(ctx, -7, "one break period per call");
+      chow = true; chow_bp = s.arg0;
+      if (s.kind <= DFM_STAT_WALD && (s.arg1 < 0 || s.arg1 >= N)) return fail(ctx, -7, "variable index");
+    }
+    sd[i] = {s.kind, s.arg0, s.arg1, (int)width};
+    width += (s.kind >= DFM_STAT_LR_ALL) ? N : 1;
+  }
+  const int p = eig_block_p(m, r, ctx->block);
+  const int P = p <= 16 ? 16 : 32;
+  int64_t nb = M->batch;
+  if (nb <= 0) {
+    const double gbytes = (double)m * m * 8;
+    nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
+  }
+  nb = std::min<int64_t>(nb, B);
+  const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, nullptr, nullptr);
+  if (need > M->ws_bytes) {
+    hipFree(M->ws);
+    M->ws = nullptr; M->ws_bytes = 0;
+    HIPCHK(ctx, hipMalloc(&M->ws, need));
+    M->ws_bytes = need;
+  }
+  if (ns > M->sd_cap) {
+    hipFree(M->sd_dev);
+    HIPCHK(ctx, dalloc(&M->sd_dev, ns));
+    M->sd_cap = ns;
+  }
+  if (ns) HIPCHK(ctx, hipMemcpyAsync(M->sd_dev, sd.data(), ns * sizeof(StatDesc), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemsetAsync(M->flag_dev, 0, 4, st));
+  BootWs w;
+  boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, &w, M->ws);
+  for (int64_t b0 = 0; b0 < B; b0 += nb) {
+    const int n = (int)std::min<int64_t>(nb, B - b0);
+    PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld};
+    {
+      Scope sc(ctx, DFM_KC_GRAM);
+      HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
+    }
+    int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
+                     w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx);
+    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+    {
+      Scope sc(ctx, DFM_KC_FACTORS);
+      launch_factors(M->orient, src, T, N, r, n, w.Uk, w.F, w.L, nullptr, st);
+    }
+    {
+      Scope sc(ctx, DFM_KC_OLS);
+      hipLaunchKernelGGL(ols_hc2_kernel, dim3(n), dim3(256), 0, st, M->y, M->w, q, w.F, T, r, w.coef,
+                         w.tstat, nullptr, nullptr, w.ost);
+    }
+    {
+      Scope sc(ctx, DFM_KC_STATS);
+      if (ns)
+        hipLaunchKernelGGL(stats_kernel, dim3((n + 127) / 128), dim3(128), 0, st, n, T, N, r, q,
+                           M->crit, M->sigma2, w.lam, w.trace, w.coef, w.tstat, M->sd_dev, ns,
+                           out + b0 * width, width);
+      hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
+                         n, M->flag_dev);
+    }
+    if (chow) {
+      Scope sc(ctx, DFM_KC_CHOW);
+      // per-variable statistics for every requested Chow stat share one pass
+      double *LR = nullptr, *LM = nullptr, *WD = nullptr;
+      int64_t ostride = width;
+      for (int i = 0; i < ns; ++i) {
+        double *base = out + b0 * width + sd[i].off;
+        switch (sd[i].kind) {
+          case DFM_STAT_LR_ALL: LR = base; break;
+          case DFM_STAT_LM_ALL: LM = base; break;
+          case DFM_STAT_WALD_ALL: WD = base; break;
+          default: break;
+        }
+      }
+      // single-variable Chow stats are served by a full pass too (cheap); they
+      // are copied out of a scratch row afterwards.
+      HIPCHK(ctx, launch_chow(M->orient, src, T, N, r, chow_bp, n, w.F, w.L, LR, LM, WD, ostride,
+                              w.chow, w.chow_bytes, st));
+      for (int i = 0; i < ns; ++i) {
+        if (sd[i].kind < DFM_STAT_LR || sd[i].kind > DFM_STAT_WALD) continue;
+        // scratch rows live at the end of the chow workspace: [3][nb][N]
+        const double *scr = (const double *)(w.chow + w.chow_bytes) - (size_t)3 * nb * N;
+        const int which = sd[i].kind - DFM_STAT_LR;
+        HIPCHK(ctx, hipMemcpy2DAsync(out + b0 * width + sd[i].off, (size_t)width * 8,
+                                     scr + ((size_t)which * nb) * N + sd[i].arg1, (size_t)N * 8, 8, n,
+                                     hipMemcpyDeviceToDevice, st));
+      }
+    }
+  }
+  int flag = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&flag, M->flag_dev, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (flag & 1) return fail(ctx, 2, "eigensolver did not converge for some replicate");
+  if (flag & 2) return fail(ctx, 3, "singular design matrix in some replicate");
+  return 0;
+}
+
+int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+                  const dfm_stat *stats, int ns, double *out) {
+  if (!M) return -1;
+  dfm_ctx *ctx = M->ctx;
+  if (B < 0 || !idx || (kind == DFM_BOOT_WILD && !eta)) return fail(ctx, -2, "dfm_bootstrap: bad arguments");
+  if (B == 0) return 0;
+  for (int64_t i = 0; i < B * M->T; ++i)
+    if (idx[i] < 0 || idx[i] >= M->T) return fail(ctx, -8, "resample index out of range at %lld", (long long)i);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  const int64_t width = dfm_stats_width(M, stats, ns);
+  int32_t *di = nullptr;
+  double *de = nullptr, *dout = nullptr;
+  HIPCHK(ctx, dalloc(&di, (size_t)B * M->T));
+  if (eta) HIPCHK(ctx, dalloc(&de, (size_t)B * M->T));
+  HIPCHK(ctx, dalloc(&dout, (size_t)B * std::max<int64_t>(width, 1)));
+  HIPCHK(ctx, hipMemcpyAsync(di, idx, (size_t)B * M->T * 4, hipMemcpyHostToDevice, st));
+  if (eta) HIPCHK(ctx, hipMemcpyAsync(de, eta, (size_t)B * M->T * 8, hipMemcpyHostToDevice, st));
+  int rc = dfm_bootstrap_dev(M, kind, B, di, kind == DFM_BOOT_WILD ? de : nullptr, stats, ns, dout);
+  if (rc == 0 && width > 0)
+    rc = hipMemcpyAsync(out, dout, (size_t)B * width * 8, hipMemcpyDeviceToHost, st) == hipSuccess ? 0 : 1001;
+  hipStreamSynchronize(st);
+  hipFree(di); hipFree(de); hipFree(dout);
+  return rc;
+}
+
+}  // extern "C"
+
+// --------------------------------------------------------- stand-alone entry points
+namespace {
+struct DevPanel {
+  double *raw = nullptr, *P = nullptr;
+  int64_t ld = 0;
+  ~DevPanel() { hipFree(raw); hipFree(P); }
+};
+int upload_panel(dfm_ctx *ctx, const double *X, int T, int N, int64_t ldx, DevPanel &dp) {
+  hipStream_t st = ctx->stream;
+  dp.ld = round_up(N, 16);
+  HIPCHK(ctx, dalloc(&dp.raw, (size_t)T * N));
+  HIPCHK(ctx, dalloc(&dp.P, (size_t)T * dp.ld));
+  HIPCHK(ctx, hipMemcpy2DAsync(dp.raw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N,
+                               hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(panel_from_colmajor_kernel, dim3((unsigned)((dp.ld + 31) / 32), (T + 31) / 32),
+                     dim3(256), 0, st, dp.raw, (int64_t)T, T, N, dp.P, dp.ld);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+void rows_to_colmajor_host(const std::vector<double> &src, int rows, int cols, double *dst) {
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) dst[(size_t)j * rows + i] = src[(size_t)i * cols + j];
+}
+}  // namespace
+
+extern "C" {
+
+int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, int64_t ldx, int k,
+            double *eigvals, double *F, double *L, double *trace_G) {
+  if (!ctx) return -1;
+  if (!X || T64 < 1 || N64 < 1 || ldx < T64 || k < 1) return fail(ctx, -2, "dfm_pca: bad arguments");
+  const int T = (int)T64, N = (int)N64, m = std::min(T, N);
+  if (k > m) return fail(ctx, -2, "dfm_pca: k=%d > min(T,N)=%d", k, m);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  DevPanel dp;
+  int rc = upload_panel(ctx, X, T, N, ldx, dp);
+  if (rc) return rc;
+  const int orient = (N > T) ? 0 : 1;
+  double *G = nullptr, *lam = nullptr, *Uk = nullptr, *tr = nullptr, *Fd = nullptr, *Ld = nullptr;
+  int *sd = nullptr;
+  HIPCHK(ctx, dalloc(&G, (size_t)m * m));
+  HIPCHK(ctx, dalloc(&lam, k)); HIPCHK(ctx, dalloc(&Uk, (size_t)m * k)); HIPCHK(ctx, dalloc(&tr, 1));
+  HIPCHK(ctx, dalloc(&Fd, (size_t)T * k)); HIPCHK(ctx, dalloc(&Ld, (size_t)N * k)); HIPCHK(ctx, dalloc(&sd, 1));
+  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld};
+  {
+    Scope sc(ctx, DFM_KC_GRAM);
+    HIPCHK(ctx, launch_gram(orient, src, m, orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
+  }
+  rc = run_eig(ctx, G, m, 1, k, nullptr, 0, lam, Uk, tr, sd);
+  int est = 0;
+  if (!rc) {
+    Scope sc(ctx, DFM_KC_FACTORS);
+    if (launch_factors(orient, src, T, N, k, 1, Uk, Fd, Ld, nullptr, st)) rc = fail(ctx, -4, "k too large");
+  }
+  std::vector<double> hF((size_t)T * k), hL((size_t)N * k);
+  if (!rc) {
+    if (eigvals) HIPCHK(ctx, hipMemcpyAsync(eigvals, lam, (size_t)k * 8, hipMemcpyDeviceToHost, st));
+    if (trace_G) HIPCHK(ctx, hipMemcpyAsync(trace_G, tr, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hF.data(), Fd, hF.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hL.data(), Ld, hL.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&est, sd, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (F) rows_to_colmajor_host(hF, T, k, F);
+    if (L) rows_to_colmajor_host(hL, N, k, L);
+  }
+  for (double *p : {G, lam, Uk, tr, Fd, Ld}) hipFree(p);
+  hipFree(sd);
+  if (rc) return rc;
+  if (est) return fail(ctx, 2, "eigensolver did not converge");
+  return 0;
+}
+
+int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, int64_t ldx,
+                      double *eigvals_m, double *trace_G) {
+  if (!ctx) return -1;
+  if (!X || !eigvals_m || T64 < 1 || N64 < 1 || ldx < T64) return fail(ctx, -2, "bad arguments");
+  const int T = (int)T64, N = (int)N64, m = std::min(T, N);
+  if (m > spectrum_max()) return fail(ctx, -30, "full spectrum supported for min(T,N) <= %d", spectrum_max());
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  DevPanel dp;
+  int rc = upload_panel(ctx, X, T, N, ldx, dp);
+  if (rc) return rc;
+  const int orient = (N > T) ? 0 : 1;
+  double *G = nullptr, *ev = nullptr;
+  HIPCHK(ctx, dalloc(&G, (size_t)m * m));
+  HIPCHK(ctx, dalloc(&ev, m));
+  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld};
+  {
+    Scope sc(ctx, DFM_KC_GRAM);
+    HIPCHK(ctx, launch_gram(orient, src, m, orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
+  }
+  {
+    Scope sc(ctx, DFM_KC_EIG_OTHER);
+    HIPCHK(ctx, launch_spectrum(G, m, (int64_t)m * m, m, 1, ev, st));
+  }
+  HIPCHK(ctx, hipMemcpyAsync(eigvals_m, ev, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+  if (trace_G) {
+    std::vector<double> g((size_t)m * m);
+    HIPCHK(ctx, hipMemcpyAsync(g.data(), G, g.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    double s = 0;
+    for (int i = 0; i < m; ++i) s += g[(size_t)i * m + i];
+    *trace_G = s;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  hipFree(G); hipFree(ev);
+  return 0;
+}
+
+int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald) {
+  if (!M) return -1;
+  dfm_ctx *ctx = M->ctx;
+  if (bp < M->r || bp > M->T - M->r) return fail(ctx, -7, "break period %lld out of range", (long long)bp);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  const size_t bytes = chow_workspace_bytes(M->T, M->N, M->r, 1);
+  char *ws = nullptr;
+  HIPCHK(ctx, hipMalloc(&ws, bytes));
+  PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld};
+  {
+    Scope sc(ctx, DFM_KC_CHOW);
+    HIPCHK(ctx, launch_chow(M->orient, src, M->T, M->N, M->r, (int)bp, 1, M->F, M->L, nullptr, nullptr,
+                            nullptr, M->N, ws, bytes, st));
+  }
+  const double *scr = (const double *)(ws + bytes) - (size_t)3 * M->N;
+  double *outs[3] = {LR, LM, Wald};
+  for (int i = 0; i < 3; ++i)
+    if (outs[i]) HIPCHK(ctx, hipMemcpyAsync(outs[i], scr + (size_t)i * M->N, (size_t)M->N * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  hipFree(ws);
+  return 0;
+}
+
+int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                      const double *X, int64_t T64, int64_t N64, int64_t ldx, int mode,
+                      double crit_value, double *tstat, uint8_t *mask) {
+  if (!ctx) return -1;
+  if (!y || !X || !tstat || !mask || T64 < 2 || N64 < 1 || ldx < T64 || q < 0 || (q > 0 && (!w || ldw < T64)))
+    return fail(ctx, -2, "dfm_targeted_hard: bad arguments");
+  if (mode != DFM_TP_JOINT && mode != DFM_TP_PER_CANDIDATE) return fail(ctx, -2, "bad mode");
+  const int T = (int)T64, N = (int)N64;
+  if (mode == DFM_TP_JOINT && q + N >= T)
+    return fail(ctx, 3, "joint hard thresholding is singular for q + N >= T (defect D8); use PER_CANDIDATE");
+  if (mode == DFM_TP_JOINT && q + N > 64) return fail(ctx, -32, "JOINT mode supports q + N <= 64");
+  if (mode == DFM_TP_PER_CANDIDATE && (q < 1 || q > 16)) return fail(ctx, -32, "PER_CANDIDATE needs 1 <= q <= 16");
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  DevPanel dp;
+  int rc = upload_panel(ctx, X, T, N, ldx, dp);
+  if (rc) return rc;
+  double *dy = nullptr, *dw = nullptr, *dt = nullptr;
+  uint8_t *dm = nullptr;
+  int *bad = nullptr;
+  char *ws = nullptr;
+  const size_t wsb = targeted_workspace_bytes(mode, T, N, q);
+  HIPCHK(ctx, dalloc(&dy, T)); HIPCHK(ctx, dalloc(&dw, (size_t)T * std::max(q, 1)));
+  HIPCHK(ctx, dalloc(&dt, N)); HIPCHK(ctx, hipMalloc(&dm, N)); HIPCHK(ctx, dalloc(&bad, 1));
+  HIPCHK(ctx, hipMalloc(&ws, wsb));
+  HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
+  if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  {
+    Scope sc(ctx, DFM_KC_MISC);
+    HIPCHK(ctx, launch_targeted(mode, dy, dw, q, dp.P, dp.ld, T, N, crit_value, dt, dm, ws, wsb, st, bad));
+  }
+  int hb = 0;
+  HIPCHK(ctx, hipMemcpyAsync(tstat, dt, (size_t)N * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(mask, dm, (size_t)N, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&hb, bad, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  hipFree(dy); hipFree(dw); hipFree(dt); hipFree(dm); hipFree(bad); hipFree(ws);
+  if (hb) return fail(ctx, 3, "singular design matrix");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// dfm_common.h — shared device types and helpers for libdfm (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DFM_DEV __device__ __forceinline__
+
+namespace dfm {
+
+// A resampled panel X*, never materialised: for row t of replicate b
+//   X*[t, n] = C[t, n] + eta_b[t] * E[idx_b[t], n]
+// C == nullptr -> 0, eta == nullptr -> 1, idx == nullptr -> identity.
+// C and E are row-major T x N with row stride `ld` (elements); idx/eta are
+// B x T row-major.  This is the wild/residual bootstrap of
+// src/bootstrap.jl:44-45 (:24 for the residual form) and, with C = E = X and
+// no idx/eta, the plain panel of principal_components (src/DynamicFactorModel.jl:75).
+struct PanelSrc {
+  const double *C;
+  const double *E;
+  const int32_t *idx;
+  const double *eta;
+  int64_t ld;
+};
+
+// v_mfma_f64_4x4x4_4b_f64: 4 independent 4x4x4 blocks per instruction
+// (75 TF/s measured on MI355X vs 49.5 for 16x16x4 — tools/mfma_f64_probe.hip).
+// Lane l: k = l>>4, blk = (l>>2)&3, i = l&3.
+//   A[blk][i][k] at lane 16k + 4blk + i, B[blk][k][j] at 16k + 4blk + j,
+//   C[blk][i][j] at lane 16i + 4blk + j  (tools/mfma4_layout.hip, one-hot probe).
+DFM_DEV double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+DFM_DEV double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Deterministic pseudo-random start vectors for the subspace iteration.
+DFM_DEV double hash_unit(uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full ^
+               (c + 0x165667B19E3779F9ull) * 0x27D4EB2F165667C5ull;
+  x ^= x >> 31; x *= 0x7FB5D329728EA185ull; x ^= x >> 27; x *= 0x81DADEF4BC2DD44Dull; x ^= x >> 33;
+  return (double)(x >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+}
+
+}  // namespace dfm
+
+// Kernel classes for per-kernel HIP-event timing (dfm_ctx_read_timing).
+enum {
+  DFM_KC_GRAM = 0, DFM_KC_EIG_GQ, DFM_KC_EIG_SMALL, DFM_KC_EIG_APPLY, DFM_KC_EIG_OTHER,
+  DFM_KC_FACTORS, DFM_KC_OLS, DFM_KC_STATS, DFM_KC_CHOW, DFM_KC_MISC, DFM_KC_COUNT
+};

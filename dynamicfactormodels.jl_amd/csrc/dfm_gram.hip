@@ -1,0 +1,206 @@
+// dfm_gram.hip — K1: batched fp64 Gram of resampled panels, fused gather, MFMA.
+//
+// Replaces the Gram + LAPACK front of principal_components
+// (src/DynamicFactorModel.jl:78 `x'x` for T >= N, :87 `x*x'` for N > T),
+// evaluated on the bootstrap panel X* = F_r L_r' + diag(eta) E[idx, :]
+// (src/bootstrap.jl:44-45) without materialising X*.
+//
+// Orientation ROWS (N > T): G = X* X*'  (m = T, reduction over n = 0..N-1)
+// Orientation COLS (T >= N): G = X*' X* (m = N, reduction over t = 0..T-1)
+//
+// Tiling: one 256-thread workgroup per 64x64 lower-triangular output tile of
+// one replicate; 4 waves each own a 32x32 sub-tile = 8x8 fragments of 4x4.
+// Each 16-deep k-step issues 64 v_mfma_f64_4x4x4_4b_f64 per wave: the four
+// MFMA blocks split the 16-deep reduction 4 ways and are summed once in the
+// epilogue (transpose-reduce: 3 shuffles per 4 accumulators).  Operands are
+// gathered + fused (C + eta*E[idx]) while staged through a double-buffered,
+// XOR-swizzled LDS image (conflict-free ds_read_b64 for the MFMA lane maps,
+// conflict-free ds_write_b128 for the staging rows).  One barrier per k-step.
+//
+// Requirements: panels C/E have zero-filled padding columns N..ld-1 and
+// ld % 16 == 0.  Output G is the full symmetric m x m matrix (row-major, ldg).
+#include "dfm_common.h"
+
+namespace dfm {
+
+constexpr int GT = 64;  // workgroup output tile
+constexpr int KS = 16;  // k per stage == one MFMA k-step
+enum { ORIENT_ROWS = 0, ORIENT_COLS = 1 };
+
+// LDS image of one 64 x 16 operand tile (1024 doubles).
+template <int ORIENT>
+DFM_DEV int lds_off(int a, int kc) {
+  if constexpr (ORIENT == ORIENT_ROWS) return a * KS + (kc ^ (((a >> 1) & 1) << 3));
+  else return kc * GT + (a ^ ((kc & 7) << 2));
+}
+
+template <int ORIENT, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
+__global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K, int T,
+                                                      double *__restrict__ G, int64_t ldg,
+                                                      int64_t strideG) {
+  __shared__ __attribute__((aligned(16))) double lds[2][2][GT * KS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int rep = blockIdx.y;
+  // lower-triangular tile enumeration: t -> (I, J), I >= J
+  const int tt = blockIdx.x;
+  int I = (int)((sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= tt) ++I;
+  while (I * (I + 1) / 2 > tt) --I;
+  const int J = tt - I * (I + 1) / 2;
+  const bool diag = (I == J);
+  const int abase = I * GT, bbase = J * GT;
+
+  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * T : nullptr;
+  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * T : nullptr;
+  const int64_t ld = src.ld;
+
+  // ---------------- staging state: each thread moves 2 x 16-B chunks per operand
+  double2 rc[2][2], re[2][2];  // [operand][chunk] raw C and E values
+  double ev[2][2];             // ROWS: per-row eta for [operand][chunk]
+  const double *pC[2][2], *pE[2][2];
+  bool rowok[2][2];
+
+  if constexpr (ORIENT == ORIENT_ROWS) {
+    // chunk c = tid + 256*h: row a = c >> 3, 16-B column pair j = c & 7
+#pragma unroll
+    for (int op = 0; op < 2; ++op)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int a = (tid >> 3) + 32 * h;
+        const int row = (op == 0 ? abase : bbase) + a;
+        rowok[op][h] = row < m;
+        const int rr = rowok[op][h] ? row : 0;
+        const int er = HAS_IDX ? idx[rr] : rr;
+        ev[op][h] = HAS_ETA ? eta[rr] : 1.0;
+        pC[op][h] = HAS_C ? src.C + (int64_t)rr * ld + 2 * (tid & 7) : nullptr;
+        pE[op][h] = src.E + (int64_t)er * ld + 2 * (tid & 7);
+      }
+  }
+
+  auto load_stage = [&](int k0) {
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      if (op == 1 && diag) break;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (ORIENT == ORIENT_ROWS) {
+          if (rowok[op][h]) {
+            re[op][h] = *reinterpret_cast<const double2 *>(pE[op][h] + k0);
+            if (HAS_C) rc[op][h] = *reinterpret_cast<const double2 *>(pC[op][h] + k0);
+          }
+        } else {
+          // chunk c: k-row kc = c >> 5 (t = k0 + kc), column pair j = c & 31
+          const int kc = (tid >> 5) + 8 * h;
+          const int t = k0 + kc;
+          const int col = (op == 0 ? abase : bbase) + 2 * (tid & 31);
+          const bool ok = (t < K) && (col < ld);
+          rowok[op][h] = ok;
+          if (ok) {
+            const int er = HAS_IDX ? idx[t] : t;
+            ev[op][h] = HAS_ETA ? eta[t] : 1.0;
+            re[op][h] = *reinterpret_cast<const double2 *>(src.E + (int64_t)er * ld + col);
+            if (HAS_C) rc[op][h] = *reinterpret_cast<const double2 *>(src.C + (int64_t)t * ld + col);
+          }
+        }
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      if (op == 1 && diag) break;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double2 v = {0.0, 0.0};
+        if (rowok[op][h]) {
+          const double e = ev[op][h];
+          v.x = HAS_C ? fma(e, re[op][h].x, rc[op][h].x) : (HAS_ETA ? e * re[op][h].x : re[op][h].x);
+          v.y = HAS_C ? fma(e, re[op][h].y, rc[op][h].y) : (HAS_ETA ? e * re[op][h].y : re[op][h].y);
+        }
+        int off;
+        if constexpr (ORIENT == ORIENT_ROWS) off = lds_off<ORIENT>((tid >> 3) + 32 * h, 2 * (tid & 7));
+        else off = lds_off<ORIENT>(2 * (tid & 31), (tid >> 5) + 8 * h);
+        *reinterpret_cast<double2 *>(&lds[buf][op][off]) = v;
+      }
+    }
+  };
+
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
+
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int nst = (K + KS - 1) / KS;
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) load_stage((s + 1) * KS);
+    const double *la = lds[buf][0];
+    const double *lb = diag ? lds[buf][0] : lds[buf][1];
+    double af[8], bf[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = la[lds_off<ORIENT>(wr * 32 + 4 * f + fi, fkc)];
+      bf[f] = lb[lds_off<ORIENT>(wc * 32 + 4 * f + fi, fkc)];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma4(af[i], bf[j], acc[i][j]);
+    if (s + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: transpose-reduce over the 4 MFMA blocks, store
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+  double *Gr = G + (int64_t)rep * strideG;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double a0 = acc[fa][4 * q + 0], a1 = acc[fa][4 * q + 1];
+      const double a2 = acc[fa][4 * q + 2], a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int row = abase + wr * 32 + 4 * fa + oi;
+      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+      if (row < m && col < m) {
+        Gr[(int64_t)row * ldg + col] = v;
+        if (!diag) Gr[(int64_t)col * ldg + row] = v;
+      }
+    }
+}
+
+// Dispatch.  Returns hipError of the launch.
+hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G,
+                       int64_t ldg, int64_t strideG, int nrep, hipStream_t st) {
+  const int nt = (m + GT - 1) / GT;
+  dim3 grid(nt * (nt + 1) / 2, nrep), block(256);
+  const bool c = src.C != nullptr, e = src.eta != nullptr, x = src.idx != nullptr;
+#define DFM_GRAM_L(O, C_, E_, X_) \
+  hipLaunchKernelGGL((gram_kernel<O, C_, E_, X_>), grid, block, 0, st, src, m, K, T, G, ldg, strideG)
+  if (orient == ORIENT_ROWS) {
+    if (c && e && x) DFM_GRAM_L(ORIENT_ROWS, true, true, true);
+    else if (c && !e && x) DFM_GRAM_L(ORIENT_ROWS, true, false, true);
+    else if (!c && !e && !x) DFM_GRAM_L(ORIENT_ROWS, false, false, false);
+    else if (!c && e && x) DFM_GRAM_L(ORIENT_ROWS, false, true, true);
+    else return hipErrorInvalidValue;
+  } else {
+    if (c && e && x) DFM_GRAM_L(ORIENT_COLS, true, true, true);
+    else if (c && !e && x) DFM_GRAM_L(ORIENT_COLS, true, false, true);
+    else if (!c && !e && !x) DFM_GRAM_L(ORIENT_COLS, false, false, false);
+    else if (!c && e && x) DFM_GRAM_L(ORIENT_COLS, false, true, true);
+    else return hipErrorInvalidValue;
+  }
+#undef DFM_GRAM_L
+  return hipGetLastError();
+}
+
+}  // namespace dfm

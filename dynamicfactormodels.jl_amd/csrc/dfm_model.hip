@@ -1,0 +1,409 @@
+// dfm_model.hip — K3: the fused, HBM-bound kernels around the eigensolver:
+// factor/loading passes, common-component / factor-residual panels, the
+// OLS + HC2 regression of y on [w F_r], and the per-replicate statistics.
+#include "dfm_common.h"
+
+namespace dfm {
+
+// Column-major T x N (ld ldx) -> row-major panel T x ld, zero padding.
+__global__ void panel_from_colmajor_kernel(const double *__restrict__ X, int64_t ldx, int T, int N,
+                                           double *__restrict__ P, int64_t ld) {
+  __shared__ double tile[32][33];
+  const int n0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int r = ty; r < 32; r += 8) {
+    const int n = n0 + r, t = t0 + tx;
+    tile[r][tx] = (n < N && t < T) ? X[(int64_t)n * ldx + t] : 0.0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int t = t0 + r, n = n0 + tx;
+    if (t < T && n < ld) P[(int64_t)t * ld + n] = tile[tx][r];
+  }
+}
+
+// Row-major (rep x rows x ld) -> column-major host layout helper on device.
+__global__ void colmajor_from_rows_kernel(const double *__restrict__ P, int64_t ld, int T, int N,
+                                          double *__restrict__ X) {
+  __shared__ double tile[32][33];
+  const int n0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int t = t0 + r, n = n0 + tx;
+    tile[r][tx] = (t < T && n < N) ? P[(int64_t)t * ld + n] : 0.0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int n = n0 + r, t = t0 + tx;
+    if (n < N && t < T) X[(int64_t)n * T + t] = tile[tx][r];
+  }
+}
+
+// ----------------------------------------------------------------- factors
+// N > T branch (src/DynamicFactorModel.jl:87-90): F = sqrt(T) U, L = X*' F / T.
+// One thread per variable n; F rows staged in LDS.  Also ||x*_n||^2 and the
+// per-variable factor-residual SSR ||x_n - F l_n||^2 = ||x_n||^2 - T ||l_n||^2.
+template <int KM, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
+__global__ __launch_bounds__(256) void factors_rows_kernel(PanelSrc src, int T, int N, int k,
+                                                           const double *__restrict__ Uk,
+                                                           double *__restrict__ F,
+                                                           double *__restrict__ L,
+                                                           double *__restrict__ colssr) {
+  constexpr int TR = 64;
+  __shared__ double sF[TR * KM];
+  __shared__ double sE[TR];
+  __shared__ int sI[TR];
+  const int rep = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  const double sT = sqrt((double)T);
+  const double *U = Uk + (int64_t)rep * T * k;
+  double *Fr = F + (int64_t)rep * T * k;
+  if (blockIdx.x == 0)
+    for (int e = threadIdx.x; e < T * k; e += 256) Fr[e] = sT * U[e];
+  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * T : nullptr;
+  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * T : nullptr;
+  double acc[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) acc[j] = 0.0;
+  double ss = 0.0;
+  const bool ok = n < N;
+  for (int t0 = 0; t0 < T; t0 += TR) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < TR * KM; e += 256) {
+      const int r = e / KM, j = e % KM;
+      sF[e] = (t0 + r < T && j < k) ? sT * U[(int64_t)(t0 + r) * k + j] : 0.0;
+    }
+    if (threadIdx.x < TR) {
+      const int t = t0 + threadIdx.x;
+      sE[threadIdx.x] = (HAS_ETA && t < T) ? eta[t] : 1.0;
+      sI[threadIdx.x] = (t < T) ? (HAS_IDX ? idx[t] : t) : 0;
+    }
+    __syncthreads();
+    const int tn = min(TR, T - t0);
+    if (ok) {
+      for (int r = 0; r < tn; ++r) {
+        const int t = t0 + r;
+        double x = src.E[(int64_t)sI[r] * src.ld + n];
+        if (HAS_ETA) x *= sE[r];
+        if (HAS_C) x += src.C[(int64_t)t * src.ld + n];
+        ss = fma(x, x, ss);
+#pragma unroll
+        for (int j = 0; j < KM; ++j) acc[j] = fma(x, sF[r * KM + j], acc[j]);
+      }
+    }
+  }
+  if (ok) {
+    double l2 = 0.0;
+    double *Lr = L + (int64_t)rep * N * k + (int64_t)n * k;
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) { const double l = acc[j] / T; Lr[j] = l; l2 = fma(l, l, l2); }
+    if (colssr) colssr[(int64_t)rep * N + n] = ss - T * l2;
+  }
+}
+
+// T >= N branch (src/DynamicFactorModel.jl:78-81): L = sqrt(N) V, F = X* L / N.
+// One wave per time row t.
+template <int KM, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
+__global__ __launch_bounds__(256) void factors_cols_kernel(PanelSrc src, int T, int N, int k,
+                                                           const double *__restrict__ Uk,
+                                                           double *__restrict__ F,
+                                                           double *__restrict__ L) {
+  const int rep = blockIdx.y, lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const double sN = sqrt((double)N);
+  const double *U = Uk + (int64_t)rep * N * k;
+  if (blockIdx.x == 0) {
+    double *Lr = L + (int64_t)rep * N * k;
+    for (int e = threadIdx.x; e < N * k; e += 256) Lr[e] = sN * U[e];
+  }
+  if (t >= T) return;
+  const int er = HAS_IDX ? src.idx[(int64_t)rep * T + t] : t;
+  const double ev = HAS_ETA ? src.eta[(int64_t)rep * T + t] : 1.0;
+  double acc[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) acc[j] = 0.0;
+  for (int n = lane; n < N; n += 64) {
+    double x = src.E[(int64_t)er * src.ld + n] * ev;
+    if (HAS_C) x += src.C[(int64_t)t * src.ld + n];
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) acc[j] = fma(x, U[(int64_t)n * k + j], acc[j]);
+  }
+  double *Fr = F + (int64_t)rep * T * k + (int64_t)t * k;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    const double s = wave_sum(acc[j]);
+    if (j < k && lane == 0) Fr[j] = s * sN / N;   // X (sqrt(N) V) / N
+  }
+}
+
+// Per-variable SSR in the T >= N branch: ||x_n||^2 - sum_j lambda_j U[n][j]^2
+// (G_nn from the Gram diagonal).
+__global__ void colssr_cols_kernel(const double *__restrict__ G, int64_t ldg, int64_t strideG, int N,
+                                   int k, const double *__restrict__ lam,
+                                   const double *__restrict__ Uk, double *__restrict__ colssr) {
+  const int rep = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  double s = G[(int64_t)rep * strideG + (int64_t)n * ldg + n];
+  for (int j = 0; j < k; ++j) {
+    const double u = Uk[(int64_t)rep * N * k + (int64_t)n * k + j];
+    s -= lam[(int64_t)rep * k + j] * u * u;
+  }
+  colssr[(int64_t)rep * N + n] = s;
+}
+
+// Common component C = F L' and factor residuals E = X - C
+// (src/DynamicFactorModel.jl:33), row-major panels with zero padding.
+__global__ void common_residual_kernel(const double *__restrict__ X, int64_t ld, int T, int N, int k,
+                                       const double *__restrict__ F, const double *__restrict__ L,
+                                       double *__restrict__ C, double *__restrict__ E) {
+  const int t = blockIdx.y;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= ld) return;
+  double c = 0.0;
+  if (n < N)
+    for (int j = 0; j < k; ++j) c = fma(F[(int64_t)t * k + j], L[(int64_t)n * k + j], c);
+  const double x = X[(int64_t)t * ld + n];
+  C[(int64_t)t * ld + n] = c;
+  E[(int64_t)t * ld + n] = (n < N) ? x - c : 0.0;
+}
+
+// ------------------------------------------------------------------- OLS
+// src/DynamicFactorModel.jl:40-48: D = [w F_r], beta = (D'D)^-1 D'y,
+// u = y - D beta, h_t = d_t'(D'D)^-1 d_t, sigma2_t = u_t^2 / (1 - h_t) (HC2),
+// Sigma = (D'D)^-1 (sum_t sigma2_t d_t d_t') (D'D)^-1, t = beta / sqrt(diag).
+// One 256-thread workgroup per replicate; d = q + k <= 32.
+constexpr int OLS_DMAX = 32;
+constexpr int OLS_TR = 128;
+__global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__ y,
+                                                      const double *__restrict__ w, int q,
+                                                      const double *__restrict__ F, int T, int k,
+                                                      double *__restrict__ coef,
+                                                      double *__restrict__ tstat,
+                                                      double *__restrict__ cov_out,
+                                                      double *__restrict__ resid_out,
+                                                      int *__restrict__ status) {
+  constexpr int S = OLS_DMAX + 1;
+  __shared__ double sD[OLS_TR * S];
+  __shared__ double sy[OLS_TR], ssig[OLS_TR];
+  __shared__ double M[OLS_DMAX * S], Li[OLS_DMAX * S], Inv[OLS_DMAX * S], Meat[OLS_DMAX * S],
+      Tmp[OLS_DMAX * S];
+  __shared__ double sb[OLS_DMAX], sDy[OLS_DMAX];
+  __shared__ int sbad;
+  const int tid = threadIdx.x, rep = blockIdx.x;
+  const int d = q + k;
+  const double *Fr = F + (int64_t)rep * T * k;
+  auto stage = [&](int t0) {
+    for (int e = tid; e < OLS_TR * d; e += 256) {
+      const int r = e / d, c = e % d, t = t0 + r;
+      double v = 0.0;
+      if (t < T) v = c < q ? w[(int64_t)c * T + t] : Fr[(int64_t)t * k + (c - q)];
+      sD[r * S + c] = v;
+    }
+    for (int r = tid; r < OLS_TR; r += 256) sy[r] = (t0 + r < T) ? y[t0 + r] : 0.0;
+  };
+  // pass 1: D'D, D'y
+  double accm[4] = {0, 0, 0, 0}, accy = 0.0;
+  for (int t0 = 0; t0 < T; t0 += OLS_TR) {
+    __syncthreads();
+    stage(t0);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      if (e < d * d) {
+        const int a = e / d, c = e % d;
+        double s = accm[u];
+        for (int r = 0; r < OLS_TR; ++r) s = fma(sD[r * S + a], sD[r * S + c], s);
+        accm[u] = s;
+      }
+    }
+    if (tid < d) {
+      double s = accy;
+      for (int r = 0; r < OLS_TR; ++r) s = fma(sD[r * S + tid], sy[r], s);
+      accy = s;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + 256 * u;
+    if (e < d * d) M[(e / d) * S + e % d] = accm[u];
+  }
+  if (tid < d) sDy[tid] = accy;
+  if (tid == 0) sbad = 0;
+  __syncthreads();
+  // Cholesky D'D = L L' (all threads step through j), then Inv = L^-T L^-1
+  for (int e = tid; e < OLS_DMAX * S; e += 256) Li[e] = 0.0;
+  __syncthreads();
+  for (int j = 0; j < d; ++j) {
+    if (tid == 0) {
+      double s = M[j * S + j];
+      for (int p = 0; p < j; ++p) s -= Li[j * S + p] * Li[j * S + p];
+      if (!(s > 0.0)) { sbad = 1; s = 1.0; }
+      Li[j * S + j] = sqrt(s);
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < d; i += 256) {
+      double s = M[i * S + j];
+      for (int p = 0; p < j; ++p) s -= Li[i * S + p] * Li[j * S + p];
+      Li[i * S + j] = s / Li[j * S + j];
+    }
+    __syncthreads();
+  }
+  // Tmp = L^-1 (column c per thread, forward substitution on e_c)
+  for (int c = tid; c < d; c += 256)
+    for (int i = 0; i < d; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int p = c; p < i; ++p) s -= Li[i * S + p] * Tmp[p * S + c];
+      Tmp[i * S + c] = i < c ? 0.0 : s / Li[i * S + i];
+    }
+  __syncthreads();
+  for (int e = tid; e < d * d; e += 256) {
+    const int a = e / d, c = e % d;
+    double s = 0.0;
+    for (int p = max(a, c); p < d; ++p) s = fma(Tmp[p * S + a], Tmp[p * S + c], s);
+    Inv[a * S + c] = s;
+  }
+  __syncthreads();
+  if (tid < d) {
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Inv[tid * S + p], sDy[p], s);
+    sb[tid] = s;
+  }
+  __syncthreads();
+  // pass 2: residuals, leverages, HC2 meat
+  double accq[4] = {0, 0, 0, 0};
+  for (int t0 = 0; t0 < T; t0 += OLS_TR) {
+    __syncthreads();
+    stage(t0);
+    __syncthreads();
+    for (int r = tid; r < OLS_TR; r += 256) {
+      const int t = t0 + r;
+      if (t >= T) { ssig[r] = 0.0; continue; }
+      double fit = 0.0, h = 0.0;
+      for (int a = 0; a < d; ++a) {
+        const double da = sD[r * S + a];
+        fit = fma(da, sb[a], fit);
+        double ia = 0.0;
+        for (int c = 0; c < d; ++c) ia = fma(Inv[a * S + c], sD[r * S + c], ia);
+        h = fma(da, ia, h);
+      }
+      const double u = sy[r] - fit;
+      if (resid_out) resid_out[t] = u;
+      ssig[r] = u * u / (1.0 - h);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      if (e < d * d) {
+        const int a = e / d, c = e % d;
+        double s = accq[u];
+        for (int r = 0; r < OLS_TR; ++r) s = fma(ssig[r] * sD[r * S + a], sD[r * S + c], s);
+        accq[u] = s;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + 256 * u;
+    if (e < d * d) Meat[(e / d) * S + e % d] = accq[u];
+  }
+  __syncthreads();
+  for (int e = tid; e < d * d; e += 256) {
+    const int a = e / d, c = e % d;
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Meat[a * S + p], Inv[p * S + c], s);
+    Tmp[a * S + c] = s;
+  }
+  __syncthreads();
+  for (int e = tid; e < d * d; e += 256) {
+    const int a = e / d, c = e % d;
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Inv[a * S + p], Tmp[p * S + c], s);
+    M[a * S + c] = s;   // coefficient covariance
+  }
+  __syncthreads();
+  if (tid < d) {
+    coef[(int64_t)rep * d + tid] = sb[tid];
+    tstat[(int64_t)rep * d + tid] = sb[tid] / sqrt(M[tid * S + tid]);
+  }
+  if (cov_out)
+    for (int e = tid; e < d * d; e += 256) cov_out[(int64_t)rep * d * d + (e % d) * d + e / d] = M[(e / d) * S + e % d];
+  if (tid == 0 && status) status[rep] = sbad ? 2 : 0;
+}
+
+// ---------------------------------------------------------------- stats
+// Criteria, src/criteria.jl:17-53 (V from the trace identity).
+DFM_DEV double criterion_dev(int code, double V, int k, int T, int N, double sigma2) {
+  const double c = (double)(N + T) / ((double)N * (double)T);
+  const double m = (double)min(T, N);
+  switch (code) {
+    case 0: return V + k * sigma2 * c * log(1.0 / c);
+    case 1: return V + k * sigma2 * c * log(m);
+    case 2: return V + k * sigma2 * log(m) / m;
+    case 3: return log(V) + k * c * log(1.0 / c);
+    case 4: return log(V) + k * c * log(m);
+    case 5: return log(V) + k * log(m) / m;
+    case 6: return V + k * log((double)T) / T;
+  }
+  return NAN;
+}
+
+struct StatDesc { int kind, arg0, arg1, off; };
+
+// One thread per replicate.  out row stride = width.
+__global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, double sigma2,
+                             const double *__restrict__ lam, const double *__restrict__ trace,
+                             const double *__restrict__ coef, const double *__restrict__ tstat,
+                             const StatDesc *__restrict__ sd, int ns, double *__restrict__ out,
+                             int64_t width) {
+  const int rep = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rep >= nb) return;
+  double s = trace[rep];
+  for (int j = 0; j < r; ++j) s -= lam[(int64_t)rep * r + j];
+  const double V = s / ((double)N * (double)T);
+  const int d = q + r;
+  for (int i = 0; i < ns; ++i) {
+    const StatDesc st = sd[i];
+    double v = NAN;
+    switch (st.kind) {
+      case 0: v = V; break;
+      case 1: v = criterion_dev(st.arg0 >= 0 ? st.arg0 : crit, V, r, T, N, sigma2); break;
+      case 2: v = st.arg0 < r ? lam[(int64_t)rep * r + st.arg0] : NAN; break;
+      case 3: v = st.arg0 < d ? coef[(int64_t)rep * d + st.arg0] : NAN; break;
+      case 4: v = st.arg0 < d ? tstat[(int64_t)rep * d + st.arg0] : NAN; break;
+      case 5: v = trace[rep]; break;
+      default: continue;   // per-variable stats are written by the Chow kernel
+    }
+    out[(int64_t)rep * width + st.off] = v;
+  }
+}
+
+template <int KM>
+static void launch_factors_km(int orient, const PanelSrc &src, int T, int N, int k, int nb,
+                              const double *Uk, double *F, double *L, double *colssr, hipStream_t st) {
+  const bool c = src.C, e = src.eta, x = src.idx;
+#define DFM_FR(C_, E_, X_)                                                                         \
+  if (orient == 0)                                                                                 \
+    hipLaunchKernelGGL((factors_rows_kernel<KM, C_, E_, X_>), dim3((N + 255) / 256, nb), dim3(256), \
+                       0, st, src, T, N, k, Uk, F, L, colssr);                                     \
+  else                                                                                             \
+    hipLaunchKernelGGL((factors_cols_kernel<KM, C_, E_, X_>), dim3((T + 3) / 4, nb), dim3(256), 0, \
+                       st, src, T, N, k, Uk, F, L);
+  if (c && e && x) { DFM_FR(true, true, true) }
+  else if (c && !e && x) { DFM_FR(true, false, true) }
+  else { DFM_FR(false, false, false) }
+#undef DFM_FR
+}
+int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb,
+                          const double *Uk, double *F, double *L, double *colssr, hipStream_t st) {
+  if (k <= 8) launch_factors_km<8>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
+  else if (k <= 16) launch_factors_km<16>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
+  else if (k <= 32) launch_factors_km<32>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
+  else return -1;
+  return 0;
+}
+
+
+}  // namespace dfm

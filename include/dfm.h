@@ -1,0 +1,167 @@
+/*
+ * dfm.h — C ABI of libdfm, the MI355X-native engine for the data-parallel core
+ * of DynamicFactorModels.jl (joidegn/DynamicFactorModels.jl).
+ *
+ * The reference has no FFI: its boundary is the exported Julia API
+ * (src/DynamicFactorModels.jl:16-20).  Each entry point below replaces the
+ * reference function cited next to it; the Julia `ccall` shim and the Python
+ * ctypes mirror that bind them are shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Return codes: 0 ok; <0 invalid argument / shape; >0 HIP or numerical
+ *     error (singular design, eigensolver not converged).  No exception,
+ *     abort or exit crosses the ABI; dfm_last_error() has the message.
+ *   - Host arrays are caller-owned; the library copies in/out and never
+ *     retains host pointers.  Matrices passed from the host are COLUMN-major
+ *     (Julia) with a leading dimension; vectors are contiguous.
+ *   - *_dev entry points take DEVICE pointers on the context's device and run
+ *     on the context's stream (dfm_ctx_set_stream lets the caller supply its
+ *     own, e.g. PyTorch's current stream).  They never synchronise the host
+ *     except where a convergence poll needs a 4-byte read-back.
+ *   - Indices are 0-based int32 (the Julia shim subtracts 1).
+ *   - One context per GPU, used by one host thread at a time.
+ */
+#ifndef DFM_H
+#define DFM_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dfm_ctx dfm_ctx;
+typedef struct dfm_model dfm_model; /* a fitted base model resident in HBM */
+
+/* Information criteria, src/criteria.jl:17-53 (name-based dispatch at
+ * src/DynamicFactorModel.jl:138 becomes this code). */
+enum dfm_criterion {
+  DFM_CRIT_NONE = -1,
+  DFM_CRIT_PCP1 = 0, DFM_CRIT_PCP2 = 1, DFM_CRIT_PCP3 = 2,
+  DFM_CRIT_ICP1 = 3, DFM_CRIT_ICP2 = 4, DFM_CRIT_ICP3 = 5,
+  DFM_CRIT_BIC = 6
+};
+
+/* Replicate statistics.  The reference's `stat::Function` callback
+ * (src/bootstrap.jl:21, :41) cannot run on the device, so it is this fixed
+ * menu.  Each dfm_stat yields ONE double per replicate, except the *_ALL
+ * kinds which yield N doubles (one per variable). */
+enum dfm_stat_kind {
+  DFM_STAT_V = 0,          /* factor_residual_variance, src/criteria.jl:5       */
+  DFM_STAT_CRIT = 1,       /* criterion value (arg0 = dfm_criterion code)       */
+  DFM_STAT_EIGVAL = 2,     /* eigenvalue arg0 (0-based, descending)             */
+  DFM_STAT_COEF = 3,       /* OLS coefficient arg0, src/DynamicFactorModel.jl:41 */
+  DFM_STAT_TSTAT = 4,      /* HC2 t-stat arg0, src/DynamicFactorModel.jl:48     */
+  DFM_STAT_TRACE = 5,      /* trace of the Gram (= ||X*||_F^2)                  */
+  DFM_STAT_LR = 6,         /* LR_test(dfm, bp=arg0, i=arg1), src/chowtest.jl:19 */
+  DFM_STAT_LM = 7,         /* LM_test, src/chowtest.jl:35                       */
+  DFM_STAT_WALD = 8,       /* Wald_test, src/chowtest.jl:25                     */
+  DFM_STAT_LR_ALL = 9,     /* LR for every variable i (N values), bp = arg0     */
+  DFM_STAT_LM_ALL = 10,
+  DFM_STAT_WALD_ALL = 11
+};
+typedef struct dfm_stat { int32_t kind, arg0, arg1, pad; } dfm_stat;
+
+enum dfm_boot_kind { DFM_BOOT_WILD = 0, DFM_BOOT_RESIDUAL = 1 };
+enum dfm_tp_mode { DFM_TP_JOINT = 0, DFM_TP_PER_CANDIDATE = 1 };
+
+/* ---------------------------------------------------------------- context */
+int dfm_ctx_create(int device, dfm_ctx **out);
+int dfm_ctx_destroy(dfm_ctx *ctx);
+const char *dfm_last_error(const dfm_ctx *ctx);
+int dfm_ctx_set_stream(dfm_ctx *ctx, void *hip_stream); /* NULL = own stream */
+int dfm_ctx_synchronize(dfm_ctx *ctx);
+/* Eigensolver controls: relative residual tolerance (default 1e-12), maximum
+ * subspace iterations (default 400), block width (0 = auto). */
+int dfm_ctx_set_eig_params(dfm_ctx *ctx, double tol, int max_iter, int block);
+/* Per-kernel HIP-event timing on the context stream (bench/roofline use). */
+int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable);
+/* ms accumulated per kernel class (see DFM_KCLASS_* in the implementation);
+ * returns the number of classes written into ms_out/launches_out. */
+int dfm_ctx_read_timing(dfm_ctx *ctx, double *ms_out, int64_t *launches_out, int cap);
+int dfm_ctx_reset_timing(dfm_ctx *ctx);
+const char *dfm_kernel_class_name(int cls);
+
+/* ------------------------------------------------ principal components
+ * principal_components (src/DynamicFactorModel.jl:75-95), no breaks:
+ *   T >= N: G = X'X, L = sqrt(N) V, F = X L / N
+ *   N >  T: G = XX', F = sqrt(T) U, L = X' F / T
+ * Top-k eigenpairs only (the reference consumes [:,1:r]; :33, :131).
+ * X column-major T x N (ldx >= T).  Outputs: eigvals[k] descending,
+ * F (T x k, col-major, ld T), L (N x k, col-major, ld N), trace_G (may be NULL).
+ * Eigenvectors are sign-canonicalised (largest-|.| entry positive). */
+int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T, int64_t N, int64_t ldx,
+            int k, double *eigvals, double *F, double *L, double *trace_G);
+
+/* Full spectrum of the Gram (eigenvalues only, descending) for
+ * min(T,N) <= dfm_full_spectrum_max(); used by PCp's unrestricted sigma^2
+ * (src/criteria.jl:18) and full IC sweeps. */
+int dfm_full_spectrum_max(void);
+int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T, int64_t N,
+                      int64_t ldx, double *eigvals_m, double *trace_G);
+
+/* ----------------------------------------------------- IC sweep (host math)
+ * Criteria for k = 1..kmax from the eigenvalues (identity ||E_k||_F^2 =
+ * trace(G) - sum_{j<=k} lambda_j).  sigma2 < 0 means "compute
+ * V(ceil(m/2)) from eigvals" (needs ceil(m/2) eigenvalues).  crit_out is
+ * 7 x kmax row-major in dfm_criterion order.  Pure arithmetic; no device. */
+int dfm_ic_sweep(const double *eigvals, int n_eig, int kmax, double trace_G,
+                 int64_t T, int64_t N, double sigma2, double *crit_out);
+
+/* ------------------------------------------------------------ model fit
+ * Workhorse constructor (src/DynamicFactorModel.jl:28-51) at fixed r, and
+ * the IC-sweep constructor (:53-66) when r <= 0: r is then chosen by
+ * criterion `crit` over k = 1..kmax (kmax <= 0 -> ceil(m/2), defect D11).
+ * y (T), w (T x q col-major, ldw >= T), X (T x N col-major).  The fitted
+ * model (factors, loadings, common component, factor residuals) stays in HBM
+ * for the bootstrap and Chow entry points. */
+int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                  const double *X, int64_t T, int64_t N, int64_t ldx,
+                  int r, int crit, int kmax, dfm_model **out);
+int dfm_model_destroy(dfm_model *m);
+/* Scalars: [r, V(r), criterion value, trace_G]. */
+int dfm_model_scalars(const dfm_model *m, int64_t *r_out, double *V, double *crit_value,
+                      double *trace_G);
+/* Host copies (any pointer may be NULL): eigvals (kmax), coefficients and
+ * t-stats (q+r), coefficient covariance ((q+r)^2 col-major), OLS residuals
+ * (T), F (T x r col-major), L (N x r col-major), factor residuals E (T x N
+ * col-major, ld T), criteria for k=1..kmax (7 x kmax) when crit >= 0. */
+int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *tstat,
+                   double *coef_cov, double *ols_resid, double *F, double *L,
+                   double *E, double *ic_values);
+
+/* ------------------------------------------------------------- bootstrap
+ * wild_bootstrap (src/bootstrap.jl:41-51) / residual_bootstrap (:21-39):
+ * for b < B: X*_b = F_r L_r' + diag(eta_b) E[idx_b, :]  (eta == NULL for
+ * RESIDUAL), refit at the model's r and criterion, emit the stats.
+ * idx: B x T int32 (row-major, 0-based), eta: B x T.  out: B rows of
+ * sum(width(stat)) doubles (row-major). */
+int dfm_bootstrap(dfm_model *m, int kind, int64_t B, const int32_t *idx,
+                  const double *eta, const dfm_stat *stats, int nstats, double *out);
+/* Same, all pointers on the device (inputs resident in HBM). */
+int dfm_bootstrap_dev(dfm_model *m, int kind, int64_t B, const int32_t *idx_dev,
+                      const double *eta_dev, const dfm_stat *stats, int nstats,
+                      double *out_dev);
+/* Width of one replicate's output row for a stat list. */
+int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats);
+/* Replicates per device batch (0 = auto). */
+int dfm_model_set_batch(dfm_model *m, int64_t batch);
+
+/* ------------------------------------------------------------ Chow tests
+ * LR_test / LM_test / Wald_test (src/chowtest.jl:19-42) for EVERY variable
+ * i = 0..N-1 of the fitted model at break period bp (rows 0..bp-1 | bp..T-1).
+ * Any output pointer may be NULL. */
+int dfm_chow_all(dfm_model *m, int64_t bp, double *LR, double *LM, double *Wald);
+
+/* --------------------------------------------------- targeted predictors
+ * targeted_predictors(..., thresholding="hard") (src/targeted_predictors.jl:9-30).
+ * JOINT: OLS of y on [w x], White HC0, |t_x| > crit_value (the reference's
+ * t_{0.975}(T-q-N) is passed in by the caller: no quantile code on device).
+ * PER_CANDIDATE: y on [w x_i] for each i (extension, defect D8).
+ * tstat (N) and mask (N, 0/1) are host outputs. */
+int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                      const double *X, int64_t T, int64_t N, int64_t ldx, int mode,
+                      double crit_value, double *tstat, uint8_t *mask);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFM_H */

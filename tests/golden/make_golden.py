@@ -1,0 +1,90 @@
+"""Generate the golden fixtures under tests/golden/ from the CPU oracle.
+
+The reference (Julia 0.3) cannot run here and ships no vectors of its own
+(SURVEY §4, §8(c)), so these fixtures are produced by the reference-faithful
+oracle (oracle/dfm_oracle.py) on the BASELINE configs' shapes at reduced B.
+They freeze the oracle's outputs (so a later edit cannot drift silently) and
+are the inputs/expected outputs of the GPU parity tests.
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import dfm_oracle as O  # noqa: E402
+
+
+def c1():
+    """C1: Bai–Ng DGP T=200 N=100 r=3, fit at r=3 + IC sweep k<=8, all criteria."""
+    rng = np.random.default_rng(20261015 + 1)
+    T, N, r = 200, 100, 3
+    y, x, *_ = O.factor_model_DGP(T, N, r, rng)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    fit = O.DynamicFactorModel(y, w, x, r, "ICp2")
+    ic = O.ic_sweep_values(y, w, x, 8)
+    best = O.DynamicFactorModel_ic(y, w, x, "ICp2", kmax=8)
+    np.savez_compressed(
+        os.path.join(HERE, "c1_bai_ng_T200_N100_r3.npz"),
+        y=y, w=w, x=x, r=r, eigvals=fit.eigenvalues[0][:16], F=fit.F, L=fit.loadings[0][:, :r],
+        coefficients=fit.coefficients, t_stats=fit.t_stats, coef_cov=fit.coefficient_covariance,
+        residuals=fit.residuals, V=O.factor_residual_variance(fit),
+        crit_ICp2=fit.number_of_factors_criterion_value, ic_values=ic,
+        ic_best_r=best.number_of_factors, factor_residuals=fit.factor_residuals)
+
+
+def c2():
+    """C2: Breitung–Eickmeier DGP T=600 N=130 b=0.5, r by ICp2 over 1..8, wild
+    bootstrap B=16 with V, ICp2 and the Chow LR/LM/Wald of variables 1..6."""
+    rng = np.random.default_rng(20261015 + 2)
+    T, N = 600, 130
+    y, x, *_ = O.factor_model_DGP(T, N, 3, rng, model="Breitung_Eickmeier_2011", b=0.5)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    base = O.DynamicFactorModel_ic(y, w, x, "ICp2", kmax=8)
+    r = base.number_of_factors
+    B, bp, nv = 16, 300, 6
+    idx, eta = O.draw_wild(np.random.default_rng(99), B, T)
+    common, E = base.common_component, base.factor_residuals
+    rows = []
+    for b in range(B):
+        d = O.DynamicFactorModel(y, w, common + eta[b][:, None] * E[idx[b]], r, "ICp2")
+        row = [O.factor_residual_variance(d), d.number_of_factors_criterion_value]
+        row += [O.LR_test(d, bp, i) for i in range(nv)]
+        row += [O.LM_test(d, bp, i) for i in range(nv)]
+        row += [O.Wald_test(d, bp, i) for i in range(nv)]
+        rows.append(row)
+    base_chow = np.array([[O.LR_test(base, bp, i), O.LM_test(base, bp, i), O.Wald_test(base, bp, i)]
+                          for i in range(N)])
+    np.savez_compressed(
+        os.path.join(HERE, "c2_breitung_eickmeier_T600_N130_B16.npz"),
+        y=y, w=w, x=x, r=r, bp=bp, nv=nv, idx=idx, eta=eta, boot=np.array(rows),
+        base_V=O.factor_residual_variance(base), base_crit=base.number_of_factors_criterion_value,
+        base_chow=base_chow, base_eigvals=base.eigenvalues[0][:16])
+
+
+def tp():
+    """Targeted predictors (hard): JOINT at T=200, N=40 and PER_CANDIDATE at
+    a C4-shaped T=400, N=250 slice."""
+    rng = np.random.default_rng(20261015 + 4)
+    y, x, *_ = O.factor_model_DGP(200, 40, 3, rng)
+    x = O.normalize(x)
+    w = np.ones((200, 1))
+    tj, mj = O.targeted_predictors_hard(y, w, x, "joint")
+    y2, x2, *_ = O.factor_model_DGP(400, 250, 5, rng)
+    x2 = O.normalize(x2)
+    w2 = np.ones((400, 1))
+    tc, mc = O.targeted_predictors_hard(y2, w2, x2, "per_candidate")
+    np.savez_compressed(os.path.join(HERE, "tp_hard.npz"), y=y, w=w, x=x, t_joint=tj, m_joint=mj,
+                        y2=y2, w2=w2, x2=x2, t_cand=tc, m_cand=mc)
+
+
+if __name__ == "__main__":
+    c1()
+    c2()
+    tp()
+    print("golden fixtures written to", HERE)

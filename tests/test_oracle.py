@@ -1,0 +1,184 @@
+"""CPU checks that pin the oracle (oracle/dfm_oracle.py).
+
+The reference has no golden vectors or assertions and cannot run
+here (§8(c)): the oracle is therefore pinned by analytic known answers,
+invariants of the reference algebra, an independent SVD
+cross-implementation, the Bai–Ng (2002) selection known answer that the
+reference's MC script (src/Bai_Ng.jl) targets, and the committed fixtures
+(tests/golden/, which freeze the oracle against drift).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _panel(O, T, N, r, seed, model="Bai_Ng_2002", **kw):
+    rng = np.random.default_rng(seed)
+    out = O.factor_model_DGP(T, N, r, rng, model=model, **kw)
+    return out[0], O.normalize(out[1]), np.ones((T, 1))
+
+
+# ---------------------------------------------------------- analytic answers
+@pytest.mark.parametrize("T,N", [(40, 20), (20, 40)])
+def test_exact_rank_panel_has_zero_residual(oracle, T, N):
+    rng = np.random.default_rng(0)
+    r = 3
+    x = rng.standard_normal((T, r)) @ rng.standard_normal((N, r)).T
+    y = rng.standard_normal(T)
+    d = oracle.DynamicFactorModel(y, np.ones((T, 1)), x, r)
+    assert oracle.factor_residual_variance(d) < 1e-24 * np.sum(x ** 2)
+    assert np.all(np.abs(d.eigenvalues[0][r:]) < 1e-10 * d.eigenvalues[0][0])
+
+
+@pytest.mark.parametrize("T,N", [(120, 50), (50, 120), (60, 60)])
+def test_normalisation_identities(oracle, T, N):
+    """src/DynamicFactorModel.jl:80 (L'L/N = I for T >= N) and :89 (F'F/T = I)."""
+    _, x, _ = _panel(oracle, T, N, 3, 1)
+    F, L, _ = oracle.principal_components(x, T, N)
+    if T >= N:
+        assert np.allclose(L.T @ L / N, np.eye(N), atol=1e-12)
+    else:
+        assert np.allclose(F.T @ F / T, np.eye(T), atol=1e-12)
+    assert np.allclose(F @ L.T, x, atol=1e-10)   # full width reproduces x
+
+
+@pytest.mark.parametrize("T,N", [(150, 60), (60, 150)])
+def test_pca_matches_svd(oracle, T, N):
+    """Independent cross-implementation: eigenvalues = squared singular values,
+    the factor space = leading left singular space."""
+    _, x, _ = _panel(oracle, T, N, 4, 2)
+    F, L, w = oracle.principal_components(x, T, N)
+    U, s, Vt = np.linalg.svd(x, full_matrices=False)
+    m = min(T, N)
+    assert np.allclose(w[:m], s ** 2, rtol=1e-11, atol=1e-9 * s[0] ** 2)
+    k = 4
+    Fk = F[:, :k] / np.linalg.norm(F[:, :k], axis=0)
+    cosines = np.linalg.svd(U[:, :k].T @ Fk, compute_uv=False)
+    assert np.all(cosines > 1 - 1e-12)
+
+
+def test_V_trace_identity(oracle):
+    """||E_k||^2 = tr(G) - sum_{j<=k} lambda_j (both branches)."""
+    for T, N in [(200, 100), (80, 160)]:
+        y, x, w = _panel(oracle, T, N, 3, 3)
+        for k in (1, 3, 5):
+            d = oracle.DynamicFactorModel(y, w, x, k)
+            lam = d.eigenvalues[0]
+            V = (np.sum(x * x) - lam[:k].sum()) / (T * N)
+            assert abs(V - oracle.factor_residual_variance(d)) <= 1e-12 * V
+
+
+def test_hc2_matches_leverage_form(oracle):
+    """:43-46 with the T x T hat matrix equals the leverage-vector form."""
+    rng = np.random.default_rng(4)
+    T = 80
+    D = np.hstack([np.ones((T, 1)), rng.standard_normal((T, 3))])
+    y = D @ np.array([1.0, -2, 0.5, 3]) + rng.standard_normal(T)
+    b, cov, t, u = oracle._ols_hc2(D, y)
+    Q, _ = np.linalg.qr(D)
+    h = np.sum(Q * Q, axis=1)
+    DtDi = np.linalg.inv(D.T @ D)
+    cov2 = DtDi @ (D.T * (u ** 2 / (1 - h))) @ D @ DtDi
+    assert np.allclose(cov, cov2, rtol=1e-12)
+    assert np.allclose(b, np.linalg.lstsq(D, y, rcond=None)[0], rtol=1e-12)
+
+
+def test_bai_ng_selects_true_r(oracle):
+    """Known answer of Bai & Ng (2002) Table 2 for (T, N) = (200, 100), r = 3:
+    ICp1/ICp2 select the true r (the MC script src/Bai_Ng.jl:12-39)."""
+    hits = 0
+    for seed in range(5):
+        y, x, w = _panel(oracle, 200, 100, 3, 100 + seed)
+        ic = oracle.ic_sweep_values(y, w, x, 8, criteria=("ICp1", "ICp2"))
+        hits += int(np.argmin(ic[0]) + 1 == 3 and np.argmin(ic[1]) + 1 == 3)
+    assert hits >= 4
+
+
+def test_ic_sweep_constructor_is_first_argmin(oracle):
+    y, x, w = _panel(oracle, 150, 80, 2, 5)
+    best = oracle.DynamicFactorModel_ic(y, w, x, "BIC", kmax=6)
+    vals = oracle.ic_sweep_values(y, w, x, 6, criteria=("BIC",))[0]
+    assert best.number_of_factors == int(np.argmin(vals)) + 1
+
+
+def test_chow_stats_sign_invariant(oracle):
+    """LR/LM/Wald are invariant to factor sign flips."""
+    y, x, w = _panel(oracle, 120, 30, 2, 6, model="Breitung_Eickmeier_2011", b=1.0)
+    d = oracle.DynamicFactorModel(y, w, x, 2)
+    s = [oracle.LR_test(d, 60, 3), oracle.LM_test(d, 60, 3), oracle.Wald_test(d, 60, 3)]
+    d.factors = [d.factors[0] * np.r_[-1.0, 1.0, np.ones(d.factors[0].shape[1] - 2)]]
+    d.loadings = [d.loadings[0] * np.r_[-1.0, 1.0, np.ones(d.loadings[0].shape[1] - 2)]]
+    s2 = [oracle.LR_test(d, 60, 3), oracle.LM_test(d, 60, 3), oracle.Wald_test(d, 60, 3)]
+    assert np.allclose(s, s2, rtol=1e-10)
+
+
+def test_chow_detects_break(oracle):
+    """A loading break of size b (src/utils.jl:80-91) inflates LR/Wald."""
+    y, x, w = _panel(oracle, 400, 40, 1, 7, model="Breitung_Eickmeier_2011", b=1.5)
+    d = oracle.DynamicFactorModel(y, w, x, 1)
+    y0, x0, _ = _panel(oracle, 400, 40, 1, 7, model="Breitung_Eickmeier_2011", b=0.0)
+    d0 = oracle.DynamicFactorModel(y0, w, x0, 1)
+    lr = np.mean([oracle.LR_test(d, 200, i) for i in range(10)])
+    lr0 = np.mean([oracle.LR_test(d0, 200, i) for i in range(10)])
+    assert lr > 3 * lr0
+
+
+def test_wild_bootstrap_identity_draw_reproduces_fit(oracle):
+    """idx = identity and eta = 1 rebuild X exactly: the replicate is the fit."""
+    y, x, w = _panel(oracle, 100, 50, 2, 8)
+    d = oracle.DynamicFactorModel(y, w, x, 2, "ICp2")
+    B, T = 2, 100
+    idx = np.tile(np.arange(T, dtype=np.int32), (B, 1))
+    eta = np.ones((B, T))
+    st = oracle.wild_bootstrap(d, B, oracle.factor_residual_variance, idx, eta)
+    assert np.allclose(st, oracle.factor_residual_variance(d), rtol=1e-10)
+
+
+def test_targeted_per_candidate_matches_explicit_ols(oracle):
+    """FWL form used by the engine == the explicit OLS [w x_i] with HC0."""
+    rng = np.random.default_rng(9)
+    T, N = 120, 6
+    x = rng.standard_normal((T, N))
+    w = np.hstack([np.ones((T, 1)), rng.standard_normal((T, 1))])
+    y = x[:, 0] * 0.8 + rng.standard_normal(T)
+    t, _ = oracle.targeted_predictors_hard(y, w, x, "per_candidate")
+    for i in range(N):
+        Z = np.hstack([w, x[:, i:i + 1]])
+        Zi = np.linalg.inv(Z.T @ Z)
+        b = Zi @ Z.T @ y
+        u = y - Z @ b
+        cov = Zi @ (Z.T @ np.diag(u ** 2) @ Z) @ Zi
+        assert abs(t[i] - b[-1] / math.sqrt(cov[-1, -1])) < 1e-10 * abs(t[i])
+
+
+def test_targeted_joint_critical_value(oracle):
+    """:27 — quantile(TDist(T - q - N), 0.975)."""
+    from scipy import stats
+    y, x, w = _panel(oracle, 100, 10, 2, 10)
+    t, m = oracle.targeted_predictors_hard(y, w, x, "joint")
+    cv = stats.t.ppf(0.975, 100 - 1 - 10)
+    assert np.array_equal(m, np.abs(t) > cv)
+
+
+# ------------------------------------------------------------ golden fixtures
+def test_golden_c1_reproduces(oracle):
+    g = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
+    d = oracle.DynamicFactorModel(g["y"], g["w"], g["x"], int(g["r"]), "ICp2")
+    assert np.allclose(d.eigenvalues[0][:16], g["eigvals"], rtol=1e-12)
+    assert np.allclose(d.coefficients, g["coefficients"], rtol=1e-10)
+    assert abs(oracle.factor_residual_variance(d) - float(g["V"])) < 1e-12
+    ic = oracle.ic_sweep_values(g["y"], g["w"], g["x"], 8)
+    assert np.allclose(ic, g["ic_values"], rtol=1e-12)
+    assert int(np.argmin(ic[4])) + 1 == int(g["ic_best_r"]) == 3
+
+
+def test_golden_c2_base_reproduces(oracle):
+    g = np.load(os.path.join(GOLD, "c2_breitung_eickmeier_T600_N130_B16.npz"))
+    base = oracle.DynamicFactorModel_ic(g["y"], g["w"], g["x"], "ICp2", kmax=8)
+    assert base.number_of_factors == int(g["r"])
+    for i in (0, 7, 129):
+        assert abs(oracle.LR_test(base, 300, i) - g["base_chow"][i, 0]) < 1e-9 * max(1, abs(g["base_chow"][i, 0]))
