@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Headline benchmark: wild-bootstrap replicates/s at T=500, N=2000, r=8
+(BASELINE.json configs[2], the metric's config), one process per GPU.
+
+A step = one complete B=9999-replicate wild-bootstrap job on each GPU
+(src/bootstrap.jl:41-51: per replicate resample X* = F_r L_r' + diag(eta)
+E[idx,:], refit the DFM at r = 8 — Gram, top-8 eigenpairs, factors and
+loadings, OLS + HC2 — and evaluate the stats V(8) and ICp2), followed by the
+RCCL all-gather of the per-replicate statistics (N > 1).  Replicates shard
+across ranks (weak scaling: every rank runs its own 9999-replicate job on its
+own draws).  Inputs (the fitted base model and every replicate's idx/eta) are
+resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+T, N, R, B = 500, 2000, 8, 9999
+SYRK_FLOP = T * (T + 1) * N          # per replicate (5.01e8)
+PEAK_F64_TFLOPS = 78.6               # MI355X fp64 matrix, spec (measured 75.1 for 4x4x4_4b)
+PEAK_HBM_GBS = 8000.0
+
+
+def cpu_baseline(seconds: float = 15.0):
+    """Reference-faithful oracle (full eig, full loadings, T x T hat matrix),
+    serial replicate loop on this host's cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dfm_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    rng = np.random.default_rng(20261015 + 3)
+    y, x, *_ = O.factor_model_DGP(T, N, R, rng)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    base = O.DynamicFactorModel(y, w, x, R, "ICp2")
+    common, E = base.common_component, base.factor_residuals
+    draw = np.random.default_rng(1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        idx = draw.integers(0, T, size=T)
+        eta = draw.standard_normal(T)
+        d = O.DynamicFactorModel(y, w, common + eta[:, None] * E[idx], R, "ICp2")
+        _ = (O.factor_residual_variance(d), d.number_of_factors_criterion_value)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el > seconds and n >= 3) or el > 4 * seconds:
+            break
+    return {"value": n / el, "unit": "replicates/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} replicates of the C3 wild bootstrap (T=500 N=2000 r=8, V + ICp2) "
+                      f"in {el:.1f} s, oracle/dfm_oracle.py serial loop over OpenBLAS"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=0, help="replicates per device batch (0 = auto)")
+    ap.add_argument("--replicates", type=int, default=B)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import dfm_pkg
+    D = dfm_pkg.load()
+    ctx = D.Context(local)
+    Bn = args.replicates
+
+    # ---- base model (identical on every rank), resident in HBM
+    rng = np.random.default_rng(20261015 + 3)
+    y, x, *_ = D.factor_model_DGP(T, N, R, rng=rng)
+    x = D.normalize(x)
+    w = np.ones((T, 1))
+    model = D.DynamicFactorModel(y, w, x, R, "ICp2", ctx=ctx)
+    if args.batch:
+        model.set_batch(args.batch)
+    stats = [D.Stat.V(), D.Stat.criterion()]
+    arr = D.api._stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(model.handle, arr, len(stats)))
+
+    # ---- every step's draws, uploaded before timing (rank-specific streams)
+    nsteps = args.warmup + args.steps
+    idx_d, eta_d = [], []
+    for s in range(nsteps):
+        idx, eta = D.draw_wild_fast(1_000_003 * (rank + 1) + s, Bn, T)
+        idx_d.append(torch.from_numpy(idx).to(dev))
+        eta_d.append(torch.from_numpy(eta).to(dev))
+    out = torch.empty((Bn, width), dtype=torch.float64, device=dev)
+    gathered = [torch.empty_like(out) for _ in range(world)] if world > 1 else None
+    torch.cuda.synchronize()
+
+    def step(s):
+        ctx.check(ctx.lib.dfm_bootstrap_dev(model.handle, 0, Bn, idx_d[s].data_ptr(),
+                                            eta_d[s].data_ptr(), arr, len(stats), out.data_ptr()))
+        if world > 1:
+            dist.all_gather(gathered, out)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, nsteps):
+        step(s)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.enable_timing(False)
+    timing = ctx.read_timing()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    res = out.cpu().numpy()
+    ok = bool(np.all(np.isfinite(res)))
+
+    total = Bn * args.steps * world
+    value = total / el
+    gram_ms, gram_n = timing.get("gram", (0.0, 0))
+    roof = None
+    if gram_n:
+        per_launch_ms = gram_ms / gram_n
+        reps_per_launch = Bn * args.steps / gram_n
+        achieved = SYRK_FLOP * reps_per_launch / (per_launch_ms * 1e-3) / 1e12
+        roof = {"kernel": "gram_kernel (fused resample gather + v_mfma_f64_4x4x4_4b)",
+                "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F64_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(per_launch_ms, 4), "replicates_per_launch": reps_per_launch,
+                "flop_per_replicate": SYRK_FLOP}
+    rec = {
+        "metric": "bootstrap replicates/sec (node), T=500 N=2000 r=8; % fp64 MFMA peak",
+        "value": round(value, 2), "unit": "replicates/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"C3: wild bootstrap, Bai-Ng DGP T={T} N={N} r={R}, "
+                               f"B={Bn} replicates per GPU per step, stats V(8)+ICp2",
+                   "T": T, "N": N, "r": R, "replicates_per_gpu": Bn,
+                   "parallelism": f"replicate-sharded x{world}"},
+        "roofline": roof,
+        "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
+        "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
+        "outputs_finite": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

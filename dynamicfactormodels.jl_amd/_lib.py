@@ -6,6 +6,7 @@ object is missing or no GPU is visible, every entry point raises.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import threading
@@ -46,6 +47,7 @@ SIGNATURES = [
                                 c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                 C.c_int, C.POINTER(C.c_void_p)]),
     ("dfm_model_destroy", C.c_int, [C.c_void_p]),
+    ("dfm_model_dims", C.c_int, [C.c_void_p, c_int64_p, c_int64_p, c_int64_p]),
     ("dfm_model_scalars", C.c_int, [C.c_void_p, c_int64_p, c_double_p, c_double_p, c_double_p]),
     ("dfm_model_read", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                  c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
@@ -63,6 +65,21 @@ SIGNATURES = [
 
 _lock = threading.Lock()
 _lib = None
+_shutdown = False
+
+
+def _mark_shutdown():
+    global _shutdown
+    _shutdown = True
+
+
+atexit.register(_mark_shutdown)
+
+
+def shutting_down() -> bool:
+    """True once the interpreter is exiting: handles are then left to the OS
+    (the HIP runtime may already be tearing down)."""
+    return _shutdown
 
 
 class LibraryMissing(RuntimeError):

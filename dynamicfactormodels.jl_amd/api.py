@@ -83,7 +83,7 @@ class Context:
         self.check(self.lib.dfm_ctx_reset_timing(self.h))
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not _lib.shutting_down():
             self.lib.dfm_ctx_destroy(self.h)
             self.h = None
 
@@ -203,10 +203,13 @@ class DynamicFactorModelResult:
         self.V = float(V.value)
         self.number_of_factors_criterion_value = float(cv.value) if criterion else float("nan")  # D3
         self.trace_G = float(tr.value)
+        rd, kd, nd = C.c_int64(), C.c_int64(), C.c_int64()
+        ctx.check(ctx.lib.dfm_model_dims(handle, C.byref(rd), C.byref(kd), C.byref(nd)))
+        kmax = int(kd.value)
         self.kmax = kmax
         q, rr = w.shape[1], self.number_of_factors
         d = q + rr
-        ne = max(kmax, rr)
+        ne = int(nd.value)
         self.eigenvalues = np.zeros(ne)
         self.coefficients = np.zeros(d)
         self.t_stats = np.zeros(d)
@@ -214,7 +217,7 @@ class DynamicFactorModelResult:
         self.residuals = np.zeros(T)
         F = np.zeros((T, rr), order="F")
         L = np.zeros((N, rr), order="F")
-        self.ic_values = np.zeros((7, kmax)) if (kmax and criterion) else None
+        self.ic_values = np.zeros((7, kmax)) if kmax else None
         ctx.check(ctx.lib.dfm_model_read(
             handle, _lib.ptr(self.eigenvalues), _lib.ptr(self.coefficients), _lib.ptr(self.t_stats),
             self.coefficient_covariance.ctypes.data_as(_lib.c_double_p), _lib.ptr(self.residuals),
@@ -248,7 +251,7 @@ class DynamicFactorModelResult:
 
     def __del__(self):
         try:
-            if self._h:
+            if self._h and not _lib.shutting_down():
                 self._ctx.lib.dfm_model_destroy(self._h)
                 self._h = None
         except Exception:
@@ -304,9 +307,7 @@ def DynamicFactorModel(y, w, x, number_of_factors: Union[int, str, None] = None,
     ctx.check(ctx.lib.dfm_model_fit(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p),
                                     w.shape[1], T, xc.ctypes.data_as(_lib.c_double_p), T, N, T,
                                     r, code, km, C.byref(h)))
-    mfn = int(math.ceil(min(T, N) / 2))
-    kk = min(km if km > 0 else mfn, mfn) if r == 0 else 0
-    res = DynamicFactorModelResult(ctx, h, y, w, x, crit, break_indices, kk)
+    res = DynamicFactorModelResult(ctx, h, y, w, x, crit, break_indices)
     res.targeted_predictors = (np.ones(N, dtype=bool) if targeted_predictors is None
                                else np.asarray(targeted_predictors, dtype=bool))
     return res

@@ -18,7 +18,7 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
             const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
-            timer_fn tf, void *tctx);
+            timer_fn tf, void *tctx, int64_t rep0);
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
 int spectrum_max();
@@ -33,6 +33,8 @@ __global__ void colssr_cols_kernel(const double *, int64_t, int64_t, int, int, c
                                    const double *, double *);
 __global__ void common_residual_kernel(const double *, int64_t, int, int, int, const double *,
                                        const double *, double *, double *);
+__global__ void panel_row_ssq_kernel(const double *, int64_t, int, double *);
+__global__ void ordered_sum_kernel(const double *, int, double *);
 __global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, double *,
                                double *, double *, double *, int *);
 struct StatDesc { int kind, arg0, arg1, off; };
@@ -57,9 +59,11 @@ static const char *kclass_names[DFM_KC_COUNT] = {"gram", "eig_gq", "eig_small", 
 
 struct dfm_ctx {
   int device = 0;
+  int refs = 1;            // the caller's handle + one per live dfm_model
+  bool closed = false;
   hipStream_t own = nullptr, stream = nullptr;
   std::string err;
-  double tol = 1e-12;
+  double tol = 1e-12;   // residual <= tol * eigen-gap (see eig_gq_kernel)
   int maxit = 400, block = 0, poll = 4;
   bool timing = false;
   std::vector<hipEvent_t> pool;
@@ -73,6 +77,7 @@ struct dfm_ctx {
 struct dfm_model {
   dfm_ctx *ctx = nullptr;
   int T = 0, N = 0, q = 0, r = 0, crit = -1, kmax = 0, m = 0, orient = 0, k_eig = 0;
+  bool swept = false;   // IC sweep ran (r chosen by criterion)
   int64_t ld = 0;
   double *Xp = nullptr, *Cp = nullptr, *Ep = nullptr, *y = nullptr, *w = nullptr;
   double *F = nullptr, *L = nullptr, *Ub = nullptr, *colssr = nullptr;
@@ -162,15 +167,21 @@ int dfm_ctx_create(int device, dfm_ctx **out) {
   return 0;
 }
 
+static void ctx_release(dfm_ctx *ctx);
 int dfm_ctx_destroy(dfm_ctx *ctx) {
-  if (!ctx) return -1;
+  if (!ctx || ctx->closed) return -1;
+  ctx->closed = true;
+  ctx_release(ctx);
+  return 0;
+}
+static void ctx_release(dfm_ctx *ctx) {
+  if (--ctx->refs > 0) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   harvest(ctx);
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
-  return 0;
 }
 
 const char *dfm_last_error(const dfm_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
@@ -258,7 +269,7 @@ static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const do
   char *ws = nullptr;
   HIPCHK(ctx, hipMalloc(&ws, bytes));
   int rc = eig_run(G, m, (int64_t)m * m, m, nb, k, p, warm, kw, ctx->tol, ctx->maxit, ctx->poll, ws,
-                   lam, Uk, trace, status_dev, nullptr, ctx->stream, timer_cb, ctx);
+                   lam, Uk, trace, status_dev, nullptr, ctx->stream, timer_cb, ctx, 0);
   hipStreamSynchronize(ctx->stream);
   hipFree(ws);
   if (rc != 0) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
@@ -275,7 +286,9 @@ int dfm_model_destroy(dfm_model *m) {
   hipFree(m->ws);
   hipFree(m->sd_dev);
   hipFree(m->flag_dev);
+  dfm_ctx *ctx = m->ctx;
   delete m;
+  ctx_release(ctx);
   return 0;
 }
 
@@ -294,6 +307,7 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   const int T = (int)T64, N = (int)N64, m = std::min(T, N);
   const int mfn = ceil_half(m);  // max_factor_number, src/DynamicFactorModel.jl:101
   dfm_model *M = new dfm_model();
+  ++ctx->refs;
   M->ctx = ctx; M->T = T; M->N = N; M->q = q; M->crit = crit; M->m = m;
   M->orient = (N > T) ? 0 : 1;  // src/DynamicFactorModel.jl:77 (T >= N) vs :86 (N > T)
   M->ld = round_up(N, 16);
@@ -375,6 +389,7 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
     M->sigma2 = s / NT;   // V of DynamicFactorModel(y, w, x), src/criteria.jl:18
   }
   if (r <= 0) {
+    M->swept = true;
     M->ic.assign(7 * kmax, 0.0);
     dfm_ic_sweep(ev.data(), (int)ev.size(), kmax, trace, T, N, need_spec ? M->sigma2 : NAN, M->ic.data());
     int best = 0;
@@ -396,8 +411,12 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
     CK(hipStreamSynchronize(st));
     if (est) { hipFree(Xraw); hipFree(G); return bail(fail(ctx, 2, "eigensolver did not converge")); }
   }
-  M->lam.assign(ev.begin(), ev.begin() + std::max<size_t>(std::min<size_t>(ev.size(), std::max(kmax, r)), 0));
-  if (M->lam.size() < (size_t)r) M->lam = lam;
+  // eigenvalues reported: kmax of the sweep (when it ran) or r
+  {
+    const size_t ne = (size_t)(M->swept ? std::max(kmax, r) : r);
+    M->lam.assign(ne, NAN);
+    for (size_t j = 0; j < ne && j < ev.size(); ++j) M->lam[j] = ev[j];
+  }
   M->k_eig = kk;
   // --- factors, loadings for r (first r canonical eigenvectors)
   CK(dalloc(&M->Ub, (size_t)m * r));
@@ -425,6 +444,17 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
                        st, M->Xp, M->ld, T, N, r, M->F, M->L, M->Cp, M->Ep);
   }
   CK(hipGetLastError());
+  // --- V(r) by brute force over the explicit residual panel (src/criteria.jl:5)
+  double essq = 0.0;
+  {
+    double *rows = nullptr, *tot = nullptr;
+    CK(dalloc(&rows, T)); CK(dalloc(&tot, 1));
+    hipLaunchKernelGGL(panel_row_ssq_kernel, dim3(T), dim3(256), 0, st, M->Ep, M->ld, T, rows);
+    hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, st, rows, T, tot);
+    CK(hipMemcpyAsync(&essq, tot, 8, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    hipFree(rows); hipFree(tot);
+  }
   // --- OLS + HC2 on [w F_r]
   const int d = q + r;
   if (d > 32) return bail(fail(ctx, -5, "q + r = %d > 32 unsupported", d));
@@ -450,9 +480,7 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   hipFree(st_d); hipFree(ost);
   if (ols_bad) return bail(fail(ctx, 3, "singular design matrix D'D"));
   M->trace = trace;
-  double s = trace;
-  for (int j = 0; j < r; ++j) s -= lam[j];
-  M->V = s / NT;
+  M->V = essq / NT;
   if (crit >= 0) {
     const double c = (double)(N + T) / NT;
     switch (crit) {
@@ -465,12 +493,19 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
       case 6: M->critval = M->V + r * std::log((double)T) / T; break;
     }
   }
-  M->lam.resize(std::max<size_t>(M->lam.size(), (size_t)r));
-  for (int j = 0; j < r; ++j) M->lam[j] = lam[j];
+  for (int j = 0; j < r && j < (int)M->lam.size(); ++j) M->lam[j] = lam[j];
   CK(dalloc(&M->flag_dev, 4));
   *out = M;
   return 0;
 #undef CK
+}
+
+int dfm_model_dims(const dfm_model *m, int64_t *r, int64_t *kmax, int64_t *n_eig) {
+  if (!m) return -1;
+  if (r) *r = m->r;
+  if (kmax) *kmax = m->swept ? m->kmax : 0;
+  if (n_eig) *n_eig = (int64_t)m->lam.size();
+  return 0;
 }
 
 int dfm_model_scalars(const dfm_model *m, int64_t *r, double *V, double *cv, double *tr) {
@@ -489,7 +524,7 @@ int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *ts
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   const int d = m->q + m->r;
-  if (eigvals) std::copy(m->lam.begin(), m->lam.begin() + std::min<size_t>(m->lam.size(), std::max(m->kmax, m->r)), eigvals);
+  if (eigvals) std::copy(m->lam.begin(), m->lam.end(), eigvals);
   if (coef) std::copy(m->coef.begin(), m->coef.end(), coef);
   if (tstat) std::copy(m->tstat.begin(), m->tstat.end(), tstat);
   if (coef_cov) std::copy(m->cov.begin(), m->cov.end(), coef_cov);
@@ -637,7 +672,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
     }
     int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
-                     w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx);
+                     w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
     if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
     {
       Scope sc(ctx, DFM_KC_FACTORS);

@@ -32,19 +32,19 @@ struct EigWork {
   int *done, *iters, *active;
   double *trace;           // nb
 };
-template <int P> constexpr int small_stride() { return 2 * P * P + 2 * P; }
+template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
 
 // ----------------------------------------------------------------- init
 template <int P>
 __global__ void eig_init_kernel(double *__restrict__ Q, int m, int p, const double *__restrict__ warm,
-                                int kw, int *__restrict__ done, uint64_t seed) {
+                                int kw, int *__restrict__ done, uint64_t seed, int64_t rep0) {
   const int rep = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)m * P) return;
   const int row = (int)(e / P), c = (int)(e % P);
   double v = 0.0;
   if (c < kw) v = warm[(int64_t)row * kw + c];
-  else if (c < p) v = hash_unit(seed + rep, row, c);
+  else if (c < p) v = hash_unit(seed, row, c);   // same start for every replicate: call/batch/shard-invariant
   Q[(int64_t)rep * m * P + e] = v;
   if (e == 0) done[rep] = 0;
 }
@@ -63,7 +63,7 @@ __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int6
 template <int P>
 __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ G, int64_t ldg,
                                                      int64_t strideG, EigWork w, int m, int k,
-                                                     double tol, int it, int check_only) {
+                                                     int p, double tol, int it, int check_only) {
   constexpr int SQ = P + 4;  // padded LDS row stride (conflict-free B-fragment reads)
   __shared__ __attribute__((aligned(16))) double sQ[EROWS * SQ];
   __shared__ __attribute__((aligned(16))) double sY[EROWS * SQ];
@@ -74,12 +74,25 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   if (tid == 0) {
     int d = w.done[rep];
     if (!d && it > 0) {
-      const double th0 = fabs(small[2 * P * P]);
+      // Converged when every wanted Ritz pair j < k satisfies
+      //   res_j <= tol * gap_j            (eigenvector error ~ res/gap <= tol)
+      // or sits at the rounding floor: res_j <= 2e-14 |theta_1|, or
+      //   res_j <= 1e-11 |theta_1| and stagnating (no 2x decrease).
+      const double *th = small + 2 * P * P;
+      const double *prev = small + 2 * P * P + 2 * P + ((it - 1) & 1) * P;
+      double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
+      const double th0 = fabs(th[0]);
       bool ok = true;
       for (int j = 0; j < k; ++j) {
         double s = 0.0;
         for (int r = 0; r < nrb; ++r) s += w.rpart[((int64_t)rep * nrb + r) * P + j];
-        if (!(sqrt(s) <= tol * th0)) ok = false;
+        const double res = sqrt(s);
+        double gap = INFINITY;
+        if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+        if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+        const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
+        if (!(res <= tol * gap || res <= 2e-14 * th0 || stagn)) ok = false;
+        if (rb == 0) next[j] = res;
       }
       if (ok) {
         d = 1;
@@ -371,7 +384,7 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
 // ---------------------------------------------------------------- apply
 template <int P>
 __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p, int k, int it,
-                                                        uint64_t seed) {
+                                                        uint64_t seed, int64_t rep0) {
   constexpr int SQ = P + 1;
   __shared__ double sQ[EROWS * SQ], sY[EROWS * SQ], sW[EROWS * P];
   __shared__ double sA[P * P], sB[P * P], sT[2 * P];
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
       ya = fma(sY[r * SQ + a], sA[a * P + c], ya);
       qn = fma(sY[r * SQ + a], sB[a * P + c], qn);
     }
-    if (c < p && sT[P + c] != 0.0) qn = hash_unit(seed + rep, row, 1000003ull * (it + 1) + c);
+    if (c < p && sT[P + c] != 0.0) qn = hash_unit(seed, row, 1000003ull * (it + 1) + c);
     if (c >= p) qn = 0.0;
     if (c < k) { const double wv = ya - sT[c] * u; sW[r * P + c] = row < m ? wv * wv : 0.0; }
     if (row < m) { Ur[(int64_t)row * P + c] = u; Qr[(int64_t)row * P + c] = qn; }
@@ -456,7 +469,7 @@ size_t eig_workspace_bytes(int m, int nb, int P, int maxit) {
   s += 3 * (size_t)nb * m * P * 8;               // Q, Y, U
   s += (size_t)nb * nrb * 3 * P * P * 8;         // part
   s += (size_t)nb * nrb * P * 8;                 // rpart
-  s += (size_t)nb * (2 * P * P + 2 * P) * 8;     // small
+  s += (size_t)nb * (2 * P * P + 4 * P) * 8;     // small
   s += (size_t)nb * 8;                           // trace
   s += (size_t)(2 * nb + maxit + 2) * 4 + 256;   // done, iters, active
   return s;
@@ -471,7 +484,7 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   w.U = (double *)take((size_t)nb * m * P * 8);
   w.part = (double *)take((size_t)nb * nrb * 3 * P * P * 8);
   w.rpart = (double *)take((size_t)nb * nrb * P * 8);
-  w.small = (double *)take((size_t)nb * (2 * P * P + 2 * P) * 8);
+  w.small = (double *)take((size_t)nb * (2 * P * P + 4 * P) * 8);
   w.trace = (double *)take((size_t)nb * 8);
   w.done = (int *)take((size_t)nb * 4);
   w.iters = (int *)take((size_t)nb * 4);
@@ -491,7 +504,7 @@ template <int P>
 static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                      double *lam, double *Uk, double *trace_out, int *status, int *iters_host,
-                     hipStream_t st, timer_fn tf, void *tctx) {
+                     hipStream_t st, timer_fn tf, void *tctx, int64_t rep0) {
   const int nrb = (m + EROWS - 1) / EROWS;
   EigWork w = carve(ws, m, nb, P, maxit);
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
@@ -501,7 +514,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   {
     const int64_t n = (int64_t)m * P;
     dim3 grid((unsigned)((n + 255) / 256), nb);
-    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed);
+    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, rep0);
     hipLaunchKernelGGL(eig_trace_kernel, dim3(nb), dim3(64), 0, st, G, ldg, strideG, m, w.trace);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
@@ -512,14 +525,14 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     const int check_only = (it == maxit);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
     hipLaunchKernelGGL(eig_gq_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, k,
-                       tol, it, check_only);
+                       p, tol, it, check_only);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (check_only) break;
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed);
+    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it > 0 && (it % poll) == 0) {
       int a = -1;
@@ -555,13 +568,13 @@ int eig_block_p(int m, int k, int req) {
 int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
             const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
-            timer_fn tf, void *tctx) {
+            timer_fn tf, void *tctx, int64_t rep0) {
   if (p < k || p > 32 || p > m) return -1;
   if (p <= 16)
     return eig_run_t<16>(G, ldg, strideG, m, nb, k, p, warm, kw, tol, maxit, poll, ws, lam, Uk,
-                         trace_out, status, iters_host, st, tf, tctx);
+                         trace_out, status, iters_host, st, tf, tctx, rep0);
   return eig_run_t<32>(G, ldg, strideG, m, nb, k, p, warm, kw, tol, maxit, poll, ws, lam, Uk,
-                       trace_out, status, iters_host, st, tf, tctx);
+                       trace_out, status, iters_host, st, tf, tctx, rep0);
 }
 
 // ------------------------------------------------------------ full spectrum

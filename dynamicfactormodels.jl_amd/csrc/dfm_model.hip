@@ -168,6 +168,30 @@ __global__ void common_residual_kernel(const double *__restrict__ X, int64_t ld,
   E[(int64_t)t * ld + n] = (n < N) ? x - c : 0.0;
 }
 
+// ||E||_F^2 of a row-major panel (T x ld, zero padding): per-row partial sums
+// then a fixed-order sum — the brute-force sum(E.^2) of src/criteria.jl:5.
+__global__ void panel_row_ssq_kernel(const double *__restrict__ E, int64_t ld, int T,
+                                     double *__restrict__ rows) {
+  __shared__ double red[256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  double s = 0.0;
+  for (int64_t n = tid; n < ld; n += 256) { const double v = E[(int64_t)t * ld + n]; s = fma(v, v, s); }
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) { if (tid < o) red[tid] += red[tid + o]; __syncthreads(); }
+  if (tid == 0) rows[t] = red[0];
+}
+__global__ void ordered_sum_kernel(const double *__restrict__ v, int n, double *__restrict__ out) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  for (int i = tid; i < n; i += 256) s += v[i];
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) { if (tid < o) red[tid] += red[tid + o]; __syncthreads(); }
+  if (tid == 0) *out = red[0];
+}
+
 // ------------------------------------------------------------------- OLS
 // src/DynamicFactorModel.jl:40-48: D = [w F_r], beta = (D'D)^-1 D'y,
 // u = y - D beta, h_t = d_t'(D'D)^-1 d_t, sigma2_t = u_t^2 / (1 - h_t) (HC2),

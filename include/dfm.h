@@ -117,13 +117,17 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
                   const double *X, int64_t T, int64_t N, int64_t ldx,
                   int r, int crit, int kmax, dfm_model **out);
 int dfm_model_destroy(dfm_model *m);
+/* Sizes of the arrays dfm_model_read fills: r, the IC-sweep kmax (0 when r was
+ * given), n_eig = number of eigenvalues returned (max(r, kmax)). */
+int dfm_model_dims(const dfm_model *m, int64_t *r, int64_t *kmax, int64_t *n_eig);
 /* Scalars: [r, V(r), criterion value, trace_G]. */
 int dfm_model_scalars(const dfm_model *m, int64_t *r_out, double *V, double *crit_value,
                       double *trace_G);
 /* Host copies (any pointer may be NULL): eigvals (kmax), coefficients and
  * t-stats (q+r), coefficient covariance ((q+r)^2 col-major), OLS residuals
  * (T), F (T x r col-major), L (N x r col-major), factor residuals E (T x N
- * col-major, ld T), criteria for k=1..kmax (7 x kmax) when crit >= 0. */
+ * col-major, ld T), criteria for k=1..kmax (7 x kmax, row-major) when the IC
+ * sweep ran.  eigvals holds n_eig values (dfm_model_dims). */
 int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *tstat,
                    double *coef_cov, double *ols_resid, double *F, double *L,
                    double *E, double *ic_values);

@@ -1,0 +1,316 @@
+"""GPU parity: libdfm (through its C ABI) vs the CPU oracle and the golden
+fixtures.  Tolerances are the north star's (BASELINE.json): statistics and
+criteria within 1e-10 relative in fp64; factors equal up to sign with max
+principal angle < 1e-8; resample indices are host-generated and shared
+(bit-exact by construction)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+STAT_RTOL = 1e-10
+ANGLE_TOL = 1e-8
+
+
+def rel(a, b):
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
+
+
+def max_sin_angle(A, B):
+    """sin of the largest principal angle between span(A) and span(B)."""
+    Qa, _ = np.linalg.qr(A)
+    Qb, _ = np.linalg.qr(B)
+    return float(np.linalg.norm(Qa - Qb @ (Qb.T @ Qa), 2))
+
+
+def column_angles(A, B):
+    """Per-factor angles (columns matched in order, sign-free)."""
+    out = []
+    for j in range(A.shape[1]):
+        a = A[:, j] / np.linalg.norm(A[:, j])
+        b = B[:, j] / np.linalg.norm(B[:, j])
+        b = b * np.sign(a @ b)
+        out.append(float(np.linalg.norm(a - b)))
+    return np.array(out)
+
+
+def signs(F, Fo):
+    s = np.sign(np.sum(F * Fo, axis=0))
+    s[s == 0] = 1
+    return s
+
+
+def panel(oracle, T, N, r, seed, model="Bai_Ng_2002", **kw):
+    rng = np.random.default_rng(seed)
+    out = oracle.factor_model_DGP(T, N, r, rng, model=model, **kw)
+    return out[0], oracle.normalize(out[1]), np.ones((T, 1))
+
+
+def assert_fit_matches(g, o, oracle, q=1):
+    r = o.number_of_factors
+    assert g.number_of_factors == r
+    assert rel(g.eigenvalues[:r], o.eigenvalues[0][:r]) < STAT_RTOL
+    Fo = o.F
+    assert max_sin_angle(g.factors[0], Fo) < ANGLE_TOL
+    assert np.all(column_angles(g.factors[0], Fo) < ANGLE_TOL)
+    s = signs(g.factors[0], Fo)
+    assert rel(g.factors[0] * s, Fo) < 1e-8
+    assert abs(g.V - oracle.factor_residual_variance(o)) < STAT_RTOL * oracle.factor_residual_variance(o)
+    cg = g.coefficients.copy()
+    cg[q:] *= s
+    tg = g.t_stats.copy()
+    tg[q:] *= s
+    assert rel(cg, o.coefficients) < 1e-9
+    assert rel(tg, o.t_stats) < 1e-9
+    assert np.max(np.abs(g.factor_residuals - o.factor_residuals)) < 1e-9 * np.max(np.abs(o.factor_residuals))
+    if o.number_of_factors_criterion:
+        assert abs(g.number_of_factors_criterion_value - o.number_of_factors_criterion_value) <= \
+            STAT_RTOL * abs(o.number_of_factors_criterion_value)
+
+
+# ------------------------------------------------------------------ fixtures
+def test_golden_c1_fit(dfm, oracle):
+    g = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
+    d = dfm.DynamicFactorModel(g["y"], g["w"], g["x"], int(g["r"]), "ICp2")
+    assert rel(d.eigenvalues[:3], g["eigvals"][:3]) < STAT_RTOL
+    assert max_sin_angle(d.factors[0], g["F"]) < ANGLE_TOL
+    s = signs(d.factors[0], g["F"])
+    c = d.coefficients.copy(); c[1:] *= s
+    t = d.t_stats.copy(); t[1:] *= s
+    assert rel(c, g["coefficients"]) < 1e-9 and rel(t, g["t_stats"]) < 1e-9
+    assert abs(d.V - float(g["V"])) < STAT_RTOL * float(g["V"])
+    assert abs(d.number_of_factors_criterion_value - float(g["crit_ICp2"])) < STAT_RTOL * abs(float(g["crit_ICp2"]))
+    assert np.allclose(d.residuals, g["residuals"], rtol=0, atol=1e-10 * np.abs(g["residuals"]).max())
+
+
+def test_golden_c1_ic_sweep(dfm):
+    g = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
+    d = dfm.DynamicFactorModel(g["y"], g["w"], g["x"], "ICp2", kmax=8)
+    assert d.number_of_factors == int(g["ic_best_r"]) == 3
+    assert rel(d.ic_values, g["ic_values"]) < STAT_RTOL
+
+
+@pytest.mark.parametrize("crit", ["PCp1", "PCp2", "PCp3", "ICp1", "ICp3", "BIC"])
+def test_golden_c1_ic_sweep_every_criterion(dfm, crit):
+    g = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
+    d = dfm.DynamicFactorModel(g["y"], g["w"], g["x"], crit, kmax=8)
+    row = list(dfm.CRITERIA).index(crit)
+    assert d.number_of_factors == int(np.argmin(g["ic_values"][row])) + 1
+    assert abs(d.number_of_factors_criterion_value - g["ic_values"][row, d.number_of_factors - 1]) \
+        <= STAT_RTOL * abs(g["ic_values"][row, d.number_of_factors - 1])
+
+
+def test_golden_c2_base_and_chow(dfm):
+    g = np.load(os.path.join(GOLD, "c2_breitung_eickmeier_T600_N130_B16.npz"))
+    d = dfm.DynamicFactorModel(g["y"], g["w"], g["x"], "ICp2", kmax=8)
+    assert d.number_of_factors == int(g["r"])
+    assert abs(d.V - float(g["base_V"])) < STAT_RTOL * float(g["base_V"])
+    LR, LM, W = dfm.chow_all(d, int(g["bp"]))
+    assert rel(LR, g["base_chow"][:, 0]) < 1e-9
+    assert rel(LM, g["base_chow"][:, 1]) < 1e-9
+    assert rel(W, g["base_chow"][:, 2]) < 1e-9
+    assert abs(dfm.LR_test(d, int(g["bp"]), 5) - g["base_chow"][4, 0]) < 1e-9 * abs(g["base_chow"][4, 0])
+
+
+def test_golden_c2_wild_bootstrap(dfm):
+    g = np.load(os.path.join(GOLD, "c2_breitung_eickmeier_T600_N130_B16.npz"))
+    d = dfm.DynamicFactorModel(g["y"], g["w"], g["x"], "ICp2", kmax=8)
+    bp, nv = int(g["bp"]), int(g["nv"])
+    S = dfm.Stat
+    stats = [S.V(), S.criterion()] + [S.LR(bp, i + 1) for i in range(nv)] + \
+        [S.LM(bp, i + 1) for i in range(nv)] + [S.Wald(bp, i + 1) for i in range(nv)]
+    out = dfm.wild_bootstrap(d, 16, stats, idx=g["idx"], eta=g["eta"])
+    assert rel(out[:, :2], g["boot"][:, :2]) < STAT_RTOL
+    assert rel(out[:, 2:], g["boot"][:, 2:]) < 1e-9
+    # the all-variables form gives the same numbers
+    allv = dfm.wild_bootstrap(d, 16, [S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp)], idx=g["idx"], eta=g["eta"])
+    N = g["x"].shape[1]
+    assert np.array_equal(allv[:, :nv], out[:, 2:2 + nv])
+    assert np.array_equal(allv[:, 2 * N:2 * N + nv], out[:, 2 + 2 * nv:])
+
+
+def test_golden_targeted(dfm):
+    g = np.load(os.path.join(GOLD, "tp_hard.npz"))
+    m, t = dfm.targeted_predictors(g["y"], g["w"], g["x"], return_tstats=True)
+    assert rel(t, g["t_joint"]) < 1e-9 and np.array_equal(m, g["m_joint"])
+    m2, t2 = dfm.targeted_predictors(g["y2"], g["w2"], g["x2"], mode="per_candidate", return_tstats=True)
+    assert rel(t2, g["t_cand"]) < 1e-9 and np.array_equal(m2, g["m_cand"])
+
+
+# -------------------------------------------------- oracle on seeded inputs
+@pytest.mark.parametrize("T,N,r,crit", [
+    (200, 100, 3, "ICp2"),      # C1 shape, T >= N branch
+    (120, 120, 2, "BIC"),       # T == N takes the T >= N branch (:77)
+    (60, 150, 4, "ICp1"),       # N > T branch
+    (500, 2000, 8, "ICp2"),     # C3 shape
+    (12, 9, 2, "ICp3"),         # m < the eigensolver block (p = m)
+    (10, 25, 1, ""),            # r = 1, no criterion (D3: NaN)
+])
+def test_fit_matches_oracle(dfm, oracle, T, N, r, crit):
+    y, x, w = panel(oracle, T, N, r, 1000 + T + N)
+    g = dfm.DynamicFactorModel(y, w, x, r, crit)
+    o = oracle.DynamicFactorModel(y, w, x, r, crit)
+    assert_fit_matches(g, o, oracle)
+    if not crit:
+        assert math.isnan(g.number_of_factors_criterion_value)
+
+
+def test_fit_with_extra_regressors(dfm, oracle):
+    """w = [1, y_{t-1..t-4}] as in test/DynamicFactorModel.jl:13-18."""
+    rng = np.random.default_rng(11)
+    y, x, *_ = oracle.factor_model_DGP(204, 80, 3, rng)
+    x = oracle.normalize(x)[4:]
+    yl = np.column_stack([y[4 - k:-k] for k in range(1, 5)])
+    w = np.hstack([np.ones((200, 1)), yl])
+    y = y[4:]
+    g = dfm.DynamicFactorModel(y, w, x, 3, "ICp2")
+    o = oracle.DynamicFactorModel(y, w, x, 3, "ICp2")
+    assert_fit_matches(g, o, oracle, q=5)
+
+
+def test_exact_rank_panel(dfm):
+    rng = np.random.default_rng(12)
+    T, N, r = 40, 20, 3
+    x = rng.standard_normal((T, r)) @ rng.standard_normal((N, r)).T
+    d = dfm.DynamicFactorModel(rng.standard_normal(T), np.ones((T, 1)), x, r)
+    assert abs(d.V) < 1e-26 * np.sum(x * x)
+    assert np.max(np.abs(d.factor_residuals)) < 1e-10
+
+
+def test_r_clamped_to_half_min(dfm, oracle):
+    """src/DynamicFactorModel.jl:116-119."""
+    y, x, w = panel(oracle, 30, 8, 2, 13)
+    d = dfm.DynamicFactorModel(y, w, x, 7)
+    assert d.number_of_factors == 4
+
+
+def test_principal_components_and_spectrum(dfm, oracle):
+    for T, N in [(150, 60), (60, 150)]:
+        _, x, _ = panel(oracle, T, N, 4, 14)
+        ev, F, L, tr = dfm.principal_components(x, 5)
+        Fo, Lo, wo = oracle.principal_components(x, T, N)
+        assert rel(ev, wo[:5]) < STAT_RTOL
+        assert max_sin_angle(F, Fo[:, :5]) < ANGLE_TOL
+        assert rel(L * signs(F, Fo[:, :5]), Lo[:, :5]) < 1e-8
+        full, tr2 = dfm.gram_spectrum(x)
+        assert rel(full[:40], wo[:40]) < 1e-9
+        assert abs(tr - np.sum(x * x)) < 1e-12 * tr
+
+
+def test_ic_sweep_default_kmax(dfm, oracle):
+    """kmax = ceil(m/2) (src/DynamicFactorModel.jl:54) with m <= 140."""
+    y, x, w = panel(oracle, 80, 30, 2, 15)
+    d = dfm.DynamicFactorModel(y, w, x, "ICp2")
+    o = oracle.DynamicFactorModel_ic(y, w, x, "ICp2")
+    assert d.number_of_factors == o.number_of_factors
+    assert abs(d.number_of_factors_criterion_value - o.number_of_factors_criterion_value) < \
+        STAT_RTOL * abs(o.number_of_factors_criterion_value)
+
+
+@pytest.mark.parametrize("T,N,r", [(200, 100, 3), (60, 150, 4)])
+def test_wild_bootstrap_matches_oracle(dfm, oracle, T, N, r):
+    y, x, w = panel(oracle, T, N, r, 2000 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    B = 6
+    idx, eta = oracle.draw_wild(np.random.default_rng(3), B, T)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.criterion("BIC"), S.eigenvalue(1), S.eigenvalue(r), S.trace(),
+             S.coefficient(1), S.t_stat(1)]
+    out = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, r, "ICp2")
+        ref = [oracle.factor_residual_variance(d), d.number_of_factors_criterion_value,
+               oracle.criterion_value("BIC", d), d.eigenvalues[0][0], d.eigenvalues[0][r - 1],
+               np.sum(xs * xs), d.coefficients[0], d.t_stats[0]]
+        assert rel(out[b, :6], ref[:6]) < STAT_RTOL
+        assert rel(out[b, 6:], ref[6:]) < 1e-9      # w-column coef/t: sign-invariant
+
+
+def test_residual_bootstrap_matches_oracle(dfm, oracle):
+    y, x, w = panel(oracle, 150, 70, 2, 16)
+    g = dfm.DynamicFactorModel(y, w, x, 2, "ICp1")
+    o = oracle.DynamicFactorModel(y, w, x, 2, "ICp1")
+    idx = oracle.draw_residual(np.random.default_rng(4), 5, 150)
+    out = dfm.residual_bootstrap(g, 5, [dfm.Stat.V(), dfm.Stat.criterion()], idx=idx)
+    ref = oracle.residual_bootstrap(o, 5, lambda d: oracle.factor_residual_variance(d), idx)
+    assert rel(out[:, 0], ref) < STAT_RTOL
+
+
+def test_bootstrap_chow_all_matches_oracle(dfm, oracle):
+    y, x, w = panel(oracle, 160, 24, 2, 17, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, 2)
+    o = oracle.DynamicFactorModel(y, w, x, 2)
+    idx, eta = oracle.draw_wild(np.random.default_rng(5), 3, 160)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, 3, [S.LR_all(80), S.LM_all(80), S.Wald_all(80)], idx=idx, eta=eta)
+    for b in range(3):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]], 2)
+        ref = np.array([[oracle.LR_test(d, 80, i), oracle.LM_test(d, 80, i), oracle.Wald_test(d, 80, i)]
+                        for i in range(24)])
+        assert rel(out[b, :24], ref[:, 0]) < 1e-9
+        assert rel(out[b, 24:48], ref[:, 1]) < 1e-9
+        assert rel(out[b, 48:], ref[:, 2]) < 1e-9
+
+
+# -------------------------------------- full-size (C3) size-independent props
+def test_c3_identity_draw_reproduces_base(dfm, oracle):
+    """At T=500, N=2000, r=8: idx = identity, eta = 1 rebuilds X exactly, so
+    every replicate must reproduce the base fit's V and eigenvalues."""
+    y, x, w = panel(oracle, 500, 2000, 8, 18)
+    g = dfm.DynamicFactorModel(y, w, x, 8, "ICp2")
+    B = 32
+    idx = np.tile(np.arange(500, dtype=np.int32), (B, 1))
+    eta = np.ones((B, 500))
+    out = dfm.wild_bootstrap(g, B, [dfm.Stat.V(), dfm.Stat.eigenvalue(1), dfm.Stat.eigenvalue(8)],
+                             idx=idx, eta=eta)
+    assert rel(out[:, 0], np.full(B, g.V)) < 1e-11
+    assert rel(out[:, 1], np.full(B, g.eigenvalues[0])) < 1e-12
+    assert rel(out[:, 2], np.full(B, g.eigenvalues[7])) < 1e-12
+
+
+def test_c3_replicates_match_oracle(dfm, oracle):
+    y, x, w = panel(oracle, 500, 2000, 8, 19)
+    g = dfm.DynamicFactorModel(y, w, x, 8, "ICp2")
+    o = oracle.DynamicFactorModel(y, w, x, 8, "ICp2")
+    idx, eta = oracle.draw_wild(np.random.default_rng(6), 3, 500)
+    out = dfm.wild_bootstrap(g, 3, [dfm.Stat.V(), dfm.Stat.criterion()], idx=idx, eta=eta)
+    ref = oracle.wild_bootstrap(o, 3, lambda d: d.number_of_factors_criterion_value, idx, eta)
+    assert rel(out[:, 1], ref) < STAT_RTOL
+
+
+def test_batching_is_bit_identical(dfm, oracle):
+    """Per-replicate results do not depend on batch composition — the property
+    behind bit-identical 1-GPU vs 8-GPU sharding."""
+    y, x, w = panel(oracle, 200, 300, 4, 20)
+    g = dfm.DynamicFactorModel(y, w, x, 4, "ICp2")
+    B = 24
+    idx, eta = dfm.draw_wild_fast(7, B, 200)
+    stats = [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.t_stat(2)]
+    g.set_batch(24)
+    a = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    g.set_batch(5)
+    b = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    c = dfm.wild_bootstrap(g, 8, stats, idx=idx[16:], eta=eta[16:])
+    assert np.array_equal(a, b)
+    assert np.array_equal(a[16:], c)
+
+
+# ----------------------------------------------------------- error behaviour
+def test_errors_are_reported(dfm, oracle):
+    y, x, w = panel(oracle, 50, 20, 2, 21)
+    g = dfm.DynamicFactorModel(y, w, x, 2, "PCp2")
+    idx, eta = oracle.draw_wild(np.random.default_rng(0), 2, 50)
+    with pytest.raises(dfm.DFMError):      # PCp inside a replicate: not built yet
+        dfm.wild_bootstrap(g, 2, dfm.Stat.criterion(), idx=idx, eta=eta)
+    with pytest.raises(dfm.DFMError):      # break period leaves < r rows
+        dfm.chow_all(g, 1)
+    with pytest.raises(dfm.DFMError):      # D8: joint thresholding singular
+        dfm.targeted_predictors(y, w, np.random.default_rng(0).standard_normal((50, 60)))
+    with pytest.raises(dfm.DFMError):
+        dfm.wild_bootstrap(g, 1, dfm.Stat.V(), idx=np.full((1, 50), 99, dtype=np.int32), eta=eta[:1])
