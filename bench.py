@@ -63,6 +63,11 @@ def cpu_baseline(seconds: float = 15.0):
                       f"in {el:.1f} s, oracle/dfm_oracle.py serial loop over OpenBLAS"}
 
 
+def model_batch(Bn, T):
+    """The engine's auto batch (dfm_bootstrap_dev): floor(1.5e9 / (8 T^2)), <= 4096."""
+    return int(min(Bn, max(1, min(4096, 1.5e9 // (T * T * 8)))))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +75,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0, help="replicates per device batch (0 = auto)")
     ap.add_argument("--replicates", type=int, default=B)
+    ap.add_argument("--mode", default="auto", choices=["auto", "direct", "factored"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -98,6 +104,7 @@ def main():
     model = D.DynamicFactorModel(y, w, x, R, "ICp2", ctx=ctx)
     if args.batch:
         model.set_batch(args.batch)
+    model.set_bootstrap_mode(args.mode)
     stats = [D.Stat.V(), D.Stat.criterion()]
     arr = D.api._stat_array(stats)
     width = int(ctx.lib.dfm_stats_width(model.handle, arr, len(stats)))
@@ -148,8 +155,21 @@ def main():
     total = Bn * args.steps * world
     value = total / el
     gram_ms, gram_n = timing.get("gram", (0.0, 0))
+    gemm_ms, gemm_n = timing.get("gemm", (0.0, 0))
     roof = None
-    if gram_n:
+    if gemm_n:
+        # factored path: every eigen-iteration is one GEMM H (T x T) x Z (T x nb*P)
+        nb = model_batch(Bn, T)
+        P = 16
+        flop_launch = 2.0 * T * T * nb * P
+        per_launch_ms = gemm_ms / gemm_n
+        achieved = flop_launch / (per_launch_ms * 1e-3) / 1e12
+        roof = {"kernel": "gemm_kernel<A=H> (batched eigen-iteration H.Z, v_mfma_f64_4x4x4_4b)",
+                "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F64_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4), "traffic": None,
+                "avg_launch_ms": round(per_launch_ms, 4), "flop_per_launch": flop_launch,
+                "launches": gemm_n}
+    elif gram_n:
         per_launch_ms = gram_ms / gram_n
         reps_per_launch = Bn * args.steps / gram_n
         achieved = SYRK_FLOP * reps_per_launch / (per_launch_ms * 1e-3) / 1e12
@@ -172,6 +192,8 @@ def main():
         "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
         "outputs_finite": ok,
+        "mode": args.mode,
+        "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

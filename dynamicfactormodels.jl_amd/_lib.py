@@ -57,6 +57,7 @@ SIGNATURES = [
                                     C.POINTER(dfm_stat), C.c_int, C.c_void_p]),
     ("dfm_stats_width", C.c_int64, [C.c_void_p, C.POINTER(dfm_stat), C.c_int]),
     ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
+    ("dfm_model_set_mode", C.c_int, [C.c_void_p, C.c_int]),
     ("dfm_chow_all", C.c_int, [C.c_void_p, C.c_int64, c_double_p, c_double_p, c_double_p]),
     ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,

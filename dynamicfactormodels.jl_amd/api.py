@@ -249,6 +249,10 @@ class DynamicFactorModelResult:
     def set_batch(self, batch: int):
         self._ctx.check(self._ctx.lib.dfm_model_set_batch(self._h, int(batch)))
 
+    def set_bootstrap_mode(self, mode: str = "auto"):
+        """'auto' | 'direct' | 'factored' (N > T panels; see include/dfm.h)."""
+        self._ctx.check(self._ctx.lib.dfm_model_set_mode(self._h, {"auto": 0, "direct": 1, "factored": 2}[mode]))
+
     def __del__(self):
         try:
             if self._h and not _lib.shutting_down():

@@ -45,6 +45,22 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
                        const double *F, const double *Lm, double *LR, double *LM, double *Wald,
                        int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st);
 size_t chow_workspace_bytes(int T, int N, int r, int nb);
+struct FactBase {
+  int T, r;
+  int64_t ldH;
+  const double *F, *EL, *S, *H, *cF, *hd;
+};
+int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
+                     const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
+                     double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
+                     timer_fn tf, void *tctx, int *off, int *lst);
+size_t fact_workspace_bytes(int T, int nb, int P);
+int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
+                  const double *Uk, const double *eta, const int *off, const int *lst, int nb,
+                  double *Fout, double *Lout, char *ws, hipStream_t st);
+size_t fact_loadings_bytes(int T, int N, int r, int nb);
+int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
+                    const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st);
 hipError_t launch_targeted(int mode, const double *y, const double *w, int q, const double *Xp,
                            int64_t ld, int T, int N, double cv, double *tstat, uint8_t *mask,
                            char *ws, size_t ws_bytes, hipStream_t st, int *bad);
@@ -55,7 +71,7 @@ using namespace dfm;
 
 static const char *kclass_names[DFM_KC_COUNT] = {"gram", "eig_gq", "eig_small", "eig_apply",
                                                  "eig_other", "factors", "ols", "stats", "chow",
-                                                 "misc"};
+                                                 "misc", "gemm"};
 
 struct dfm_ctx {
   int device = 0;
@@ -89,6 +105,11 @@ struct dfm_model {
   StatDesc *sd_dev = nullptr;
   int sd_cap = 0;
   int *flag_dev = nullptr;
+  // factored bootstrap (N > T): H = E E', EL = E L, S = L'L, cF, hd
+  int mode = 0;   // 0 auto, 1 direct Gram, 2 factored
+  bool fact_ready = false;
+  int64_t ldH = 0;
+  double *H = nullptr, *EL = nullptr, *S = nullptr, *cF = nullptr, *hd = nullptr;
 };
 
 static int fail(dfm_ctx *ctx, int code, const char *fmt, ...) {
@@ -282,7 +303,9 @@ int dfm_model_destroy(dfm_model *m) {
   if (!m) return -1;
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
-  for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->L, m->Ub, m->colssr}) hipFree(p);
+  for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->L, m->Ub, m->colssr, m->H, m->EL, m->S,
+                    m->cF, m->hd})
+    hipFree(p);
   hipFree(m->ws);
   hipFree(m->sd_dev);
   hipFree(m->flag_dev);
@@ -554,6 +577,12 @@ int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *ts
   return 0;
 }
 
+int dfm_model_set_mode(dfm_model *m, int mode) {
+  if (!m || mode < 0 || mode > 2) return -1;
+  m->mode = mode;
+  return 0;
+}
+
 int dfm_model_set_batch(dfm_model *m, int64_t batch) {
   if (!m || batch < 0) return -1;
   m->batch = batch;
@@ -570,16 +599,17 @@ int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
 // Per-batch device workspace layout for the bootstrap.
 struct BootWs {
   double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat;
-  int *status, *ost;
-  char *eig, *chow;
-  size_t eig_bytes, chow_bytes;
+  int *status, *ost, *off, *lst;
+  char *eig, *chow, *fact, *fload;
+  size_t eig_bytes, chow_bytes, fact_bytes, fload_bytes;
 };
-static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool chow, BootWs *o, char *base) {
+static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool chow, bool fact, BootWs *o,
+                            char *base) {
   const int m = M->m, r = M->r, T = M->T, N = M->N, d = M->q + M->r;
   size_t off = 0;
   auto take = [&](size_t bytes) { char *p = base ? base + off : nullptr; off += (bytes + 255) & ~size_t(255); return p; };
   BootWs w{};
-  w.G = (double *)take((size_t)nb * m * m * 8);
+  w.G = (double *)take(fact ? 8 : (size_t)nb * m * m * 8);
   w.lam = (double *)take((size_t)nb * r * 8);
   w.Uk = (double *)take((size_t)nb * m * r * 8);
   w.trace = (double *)take((size_t)nb * 8);
@@ -594,6 +624,12 @@ static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool c
   w.eig = take(w.eig_bytes);
   w.chow_bytes = chow ? chow_workspace_bytes(T, N, r, nb) : 0;
   w.chow = take(w.chow_bytes);
+  w.fact_bytes = fact ? fact_workspace_bytes(T, nb, P) : 0;
+  w.fact = take(w.fact_bytes);
+  w.fload_bytes = fact ? fact_loadings_bytes(T, N, r, nb) : 0;
+  w.fload = take(w.fload_bytes);
+  w.off = (int *)take(fact ? (size_t)nb * (T + 1) * 4 : 4);
+  w.lst = (int *)take(fact ? (size_t)nb * T * 4 : 4);
   if (o) *o = w;
   return off;
 }
@@ -648,7 +684,27 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
   }
   nb = std::min<int64_t>(nb, B);
-  const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, nullptr, nullptr);
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32;
+  if (fact && !M->fact_ready) {
+    // H = E E' by the MFMA Gram kernel (K1), then EL, S, cF, diag(H)
+    M->ldH = round_up(T, 16);
+    HIPCHK(ctx, dalloc(&M->H, (size_t)T * M->ldH));
+    HIPCHK(ctx, dalloc(&M->EL, (size_t)T * r));
+    HIPCHK(ctx, dalloc(&M->S, (size_t)r * r));
+    HIPCHK(ctx, dalloc(&M->cF, T));
+    HIPCHK(ctx, dalloc(&M->hd, T));
+    HIPCHK(ctx, hipMemsetAsync(M->H, 0, (size_t)T * M->ldH * 8, st));
+    PanelSrc es{nullptr, M->Ep, nullptr, nullptr, M->ld};
+    {
+      Scope sc(ctx, DFM_KC_GRAM);
+      HIPCHK(ctx, launch_gram(0, es, T, N, T, M->H, M->ldH, 0, 1, st));
+    }
+    int rc0 = fact_precompute(M->Ep, M->ld, T, N, r, M->L, M->F, M->H, M->ldH, M->EL, M->S, M->cF, M->hd, st);
+    if (rc0) return fail(ctx, rc0, "factored precompute failed");
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    M->fact_ready = true;
+  }
+  const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, nullptr, nullptr);
   if (need > M->ws_bytes) {
     hipFree(M->ws);
     M->ws = nullptr; M->ws_bytes = 0;
@@ -663,18 +719,27 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   if (ns) HIPCHK(ctx, hipMemcpyAsync(M->sd_dev, sd.data(), ns * sizeof(StatDesc), hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemsetAsync(M->flag_dev, 0, 4, st));
   BootWs w;
-  boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, &w, M->ws);
+  boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, &w, M->ws);
+  FactBase fb{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd};
   for (int64_t b0 = 0; b0 < B; b0 += nb) {
     const int n = (int)std::min<int64_t>(nb, B - b0);
     PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld};
-    {
-      Scope sc(ctx, DFM_KC_GRAM);
-      HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
-    }
-    int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
-                     w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
-    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-    {
+    if (fact) {
+      const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
+      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
+                                w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst);
+      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      Scope sc(ctx, DFM_KC_FACTORS);
+      rc = fact_loadings(fb, M->Ep, M->ld, N, M->L, w.Uk, et, w.off, w.lst, n, w.F, w.L, w.fload, st);
+      if (rc) return fail(ctx, rc, "factored loadings failed");
+    } else {
+      {
+        Scope sc(ctx, DFM_KC_GRAM);
+        HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
+      }
+      int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
+                       w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
+      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       Scope sc(ctx, DFM_KC_FACTORS);
       launch_factors(M->orient, src, T, N, r, n, w.Uk, w.F, w.L, nullptr, st);
     }

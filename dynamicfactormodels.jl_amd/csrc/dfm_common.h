@@ -50,5 +50,5 @@ DFM_DEV double hash_unit(uint64_t a, uint64_t b, uint64_t c) {
 // Kernel classes for per-kernel HIP-event timing (dfm_ctx_read_timing).
 enum {
   DFM_KC_GRAM = 0, DFM_KC_EIG_GQ, DFM_KC_EIG_SMALL, DFM_KC_EIG_APPLY, DFM_KC_EIG_OTHER,
-  DFM_KC_FACTORS, DFM_KC_OLS, DFM_KC_STATS, DFM_KC_CHOW, DFM_KC_MISC, DFM_KC_COUNT
+  DFM_KC_FACTORS, DFM_KC_OLS, DFM_KC_STATS, DFM_KC_CHOW, DFM_KC_MISC, DFM_KC_GEMM, DFM_KC_COUNT
 };

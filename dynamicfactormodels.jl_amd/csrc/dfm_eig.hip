@@ -59,6 +59,56 @@ __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int6
   if (lane == 0) trace[rep] = s;
 }
 
+// Convergence test of iteration it-1's Ritz pairs (explicit residual partials
+// written by eig_apply).  Every workgroup of a replicate evaluates it on the
+// same data (so they agree); row block 0 records the verdict.
+template <int P>
+DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb, int k, int p,
+                            double tol, int it, int check_only) {
+  int d = w.done[rep];
+  if (!d && it > 0) {
+    // Converged when every wanted Ritz pair j < k satisfies
+    //   res_j <= tol * gap_j            (eigenvector error ~ res/gap <= tol)
+    // or sits at the rounding floor: res_j <= 2e-14 |theta_1|, or
+    //   res_j <= 1e-11 |theta_1| and stagnating (no 2x decrease).
+    const double *th = small + 2 * P * P;
+    const double *prev = small + 2 * P * P + 2 * P + ((it - 1) & 1) * P;
+    double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
+    const double th0 = fabs(th[0]);
+    bool ok = true;
+    for (int j = 0; j < k; ++j) {
+      double s = 0.0;
+      for (int r = 0; r < nrb; ++r) s += w.rpart[((int64_t)rep * nrb + r) * P + j];
+      const double res = sqrt(s);
+      double gap = INFINITY;
+      if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+      if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+      const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
+      if (!(res <= tol * gap || res <= 2e-14 * th0 || stagn)) ok = false;
+      if (rb == 0) next[j] = res;
+    }
+    if (ok) {
+      d = 1;
+      if (rb == 0) { w.done[rep] = 1; w.iters[rep] = it; }
+    }
+  }
+  if (rb == 0 && !d) atomicAdd(&w.active[it], 1);
+  return d || check_only;
+}
+
+// Partial Q'Y, Y'Y, Q'Q over one 64-row block (fixed order), LDS images sQ/sY.
+template <int P, int SQ>
+DFM_DEV void emit_partials(const double *sQ, const double *sY, double *pp) {
+  for (int e = threadIdx.x; e < 3 * P * P; e += blockDim.x) {
+    const int which = e / (P * P), a = (e / P) % P, c = e % P;
+    const double *X1 = (which == 1) ? sY : sQ;
+    const double *X2 = (which == 2) ? sQ : sY;
+    double s = 0.0;
+    for (int r = 0; r < EROWS; ++r) s = fma(X1[r * SQ + a], X2[r * SQ + c], s);
+    pp[e] = s;
+  }
+}
+
 // ------------------------------------------------------------------- gq
 template <int P>
 __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ G, int64_t ldg,
@@ -71,37 +121,7 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x;
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  if (tid == 0) {
-    int d = w.done[rep];
-    if (!d && it > 0) {
-      // Converged when every wanted Ritz pair j < k satisfies
-      //   res_j <= tol * gap_j            (eigenvector error ~ res/gap <= tol)
-      // or sits at the rounding floor: res_j <= 2e-14 |theta_1|, or
-      //   res_j <= 1e-11 |theta_1| and stagnating (no 2x decrease).
-      const double *th = small + 2 * P * P;
-      const double *prev = small + 2 * P * P + 2 * P + ((it - 1) & 1) * P;
-      double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
-      const double th0 = fabs(th[0]);
-      bool ok = true;
-      for (int j = 0; j < k; ++j) {
-        double s = 0.0;
-        for (int r = 0; r < nrb; ++r) s += w.rpart[((int64_t)rep * nrb + r) * P + j];
-        const double res = sqrt(s);
-        double gap = INFINITY;
-        if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
-        if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
-        const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
-        if (!(res <= tol * gap || res <= 2e-14 * th0 || stagn)) ok = false;
-        if (rb == 0) next[j] = res;
-      }
-      if (ok) {
-        d = 1;
-        if (rb == 0) { w.done[rep] = 1; w.iters[rep] = it; }
-      }
-    }
-    s_skip = d || check_only;
-    if (rb == 0 && !d) atomicAdd(&w.active[it], 1);
-  }
+  if (tid == 0) s_skip = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only);
   __syncthreads();
   if (s_skip) return;
 
@@ -164,15 +184,7 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   }
   __syncthreads();
   // partial Q'Y, Y'Y, Q'Q over this block's rows (fixed order)
-  double *pp = w.part + ((int64_t)rep * nrb + rb) * 3 * P * P;
-  for (int e = tid; e < 3 * P * P; e += 256) {
-    const int which = e / (P * P), a = (e / P) % P, c = e % P;
-    const double *X1 = (which == 1) ? sY : sQ;
-    const double *X2 = (which == 2) ? sQ : sY;
-    double s = 0.0;
-    for (int r = 0; r < EROWS; ++r) s = fma(X1[r * SQ + a], X2[r * SQ + c], s);
-    pp[e] = s;
-  }
+  emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
 }
 
 // ---------------------------------------------------------------- small
@@ -575,6 +587,343 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
                          trace_out, status, iters_host, st, tf, tctx, rep0);
   return eig_run_t<32>(G, ldg, strideG, m, nb, k, p, warm, kw, tol, maxit, poll, ws, lam, Uk,
                        trace_out, status, iters_host, st, tf, tctx, rep0);
+}
+
+
+// ===================================================================== factored
+// Factored bootstrap (N > T).  With X* = F L' + D P E  (F = F_r, L = L_r of the
+// base fit, D = diag(eta), P the row selection of idx; src/bootstrap.jl:45):
+//   G* Q = X* X*' Q = F [S a + (EL)' Z] + D P [(EL) a + H Z]
+//   a = F'Q (r x p), Z = P' D Q (T x p, scatter through a CSR of idx),
+//   S = L'L, EL = E L (T x r), H = E E' (T x T)  — S, EL, H shared by all
+// replicates.  H Z for a whole batch is ONE MFMA GEMM (dfm_gemm.hip) with H
+// resident in L2; everything else is O(T r p) per replicate.
+struct FactBase {
+  int T, r;
+  int64_t ldH;
+  const double *F, *EL, *S, *H, *cF, *hd;   // T x r, T x r, r x r, T x ldH, T, T
+};
+
+// Per replicate: CSR of idx (bucket s lists t ascending — fixed summation
+// order, bit-reproducible), and trace(G*) = sum_t ||x*_t||^2 =
+// sum_t [F_t S F_t' + 2 eta_t F_t.(EL)_idx_t + eta_t^2 H_idx_t,idx_t].
+__global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
+                                                        const double *__restrict__ eta, int *__restrict__ off,
+                                                        int *__restrict__ lst, double *__restrict__ trace) {
+  extern __shared__ int sh[];   // cnt[T+1], cur[T]
+  __shared__ double red[256];
+  const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
+  const int32_t *ix = idx + (int64_t)rep * T;
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  int *cnt = sh, *cur = sh + T + 1;
+  for (int s = tid; s <= T; s += 256) cnt[s] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += 256) atomicAdd(&cnt[ix[t] + 1], 1);
+  __syncthreads();
+  if (tid == 0) {
+    for (int s = 1; s <= T; ++s) cnt[s] += cnt[s - 1];
+    for (int s = 0; s < T; ++s) cur[s] = cnt[s];
+    int *L = lst + (int64_t)rep * T;
+    for (int t = 0; t < T; ++t) L[cur[ix[t]]++] = t;   // stable: ascending t per bucket
+  }
+  __syncthreads();
+  for (int s = tid; s <= T; s += 256) off[(int64_t)rep * (T + 1) + s] = cnt[s];
+  double acc = 0.0;
+  for (int t = tid; t < T; t += 256) {
+    const int i = ix[t];
+    const double e = et ? et[t] : 1.0;
+    double fe = 0.0;
+    for (int j = 0; j < r; ++j) fe = fma(fb.F[(int64_t)t * r + j], fb.EL[(int64_t)i * r + j], fe);
+    acc += fb.cF[t] + 2.0 * e * fe + e * e * fb.hd[i];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) { if (tid < o) red[tid] += red[tid + o]; __syncthreads(); }
+  if (tid == 0) trace[rep] = red[0];
+}
+
+// Z = P' D Q into the GEMM operand Zc[s][rep*P + c]; a = F'Q, cc = EL' Z
+// (r x P each) into ab[rep][2][r][P].
+template <int P>
+__global__ __launch_bounds__(256) void boot_fz_kernel(FactBase fb, EigWork w, int m, const double *__restrict__ eta,
+                                                      const int *__restrict__ off, const int *__restrict__ lst,
+                                                      double *__restrict__ Zc, int64_t ldz,
+                                                      double *__restrict__ ab) {
+  const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
+  if (w.done[rep]) return;
+  const double *Q = w.Q + (int64_t)rep * m * P;
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  const int *o = off + (int64_t)rep * (T + 1);
+  const int *L = lst + (int64_t)rep * T;
+  for (int e = tid; e < T * P; e += 256) {
+    const int sI = e / P, c = e % P;
+    double z = 0.0;
+    for (int q = o[sI]; q < o[sI + 1]; ++q) {
+      const int t = L[q];
+      z = fma(et ? et[t] : 1.0, Q[(int64_t)t * P + c], z);
+    }
+    Zc[(int64_t)sI * ldz + (int64_t)rep * P + c] = z;
+  }
+  __syncthreads();
+  double *abr = ab + (int64_t)rep * 2 * r * P;
+  for (int e = tid; e < 2 * r * P; e += 256) {
+    const int which = e / (r * P), j = (e / P) % r, c = e % P;
+    double sacc = 0.0;
+    if (which == 0)
+      for (int t = 0; t < T; ++t) sacc = fma(fb.F[(int64_t)t * r + j], Q[(int64_t)t * P + c], sacc);
+    else
+      for (int t = 0; t < T; ++t)
+        sacc = fma(fb.EL[(int64_t)t * r + j], Zc[(int64_t)t * ldz + (int64_t)rep * P + c], sacc);
+    abr[e] = sacc;
+  }
+}
+
+// Y[t] = F_t (S a + cc) + eta_t ((EL)_idx_t a + (H Z)_idx_t), then the same
+// partial products as eig_gq (the convergence preamble first).
+template <int P>
+__global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, int m, int k, int p, double tol,
+                                                      int it, int check_only, const int32_t *__restrict__ idx,
+                                                      const double *__restrict__ eta,
+                                                      const double *__restrict__ HZ, int64_t ldz,
+                                                      const double *__restrict__ ab) {
+  constexpr int SQ = P + 4;
+  constexpr int RM = 32;
+  __shared__ __attribute__((aligned(16))) double sQ[EROWS * SQ];
+  __shared__ __attribute__((aligned(16))) double sY[EROWS * SQ];
+  __shared__ double sA[RM * P], sB[RM * P];
+  __shared__ int s_skip;
+  const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, r = fb.r;
+  double *small = w.small + (int64_t)rep * small_stride<P>();
+  if (tid == 0) s_skip = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only);
+  __syncthreads();
+  if (s_skip) return;
+  const double *abr = ab + (int64_t)rep * 2 * r * P;
+  // sA = a, sB = S a + cc
+  for (int e = tid; e < r * P; e += 256) {
+    const int j = e / P, c = e % P;
+    double v = abr[r * P + e];
+    for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], abr[i * P + c], v);
+    sA[e] = abr[e];
+    sB[e] = v;
+  }
+  __syncthreads();
+  const double *Qr = w.Q + (int64_t)rep * m * P;
+  double *Yr = w.Y + (int64_t)rep * m * P;
+  const int32_t *ix = idx + (int64_t)rep * fb.T;
+  const double *et = eta ? eta + (int64_t)rep * fb.T : nullptr;
+  for (int e = tid; e < EROWS * P; e += 256) {
+    const int lr = e / P, c = e % P, t = rb * EROWS + lr;
+    double y = 0.0, q = 0.0;
+    if (t < m) {
+      const int i = ix[t];
+      double u = HZ[(int64_t)i * ldz + (int64_t)rep * P + c];
+      double v = 0.0;
+      for (int j = 0; j < r; ++j) {
+        u = fma(fb.EL[(int64_t)i * r + j], sA[j * P + c], u);
+        v = fma(fb.F[(int64_t)t * r + j], sB[j * P + c], v);
+      }
+      y = fma(et ? et[t] : 1.0, u, v);
+      q = Qr[(int64_t)t * P + c];
+      Yr[(int64_t)t * P + c] = y;
+    }
+    sY[lr * SQ + c] = y;
+    sQ[lr * SQ + c] = q;
+  }
+  __syncthreads();
+  emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
+}
+
+hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
+                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st);
+
+size_t fact_workspace_bytes(int T, int nb, int P) {
+  const int64_t ldz = (int64_t)nb * P;
+  return 2 * (size_t)T * ldz * 8 + (size_t)nb * 2 * 32 * P * 8 + (size_t)nb * (2 * T + 1) * 4 + 4096;
+}
+
+template <int P>
+static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
+                          const double *warm, int kw, double tol, int maxit, int poll, char *ws,
+                          char *fws, double *lam, double *Uk, double *trace_out, int *status,
+                          hipStream_t st, timer_fn tf, void *tctx, int *off_out, int *lst_out) {
+  const int m = fb.T, nrb = (m + EROWS - 1) / EROWS;
+  EigWork w = carve(ws, m, nb, P, maxit);
+  const int64_t ldz = (int64_t)nb * P;
+  double *Zc = (double *)fws;
+  double *HZ = Zc + (size_t)m * ldz;
+  double *ab = HZ + (size_t)m * ldz;
+  int *off = off_out, *lst = lst_out;
+  hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
+  hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
+  const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
+  {
+    const int64_t n = (int64_t)m * P;
+    dim3 grid((unsigned)((n + 255) / 256), nb);
+    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, (int64_t)0);
+    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
+                       off, lst, w.trace);
+  }
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
+  for (int it = 0; it <= maxit; ++it) {
+    const int check_only = (it == maxit);
+    if (!check_only) {
+      if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
+      hipLaunchKernelGGL(boot_fz_kernel<P>, dim3(nb), dim3(256), 0, st, fb, w, m, eta, off, lst, Zc, ldz, ab);
+      if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
+      if (tf) tf(tctx, DFM_KC_GEMM, 1);
+      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st);
+      if (tf) tf(tctx, DFM_KC_GEMM, 0);
+      if (e != hipSuccess) return 1000 + (int)e;
+    }
+    if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
+    hipLaunchKernelGGL(boot_gq_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, fb, w, m, k, p, tol, it, check_only,
+                       idx, eta, HZ, ldz, ab);
+    if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
+    if (check_only) break;
+    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb);
+    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
+    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
+    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0);
+    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+    if (it > 0 && (it % poll) == 0) {
+      int a = -1;
+      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
+      hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return 1000 + (int)e;
+      if (a == 0) break;
+    }
+  }
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
+  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
+  if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return 1000 + (int)e;
+  return 0;
+}
+
+int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
+                     const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
+                     double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
+                     timer_fn tf, void *tctx, int *off, int *lst) {
+  if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
+  if (p <= 16)
+    return eig_run_fact_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                              trace_out, status, st, tf, tctx, off, lst);
+  return eig_run_fact_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                            trace_out, status, st, tf, tctx, off, lst);
+}
+
+
+// ---- factored loadings pass: L* = X*' F* / T = (L (F'F*) + E' P' D F*) / T
+// boot_zf: ZF[s][rep*r + j] = sum_{t in bucket s} eta_t F*[t][j]  and
+//          M1[rep] = F' F* (r x r);  F* = sqrt(T) U*  written to Fout.
+__global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double *__restrict__ Uk,
+                                                      const double *__restrict__ eta,
+                                                      const int *__restrict__ off, const int *__restrict__ lst,
+                                                      double *__restrict__ Fout, double *__restrict__ ZF,
+                                                      int64_t ldzf, double *__restrict__ M1) {
+  const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
+  const double sT = sqrt((double)T);
+  const double *U = Uk + (int64_t)rep * T * r;
+  double *Fr = Fout + (int64_t)rep * T * r;
+  for (int e = tid; e < T * r; e += 256) Fr[e] = sT * U[e];
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  const int *o = off + (int64_t)rep * (T + 1);
+  const int *L = lst + (int64_t)rep * T;
+  for (int e = tid; e < T * r; e += 256) {
+    const int sI = e / r, j = e % r;
+    double z = 0.0;
+    for (int q = o[sI]; q < o[sI + 1]; ++q) {
+      const int t = L[q];
+      z = fma(et ? et[t] : 1.0, sT * U[(int64_t)t * r + j], z);
+    }
+    ZF[(int64_t)sI * ldzf + (int64_t)rep * r + j] = z;
+  }
+  for (int e = tid; e < r * r; e += 256) {
+    const int i = e / r, j = e % r;
+    double acc = 0.0;
+    for (int t = 0; t < T; ++t) acc = fma(fb.F[(int64_t)t * r + i], sT * U[(int64_t)t * r + j], acc);
+    M1[(int64_t)rep * r * r + e] = acc;
+  }
+}
+
+// L*[rep][n][j] = (sum_i L[n][i] M1[rep][i][j] + GL[n][rep*r + j]) / T
+__global__ void boot_lfinish_kernel(const double *__restrict__ Lb, int N, int r, int T,
+                                    const double *__restrict__ M1, const double *__restrict__ GL,
+                                    int64_t ldgl, double *__restrict__ Lout) {
+  const int rep = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * r) return;
+  const int n = (int)(e / r), j = (int)(e % r);
+  double v = GL[(int64_t)n * ldgl + (int64_t)rep * r + j];
+  for (int i = 0; i < r; ++i) v = fma(Lb[(int64_t)n * r + i], M1[(int64_t)rep * r * r + i * r + j], v);
+  Lout[(int64_t)rep * N * r + e] = v / T;
+}
+
+int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
+                  const double *Uk, const double *eta, const int *off, const int *lst, int nb,
+                  double *Fout, double *Lout, char *ws, hipStream_t st) {
+  const int T = fb.T, r = fb.r;
+  const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
+  double *ZF = (double *)ws;
+  double *GL = ZF + (size_t)T * ldzf;
+  double *M1 = GL + (size_t)N * ldzf;
+  hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, ldzf, M1);
+  hipError_t e = launch_gemm(true, Ep, ld, ZF, ldzf, GL, ldzf, N, (int)ldzf, T, st);
+  if (e != hipSuccess) return 1000 + (int)e;
+  hipLaunchKernelGGL(boot_lfinish_kernel, dim3((unsigned)(((int64_t)N * r + 255) / 256), nb), dim3(256), 0, st,
+                     Lb, N, r, T, M1, GL, ldzf, Lout);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : 1000 + (int)e;
+}
+size_t fact_loadings_bytes(int T, int N, int r, int nb) {
+  const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
+  return ((size_t)T * ldzf + (size_t)N * ldzf + (size_t)nb * r * r) * 8 + 1024;
+}
+
+// ---- model-level precompute: EL = E L (T x r), S = L'L, cF, hd
+__global__ void fact_pre_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N, int r,
+                                const double *__restrict__ Lb, const double *__restrict__ Fb,
+                                const double *__restrict__ H, int64_t ldH, double *__restrict__ EL,
+                                double *__restrict__ S, double *__restrict__ cF, double *__restrict__ hd) {
+  const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x < r * r) {
+    const int i = threadIdx.x / r, j = threadIdx.x % r;
+    double acc = 0.0;
+    for (int n = 0; n < N; ++n) acc = fma(Lb[(int64_t)n * r + i], Lb[(int64_t)n * r + j], acc);
+    S[threadIdx.x] = acc;
+  }
+  if (t >= T) return;
+  for (int j = 0; j < r; ++j) {
+    double acc = 0.0;
+    for (int n = lane; n < N; n += 64) acc = fma(Ep[(int64_t)t * ld + n], Lb[(int64_t)n * r + j], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) EL[(int64_t)t * r + j] = acc;
+  }
+  if (lane == 0) hd[t] = H[(int64_t)t * ldH + t];
+}
+__global__ void fact_cf_kernel(int T, int r, const double *__restrict__ Fb, const double *__restrict__ S,
+                               double *__restrict__ cF) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  double acc = 0.0;
+  for (int i = 0; i < r; ++i) {
+    double u = 0.0;
+    for (int j = 0; j < r; ++j) u = fma(S[i * r + j], Fb[(int64_t)t * r + j], u);
+    acc = fma(Fb[(int64_t)t * r + i], u, acc);
+  }
+  cF[t] = acc;
+}
+int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
+                    const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st) {
+  hipLaunchKernelGGL(fact_pre_kernel, dim3((T + 3) / 4), dim3(256), 0, st, Ep, ld, T, N, r, Lb, Fb, H, ldH,
+                     EL, S, cF, hd);
+  hipLaunchKernelGGL(fact_cf_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, r, Fb, S, cF);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : 1000 + (int)e;
 }
 
 // ------------------------------------------------------------ full spectrum

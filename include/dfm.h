@@ -148,6 +148,11 @@ int dfm_bootstrap_dev(dfm_model *m, int kind, int64_t B, const int32_t *idx_dev,
 int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats);
 /* Replicates per device batch (0 = auto). */
 int dfm_model_set_batch(dfm_model *m, int64_t batch);
+/* Bootstrap algorithm for N > T panels: 0 auto (= factored), 1 direct (per-
+ * replicate fused-gather Gram + eigensolver on it), 2 factored (the replicate
+ * Gram is never formed: every eigen-iteration is one MFMA GEMM of the shared
+ * H = E E' against the batch's iterates).  Results agree to rounding. */
+int dfm_model_set_mode(dfm_model *m, int mode);
 
 /* ------------------------------------------------------------ Chow tests
  * LR_test / LM_test / Wald_test (src/chowtest.jl:19-42) for EVERY variable

@@ -211,10 +211,12 @@ def test_ic_sweep_default_kmax(dfm, oracle):
         STAT_RTOL * abs(o.number_of_factors_criterion_value)
 
 
-@pytest.mark.parametrize("T,N,r", [(200, 100, 3), (60, 150, 4)])
-def test_wild_bootstrap_matches_oracle(dfm, oracle, T, N, r):
+@pytest.mark.parametrize("T,N,r,mode", [(200, 100, 3, "auto"), (60, 150, 4, "direct"),
+                                        (60, 150, 4, "factored"), (37, 101, 3, "factored")])
+def test_wild_bootstrap_matches_oracle(dfm, oracle, T, N, r, mode):
     y, x, w = panel(oracle, T, N, r, 2000 + T)
     g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    g.set_bootstrap_mode(mode)
     o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
     B = 6
     idx, eta = oracle.draw_wild(np.random.default_rng(3), B, T)
@@ -232,38 +234,44 @@ def test_wild_bootstrap_matches_oracle(dfm, oracle, T, N, r):
         assert rel(out[b, 6:], ref[6:]) < 1e-9      # w-column coef/t: sign-invariant
 
 
-def test_residual_bootstrap_matches_oracle(dfm, oracle):
-    y, x, w = panel(oracle, 150, 70, 2, 16)
+@pytest.mark.parametrize("T,N", [(150, 70), (70, 150)])
+def test_residual_bootstrap_matches_oracle(dfm, oracle, T, N):
+    y, x, w = panel(oracle, T, N, 2, 16)
     g = dfm.DynamicFactorModel(y, w, x, 2, "ICp1")
     o = oracle.DynamicFactorModel(y, w, x, 2, "ICp1")
-    idx = oracle.draw_residual(np.random.default_rng(4), 5, 150)
+    idx = oracle.draw_residual(np.random.default_rng(4), 5, T)
     out = dfm.residual_bootstrap(g, 5, [dfm.Stat.V(), dfm.Stat.criterion()], idx=idx)
     ref = oracle.residual_bootstrap(o, 5, lambda d: oracle.factor_residual_variance(d), idx)
     assert rel(out[:, 0], ref) < STAT_RTOL
 
 
-def test_bootstrap_chow_all_matches_oracle(dfm, oracle):
-    y, x, w = panel(oracle, 160, 24, 2, 17, model="Breitung_Eickmeier_2011", b=0.5)
+@pytest.mark.parametrize("T,N", [(160, 24), (80, 120)])
+def test_bootstrap_chow_all_matches_oracle(dfm, oracle, T, N):
+    y, x, w = panel(oracle, T, N, 2, 17, model="Breitung_Eickmeier_2011", b=0.5)
     g = dfm.DynamicFactorModel(y, w, x, 2)
     o = oracle.DynamicFactorModel(y, w, x, 2)
-    idx, eta = oracle.draw_wild(np.random.default_rng(5), 3, 160)
+    idx, eta = oracle.draw_wild(np.random.default_rng(5), 3, T)
     S = dfm.Stat
-    out = dfm.wild_bootstrap(g, 3, [S.LR_all(80), S.LM_all(80), S.Wald_all(80)], idx=idx, eta=eta)
+    bp = T // 2
+    out = dfm.wild_bootstrap(g, 3, [S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp)], idx=idx, eta=eta)
+    nv = min(N, 24)
     for b in range(3):
         d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]], 2)
-        ref = np.array([[oracle.LR_test(d, 80, i), oracle.LM_test(d, 80, i), oracle.Wald_test(d, 80, i)]
-                        for i in range(24)])
-        assert rel(out[b, :24], ref[:, 0]) < 1e-9
-        assert rel(out[b, 24:48], ref[:, 1]) < 1e-9
-        assert rel(out[b, 48:], ref[:, 2]) < 1e-9
+        ref = np.array([[oracle.LR_test(d, bp, i), oracle.LM_test(d, bp, i), oracle.Wald_test(d, bp, i)]
+                        for i in range(nv)])
+        assert rel(out[b, :nv], ref[:, 0]) < 1e-9
+        assert rel(out[b, N:N + nv], ref[:, 1]) < 1e-9
+        assert rel(out[b, 2 * N:2 * N + nv], ref[:, 2]) < 1e-9
 
 
 # -------------------------------------- full-size (C3) size-independent props
-def test_c3_identity_draw_reproduces_base(dfm, oracle):
+@pytest.mark.parametrize("mode", ["direct", "factored"])
+def test_c3_identity_draw_reproduces_base(dfm, oracle, mode):
     """At T=500, N=2000, r=8: idx = identity, eta = 1 rebuilds X exactly, so
     every replicate must reproduce the base fit's V and eigenvalues."""
     y, x, w = panel(oracle, 500, 2000, 8, 18)
     g = dfm.DynamicFactorModel(y, w, x, 8, "ICp2")
+    g.set_bootstrap_mode(mode)
     B = 32
     idx = np.tile(np.arange(500, dtype=np.int32), (B, 1))
     eta = np.ones((B, 500))
@@ -274,21 +282,30 @@ def test_c3_identity_draw_reproduces_base(dfm, oracle):
     assert rel(out[:, 2], np.full(B, g.eigenvalues[7])) < 1e-12
 
 
-def test_c3_replicates_match_oracle(dfm, oracle):
+@pytest.mark.parametrize("mode", ["direct", "factored"])
+def test_c3_replicates_match_oracle(dfm, oracle, mode):
     y, x, w = panel(oracle, 500, 2000, 8, 19)
     g = dfm.DynamicFactorModel(y, w, x, 8, "ICp2")
+    g.set_bootstrap_mode(mode)
     o = oracle.DynamicFactorModel(y, w, x, 8, "ICp2")
     idx, eta = oracle.draw_wild(np.random.default_rng(6), 3, 500)
-    out = dfm.wild_bootstrap(g, 3, [dfm.Stat.V(), dfm.Stat.criterion()], idx=idx, eta=eta)
-    ref = oracle.wild_bootstrap(o, 3, lambda d: d.number_of_factors_criterion_value, idx, eta)
-    assert rel(out[:, 1], ref) < STAT_RTOL
+    out = dfm.wild_bootstrap(g, 3, [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.t_stat(1)],
+                             idx=idx, eta=eta)
+    ref = np.array([[oracle.factor_residual_variance(d), d.number_of_factors_criterion_value, d.t_stats[0]]
+                    for d in [oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] *
+                                                        o.factor_residuals[idx[b]], 8, "ICp2")
+                              for b in range(3)]])
+    assert rel(out[:, :2], ref[:, :2]) < STAT_RTOL
+    assert rel(out[:, 2], ref[:, 2]) < 1e-9
 
 
-def test_batching_is_bit_identical(dfm, oracle):
+@pytest.mark.parametrize("mode", ["direct", "factored"])
+def test_batching_is_bit_identical(dfm, oracle, mode):
     """Per-replicate results do not depend on batch composition — the property
     behind bit-identical 1-GPU vs 8-GPU sharding."""
     y, x, w = panel(oracle, 200, 300, 4, 20)
     g = dfm.DynamicFactorModel(y, w, x, 4, "ICp2")
+    g.set_bootstrap_mode(mode)
     B = 24
     idx, eta = dfm.draw_wild_fast(7, B, 200)
     stats = [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.t_stat(2)]
@@ -302,6 +319,22 @@ def test_batching_is_bit_identical(dfm, oracle):
 
 
 # ----------------------------------------------------------- error behaviour
+def test_direct_and_factored_agree(dfm, oracle):
+    """The two N > T algorithms give the same replicates to rounding, incl.
+    per-variable Chow statistics (which read the factored loadings)."""
+    y, x, w = panel(oracle, 120, 400, 3, 22, model="Breitung_Eickmeier_2011", b=0.3)
+    g = dfm.DynamicFactorModel(y, w, x, 3, "ICp2")
+    idx, eta = dfm.draw_wild_fast(9, 40, 120)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.eigenvalue(3), S.t_stat(1), S.LR_all(60), S.Wald_all(60)]
+    g.set_bootstrap_mode("direct")
+    a = dfm.wild_bootstrap(g, 40, stats, idx=idx, eta=eta)
+    g.set_bootstrap_mode("factored")
+    b = dfm.wild_bootstrap(g, 40, stats, idx=idx, eta=eta)
+    assert rel(b[:, :4], a[:, :4]) < STAT_RTOL
+    assert rel(b[:, 4:], a[:, 4:]) < 1e-9
+
+
 def test_errors_are_reported(dfm, oracle):
     y, x, w = panel(oracle, 50, 20, 2, 21)
     g = dfm.DynamicFactorModel(y, w, x, 2, "PCp2")
