@@ -188,46 +188,92 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
 }
 
 // ---------------------------------------------------------------- small
-// Single-wave p x p linear algebra in LDS.
+// One wave per replicate, all p x p algebra in LDS, written for latency:
+// Cholesky with the pivot broadcast by a lane shuffle, explicit triangular
+// inverses (so every solve becomes a parallel matrix product), and a parallel
+// cyclic Jacobi whose round is ONE phase: with the pairs of a round disjoint,
+// every 2x2 block (pair s1 rows, pair s2 cols) is rotated J1' B J2 by one lane.
 template <int P>
 struct SmallLds {
   static constexpr int S = P + 1;
-  double Hq[P * S], Yq[P * S], Qq[P * S], L[P * S], Wt[P * S], V[P * S], A[P * S], Z[P * S],
-      L2[P * S], Bm[P * S];
-  double rot_c[P / 2 + 1], rot_s[P / 2 + 1];
-  int rot_a[P / 2 + 1], rot_b[P / 2 + 1], perm[P];
+  double Hq[P * S], Yq[P * S], Qq[P * S], L[P * S], Li[P * S], W[P * S], V[P * S], A[P * S];
+  double rc[P / 2], rs[P / 2];
+  int ra[P / 2], rb[P / 2], perm[P];
   int dead1[P], dead2[P];
-  double red[64];
 };
 
-// lower Cholesky of M (p x p) into Lo; tiny pivots -> dead (column zeroed).
+// lower Cholesky M = Lo Lo' (p x p), tiny pivots -> dead (unit diagonal, zero column)
 template <int P>
-DFM_DEV void wave_chol(const double *M, double *Lo, int *dead, int p, double *red) {
+DFM_DEV void wave_chol(const double *M, double *Lo, int *dead, int p) {
   constexpr int S = P + 1;
   const int lane = threadIdx.x;
   double mx = 0.0;
-  for (int j = 0; j < p; ++j) mx = fmax(mx, fabs(M[j * S + j]));
+  for (int j = lane; j < p; j += 64) mx = fmax(mx, fabs(M[j * S + j]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
   for (int e = lane; e < P * S; e += 64) Lo[e] = 0.0;
   __syncthreads();
   const double thresh = 1e-22 * mx;
   for (int j = 0; j < p; ++j) {
-    if (lane == 0) {
-      double d = M[j * S + j];
-      for (int q = 0; q < j; ++q) d -= Lo[j * S + q] * Lo[j * S + q];
-      const int dd = !(d > thresh);
-      dead[j] = dd;
-      Lo[j * S + j] = dd ? 1.0 : sqrt(d);
+    const int i = lane;
+    double sv = 0.0;
+    if (i >= j && i < p) {
+      sv = M[i * S + j];
+      for (int q = 0; q < j; ++q) sv -= Lo[i * S + q] * Lo[j * S + q];
     }
-    __syncthreads();
-    const double ljj = Lo[j * S + j];
-    const int dd = dead[j];
-    for (int i = j + 1 + lane; i < p; i += 64) {
-      double s = M[i * S + j];
-      for (int q = 0; q < j; ++q) s -= Lo[i * S + q] * Lo[j * S + q];
-      Lo[i * S + j] = dd ? 0.0 : s / ljj;
-    }
+    const double sj = __shfl(sv, j);
+    const bool dd = !(sj > thresh);
+    const double d = dd ? 1.0 : sqrt(sj);
+    if (i == j) { Lo[j * S + j] = d; dead[j] = dd; }
+    else if (i > j && i < p) Lo[i * S + j] = dd ? 0.0 : sv / d;
     __syncthreads();
   }
+}
+
+// Li = Lo^-1 (lower), column c per lane in registers; rows of dead pivots zeroed.
+template <int P>
+DFM_DEV void wave_trinv(const double *Lo, double *Li, const int *dead, int p) {
+  constexpr int S = P + 1;
+  const int c = threadIdx.x;
+  if (c < P) {
+    double x[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      double sv = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < i; ++q) sv -= Lo[i * S + q] * x[q];
+      x[i] = (i < p) ? sv / Lo[i * S + i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < P; ++i) Li[i * S + c] = (i < p && c < p && !dead[i]) ? x[i] : 0.0;
+  }
+  __syncthreads();
+}
+
+// C = op(A) op(B) for P x P LDS matrices (TA/TB transpose flags); padded
+// entries are zero so the full P x P product is exact.
+template <int P, bool TA, bool TB>
+DFM_DEV void wave_mm(const double *A, const double *B, double *C) {
+  constexpr int S = P + 1;
+  for (int e = threadIdx.x; e < P * P; e += 64) {
+    const int i = e / P, j = e % P;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+      acc = fma(TA ? A[q * S + i] : A[i * S + q], TB ? B[j * S + q] : B[q * S + j], acc);
+    C[i * S + j] = acc;
+  }
+  __syncthreads();
+}
+
+template <int P>
+DFM_DEV void wave_sym(double *M) {
+  constexpr int S = P + 1;
+  for (int e = threadIdx.x; e < P * P; e += 64) {
+    const int i = e / P, j = e % P;
+    if (i < j) { const double v = 0.5 * (M[i * S + j] + M[j * S + i]); M[i * S + j] = v; M[j * S + i] = v; }
+  }
+  __syncthreads();
 }
 
 template <int P>
@@ -236,58 +282,41 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   __shared__ SmallLds<P> sm;
   const int lane = threadIdx.x, rep = blockIdx.x;
   if (w.done[rep]) return;
-  // 1. sum partials in fixed order
+  // 1. sum partials in fixed order (entries >= p are zero: Q columns >= p are zero)
   const double *pp = w.part + (int64_t)rep * nrb * 3 * P * P;
   for (int e = lane; e < 3 * P * P; e += 64) {
-    double s = 0.0;
-    for (int r = 0; r < nrb; ++r) s += pp[(int64_t)r * 3 * P * P + e];
+    double sacc = 0.0;
+    for (int r = 0; r < nrb; ++r) sacc += pp[(int64_t)r * 3 * P * P + e];
     const int which = e / (P * P), a = (e / P) % P, c = e % P;
     double *M = which == 0 ? sm.Hq : (which == 1 ? sm.Yq : sm.Qq);
-    M[a * S + c] = s;
+    M[a * S + c] = sacc;
   }
   __syncthreads();
-  // 2. Q'Q = L L'
-  wave_chol<P>(sm.Qq, sm.L, sm.dead1, p, sm.red);
-  // 3. Wt = L^-1 Hsym (column c per lane), then Ht = L^-1 Wt'
-  for (int c = lane; c < p; c += 64) {
-    for (int i = 0; i < p; ++i) {
-      double s = 0.5 * (sm.Hq[i * S + c] + sm.Hq[c * S + i]);
-      for (int q = 0; q < i; ++q) s -= sm.L[i * S + q] * sm.Wt[q * S + c];
-      sm.Wt[i * S + c] = sm.dead1[i] ? 0.0 : s / sm.L[i * S + i];
-    }
-  }
+  wave_sym<P>(sm.Hq);
+  // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
+  wave_chol<P>(sm.Qq, sm.L, sm.dead1, p);
+  wave_trinv<P>(sm.L, sm.Li, sm.dead1, p);
+  wave_mm<P, false, false>(sm.Li, sm.Hq, sm.W);
+  wave_mm<P, false, true>(sm.W, sm.Li, sm.Hq);
+  wave_sym<P>(sm.Hq);
+  for (int e = lane; e < P * S; e += 64) sm.V[e] = ((e / S) == (e % S)) ? 1.0 : 0.0;
   __syncthreads();
-  for (int c = lane; c < p; c += 64) {
-    for (int i = 0; i < p; ++i) {
-      double s = sm.Wt[c * S + i];
-      for (int q = 0; q < i; ++q) s -= sm.L[i * S + q] * sm.Z[q * S + c];
-      sm.Z[i * S + c] = sm.dead1[i] ? 0.0 : s / sm.L[i * S + i];
-    }
-  }
-  __syncthreads();
-  // Ht (symmetrised) in Hq; V = I
-  for (int e = lane; e < P * S; e += 64) {
-    const int a = e / S, c = e % S;
-    if (a < p && c < p) sm.Hq[e] = 0.5 * (sm.Z[a * S + c] + sm.Z[c * S + a]);
-    sm.V[e] = (a == c) ? 1.0 : 0.0;
-  }
-  __syncthreads();
-  // 4. parallel cyclic Jacobi (circle-method ordering)
-  const int n = p + (p & 1);
-  for (int sweep = 0; sweep < 60; ++sweep) {
+  // 3. parallel cyclic Jacobi (circle-method pairs; index p is a dummy when p is odd)
+  const int n = p + (p & 1), h = n / 2;
+  for (int sweep = 0; sweep < 40; ++sweep) {
     double off = 0.0, fro = 0.0;
     for (int e = lane; e < p * p; e += 64) {
       const int a = e / p, c = e % p;
-      const double h = sm.Hq[a * S + c];
-      fro += h * h;
-      if (a != c) off += h * h;
+      const double v = sm.Hq[a * S + c];
+      fro = fma(v, v, fro);
+      if (a != c) off = fma(v, v, off);
     }
     off = wave_sum(off);
     fro = wave_sum(fro);
     if (off <= 1e-30 * fro || fro == 0.0) break;
     for (int r = 0; r < n - 1; ++r) {
-      for (int s = lane; s < n / 2; s += 64) {
-        const int pa = s, pb = n - 1 - s;
+      if (lane < h) {
+        const int pa = lane, pb = n - 1 - lane;
         int a = pa == 0 ? 0 : 1 + (pa - 1 + r) % (n - 1);
         int b = pb == 0 ? 0 : 1 + (pb - 1 + r) % (n - 1);
         if (a > b) { const int t = a; a = b; b = t; }
@@ -301,37 +330,35 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
             sn = t * c;
           }
         }
-        sm.rot_a[s] = a; sm.rot_b[s] = b; sm.rot_c[s] = c; sm.rot_s[s] = sn;
+        sm.ra[lane] = a; sm.rb[lane] = b; sm.rc[lane] = c; sm.rs[lane] = sn;
       }
       __syncthreads();
-      // H <- H J (columns), V <- V J
-      for (int e = lane; e < (n / 2) * p; e += 64) {
-        const int s = e / p, kk = e % p;
-        const int a = sm.rot_a[s], b = sm.rot_b[s];
-        if (b >= p) continue;
-        const double c = sm.rot_c[s], sn = sm.rot_s[s];
-        const double ha = sm.Hq[kk * S + a], hb = sm.Hq[kk * S + b];
-        sm.Hq[kk * S + a] = c * ha - sn * hb;
-        sm.Hq[kk * S + b] = sn * ha + c * hb;
-        const double va = sm.V[kk * S + a], vb = sm.V[kk * S + b];
-        sm.V[kk * S + a] = c * va - sn * vb;
-        sm.V[kk * S + b] = sn * va + c * vb;
+      // H <- J' H J by 2x2 blocks; V <- V J
+      for (int e = lane; e < h * h; e += 64) {
+        const int s1 = e / h, s2 = e % h;
+        const int i0 = sm.ra[s1], i1 = sm.rb[s1], j0 = sm.ra[s2], j1 = sm.rb[s2];
+        const double c1 = sm.rc[s1], n1 = sm.rs[s1], c2 = sm.rc[s2], n2 = sm.rs[s2];
+        const double b00 = sm.Hq[i0 * S + j0], b01 = sm.Hq[i0 * S + j1];
+        const double b10 = sm.Hq[i1 * S + j0], b11 = sm.Hq[i1 * S + j1];
+        const double t00 = c1 * b00 - n1 * b10, t01 = c1 * b01 - n1 * b11;
+        const double t10 = n1 * b00 + c1 * b10, t11 = n1 * b01 + c1 * b11;
+        sm.Hq[i0 * S + j0] = c2 * t00 - n2 * t01;
+        sm.Hq[i0 * S + j1] = n2 * t00 + c2 * t01;
+        sm.Hq[i1 * S + j0] = c2 * t10 - n2 * t11;
+        sm.Hq[i1 * S + j1] = n2 * t10 + c2 * t11;
       }
-      __syncthreads();
-      // H <- J' H (rows)
-      for (int e = lane; e < (n / 2) * p; e += 64) {
-        const int s = e / p, kk = e % p;
-        const int a = sm.rot_a[s], b = sm.rot_b[s];
-        if (b >= p) continue;
-        const double c = sm.rot_c[s], sn = sm.rot_s[s];
-        const double ha = sm.Hq[a * S + kk], hb = sm.Hq[b * S + kk];
-        sm.Hq[a * S + kk] = c * ha - sn * hb;
-        sm.Hq[b * S + kk] = sn * ha + c * hb;
+      for (int e = lane; e < p * h; e += 64) {
+        const int k = e / h, sI = e % h;
+        const int a = sm.ra[sI], b = sm.rb[sI];
+        const double c = sm.rc[sI], sn = sm.rs[sI];
+        const double va = sm.V[k * S + a], vb = sm.V[k * S + b];
+        sm.V[k * S + a] = c * va - sn * vb;
+        sm.V[k * S + b] = sn * va + c * vb;
       }
       __syncthreads();
     }
   }
-  // 5. sort descending (stable)
+  // 4. sort descending (stable)
   if (lane == 0) {
     for (int j = 0; j < p; ++j) sm.perm[j] = j;
     for (int i = 0; i < p; ++i) {
@@ -343,52 +370,25 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   }
   __syncthreads();
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  double *theta = small + 2 * P * P;
-  for (int j = lane; j < P; j += 64) theta[j] = j < p ? sm.Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
-  // 6. A = L^-T Vsorted (column c per lane, back substitution)
-  for (int c = lane; c < p; c += 64) {
-    const int pc = sm.perm[c];
-    for (int i = p - 1; i >= 0; --i) {
-      double s = sm.V[i * S + pc];
-      for (int q = i + 1; q < p; ++q) s -= sm.L[q * S + i] * sm.A[q * S + c];
-      sm.A[i * S + c] = sm.dead1[i] ? 0.0 : s / sm.L[i * S + i];
-    }
+  for (int j = lane; j < P; j += 64) small[2 * P * P + j] = j < p ? sm.Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
+  // W = V[:, perm] (zero-padded)
+  for (int e = lane; e < P * P; e += 64) {
+    const int i = e / P, c = e % P;
+    sm.W[i * S + c] = (i < p && c < p) ? sm.V[i * S + sm.perm[c]] : 0.0;
   }
   __syncthreads();
-  // 7. Z'Z = A' (Y'Y) A : Wt = Yq A, Z = A' Wt
-  for (int e = lane; e < p * p; e += 64) {
-    const int a = e / p, c = e % p;
-    double s = 0.0;
-    for (int q = 0; q < p; ++q) s = fma(sm.Yq[a * S + q], sm.A[q * S + c], s);
-    sm.Wt[a * S + c] = s;
-  }
-  __syncthreads();
-  for (int e = lane; e < p * p; e += 64) {
-    const int a = e / p, c = e % p;
-    double s = 0.0;
-    for (int q = 0; q < p; ++q) s = fma(sm.A[q * S + a], sm.Wt[q * S + c], s);
-    sm.Z[a * S + c] = s;
-  }
-  __syncthreads();
-  for (int e = lane; e < p * p; e += 64) {
-    const int a = e / p, c = e % p;
-    if (a > c) { const double v = 0.5 * (sm.Z[a * S + c] + sm.Z[c * S + a]); sm.Z[a * S + c] = v; sm.Z[c * S + a] = v; }
-  }
-  __syncthreads();
-  wave_chol<P>(sm.Z, sm.L2, sm.dead2, p, sm.red);
-  // 8. Bm = A L2^-T (row per lane): x L2' = a  ->  x_j = (a_j - sum_{i<j} x_i L2[j][i]) / L2[j][j]
-  for (int r = lane; r < p; r += 64) {
-    for (int j = 0; j < p; ++j) {
-      double s = sm.A[r * S + j];
-      for (int i = 0; i < j; ++i) s -= sm.Bm[r * S + i] * sm.L2[j * S + i];
-      sm.Bm[r * S + j] = sm.dead2[j] ? 0.0 : s / sm.L2[j * S + j];
-    }
-  }
-  __syncthreads();
+  // 5. A = L^-T Vs = Li' W ;  Z'Z = A' (Y'Y) A ;  L2 = chol ;  Bm = A L2^-T
+  wave_mm<P, true, false>(sm.Li, sm.W, sm.A);
+  wave_mm<P, false, false>(sm.Yq, sm.A, sm.W);
+  wave_mm<P, true, false>(sm.A, sm.W, sm.Qq);
+  wave_sym<P>(sm.Qq);
+  wave_chol<P>(sm.Qq, sm.L, sm.dead2, p);
+  wave_trinv<P>(sm.L, sm.Li, sm.dead2, p);
+  wave_mm<P, false, true>(sm.A, sm.Li, sm.W);   // Bm = A Li'
   for (int e = lane; e < P * P; e += 64) {
     const int a = e / P, c = e % P;
     small[e] = (a < p && c < p) ? sm.A[a * S + c] : 0.0;
-    small[P * P + e] = (a < p && c < p) ? sm.Bm[a * S + c] : 0.0;
+    small[P * P + e] = (a < p && c < p) ? sm.W[a * S + c] : 0.0;
   }
   for (int j = lane; j < P; j += 64) small[2 * P * P + P + j] = (j < p && sm.dead2[j]) ? 1.0 : 0.0;
 }
