@@ -59,6 +59,9 @@ SIGNATURES = [
     ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
     ("dfm_model_set_mode", C.c_int, [C.c_void_p, C.c_int]),
     ("dfm_chow_all", C.c_int, [C.c_void_p, C.c_int64, c_double_p, c_double_p, c_double_p]),
+    ("dfm_windows", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
+                              C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
+                              c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
     ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                     C.c_double, c_double_p, c_uint8_p]),

@@ -488,3 +488,41 @@ def targeted_predictors(y, w, x, thresholding: str = "hard", mode: str = "joint"
                                         xc.ctypes.data_as(_lib.c_double_p), T, N, T, m, cv,
                                         _lib.ptr(ts), mask.ctypes.data_as(_lib.c_uint8_p)))
     return (mask.astype(bool), ts) if return_tstats else mask.astype(bool)
+
+
+# ---------------------------------------------------------- expanding windows
+def pseudo_out_of_sample_refits(y, w, x, criterion: str = "ICp2", num_predictions: int = 200,
+                                kmax: Optional[int] = None, *, ctx: Optional[Context] = None):
+    """The refit loop of ``pseudo_out_of_sample_forecasts`` (``src/utils.jl:54-72``):
+    for date_index = T-P+1..T the IC-sweep constructor is refit on rows
+    1..date_index-1 (``:59-65``).  Returns a dict of per-window arrays
+    (window sizes, selected r, V(r), criterion value, eigenvalues, OLS
+    coefficients and HC2 t-stats)."""
+    ctx = ctx or default_context()
+    y = _f64(y).ravel()
+    w = _f64(w, 2)
+    x = _f64(x, 2)
+    T, N = x.shape
+    q, P = w.shape[1], int(num_predictions)
+    m = min(T - P, N)
+    km = int(kmax) if kmax else int(math.ceil(m / 2))
+    km = min(km, int(math.ceil(m / 2)))
+    r = np.zeros(P, dtype=np.int64)
+    V, cv = np.zeros(P), np.zeros(P)
+    ev = np.zeros((P, km))
+    coef, ts = np.zeros((P, q + km)), np.zeros((P, q + km))
+    xc, wc = _colmajor(x), _colmajor(w)
+    ctx.check(ctx.lib.dfm_windows(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T,
+                                  xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[criterion], km,
+                                  r.ctypes.data_as(_lib.c_int64_p), _lib.ptr(V), _lib.ptr(cv), _lib.ptr(ev),
+                                  _lib.ptr(coef), _lib.ptr(ts)))
+    return {"window_rows": np.arange(T - P, T), "number_of_factors": r, "V": V,
+            "criterion_value": cv, "eigenvalues": ev, "coefficients": coef, "t_stats": ts}
+
+
+def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions: int = 200):
+    """``src/utils.jl:54-72``.  The refits are built (pseudo_out_of_sample_refits);
+    the forecast step calls ``predict`` -> ``get_factors``, which reads the
+    non-existent field ``dfm.rotation`` (defect D4), so it is not reproduced."""
+    raise NotImplementedError("predict/get_factors is broken in the reference (defect D4); "
+                              "use pseudo_out_of_sample_refits for the refit loop")

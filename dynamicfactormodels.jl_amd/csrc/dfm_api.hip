@@ -35,7 +35,8 @@ __global__ void common_residual_kernel(const double *, int64_t, int, int, int, c
                                        const double *, double *, double *);
 __global__ void panel_row_ssq_kernel(const double *, int64_t, int, double *);
 __global__ void ordered_sum_kernel(const double *, int, double *);
-__global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, double *,
+__global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, const int *,
+                               const int *, double *,
                                double *, double *, double *, int *);
 struct StatDesc { int kind, arg0, arg1, off; };
 __global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *,
@@ -487,7 +488,7 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   CK(dalloc(&ost, 1));
   {
     Scope sc(ctx, DFM_KC_OLS);
-    hipLaunchKernelGGL(ols_hc2_kernel, dim3(1), dim3(256), 0, st, M->y, M->w, q, M->F, T, r, coef,
+    hipLaunchKernelGGL(ols_hc2_kernel, dim3(1), dim3(256), 0, st, M->y, M->w, q, M->F, T, r, nullptr, nullptr, coef,
                        tst, cov, res, ost);
   }
   CK(hipGetLastError());
@@ -745,7 +746,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     }
     {
       Scope sc(ctx, DFM_KC_OLS);
-      hipLaunchKernelGGL(ols_hc2_kernel, dim3(n), dim3(256), 0, st, M->y, M->w, q, w.F, T, r, w.coef,
+      hipLaunchKernelGGL(ols_hc2_kernel, dim3(n), dim3(256), 0, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
                          w.tstat, nullptr, nullptr, w.ost);
     }
     {
@@ -1000,3 +1001,151 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------- expanding windows
+// pseudo_out_of_sample_forecasts, refit part (src/utils.jl:54-72): for
+// date_index = T-P+1..T (1-based) the model is refit on rows 1..date_index-1,
+// i.e. window w = 0..P-1 uses the first n_w = T-P+w rows.  Every window is a
+// masked replicate of the full panel (idx = identity, eta_t = 1{t < n_w}):
+//  N > T : the window Gram is the leading n_w x n_w block of H = X X' (the
+//          prefix-Gram identity) -> ONE Gram for all windows,
+//          then the factored batched eigensolver (H . Z GEMMs);
+//  T >= N: per-window Grams X_w' X_w from the masked fused-gather Gram kernel.
+// Each window runs the IC sweep k = 1..kmax (the refit is the IC-sweep
+// constructor, :53-66), picks r_w, and fits OLS+HC2 on [w F_r] over its rows.
+__global__ void window_scale_kernel(const double *__restrict__ Uk, int T, int k, int Tfirst,
+                                    double *__restrict__ F) {
+  const int rep = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)T * k) return;
+  const int t = (int)(e / k), n = Tfirst + rep;
+  F[(int64_t)rep * T * k + e] = t < n ? sqrt((double)n) * Uk[(int64_t)rep * T * k + e] : 0.0;
+}
+
+extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                           const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
+                           int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
+                           double *coef_out, double *tstat_out) {
+  if (!ctx) return -1;
+  const int T = (int)T64, N = (int)N64;
+  if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
+      !r_out)
+    return fail(ctx, -2, "dfm_windows: bad arguments");
+  if (crit < 3 || crit > 6)
+    return fail(ctx, -31, "dfm_windows: criterion must be ICp1-3 or BIC (PCp needs each window's full spectrum)");
+  const int n0 = T - P;
+  const int orient = (N > T) ? 0 : 1;
+  if (orient == 1 && N > n0) return fail(ctx, -2, "dfm_windows: windows straddle the T >= N / N > T branches");
+  const int mmin = std::min(n0, N);
+  if (kmax <= 0) kmax = (mmin + 1) / 2;
+  kmax = std::min(kmax, (mmin + 1) / 2);
+  if (kmax > 24 || q + kmax > 32) return fail(ctx, -20, "dfm_windows: kmax %d unsupported (<= 24)", kmax);
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  DevPanel dp;
+  int rc = upload_panel(ctx, X, T, N, ldx, dp);
+  if (rc) return rc;
+  const int m = orient == 0 ? T : N;
+  const int p = eig_block_p(m, kmax, ctx->block);
+  if (p > 32) return fail(ctx, -20, "block too wide");
+  const int Pb = p <= 16 ? 16 : 32;
+  // host draws: identity + masks
+  std::vector<int32_t> hidx((size_t)P * T);
+  std::vector<double> heta((size_t)P * T);
+  std::vector<int> hTn(P), hkr(P);
+  for (int wi = 0; wi < P; ++wi)
+    for (int t = 0; t < T; ++t) { hidx[(size_t)wi * T + t] = t; heta[(size_t)wi * T + t] = t < n0 + wi ? 1.0 : 0.0; }
+  std::vector<void *> frees;
+  auto dal = [&](size_t bytes) -> void * { void *ptr = nullptr; if (hipMalloc(&ptr, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr; frees.push_back(ptr); return ptr; };
+  struct Freer { std::vector<void *> &v; ~Freer() { for (void *x : v) hipFree(x); } } freer{frees};
+  int32_t *didx = (int32_t *)dal(hidx.size() * 4);
+  double *deta = (double *)dal(heta.size() * 8);
+  double *dy = (double *)dal((size_t)T * 8), *dw = (double *)dal((size_t)T * std::max(q, 1) * 8);
+  double *lam = (double *)dal((size_t)P * kmax * 8), *Uk = (double *)dal((size_t)P * m * kmax * 8);
+  double *tr = (double *)dal((size_t)P * 8), *F = (double *)dal((size_t)P * T * kmax * 8);
+  double *coef = (double *)dal((size_t)P * (q + kmax) * 8), *tst = (double *)dal((size_t)P * (q + kmax) * 8);
+  int *stt = (int *)dal((size_t)P * 4), *ost = (int *)dal((size_t)P * 4);
+  int *dTn = (int *)dal((size_t)P * 4), *dkr = (int *)dal((size_t)P * 4);
+  char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
+  if (!didx || !deta || !dy || !dw || !lam || !Uk || !tr || !F || !coef || !tst || !stt || !ost || !dTn || !dkr || !ews)
+    return fail(ctx, 1002, "dfm_windows: out of device memory");
+  HIPCHK(ctx, hipMemcpyAsync(didx, hidx.data(), hidx.size() * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(deta, heta.data(), heta.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
+  if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  if (orient == 0) {
+    const int64_t ldH = round_up(T, 16);
+    double *H = (double *)dal((size_t)T * ldH * 8), *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
+    char *fws = (char *)dal(fact_workspace_bytes(T, P, Pb));
+    int *off = (int *)dal((size_t)P * (T + 1) * 4), *lst = (int *)dal((size_t)P * T * 4);
+    if (!H || !zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    HIPCHK(ctx, hipMemsetAsync(H, 0, (size_t)T * ldH * 8, st));
+    HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
+    PanelSrc es{nullptr, dp.P, nullptr, nullptr, dp.ld};
+    {
+      Scope sc(ctx, DFM_KC_GRAM);
+      HIPCHK(ctx, launch_gram(0, es, T, N, T, H, ldH, 0, 1, st));   // ONE Gram for every window
+    }
+    rc = fact_precompute(dp.P, dp.ld, T, N, 0, nullptr, nullptr, H, ldH, zero, zero, zero, hd, st);
+    if (rc) return fail(ctx, rc, "precompute");
+    HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
+    FactBase fb{T, 0, ldH, zero, zero, zero, H, zero, hd};
+    rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
+                          lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
+    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+    Scope sc(ctx, DFM_KC_FACTORS);
+    hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kmax + 255) / 256), P), dim3(256), 0, st,
+                       Uk, T, kmax, n0, F);
+  } else {
+    double *G = (double *)dal((size_t)P * N * N * 8), *Ld = (double *)dal((size_t)P * N * kmax * 8);
+    if (!G || !Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    PanelSrc src{nullptr, dp.P, didx, deta, dp.ld};
+    {
+      Scope sc(ctx, DFM_KC_GRAM);
+      HIPCHK(ctx, launch_gram(1, src, N, T, T, G, N, (int64_t)N * N, P, st));
+    }
+    rc = eig_run(G, N, (int64_t)N * N, N, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, lam, Uk,
+                 tr, stt, nullptr, st, timer_cb, ctx, 0);
+    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+    Scope sc(ctx, DFM_KC_FACTORS);
+    launch_factors(1, src, T, N, kmax, P, Uk, F, Ld, nullptr, st);
+  }
+  // IC sweep per window on the host (arithmetic only), then OLS with each r_w
+  std::vector<double> hl((size_t)P * kmax), ht(P);
+  std::vector<int> hs(P);
+  HIPCHK(ctx, hipMemcpyAsync(hl.data(), lam, hl.size() * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(ht.data(), tr, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs.data(), stt, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  for (int wi = 0; wi < P; ++wi)
+    if (hs[wi]) return fail(ctx, 2, "eigensolver did not converge for window %d", wi);
+  std::vector<double> ic(7 * (size_t)kmax);
+  for (int wi = 0; wi < P; ++wi) {
+    const int n = n0 + wi;
+    dfm_ic_sweep(&hl[(size_t)wi * kmax], kmax, kmax, ht[wi], n, N, NAN, ic.data());
+    int best = 0;
+    for (int k = 1; k < kmax; ++k)
+      if (ic[(size_t)crit * kmax + k] < ic[(size_t)crit * kmax + best]) best = k;
+    hTn[wi] = n;
+    hkr[wi] = best + 1;
+    r_out[wi] = best + 1;
+    if (crit_out) crit_out[wi] = ic[(size_t)crit * kmax + best];
+    if (V_out) {
+      double sacc = ht[wi];
+      for (int j = 0; j <= best; ++j) sacc -= hl[(size_t)wi * kmax + j];
+      V_out[wi] = sacc / ((double)N * n);
+    }
+  }
+  if (eig_out) std::copy(hl.begin(), hl.end(), eig_out);
+  HIPCHK(ctx, hipMemcpyAsync(dTn, hTn.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(dkr, hkr.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
+  {
+    Scope sc(ctx, DFM_KC_OLS);
+    hipLaunchKernelGGL(ols_hc2_kernel, dim3(P), dim3(256), 0, st, dy, dw, q, F, T, kmax, dTn, dkr, coef, tst,
+                       nullptr, nullptr, ost);
+  }
+  if (coef_out) HIPCHK(ctx, hipMemcpyAsync(coef_out, coef, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
+  if (tstat_out) HIPCHK(ctx, hipMemcpyAsync(tstat_out, tst, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}

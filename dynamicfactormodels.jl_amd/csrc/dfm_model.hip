@@ -199,9 +199,14 @@ __global__ void ordered_sum_kernel(const double *__restrict__ v, int n, double *
 // One 256-thread workgroup per replicate; d = q + k <= 32.
 constexpr int OLS_DMAX = 32;
 constexpr int OLS_TR = 128;
+// Per-replicate sample sizes Tn[rep] (rows 0..Tn-1 used) and factor counts
+// kr[rep] <= kF are optional (expanding windows, src/utils.jl:59-65); F rows
+// have stride kF, coefficient rows stride q + kF (unused tail = NaN).
 __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__ y,
                                                       const double *__restrict__ w, int q,
-                                                      const double *__restrict__ F, int T, int k,
+                                                      const double *__restrict__ F, int Tphys, int kF,
+                                                      const int *__restrict__ Tn,
+                                                      const int *__restrict__ kr,
                                                       double *__restrict__ coef,
                                                       double *__restrict__ tstat,
                                                       double *__restrict__ cov_out,
@@ -215,13 +220,15 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__
   __shared__ double sb[OLS_DMAX], sDy[OLS_DMAX];
   __shared__ int sbad;
   const int tid = threadIdx.x, rep = blockIdx.x;
-  const int d = q + k;
-  const double *Fr = F + (int64_t)rep * T * k;
+  const int T = Tn ? Tn[rep] : Tphys;
+  const int k = kr ? kr[rep] : kF;
+  const int d = q + k, dstr = q + kF;
+  const double *Fr = F + (int64_t)rep * Tphys * kF;
   auto stage = [&](int t0) {
     for (int e = tid; e < OLS_TR * d; e += 256) {
       const int r = e / d, c = e % d, t = t0 + r;
       double v = 0.0;
-      if (t < T) v = c < q ? w[(int64_t)c * T + t] : Fr[(int64_t)t * k + (c - q)];
+      if (t < T) v = c < q ? w[(int64_t)c * Tphys + t] : Fr[(int64_t)t * kF + (c - q)];
       sD[r * S + c] = v;
     }
     for (int r = tid; r < OLS_TR; r += 256) sy[r] = (t0 + r < T) ? y[t0 + r] : 0.0;
@@ -348,9 +355,9 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__
     M[a * S + c] = s;   // coefficient covariance
   }
   __syncthreads();
-  if (tid < d) {
-    coef[(int64_t)rep * d + tid] = sb[tid];
-    tstat[(int64_t)rep * d + tid] = sb[tid] / sqrt(M[tid * S + tid]);
+  if (tid < dstr) {
+    coef[(int64_t)rep * dstr + tid] = tid < d ? sb[tid] : NAN;
+    tstat[(int64_t)rep * dstr + tid] = tid < d ? sb[tid] / sqrt(M[tid * S + tid]) : NAN;
   }
   if (cov_out)
     for (int e = tid; e < d * d; e += 256) cov_out[(int64_t)rep * d * d + (e % d) * d + e / d] = M[(e / d) * S + e % d];

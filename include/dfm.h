@@ -160,6 +160,20 @@ int dfm_model_set_mode(dfm_model *m, int mode);
  * Any output pointer may be NULL. */
 int dfm_chow_all(dfm_model *m, int64_t bp, double *LR, double *LM, double *Wald);
 
+/* ---------------------------------------------------- expanding windows
+ * The refits of pseudo_out_of_sample_forecasts (src/utils.jl:54-72): window
+ * w = 0..P-1 refits the IC-sweep constructor (src/DynamicFactorModel.jl:53)
+ * on rows 0..T-P+w-1 with criterion crit (ICp1-3 or BIC) over k = 1..kmax.
+ * N > T uses the prefix-Gram identity (one Gram for all windows).
+ * Outputs per window: r (P), V(r) (P), criterion value (P), eigenvalues
+ * (P x kmax, row-major), OLS coefficients and HC2 t-stats (P x (q + kmax),
+ * row-major, NaN past q + r).  The forecast step itself is not built: the
+ * reference's predict/get_factors read a non-existent field (defect D4). */
+int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                const double *X, int64_t T, int64_t N, int64_t ldx, int P, int crit,
+                int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
+                double *coef_out, double *tstat_out);
+
 /* --------------------------------------------------- targeted predictors
  * targeted_predictors(..., thresholding="hard") (src/targeted_predictors.jl:9-30).
  * JOINT: OLS of y on [w x], White HC0, |t_x| > crit_value (the reference's

@@ -335,6 +335,25 @@ def test_direct_and_factored_agree(dfm, oracle):
     assert rel(b[:, 4:], a[:, 4:]) < 1e-9
 
 
+@pytest.mark.parametrize("T,N,P,crit", [(60, 150, 6, "ICp2"), (90, 30, 5, "BIC"), (41, 300, 3, "ICp1")])
+def test_expanding_window_refits(dfm, oracle, T, N, P, crit):
+    """src/utils.jl:54-72 refit loop: each window = IC-sweep constructor on rows
+    1..date_index-1 (N > T via the prefix-Gram identity)."""
+    y, x, w = panel(oracle, T, N, 3, 3000 + T)
+    kmax = 6
+    out = dfm.pseudo_out_of_sample_refits(y, w, x, crit, num_predictions=P, kmax=kmax)
+    fits = oracle.expanding_window_refits(y, w, x, P, lambda yy, ww, xx: oracle.DynamicFactorModel_ic(
+        yy, ww, xx, crit, kmax=kmax))
+    for j, o in enumerate(fits):
+        assert out["number_of_factors"][j] == o.number_of_factors
+        assert abs(out["criterion_value"][j] - o.number_of_factors_criterion_value) <= \
+            STAT_RTOL * abs(o.number_of_factors_criterion_value)
+        assert abs(out["V"][j] - oracle.factor_residual_variance(o)) <= STAT_RTOL * oracle.factor_residual_variance(o)
+        r = o.number_of_factors
+        assert rel(out["eigenvalues"][j][:r], o.eigenvalues[0][:r]) < STAT_RTOL
+        assert rel(out["t_stats"][j][:1], o.t_stats[:1]) < 1e-9       # intercept: sign-invariant
+
+
 def test_errors_are_reported(dfm, oracle):
     y, x, w = panel(oracle, 50, 20, 2, 21)
     g = dfm.DynamicFactorModel(y, w, x, 2, "PCp2")
