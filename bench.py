@@ -145,6 +145,7 @@ def main():
     el = time.perf_counter() - t0
     ctx.enable_timing(False)
     timing = ctx.read_timing()
+    eig = ctx.eig_stats()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -193,6 +194,7 @@ def main():
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
         "outputs_finite": ok,
         "mode": args.mode,
+        "eig_iterations": eig,
         "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -35,6 +35,7 @@ SIGNATURES = [
     ("dfm_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("dfm_ctx_read_timing", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int]),
     ("dfm_ctx_reset_timing", C.c_int, [C.c_void_p]),
+    ("dfm_ctx_eig_stats", C.c_int, [C.c_void_p, c_int64_p, c_int64_p, c_int64_p]),
     ("dfm_kernel_class_name", C.c_char_p, [C.c_int]),
     ("dfm_pca", C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                           c_double_p, c_double_p, c_double_p, c_double_p]),

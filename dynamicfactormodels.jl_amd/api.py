@@ -82,6 +82,11 @@ class Context:
     def reset_timing(self):
         self.check(self.lib.dfm_ctx_reset_timing(self.h))
 
+    def eig_stats(self):
+        b, t, m = C.c_int64(), C.c_int64(), C.c_int64()
+        self.check(self.lib.dfm_ctx_eig_stats(self.h, C.byref(b), C.byref(t), C.byref(m)))
+        return {"batches": b.value, "iterations": t.value, "max_iterations": m.value}
+
     def close(self):
         if getattr(self, "h", None) and not _lib.shutting_down():
             self.lib.dfm_ctx_destroy(self.h)

@@ -21,6 +21,7 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
             timer_fn tf, void *tctx, int64_t rep0);
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
+extern int g_last_iters;
 int spectrum_max();
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
                            hipStream_t st);
@@ -89,6 +90,7 @@ struct dfm_ctx {
   hipEvent_t cur_a[DFM_KC_COUNT] = {};
   double ms[DFM_KC_COUNT] = {};
   int64_t launches[DFM_KC_COUNT] = {};
+  int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0;
 };
 
 struct dfm_model {
@@ -244,7 +246,20 @@ int dfm_ctx_reset_timing(dfm_ctx *ctx) {
   if (!ctx) return -1;
   harvest(ctx);
   for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
+  ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = 0;
   return 0;
+}
+int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max) {
+  if (!ctx) return -1;
+  if (batches) *batches = ctx->eig_batches;
+  if (iters_total) *iters_total = ctx->eig_iters;
+  if (iters_max) *iters_max = ctx->eig_iters_max;
+  return 0;
+}
+static void note_iters(dfm_ctx *ctx) {
+  ctx->eig_batches++;
+  ctx->eig_iters += g_last_iters;
+  ctx->eig_iters_max = std::max<int64_t>(ctx->eig_iters_max, g_last_iters);
 }
 const char *dfm_kernel_class_name(int cls) {
   return (cls >= 0 && cls < DFM_KC_COUNT) ? kclass_names[cls] : "?";
@@ -730,6 +745,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);
       rc = fact_loadings(fb, M->Ep, M->ld, N, M->L, w.Uk, et, w.off, w.lst, n, w.F, w.L, w.fload, st);
       if (rc) return fail(ctx, rc, "factored loadings failed");
@@ -741,6 +757,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
                        w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);
       launch_factors(M->orient, src, T, N, r, n, w.Uk, w.F, w.L, nullptr, st);
     }

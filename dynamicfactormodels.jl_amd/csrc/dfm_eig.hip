@@ -509,6 +509,7 @@ size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit) {
 }
 
 typedef void (*timer_fn)(void *ctx, int cls, int begin);
+int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
 
 // Solve nb problems.  Returns 0 ok, 1 not converged (status per replicate),
 // negative on bad args, or a hipError_t (>1000).
@@ -555,6 +556,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     }
   }
   (void)finished;
+  g_last_iters = it;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -642,39 +644,47 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   if (tid == 0) trace[rep] = red[0];
 }
 
-// Z = P' D Q into the GEMM operand Zc[s][rep*P + c]; a = F'Q, cc = EL' Z
-// (r x P each) into ab[rep][2][r][P].
+// Z = P' D Q into the GEMM operand Zc[s][rep*P + c] for the 64 rows s of this
+// block, plus the block's partial a = F'Q (rows t of the block) and
+// cc = EL'Z (rows s of the block) into abp[rep][rb][2][r][P].
 template <int P>
 __global__ __launch_bounds__(256) void boot_fz_kernel(FactBase fb, EigWork w, int m, const double *__restrict__ eta,
                                                       const int *__restrict__ off, const int *__restrict__ lst,
                                                       double *__restrict__ Zc, int64_t ldz,
-                                                      double *__restrict__ ab) {
-  const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
+                                                      double *__restrict__ abp) {
+  constexpr int RM = 32;
+  __shared__ double sZ[EROWS * P], sQ[EROWS * P];
+  const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, T = fb.T, r = fb.r;
   if (w.done[rep]) return;
   const double *Q = w.Q + (int64_t)rep * m * P;
   const double *et = eta ? eta + (int64_t)rep * T : nullptr;
   const int *o = off + (int64_t)rep * (T + 1);
   const int *L = lst + (int64_t)rep * T;
-  for (int e = tid; e < T * P; e += 256) {
-    const int sI = e / P, c = e % P;
-    double z = 0.0;
-    for (int q = o[sI]; q < o[sI + 1]; ++q) {
-      const int t = L[q];
-      z = fma(et ? et[t] : 1.0, Q[(int64_t)t * P + c], z);
+  const int s0 = rb * EROWS;
+  for (int e = tid; e < EROWS * P; e += 256) {
+    const int ls = e / P, c = e % P, sI = s0 + ls;
+    double z = 0.0, qv = 0.0;
+    if (sI < T) {
+      for (int q = o[sI]; q < o[sI + 1]; ++q) {
+        const int t = L[q];
+        z = fma(et ? et[t] : 1.0, Q[(int64_t)t * P + c], z);
+      }
+      Zc[(int64_t)sI * ldz + (int64_t)rep * P + c] = z;
+      qv = Q[(int64_t)sI * P + c];
     }
-    Zc[(int64_t)sI * ldz + (int64_t)rep * P + c] = z;
+    sZ[e] = z;
+    sQ[e] = qv;
   }
   __syncthreads();
-  double *abr = ab + (int64_t)rep * 2 * r * P;
+  double *pp = abp + ((int64_t)rep * nrb + rb) * 2 * RM * P;
+  const int rows = min(EROWS, T - s0);
   for (int e = tid; e < 2 * r * P; e += 256) {
     const int which = e / (r * P), j = (e / P) % r, c = e % P;
-    double sacc = 0.0;
-    if (which == 0)
-      for (int t = 0; t < T; ++t) sacc = fma(fb.F[(int64_t)t * r + j], Q[(int64_t)t * P + c], sacc);
-    else
-      for (int t = 0; t < T; ++t)
-        sacc = fma(fb.EL[(int64_t)t * r + j], Zc[(int64_t)t * ldz + (int64_t)rep * P + c], sacc);
-    abr[e] = sacc;
+    const double *X = which ? sZ : sQ;
+    const double *B = which ? fb.EL : fb.F;
+    double acc = 0.0;
+    for (int ls = 0; ls < rows; ++ls) acc = fma(B[(int64_t)(s0 + ls) * r + j], X[ls * P + c], acc);
+    pp[e] = acc;
   }
 }
 
@@ -690,20 +700,25 @@ __global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, in
   constexpr int RM = 32;
   __shared__ __attribute__((aligned(16))) double sQ[EROWS * SQ];
   __shared__ __attribute__((aligned(16))) double sY[EROWS * SQ];
-  __shared__ double sA[RM * P], sB[RM * P];
+  __shared__ double sA[RM * P], sB[RM * P], sC[RM * P];
   __shared__ int s_skip;
   const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, r = fb.r;
   double *small = w.small + (int64_t)rep * small_stride<P>();
   if (tid == 0) s_skip = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only);
   __syncthreads();
   if (s_skip) return;
-  const double *abr = ab + (int64_t)rep * 2 * r * P;
-  // sA = a, sB = S a + cc
+  // a and cc: fixed-order sums of the row-block partials of boot_fz; sB = S a + cc
+  const double *abp = ab + (int64_t)rep * nrb * 2 * RM * P;
+  for (int e = tid; e < 2 * r * P; e += 256) {
+    double acc = 0.0;
+    for (int q = 0; q < nrb; ++q) acc += abp[(int64_t)q * 2 * RM * P + e];
+    (e < r * P ? sA[e] : sC[e - r * P]) = acc;
+  }
+  __syncthreads();
   for (int e = tid; e < r * P; e += 256) {
     const int j = e / P, c = e % P;
-    double v = abr[r * P + e];
-    for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], abr[i * P + c], v);
-    sA[e] = abr[e];
+    double v = sC[e];
+    for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], sA[i * P + c], v);
     sB[e] = v;
   }
   __syncthreads();
@@ -734,11 +749,13 @@ __global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, in
 }
 
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
-                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st);
+                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
+                       const int *col_done = nullptr, int col_group = 1);
 
 size_t fact_workspace_bytes(int T, int nb, int P) {
   const int64_t ldz = (int64_t)nb * P;
-  return 2 * (size_t)T * ldz * 8 + (size_t)nb * 2 * 32 * P * 8 + (size_t)nb * (2 * T + 1) * 4 + 4096;
+  const int nrb = (T + EROWS - 1) / EROWS;
+  return 2 * (size_t)T * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096;
 }
 
 template <int P>
@@ -769,10 +786,10 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     const int check_only = (it == maxit);
     if (!check_only) {
       if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-      hipLaunchKernelGGL(boot_fz_kernel<P>, dim3(nb), dim3(256), 0, st, fb, w, m, eta, off, lst, Zc, ldz, ab);
+      hipLaunchKernelGGL(boot_fz_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, fb, w, m, eta, off, lst, Zc, ldz, ab);
       if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
       if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st);
+      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
       if (tf) tf(tctx, DFM_KC_GEMM, 0);
       if (e != hipSuccess) return 1000 + (int)e;
     }
@@ -792,8 +809,9 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
       hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
       hipError_t e = hipStreamSynchronize(st);
       if (e != hipSuccess) return 1000 + (int)e;
-      if (a == 0) break;
+      if (a == 0) { g_last_iters = it; break; }
     }
+    g_last_iters = it;
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);

@@ -26,7 +26,8 @@ template <bool A_TRANS>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__ A, int64_t lda,
                                                       const double *__restrict__ B, int64_t ldb,
                                                       double *__restrict__ C, int64_t ldc, int M,
-                                                      int Nc, int K, int nrb, int ncb) {
+                                                      int Nc, int K, int nrb, int ncb,
+                                                      const int *__restrict__ col_done, int col_group) {
   __shared__ __attribute__((aligned(16))) double lds[2][2][GT * KS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -35,6 +36,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__
   const int rb = j % nrb, cb = (j / nrb) * 8 + xcd;
   if (cb >= ncb) return;
   const int abase = rb * GT, bbase = cb * GT;
+  if (col_done) {   // skip column blocks whose replicates have all converged
+    bool all = true;
+    const int r0 = bbase / col_group, r1 = min(Nc - 1, bbase + GT - 1) / col_group;
+    for (int q = r0; q <= r1; ++q) all = all && col_done[q];
+    if (all) return;
+  }
 
   double2 ra[2], rbv[2];
   bool oka[2], okb[2];
@@ -115,14 +122,17 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__
 // Requirements: lda, ldb even (16-B aligned pairs); B/A padding beyond the
 // logical size is never read (masked).
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
-                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st) {
+                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
+                       const int *col_done = nullptr, int col_group = 1) {
   const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
   if (a_trans)
-    hipLaunchKernelGGL(gemm_kernel<true>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb);
+    hipLaunchKernelGGL(gemm_kernel<true>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
+                       col_done, col_group);
   else
-    hipLaunchKernelGGL(gemm_kernel<false>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb);
+    hipLaunchKernelGGL(gemm_kernel<false>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
+                       col_done, col_group);
   return hipGetLastError();
 }
 

@@ -78,6 +78,9 @@ int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable);
  * returns the number of classes written into ms_out/launches_out. */
 int dfm_ctx_read_timing(dfm_ctx *ctx, double *ms_out, int64_t *launches_out, int cap);
 int dfm_ctx_reset_timing(dfm_ctx *ctx);
+/* Eigensolver statistics since the last reset: batches solved, total and
+ * maximum subspace iterations per batch. */
+int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max);
 const char *dfm_kernel_class_name(int cls);
 
 /* ------------------------------------------------ principal components
