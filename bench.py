@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="replicates per device batch (0 = auto)")
     ap.add_argument("--replicates", type=int, default=B)
     ap.add_argument("--mode", default="auto", choices=["auto", "direct", "factored"])
+    ap.add_argument("--eig-tol", type=float, default=-1.0, help="eigensolver gap tolerance (default 1e-12)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -94,6 +95,8 @@ def main():
     import dfm_pkg
     D = dfm_pkg.load()
     ctx = D.Context(local)
+    if args.eig_tol > 0:
+        ctx.set_eig_params(tol=args.eig_tol)
     Bn = args.replicates
 
     # ---- base model (identical on every rank), resident in HBM

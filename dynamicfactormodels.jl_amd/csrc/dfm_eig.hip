@@ -18,6 +18,8 @@
 // Deterministic: fixed-order reductions only, no float atomics.
 #include "dfm_common.h"
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace dfm {
@@ -61,10 +63,13 @@ __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int6
 
 // Convergence test of iteration it-1's Ritz pairs (explicit residual partials
 // written by eig_apply).  Every workgroup of a replicate evaluates it on the
-// same data (so they agree); row block 0 records the verdict.
+// same data (so they agree); row block 0 records the verdict.  Called by one
+// whole wave: lane (j, r) loads one partial, the sum over r is a fixed-order
+// shuffle tree — no serial chain of dependent global loads.
 template <int P>
 DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb, int k, int p,
                             double tol, int it, int check_only) {
+  const int lane = threadIdx.x & 63;
   int d = w.done[rep];
   if (!d && it > 0) {
     // Converged when every wanted Ritz pair j < k satisfies
@@ -76,23 +81,36 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
     double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
     const double th0 = fabs(th[0]);
     bool ok = true;
-    for (int j = 0; j < k; ++j) {
-      double s = 0.0;
-      for (int r = 0; r < nrb; ++r) s += w.rpart[((int64_t)rep * nrb + r) * P + j];
-      const double res = sqrt(s);
-      double gap = INFINITY;
-      if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
-      if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
-      const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
-      if (!(res <= tol * gap || res <= 2e-14 * th0 || stagn)) ok = false;
-      if (rb == 0) next[j] = res;
+    for (int j0 = 0; j0 < k; j0 += 64) {
+      // lanes: j = j0 + lane / G, r = lane % G   with G = power of two >= nrb
+      int G = 1;
+      while (G < nrb) G <<= 1;
+      const int per = 64 / G;   // residual columns handled per pass
+      for (int jj = 0; jj < 64 && j0 + jj < k; jj += per) {
+        const int j = j0 + jj + lane / G, r = lane % G;
+        double v = 0.0;
+        if (j < k && r < nrb) v = w.rpart[((int64_t)rep * nrb + r) * P + j];
+        for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        // lanes with r == 0 hold the column sums
+        bool okj = true;
+        if (j < k && r == 0) {
+          const double res = sqrt(v);
+          double gap = INFINITY;
+          if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+          if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+          const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
+          okj = (res <= tol * gap || res <= 2e-14 * th0 || stagn);
+          if (rb == 0) next[j] = res;
+        }
+        ok = ok && !__any(!okj);
+      }
     }
     if (ok) {
       d = 1;
-      if (rb == 0) { w.done[rep] = 1; w.iters[rep] = it; }
+      if (rb == 0 && lane == 0) { w.done[rep] = 1; w.iters[rep] = it; }
     }
   }
-  if (rb == 0 && !d) atomicAdd(&w.active[it], 1);
+  if (rb == 0 && lane == 0 && !d) atomicAdd(&w.active[it], 1);
   return d || check_only;
 }
 
@@ -121,7 +139,7 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x;
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  if (tid == 0) s_skip = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only);
+  if (tid < 64) { const int d = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only); if (tid == 0) s_skip = d; }
   __syncthreads();
   if (s_skip) return;
 
@@ -284,12 +302,25 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   if (w.done[rep]) return;
   // 1. sum partials in fixed order (entries >= p are zero: Q columns >= p are zero)
   const double *pp = w.part + (int64_t)rep * nrb * 3 * P * P;
-  for (int e = lane; e < 3 * P * P; e += 64) {
-    double sacc = 0.0;
-    for (int r = 0; r < nrb; ++r) sacc += pp[(int64_t)r * 3 * P * P + e];
-    const int which = e / (P * P), a = (e / P) % P, c = e % P;
-    double *M = which == 0 ? sm.Hq : (which == 1 ? sm.Yq : sm.Qq);
-    M[a * S + c] = sacc;
+  constexpr int PER = 3 * P * P / 64;   // entries per lane (12 for P = 16)
+  {
+    double acc[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc[u] = 0.0;
+    for (int r = 0; r < nrb; ++r) {   // all PER loads of a block issue together
+      double v[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) v[u] = pp[(int64_t)r * 3 * P * P + lane + 64 * u];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) acc[u] += v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = lane + 64 * u;
+      const int which = e / (P * P), a = (e / P) % P, c = e % P;
+      double *M = which == 0 ? sm.Hq : (which == 1 ? sm.Yq : sm.Qq);
+      M[a * S + c] = acc[u];
+    }
   }
   __syncthreads();
   wave_sym<P>(sm.Hq);
@@ -704,7 +735,7 @@ __global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, in
   __shared__ int s_skip;
   const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, r = fb.r;
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  if (tid == 0) s_skip = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only);
+  if (tid < 64) { const int d = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only); if (tid == 0) s_skip = d; }
   __syncthreads();
   if (s_skip) return;
   // a and cc: fixed-order sums of the row-block partials of boot_fz; sB = S a + cc
@@ -804,6 +835,23 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+    static const bool trace_on = getenv("DFM_EIG_TRACE") != nullptr;
+    if (trace_on) {   // debug: residual trajectory of replicate 0, active count
+      std::vector<double> rp((size_t)nrb * P), th(P);
+      int act = -1;
+      hipMemcpyAsync(&act, w.active + it, 4, hipMemcpyDeviceToHost, st);
+      hipMemcpyAsync(rp.data(), w.rpart, rp.size() * 8, hipMemcpyDeviceToHost, st);
+      hipMemcpyAsync(th.data(), w.small + 2 * P * P, P * 8, hipMemcpyDeviceToHost, st);
+      hipStreamSynchronize(st);
+      fprintf(stderr, "it %2d act %4d:", it, act);
+      for (int j = 0; j < k; ++j) {
+        double sacc = 0; for (int r = 0; r < nrb; ++r) sacc += rp[(size_t)r * P + j];
+        fprintf(stderr, " %.1e", sqrt(sacc) / fabs(th[0]));
+      }
+      fprintf(stderr, "  th:");
+      for (int j = 0; j < p && j < 12; ++j) fprintf(stderr, " %.6g", th[j]);
+      fprintf(stderr, "\n");
+    }
     if (it > 0 && (it % poll) == 0) {
       int a = -1;
       hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);

@@ -17,10 +17,89 @@
 namespace dfm {
 
 namespace {
-constexpr int GT = 64, KS = 16;
-DFM_DEV int off_rows(int a, int kc) { return a * KS + (kc ^ (((a >> 1) & 1) << 3)); }  // [a][k]
-DFM_DEV int off_cols(int a, int kc) { return kc * GT + (a ^ ((kc & 7) << 2)); }         // [k][a]
+// 32-deep stages: two MFMA k-steps (128 MFMA per wave) between barriers.
+// [a][k] image: 256-B rows, k XOR-swizzled by 8*(a&3) -> the 4x4x4 A/B
+// fragment reads (lanes: 4 rows x 8 k per half-wave) hit 32 distinct bank
+// pairs, and the 16-B staging writes stay conflict-free.
+// [k][a] image: 512-B rows, a XOR-swizzled by 4*(k&7) (as in dfm_gram.hip).
+constexpr int GT = 64, KS = 32;
+DFM_DEV int off_rows(int a, int kc) { return a * KS + (kc ^ ((a & 3) << 3)); }  // [a][k]
+DFM_DEV int off_cols(int a, int kc) { return kc * GT + (a ^ ((kc & 7) << 2)); }  // [k][a]
 }  // namespace
+
+// One stage of staging registers (4 A chunks + 4 B chunks of 16 B per
+// thread) kept as a plain struct of scalars: no lambdas capturing arrays by
+// reference and no conditional loads, both of which make the compiler route
+// the staging through scratch and wait on every load.
+struct Stage {
+  double2 a0, a1, a2, a3, b0, b1, b2, b3;
+  unsigned ok;
+};
+
+template <bool A_TRANS>
+DFM_DEV void stage_offsets(int h, int tid, int k0, int abase, int bbase, int M, int Nc, int K, int64_t lda,
+                           int64_t ldb, int64_t &offa, int64_t &offb, unsigned &ok) {
+  bool oka;
+  if constexpr (!A_TRANS) {   // A rows: chunk -> (row a = tid>>4 + 16h, k pair 2*(tid&15))
+    const int a = abase + (tid >> 4) + 16 * h, k = k0 + 2 * (tid & 15);
+    oka = (a < M) && (k < K);
+    offa = oka ? (int64_t)a * lda + k : 0;
+  } else {                    // A^T: k-rows of A (contiguous in a)
+    const int kc = k0 + (tid >> 5) + 8 * h, a = abase + 2 * (tid & 31);
+    oka = (kc < K) && (a < M);
+    offa = oka ? (int64_t)kc * lda + a : 0;
+  }
+  const int kb = k0 + (tid >> 5) + 8 * h, col = bbase + 2 * (tid & 31);
+  const bool okb = (kb < K) && (col < Nc);
+  offb = okb ? (int64_t)kb * ldb + col : 0;
+  ok |= ((oka ? 1u : 0u) << h) | ((okb ? 16u : 0u) << h);
+}
+
+template <bool A_TRANS>
+DFM_DEV void load_stage(Stage &sg, const double *__restrict__ A, const double *__restrict__ B, int tid,
+                        int k0, int abase, int bbase, int M, int Nc, int K, int64_t lda, int64_t ldb) {
+  int64_t oa0, oa1, oa2, oa3, ob0, ob1, ob2, ob3;
+  unsigned ok = 0;
+  stage_offsets<A_TRANS>(0, tid, k0, abase, bbase, M, Nc, K, lda, ldb, oa0, ob0, ok);
+  stage_offsets<A_TRANS>(1, tid, k0, abase, bbase, M, Nc, K, lda, ldb, oa1, ob1, ok);
+  stage_offsets<A_TRANS>(2, tid, k0, abase, bbase, M, Nc, K, lda, ldb, oa2, ob2, ok);
+  stage_offsets<A_TRANS>(3, tid, k0, abase, bbase, M, Nc, K, lda, ldb, oa3, ob3, ok);
+  sg.a0 = *reinterpret_cast<const double2 *>(A + oa0);
+  sg.a1 = *reinterpret_cast<const double2 *>(A + oa1);
+  sg.a2 = *reinterpret_cast<const double2 *>(A + oa2);
+  sg.a3 = *reinterpret_cast<const double2 *>(A + oa3);
+  sg.b0 = *reinterpret_cast<const double2 *>(B + ob0);
+  sg.b1 = *reinterpret_cast<const double2 *>(B + ob1);
+  sg.b2 = *reinterpret_cast<const double2 *>(B + ob2);
+  sg.b3 = *reinterpret_cast<const double2 *>(B + ob3);
+  sg.ok = ok;
+}
+
+template <bool A_TRANS>
+DFM_DEV void store_one(double *la, double *lb, int h, int tid, const double2 &va, const double2 &vb,
+                       unsigned ok) {
+  // component-wise selects: a select of whole double2 values is lowered
+  // through a dynamically indexed stack slot (scratch)
+  int oa;
+  if constexpr (!A_TRANS) oa = off_rows((tid >> 4) + 16 * h, 2 * (tid & 15));
+  else oa = off_cols(2 * (tid & 31), (tid >> 5) + 8 * h);
+  const bool ka = (ok >> h) & 1u, kb = (ok >> (4 + h)) & 1u;
+  double2 wa, wb;
+  wa.x = ka ? va.x : 0.0;
+  wa.y = ka ? va.y : 0.0;
+  wb.x = kb ? vb.x : 0.0;
+  wb.y = kb ? vb.y : 0.0;
+  *reinterpret_cast<double2 *>(la + oa) = wa;
+  *reinterpret_cast<double2 *>(lb + off_cols(2 * (tid & 31), (tid >> 5) + 8 * h)) = wb;
+}
+
+template <bool A_TRANS>
+DFM_DEV void store_stage(const Stage &sg, double *la, double *lb, int tid) {
+  store_one<A_TRANS>(la, lb, 0, tid, sg.a0, sg.b0, sg.ok);
+  store_one<A_TRANS>(la, lb, 1, tid, sg.a1, sg.b1, sg.ok);
+  store_one<A_TRANS>(la, lb, 2, tid, sg.a2, sg.b2, sg.ok);
+  store_one<A_TRANS>(la, lb, 3, tid, sg.a3, sg.b3, sg.ok);
+}
 
 template <bool A_TRANS>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__ A, int64_t lda,
@@ -43,38 +122,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__
     if (all) return;
   }
 
-  double2 ra[2], rbv[2];
-  bool oka[2], okb[2];
-  auto load_stage = [&](int k0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if constexpr (!A_TRANS) {   // A rows: chunk -> (row a = c>>3, k pair 2*(c&7))
-        const int a = (tid >> 3) + 32 * h, k = k0 + 2 * (tid & 7);
-        oka[h] = (abase + a < M) && (k < K);
-        if (oka[h]) ra[h] = *reinterpret_cast<const double2 *>(A + (int64_t)(abase + a) * lda + k);
-      } else {                    // A^T: k-rows of A (contiguous in a)
-        const int kc = (tid >> 5) + 8 * h, a = 2 * (tid & 31);
-        oka[h] = (k0 + kc < K) && (abase + a < M);
-        if (oka[h]) ra[h] = *reinterpret_cast<const double2 *>(A + (int64_t)(k0 + kc) * lda + abase + a);
-      }
-      const int kc = (tid >> 5) + 8 * h, col = 2 * (tid & 31);
-      okb[h] = (k0 + kc < K) && (bbase + col < Nc);
-      if (okb[h]) rbv[h] = *reinterpret_cast<const double2 *>(B + (int64_t)(k0 + kc) * ldb + bbase + col);
-    }
-  };
-  auto store_stage = [&](int buf) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const double2 z = {0.0, 0.0};
-      int oa;
-      if constexpr (!A_TRANS) oa = off_rows((tid >> 3) + 32 * h, 2 * (tid & 7));
-      else oa = off_cols(2 * (tid & 31), (tid >> 5) + 8 * h);
-      *reinterpret_cast<double2 *>(&lds[buf][0][oa]) = oka[h] ? ra[h] : z;
-      *reinterpret_cast<double2 *>(&lds[buf][1][off_cols(2 * (tid & 31), (tid >> 5) + 8 * h)]) =
-          okb[h] ? rbv[h] : z;
-    }
-  };
-
   double acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -82,24 +129,29 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__
     for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int nst = (K + KS - 1) / KS;
-  load_stage(0);
-  store_stage(0);
+  Stage sg;
+  load_stage<A_TRANS>(sg, A, B, tid, 0, abase, bbase, M, Nc, K, lda, ldb);
+  store_stage<A_TRANS>(sg, lds[0][0], lds[0][1], tid);
   __syncthreads();
   for (int s = 0; s < nst; ++s) {
     const int buf = s & 1;
-    if (s + 1 < nst) load_stage((s + 1) * KS);
-    double af[8], bf[8];
+    if (s + 1 < nst) load_stage<A_TRANS>(sg, A, B, tid, (s + 1) * KS, abase, bbase, M, Nc, K, lda, ldb);
 #pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      const int a = wr * 32 + 4 * f + fi;
-      af[f] = A_TRANS ? lds[buf][0][off_cols(a, fkc)] : lds[buf][0][off_rows(a, fkc)];
-      bf[f] = lds[buf][1][off_cols(wc * 32 + 4 * f + fi, fkc)];
+    for (int sub = 0; sub < KS / 16; ++sub) {
+      const int kc = 16 * sub + fkc;
+      double af[8], bf[8];
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const int a = wr * 32 + 4 * f + fi;
+        af[f] = A_TRANS ? lds[buf][0][off_cols(a, kc)] : lds[buf][0][off_rows(a, kc)];
+        bf[f] = lds[buf][1][off_cols(wc * 32 + 4 * f + fi, kc)];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
-    if (s + 1 < nst) store_stage(buf ^ 1);
+    if (s + 1 < nst) store_stage<A_TRANS>(sg, lds[buf ^ 1][0], lds[buf ^ 1][1], tid);
     __syncthreads();
   }
   const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
