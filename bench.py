@@ -63,9 +63,17 @@ def cpu_baseline(seconds: float = 15.0):
                       f"in {el:.1f} s, oracle/dfm_oracle.py serial loop over OpenBLAS"}
 
 
-def model_batch(Bn, T):
-    """The engine's auto batch (dfm_bootstrap_dev): floor(1.5e9 / (8 T^2)), <= 4096."""
-    return int(min(Bn, max(1, min(4096, 1.5e9 // (T * T * 8)))))
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f).get(kernel)
+    return None if rec is None else rec.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -77,6 +85,8 @@ def main():
     ap.add_argument("--replicates", type=int, default=B)
     ap.add_argument("--mode", default="auto", choices=["auto", "direct", "factored"])
     ap.add_argument("--eig-tol", type=float, default=-1.0, help="eigensolver gap tolerance (default 1e-12)")
+    ap.add_argument("--strict", action="store_true",
+                    help="eigenvector-residual stopping rule even for eigenvalue-only stats")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -97,6 +107,8 @@ def main():
     ctx = D.Context(local)
     if args.eig_tol > 0:
         ctx.set_eig_params(tol=args.eig_tol)
+    if args.strict:
+        ctx.set_value_tol(0.0)
     Bn = args.replicates
 
     # ---- base model (identical on every rank), resident in HBM
@@ -162,17 +174,21 @@ def main():
     gemm_ms, gemm_n = timing.get("gemm", (0.0, 0))
     roof = None
     if gemm_n:
-        # factored path: every eigen-iteration is one GEMM H (T x T) x Z (T x nb*P)
-        nb = model_batch(Bn, T)
+        # factored path: every eigen-iteration of a batch is one GEMM
+        # H (T x T) . Z (T x nb*P).  Algorithmic flop = 2 T^2 P per replicate
+        # still unconverged when the GEMM runs (converged replicates' column
+        # blocks are skipped), summed by the library over the timed region.
         P = 16
-        flop_launch = 2.0 * T * T * nb * P
+        flop_total = 2.0 * T * T * P * eig["replicate_iterations"]
         per_launch_ms = gemm_ms / gemm_n
-        achieved = flop_launch / (per_launch_ms * 1e-3) / 1e12
+        achieved = flop_total / (gemm_ms * 1e-3) / 1e12
         roof = {"kernel": "gemm_kernel<A=H> (batched eigen-iteration H.Z, v_mfma_f64_4x4x4_4b)",
                 "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F64_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4), "traffic": None,
-                "avg_launch_ms": round(per_launch_ms, 4), "flop_per_launch": flop_launch,
-                "launches": gemm_n}
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4),
+                "traffic": pmc_traffic("gemm_kernel<false>"),
+                "avg_launch_ms": round(per_launch_ms, 4),
+                "flop_per_launch": round(flop_total / gemm_n), "launches": gemm_n,
+                "flop_per_replicate_iteration": 2 * T * T * P}
     elif gram_n:
         per_launch_ms = gram_ms / gram_n
         reps_per_launch = Bn * args.steps / gram_n
@@ -197,6 +213,8 @@ def main():
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
         "outputs_finite": ok,
         "mode": args.mode,
+        "stopping_rule": "eigenvector residual (strict)" if args.strict else
+                         "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
         "eig_iterations": eig,
         "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
     }

@@ -70,6 +70,11 @@ class Context:
     def set_eig_params(self, tol: float = -1.0, max_iter: int = -1, block: int = -1):
         self.check(self.lib.dfm_ctx_set_eig_params(self.h, tol, max_iter, block))
 
+    def set_value_tol(self, tol: float):
+        """Eigenvalue-only bootstrap statistics: stop at `tol` relative on the
+        Kato-Temple eigenvalue bound (default 1e-12); tol <= 0 = strict rule."""
+        self.check(self.lib.dfm_ctx_set_value_tol(self.h, float(tol)))
+
     def enable_timing(self, on: bool = True):
         self.check(self.lib.dfm_ctx_enable_timing(self.h, int(on)))
 
@@ -85,7 +90,10 @@ class Context:
     def eig_stats(self):
         b, t, m = C.c_int64(), C.c_int64(), C.c_int64()
         self.check(self.lib.dfm_ctx_eig_stats(self.h, C.byref(b), C.byref(t), C.byref(m)))
-        return {"batches": b.value, "iterations": t.value, "max_iterations": m.value}
+        ri = C.c_int64()
+        self.check(self.lib.dfm_ctx_rep_iters(self.h, C.byref(ri)))
+        return {"batches": b.value, "iterations": t.value, "max_iterations": m.value,
+                "replicate_iterations": ri.value}
 
     def close(self):
         if getattr(self, "h", None) and not _lib.shutting_down():

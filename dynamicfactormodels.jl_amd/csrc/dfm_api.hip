@@ -22,6 +22,7 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
 extern int g_last_iters;
+extern int64_t g_last_rep_iters;
 int spectrum_max();
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
                            hipStream_t st);
@@ -82,6 +83,9 @@ struct dfm_ctx {
   hipStream_t own = nullptr, stream = nullptr;
   std::string err;
   double tol = 1e-12;   // residual <= tol * eigen-gap (see eig_gq_kernel)
+  // bootstrap calls whose statistics depend on eigenvalues only: Ritz values
+  // within this relative bound (Kato-Temple, check_converged); <= 0 = strict
+  double tol_values = 1e-12;
   int maxit = 400, block = 0, poll = 4;
   bool timing = false;
   std::vector<hipEvent_t> pool;
@@ -90,7 +94,7 @@ struct dfm_ctx {
   hipEvent_t cur_a[DFM_KC_COUNT] = {};
   double ms[DFM_KC_COUNT] = {};
   int64_t launches[DFM_KC_COUNT] = {};
-  int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0;
+  int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0, rep_iters = 0;
 };
 
 struct dfm_model {
@@ -227,6 +231,11 @@ int dfm_ctx_set_eig_params(dfm_ctx *ctx, double tol, int max_iter, int block) {
   if (block >= 0) ctx->block = block;
   return 0;
 }
+int dfm_ctx_set_value_tol(dfm_ctx *ctx, double tol) {
+  if (!ctx) return -1;
+  ctx->tol_values = tol;
+  return 0;
+}
 int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable) {
   if (!ctx) return -1;
   ctx->timing = enable != 0;
@@ -246,7 +255,7 @@ int dfm_ctx_reset_timing(dfm_ctx *ctx) {
   if (!ctx) return -1;
   harvest(ctx);
   for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
-  ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = 0;
+  ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = ctx->rep_iters = 0;
   return 0;
 }
 int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max) {
@@ -260,6 +269,12 @@ static void note_iters(dfm_ctx *ctx) {
   ctx->eig_batches++;
   ctx->eig_iters += g_last_iters;
   ctx->eig_iters_max = std::max<int64_t>(ctx->eig_iters_max, g_last_iters);
+  ctx->rep_iters += g_last_rep_iters;
+}
+int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters) {
+  if (!ctx || !rep_iters) return -1;
+  *rep_iters = ctx->rep_iters;
+  return 0;
 }
 const char *dfm_kernel_class_name(int cls) {
   return (cls >= 0 && cls < DFM_KC_COUNT) ? kclass_names[cls] : "?";
@@ -692,15 +707,34 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     sd[i] = {s.kind, s.arg0, s.arg1, (int)width};
     width += (s.kind >= DFM_STAT_LR_ALL) ? N : 1;
   }
+  // Statistics that read only the eigenvalues and the trace let the
+  // eigensolver stop on the (quadratic) eigenvalue bound instead of the
+  // eigenvector residual: same 1e-12-relative accuracy for what is returned.
+  bool values_only = ns > 0;
+  for (int i = 0; i < ns; ++i)
+    values_only = values_only && (stats[i].kind == DFM_STAT_V || stats[i].kind == DFM_STAT_CRIT ||
+                                  stats[i].kind == DFM_STAT_EIGVAL || stats[i].kind == DFM_STAT_TRACE);
+  const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
   const int p = eig_block_p(m, r, ctx->block);
   const int P = p <= 16 ? 16 : 32;
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32;
   int64_t nb = M->batch;
   if (nb <= 0) {
-    const double gbytes = (double)m * m * 8;
-    nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
+    if (fact) {
+      // No per-replicate Gram: a replicate's workspace is O((T + N) P) (C3:
+      // ~0.8 MB), so one batch holds the whole job up to a 16 GB budget —
+      // the latency-bound per-replicate kernels then fill the chip.
+      const double per = (double)boot_ws_bytes(M, 1024, P, ctx->maxit, chow, true, nullptr, nullptr) / 1024.0;
+      nb = (int64_t)std::max(1.0, std::min(16384.0, std::floor(16e9 / per)));
+    } else {
+      const double gbytes = (double)m * m * 8;
+      nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
+    }
+    // equal batches (no small tail batch running the iterations half-empty)
+    const int64_t nbat = (B + nb - 1) / nb;
+    nb = (B + nbat - 1) / nbat;
   }
   nb = std::min<int64_t>(nb, B);
-  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32;
   if (fact && !M->fact_ready) {
     // H = E E' by the MFMA Gram kernel (K1), then EL, S, cF, diag(H)
     M->ldH = round_up(T, 16);
@@ -742,7 +776,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld};
     if (fact) {
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
-      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
+      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
@@ -754,7 +788,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
         Scope sc(ctx, DFM_KC_GRAM);
         HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
       }
-      int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, ctx->tol, ctx->maxit, ctx->poll,
+      int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
                        w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);

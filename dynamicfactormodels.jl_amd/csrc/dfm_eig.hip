@@ -33,7 +33,9 @@ struct EigWork {
   double *small;           // nb x SMALL_STRIDE (A, Bm, theta, dead)
   int *done, *iters, *active;
   double *trace;           // nb
+  long long *dbg;          // debug phase stamps of replicate 0 (DFM_SMALL_STAMPS), else null
 };
+#define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
 
 // ----------------------------------------------------------------- init
@@ -81,6 +83,38 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
     double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
     const double th0 = fabs(th[0]);
     bool ok = true;
+    if (tol < 0.0) {
+      // Eigenvalue-only statistics (V, criteria, eigenvalues, trace): a Ritz
+      // value's error is quadratic in its residual, |theta_j - lambda_j| <=
+      // res_j^2 / gap_j (Kato-Temple; gap_j = distance to the neighbouring
+      // Ritz values, halved for safety).  Converged when every wanted
+      // eigenvalue is within -tol relative AND the summed bound moves the
+      // residual energy trace - sum_j theta_j (the numerator of V(k),
+      // src/criteria.jl:5) by at most -tol relative.
+      const double tv = -tol;
+      double bsum = 0.0, tsum = 0.0;
+      bool okall = true, floor_ok = true;
+      for (int j = lane; j < k; j += 64) {
+        double rs = 0.0;
+        for (int r = 0; r < nrb; ++r) rs += w.rpart[((int64_t)rep * nrb + r) * P + j];
+        double gap = INFINITY;
+        if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+        if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+        const double bnd = rs / (0.5 * gap);
+        bsum += bnd;
+        tsum += th[j];
+        okall = okall && (bnd <= tv * fabs(th[j]) || sqrt(rs) <= 2e-14 * th0);
+        floor_ok = floor_ok && sqrt(rs) <= 2e-14 * th0;
+        if (rb == 0) next[j] = sqrt(rs);
+      }
+      bsum = wave_sum(bsum);
+      tsum = wave_sum(tsum);
+      // residual energy floored at 1e-6 trace: below that the reference's own
+      // rounding of ||E||^2 already exceeds -tol relative (exact-rank panels)
+      const double tr = w.trace[rep];
+      const double vnum = fmax(fabs(tr - tsum), 1e-6 * fabs(tr));
+      ok = !__any(!okall) && (bsum <= tv * vnum || !__any(!floor_ok));
+    } else
     for (int j0 = 0; j0 < k; j0 += 64) {
       // lanes: j = j0 + lane / G, r = lane % G   with G = power of two >= nrb
       int G = 1;
@@ -216,13 +250,15 @@ struct SmallLds {
   static constexpr int S = P + 1;
   double Hq[P * S], Yq[P * S], Qq[P * S], L[P * S], Li[P * S], W[P * S], V[P * S], A[P * S];
   double rc[P / 2], rs[P / 2];
+  double dinv[P];   // 1 / L[j][j] of the last Cholesky (1 for dead pivots)
   int ra[P / 2], rb[P / 2], perm[P];
   int dead1[P], dead2[P];
 };
 
-// lower Cholesky M = Lo Lo' (p x p), tiny pivots -> dead (unit diagonal, zero column)
+// lower Cholesky M = Lo Lo' (p x p), tiny pivots -> dead (unit diagonal, zero column);
+// dinv[j] = 1 / Lo[j][j].  One reciprocal square root per pivot (no divide).
 template <int P>
-DFM_DEV void wave_chol(const double *M, double *Lo, int *dead, int p) {
+DFM_DEV void wave_chol(const double *M, double *Lo, double *dinv, int *dead, int p) {
   constexpr int S = P + 1;
   const int lane = threadIdx.x;
   double mx = 0.0;
@@ -234,33 +270,43 @@ DFM_DEV void wave_chol(const double *M, double *Lo, int *dead, int p) {
   const double thresh = 1e-22 * mx;
   for (int j = 0; j < p; ++j) {
     const int i = lane;
-    double sv = 0.0;
+    double s0 = 0.0, s1 = 0.0;
     if (i >= j && i < p) {
-      sv = M[i * S + j];
-      for (int q = 0; q < j; ++q) sv -= Lo[i * S + q] * Lo[j * S + q];
+      s0 = M[i * S + j];
+      int q = 0;
+      for (; q + 1 < j; q += 2) {   // two accumulators: half the dependent chain
+        s0 -= Lo[i * S + q] * Lo[j * S + q];
+        s1 -= Lo[i * S + q + 1] * Lo[j * S + q + 1];
+      }
+      if (q < j) s0 -= Lo[i * S + q] * Lo[j * S + q];
     }
+    const double sv = s0 + s1;
     const double sj = __shfl(sv, j);
     const bool dd = !(sj > thresh);
-    const double d = dd ? 1.0 : sqrt(sj);
-    if (i == j) { Lo[j * S + j] = d; dead[j] = dd; }
-    else if (i > j && i < p) Lo[i * S + j] = dd ? 0.0 : sv / d;
+    const double inv = dd ? 1.0 : rsqrt(sj);
+    if (i == j) { Lo[j * S + j] = dd ? 1.0 : sj * inv; dead[j] = dd; dinv[j] = inv; }
+    else if (i > j && i < p) Lo[i * S + j] = dd ? 0.0 : sv * inv;
     __syncthreads();
   }
 }
 
 // Li = Lo^-1 (lower), column c per lane in registers; rows of dead pivots zeroed.
 template <int P>
-DFM_DEV void wave_trinv(const double *Lo, double *Li, const int *dead, int p) {
+DFM_DEV void wave_trinv(const double *Lo, const double *dinv, double *Li, const int *dead, int p) {
   constexpr int S = P + 1;
   const int c = threadIdx.x;
   if (c < P) {
     double x[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-      double sv = (i == c) ? 1.0 : 0.0;
+      double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
 #pragma unroll
-      for (int q = 0; q < i; ++q) sv -= Lo[i * S + q] * x[q];
-      x[i] = (i < p) ? sv / Lo[i * S + i] : 0.0;
+      for (int q = 0; q + 1 < i; q += 2) {
+        s0 -= Lo[i * S + q] * x[q];
+        s1 -= Lo[i * S + q + 1] * x[q + 1];
+      }
+      if (i & 1) s0 -= Lo[i * S + i - 1] * x[i - 1];
+      x[i] = (i < p) ? (s0 + s1) * dinv[i] : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < P; ++i) Li[i * S + c] = (i < p && c < p && !dead[i]) ? x[i] : 0.0;
@@ -295,11 +341,12 @@ DFM_DEV void wave_sym(double *M) {
 }
 
 template <int P>
-__global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb) {
+__global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb, int jsweeps) {
   constexpr int S = P + 1;
   __shared__ SmallLds<P> sm;
   const int lane = threadIdx.x, rep = blockIdx.x;
   if (w.done[rep]) return;
+  SMALL_STAMP(0);
   // 1. sum partials in fixed order (entries >= p are zero: Q columns >= p are zero)
   const double *pp = w.part + (int64_t)rep * nrb * 3 * P * P;
   constexpr int PER = 3 * P * P / 64;   // entries per lane (12 for P = 16)
@@ -323,29 +370,30 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
     }
   }
   __syncthreads();
+  SMALL_STAMP(1);
   wave_sym<P>(sm.Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
-  wave_chol<P>(sm.Qq, sm.L, sm.dead1, p);
-  wave_trinv<P>(sm.L, sm.Li, sm.dead1, p);
+  wave_chol<P>(sm.Qq, sm.L, sm.dinv, sm.dead1, p);
+  SMALL_STAMP(2);
+  wave_trinv<P>(sm.L, sm.dinv, sm.Li, sm.dead1, p);
+  SMALL_STAMP(3);
   wave_mm<P, false, false>(sm.Li, sm.Hq, sm.W);
   wave_mm<P, false, true>(sm.W, sm.Li, sm.Hq);
   wave_sym<P>(sm.Hq);
+  SMALL_STAMP(4);
   for (int e = lane; e < P * S; e += 64) sm.V[e] = ((e / S) == (e % S)) ? 1.0 : 0.0;
   __syncthreads();
   // 3. parallel cyclic Jacobi (circle-method pairs; index p is a dummy when p is odd)
   const int n = p + (p & 1), h = n / 2;
-  for (int sweep = 0; sweep < 40; ++sweep) {
-    double off = 0.0, fro = 0.0;
-    for (int e = lane; e < p * p; e += 64) {
-      const int a = e / p, c = e % p;
-      const double v = sm.Hq[a * S + c];
-      fro = fma(v, v, fro);
-      if (a != c) off = fma(v, v, off);
-    }
-    off = wave_sum(off);
-    fro = wave_sum(fro);
-    if (off <= 1e-30 * fro || fro == 0.0) break;
+  // A pair is rotated only while |h_ab| > 4 eps sqrt(|h_aa h_bb|) (the classic
+  // Jacobi threshold: a smaller off-diagonal moves the eigenvalues by
+  // O(eps^2)); the sweep loop ends at the first sweep that rotates nothing.
+  // (A Frobenius off-diagonal test sits at the rounding floor for these
+  // matrices and ran every sweep to the cap.)
+  for (int sweep = 0; sweep < jsweeps; ++sweep) {
+    bool rotated = false;
     for (int r = 0; r < n - 1; ++r) {
+      bool rot = false;
       if (lane < h) {
         const int pa = lane, pb = n - 1 - lane;
         int a = pa == 0 ? 0 : 1 + (pa - 1 + r) % (n - 1);
@@ -353,16 +401,20 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
         if (a > b) { const int t = a; a = b; b = t; }
         double c = 1.0, sn = 0.0;
         if (b < p) {
-          const double hab = sm.Hq[a * S + b];
-          if (fabs(hab) > 1e-300) {
-            const double zeta = (sm.Hq[b * S + b] - sm.Hq[a * S + a]) / (2.0 * hab);
+          const double hab = sm.Hq[a * S + b], haa = sm.Hq[a * S + a], hbb = sm.Hq[b * S + b];
+          if (fabs(hab) > 1e-300 && fabs(hab) > 8.9e-16 * sqrt(fabs(haa) * fabs(hbb))) {
+            const double zeta = (hbb - haa) / (2.0 * hab);
             const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
             c = 1.0 / sqrt(1.0 + t * t);
             sn = t * c;
+            rot = true;
           }
         }
         sm.ra[lane] = a; sm.rb[lane] = b; sm.rc[lane] = c; sm.rs[lane] = sn;
       }
+      const bool any = __any(rot);
+      rotated = rotated || any;
+      if (!any) continue;   // wave-uniform: nothing to apply this round
       __syncthreads();
       // H <- J' H J by 2x2 blocks; V <- V J
       for (int e = lane; e < h * h; e += 64) {
@@ -388,16 +440,19 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
       }
       __syncthreads();
     }
+    if (w.dbg && rep == 0 && lane == 0) w.dbg[15] = sweep + 1;
+    if (!rotated) break;
   }
-  // 4. sort descending (stable)
-  if (lane == 0) {
-    for (int j = 0; j < p; ++j) sm.perm[j] = j;
+  SMALL_STAMP(5);
+  // 4. sort descending (stable): lane j computes the rank of diagonal j
+  for (int j = lane; j < p; j += 64) {
+    const double v = sm.Hq[j * S + j];
+    int rank = 0;
     for (int i = 0; i < p; ++i) {
-      int best = i;
-      for (int j = i + 1; j < p; ++j)
-        if (sm.Hq[sm.perm[j] * S + sm.perm[j]] > sm.Hq[sm.perm[best] * S + sm.perm[best]]) best = j;
-      const int t = sm.perm[i]; sm.perm[i] = sm.perm[best]; sm.perm[best] = t;
+      const double u = sm.Hq[i * S + i];
+      rank += (u > v || (u == v && i < j)) ? 1 : 0;
     }
+    sm.perm[rank] = j;
   }
   __syncthreads();
   double *small = w.small + (int64_t)rep * small_stride<P>();
@@ -408,13 +463,17 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
     sm.W[i * S + c] = (i < p && c < p) ? sm.V[i * S + sm.perm[c]] : 0.0;
   }
   __syncthreads();
+  SMALL_STAMP(6);
   // 5. A = L^-T Vs = Li' W ;  Z'Z = A' (Y'Y) A ;  L2 = chol ;  Bm = A L2^-T
   wave_mm<P, true, false>(sm.Li, sm.W, sm.A);
   wave_mm<P, false, false>(sm.Yq, sm.A, sm.W);
   wave_mm<P, true, false>(sm.A, sm.W, sm.Qq);
   wave_sym<P>(sm.Qq);
-  wave_chol<P>(sm.Qq, sm.L, sm.dead2, p);
-  wave_trinv<P>(sm.L, sm.Li, sm.dead2, p);
+  SMALL_STAMP(7);
+  wave_chol<P>(sm.Qq, sm.L, sm.dinv, sm.dead2, p);
+  SMALL_STAMP(8);
+  wave_trinv<P>(sm.L, sm.dinv, sm.Li, sm.dead2, p);
+  SMALL_STAMP(9);
   wave_mm<P, false, true>(sm.A, sm.Li, sm.W);   // Bm = A Li'
   for (int e = lane; e < P * P; e += 64) {
     const int a = e / P, c = e % P;
@@ -422,6 +481,7 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
     small[P * P + e] = (a < p && c < p) ? sm.W[a * S + c] : 0.0;
   }
   for (int j = lane; j < P; j += 64) small[2 * P * P + P + j] = (j < p && sm.dead2[j]) ? 1.0 : 0.0;
+  SMALL_STAMP(10);
 }
 
 // ---------------------------------------------------------------- apply
@@ -532,6 +592,7 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   w.done = (int *)take((size_t)nb * 4);
   w.iters = (int *)take((size_t)nb * 4);
   w.active = (int *)take((size_t)(maxit + 2) * 4);
+  w.dbg = nullptr;
   return w;
 }
 
@@ -540,7 +601,33 @@ size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit) {
 }
 
 typedef void (*timer_fn)(void *ctx, int cls, int begin);
+// Jacobi sweeps per Rayleigh-Ritz step.  The projected matrix need not be
+// diagonalised exactly at every outer iteration: the next iteration starts
+// from the (nearly) rotated basis, so the inner sweeps accumulate across outer
+// iterations, and the residual test of check_converged includes any leftover
+// off-diagonal coupling.  DFM_JACOBI_SWEEPS overrides (development).
+static int jacobi_sweeps() {
+  static const int n = [] { const char *e = getenv("DFM_JACOBI_SWEEPS"); return e ? atoi(e) : 2; }();
+  return n;
+}
 int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
+// replicate-iterations of the last run's dominant product (G.Q in eig_gq, or
+// the H.Z GEMM in the factored solver) that still had an unconverged
+// replicate: the algorithmic work the roofline figure is priced on.
+int64_t g_last_rep_iters = 0;
+
+// Sum of the unconverged-replicate counts seen by the products of iterations
+// 0..last (shift = 1: the product of iteration it runs before that
+// iteration's convergence check, so it sees active[it-1]; active[-1] = nb).
+static int64_t count_rep_iters(const int *active_dev, int last, int shift, int nb, hipStream_t st) {
+  if (last < 0) return 0;
+  std::vector<int> a((size_t)last + 2, 0);
+  hipMemcpyAsync(a.data(), active_dev, a.size() * 4, hipMemcpyDeviceToHost, st);
+  hipStreamSynchronize(st);
+  int64_t s = 0;
+  for (int it = 0; it <= last; ++it) s += (it - shift < 0) ? nb : a[it - shift];
+  return s;
+}
 
 // Solve nb problems.  Returns 0 ok, 1 not converged (status per replicate),
 // negative on bad args, or a hipError_t (>1000).
@@ -573,7 +660,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (check_only) break;
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb);
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, jacobi_sweeps());
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0);
@@ -588,6 +675,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   }
   (void)finished;
   g_last_iters = it;
+  g_last_rep_iters = count_rep_iters(w.active, std::min(it, maxit - 1), 0, nb, st);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -813,6 +901,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
                        off, lst, w.trace);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
+  int last_gemm = -1;
   for (int it = 0; it <= maxit; ++it) {
     const int check_only = (it == maxit);
     if (!check_only) {
@@ -821,6 +910,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
       if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
       if (tf) tf(tctx, DFM_KC_GEMM, 1);
       hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+      last_gemm = it;
       if (tf) tf(tctx, DFM_KC_GEMM, 0);
       if (e != hipSuccess) return 1000 + (int)e;
     }
@@ -830,7 +920,23 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (check_only) break;
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb);
+    static const bool stamps_on = getenv("DFM_SMALL_STAMPS") != nullptr;
+    static long long *dbg_dev = nullptr;
+    if (stamps_on) {
+      if (!dbg_dev) hipMalloc(&dbg_dev, 64 * 8);
+      hipMemsetAsync(dbg_dev, 0, 64 * 8, st);
+      w.dbg = dbg_dev;
+    }
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, jacobi_sweeps());
+    if (stamps_on) {
+      long long h[64];
+      hipMemcpyAsync(h, dbg_dev, 64 * 8, hipMemcpyDeviceToHost, st);
+      hipStreamSynchronize(st);
+      fprintf(stderr, "small it %d sweeps %lld:", it, h[15]);
+      for (int i = 1; i <= 10; ++i) fprintf(stderr, " %lld", h[i] ? h[i] - h[i - 1] : -1);
+      fprintf(stderr, "\n");
+      w.dbg = nullptr;
+    }
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0);
@@ -861,6 +967,455 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     }
     g_last_iters = it;
   }
+  g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
+  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
+  if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return 1000 + (int)e;
+  return 0;
+}
+
+// ================================================= fused factored iteration
+// For T * P * 8 <= F2_LDS_MAX (C3: T = 500, P = 16 -> 64 KB) one iteration of
+// the factored solver is four launches instead of five, with no per-row-block
+// partial arrays and no separate convergence pass:
+//   GEMM  HZ = H Z                          (shared H, all unconverged replicates)
+//   y2    Y = F (S a + cc) + D (EL[idx] a + HZ[idx]),  Q'Y, Y'Y, Q'Q   (one WG / replicate)
+//   small Rayleigh-Ritz on p x p            (eig_small_kernel, nrb = 1)
+//   ap2   U = Q A, Qn = Y Bm, residuals ||Y A - U diag(theta)|| -> converged?
+//         else Z = P' D Qn (CSR gather from an LDS image), a = F'Qn, cc = EL'Z
+// Every T x P product is a v_mfma_f64_16x16x4 chain whose operands are the
+// rows a lane already holds: A[i][k] at lane i + 16k, B[k][j] at lane j + 16k,
+// C[row][col] at lane col + 16 (row % 4), register row / 4
+// (tools/mfma16_layout.hip).  An accumulator register g holds rows
+// 4g .. 4g+3 in exactly the B-operand layout, so Q'Y etc. need no lane movement.
+// Reductions over waves run in a fixed order: bit-reproducible, batch-invariant.
+constexpr int F2_LDS_MAX = 96 * 1024;
+typedef double dv4 __attribute__((ext_vector_type(4)));
+DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
+// Convergence verdict from per-column squared residuals res2[j] (j < k), on
+// one whole wave (same rules as check_converged: strict eigenvector-residual
+// test, or for tol < 0 the Kato-Temple eigenvalue bound).
+DFM_DEV bool decide_converged(const double *res2, const double *th, const double *prev, double *next,
+                              int k, int p, double tol, double trace, int itc) {
+  const int lane = threadIdx.x & 63;
+  const double th0 = fabs(th[0]);
+  bool okall = true, floor_ok = true;
+  double bsum = 0.0, tsum = 0.0;
+  for (int j = lane; j < k; j += 64) {
+    const double rs = res2[j], res = sqrt(rs);
+    double gap = INFINITY;
+    if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+    if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+    bool okj;
+    if (tol < 0.0) {
+      const double bnd = rs / (0.5 * gap);
+      bsum += bnd;
+      tsum += th[j];
+      okj = bnd <= -tol * fabs(th[j]) || res <= 2e-14 * th0;
+    } else {
+      const bool stagn = itc > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
+      okj = res <= tol * gap || res <= 2e-14 * th0 || stagn;
+    }
+    floor_ok = floor_ok && res <= 2e-14 * th0;
+    okall = okall && okj;
+    next[j] = res;
+  }
+  bool ok = !__any(!okall);
+  if (tol < 0.0) {
+    bsum = wave_sum(bsum);
+    tsum = wave_sum(tsum);
+    const double vnum = fmax(fabs(trace - tsum), 1e-6 * fabs(trace));
+    ok = ok && (bsum <= -tol * vnum || !__any(!floor_ok));
+  }
+  return ok;
+}
+
+// y2: one workgroup (4 waves) per replicate; wave w takes 16-row tiles w, w+4, ...
+template <int P>
+__global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
+                                                      const double *__restrict__ eta,
+                                                      const double *__restrict__ HZ, int64_t ldz,
+                                                      const double *__restrict__ ab,
+                                                      const double *__restrict__ Qc, double *__restrict__ Yo) {
+  constexpr int NT = P / 16;
+  const int rep = blockIdx.x;
+  if (w.done[rep]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  __shared__ double sa[16 * P], sb[16 * P];          // a = F'Q, S a + cc  (rows >= r zero)
+  __shared__ double red[3 * NT * NT * 256];
+  const double *abr = ab + (int64_t)rep * 32 * P;
+  for (int e = tid; e < 16 * P; e += 256) sa[e] = abr[e];
+  __syncthreads();
+  for (int e = tid; e < 16 * P; e += 256) {
+    const int j = e / P, c = e % P;
+    double v = abr[16 * P + e];
+    if (j < r)
+      for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], sa[i * P + c], v);
+    sb[e] = v;
+  }
+  __syncthreads();
+  const int KR = (r + 3) >> 2;
+  double bA[4][NT], bB[4][NT];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
+      bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
+    }
+  dv4 acc[3][NT][NT];
+#pragma unroll
+  for (int m3 = 0; m3 < 3; ++m3)
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[m3][a][b] = dv4{0.0, 0.0, 0.0, 0.0};
+  const double *Qr = Qc + (int64_t)rep * T * P;
+  double *Yr = Yo + (int64_t)rep * T * P;
+  const int32_t *ix = idx + (int64_t)rep * T;
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  const int ntile = (T + 15) >> 4;
+  for (int tile = wave; tile < ntile; tile += 4) {
+    const int t0 = tile * 16;
+    const int ta = t0 + li;
+    const bool va = ta < T;
+    const int ia = va ? ix[ta] : 0;
+    dv4 yF[NT], yE[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) { yF[ct] = dv4{0.0, 0.0, 0.0, 0.0}; yE[ct] = yF[ct]; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < KR) {
+        const int j = 4 * kk + lk;
+        const double fA = (va && j < r) ? fb.F[(int64_t)ta * r + j] : 0.0;
+        const double eA = (va && j < r) ? fb.EL[(int64_t)ia * r + j] : 0.0;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          yF[ct] = mfma16(fA, bB[kk][ct], yF[ct]);
+          yE[ct] = mfma16(eA, bA[kk][ct], yE[ct]);
+        }
+      }
+    }
+    double Yv[NT][4], Qv[NT][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int t = t0 + 4 * g + lk;
+      const bool v = t < T;
+      const int i = v ? ix[t] : 0;
+      const double e = v ? (et ? et[t] : 1.0) : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const int c = 16 * ct + li;
+        const double hz = v ? HZ[(int64_t)i * ldz + (int64_t)rep * P + c] : 0.0;
+        const double y = v ? fma(e, yE[ct][g] + hz, yF[ct][g]) : 0.0;
+        const double q = v ? Qr[(int64_t)t * P + c] : 0.0;
+        if (v) Yr[(int64_t)t * P + c] = y;
+        Yv[ct][g] = y;
+        Qv[ct][g] = q;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) {
+          acc[0][a][b] = mfma16(Qv[a][g], Yv[b][g], acc[0][a][b]);
+          acc[1][a][b] = mfma16(Yv[a][g], Yv[b][g], acc[1][a][b]);
+          acc[2][a][b] = mfma16(Qv[a][g], Qv[b][g], acc[2][a][b]);
+        }
+  }
+  // fixed-order sum over the four waves
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int m3 = 0; m3 < 3; ++m3)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int b = 0; b < NT; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int e = ((m3 * NT + a) * NT + b) * 256 + g * 64 + lane;
+              red[e] = (wv ? red[e] : 0.0) + acc[m3][a][b][g];
+            }
+    }
+    __syncthreads();
+  }
+  double *pp = w.part + (int64_t)rep * 3 * P * P;
+  for (int e = tid; e < 3 * NT * NT * 256; e += 256) {
+    const int l = e & 63, g = (e >> 6) & 3, blk = e >> 8;
+    const int b = blk % NT, a = (blk / NT) % NT, m3 = blk / (NT * NT);
+    pp[m3 * P * P + (16 * a + 4 * g + (l >> 4)) * P + 16 * b + (l & 15)] = red[e];
+  }
+}
+
+// ap2: one workgroup per replicate.  init = 1: Qn := Q (the warm start), no
+// Ritz step.  Dynamic LDS: T x P image of eta_t Qn[t][:] for the CSR gather.
+template <int P>
+__global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
+                                                       int it, int init, int last,
+                                                       const double *__restrict__ eta,
+                                                       const int *__restrict__ off, const int *__restrict__ lst,
+                                                       const double *__restrict__ Qc, double *__restrict__ Yq,
+                                                       double *__restrict__ Zc, int64_t ldz,
+                                                       double *__restrict__ ab, uint64_t seed) {
+  constexpr int NT = P / 16, KP = P / 4;
+  const int rep = blockIdx.x;
+  if (!init && w.done[rep]) return;
+  extern __shared__ double sZ[];   // T x P
+  __shared__ double sred[NT * 256];
+  __shared__ double sres[4][P];
+  __shared__ int s_conv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  double *small = w.small + (int64_t)rep * small_stride<P>();
+  double bAm[KP][NT], bBm[KP][NT], th[NT];
+  bool dd[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) {
+    const int c = 16 * ct + li;
+    th[ct] = init ? 0.0 : small[2 * P * P + c];
+    dd[ct] = init ? false : (small[2 * P * P + P + c] != 0.0);
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) {
+      bAm[kk][ct] = init ? 0.0 : small[(4 * kk + lk) * P + c];
+      bBm[kk][ct] = init ? 0.0 : small[P * P + (4 * kk + lk) * P + c];
+    }
+  }
+  const double *Qr = Qc + (int64_t)rep * T * P;
+  double *Yr = Yq + (int64_t)rep * T * P;
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  double res2[NT];
+  dv4 aacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) { res2[ct] = 0.0; aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; }
+  const int ntile = (T + 15) >> 4;
+  for (int tile = wave; tile < ntile; tile += 4) {
+    const int t0 = tile * 16;
+    double qv[NT][4];
+    if (init) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) qv[ct][g] = t < T ? Qr[(int64_t)t * P + 16 * ct + li] : 0.0;
+      }
+    } else {
+      dv4 u[NT], ya[NT], qn[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) { u[ct] = dv4{0.0, 0.0, 0.0, 0.0}; ya[ct] = u[ct]; qn[ct] = u[ct]; }
+      const int ta = t0 + li;
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk) {
+        const double qa = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+        const double yo = ta < T ? Yr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          u[ct] = mfma16(qa, bAm[kk][ct], u[ct]);
+          ya[ct] = mfma16(yo, bAm[kk][ct], ya[ct]);
+          qn[ct] = mfma16(yo, bBm[kk][ct], qn[ct]);
+        }
+      }
+      // every wave reads only its own tile's Y rows, so Qn may overwrite them
+      // once all lanes of the wave have issued those reads
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+        const bool v = t < T;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const int c = 16 * ct + li;
+          const double wr = ya[ct][g] - th[ct] * u[ct][g];
+          if (v && c < k) res2[ct] = fma(wr, wr, res2[ct]);
+          double q = qn[ct][g];
+          if (c < p && dd[ct]) q = hash_unit(seed, t, 1000003ull * (it + 1) + c);
+          if (c >= p || !v) q = 0.0;
+          qv[ct][g] = q;
+          if (v) Yr[(int64_t)t * P + c] = q;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int t = t0 + 4 * g + lk;
+      const bool v = t < T;
+      const double e = v ? (et ? et[t] : 1.0) : 0.0;
+      const double fa = (v && li < r) ? fb.F[(int64_t)t * r + li] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        if (v) sZ[t * P + 16 * ct + li] = e * qv[ct][g];
+        aacc[ct] = mfma16(fa, qv[ct][g], aacc[ct]);
+      }
+    }
+  }
+  // residuals: sum over the 4 row-lanes of a column, then over waves (fixed order)
+  if (!init) {
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      double v = res2[ct];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lk == 0) sres[wave][16 * ct + li] = v;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int conv = 0;
+    if (!init) {
+      if (lane < P) sres[0][lane] = ((sres[0][lane] + sres[1][lane]) + sres[2][lane]) + sres[3][lane];
+      __builtin_amdgcn_wave_barrier();
+      const int itc = it + 1;
+      const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
+      double *next = small + 2 * P * P + 2 * P + (itc & 1) * P;
+      conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc) ? 1 : 0;
+    }
+    if (lane == 0) {
+      s_conv = conv;
+      if (conv) { w.done[rep] = 1; w.iters[rep] = it + 1; }
+      else if (!init) atomicAdd(&w.active[it], 1);
+    }
+  }
+  __syncthreads();
+  if (!init && (s_conv || last)) {
+    // Ritz vectors U = Q A for the final output (eig_final_kernel)
+    double *Ur = w.U + (int64_t)rep * T * P;
+    for (int tile = wave; tile < ntile; tile += 4) {
+      const int t0 = tile * 16, ta = t0 + li;
+      dv4 u[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) u[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk) {
+        const double qa = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa, bAm[kk][ct], u[ct]);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+        if (t < T)
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) Ur[(int64_t)t * P + 16 * ct + li] = u[ct][g];
+      }
+    }
+    return;
+  }
+  // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
+  const int *o = off + (int64_t)rep * (T + 1);
+  const int *L = lst + (int64_t)rep * T;
+  dv4 cacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) cacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+  for (int tile = wave; tile < ntile; tile += 4) {
+    const int s0 = tile * 16;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = s0 + 4 * g + lk;
+      const bool v = s < T;
+      double z[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) z[ct] = 0.0;
+      if (v) {
+        const int q1 = o[s + 1];
+        for (int q = o[s]; q < q1; ++q) {
+          const int t = L[q];
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) z[ct] += sZ[t * P + 16 * ct + li];
+        }
+      }
+      const double ea = (v && li < r) ? fb.EL[(int64_t)s * r + li] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + 16 * ct + li] = z[ct];
+        cacc[ct] = mfma16(ea, z[ct], cacc[ct]);
+      }
+    }
+  }
+  // a and cc: fixed-order sums over the waves -> ab[rep] = [a (16 x P); cc (16 x P)]
+  double *abr = ab + (int64_t)rep * 32 * P;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int wv = 0; wv < 4; ++wv) {
+      if (wave == wv)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int e = (ct * 4 + g) * 64 + lane;
+            const double v = pass ? cacc[ct][g] : aacc[ct][g];
+            sred[e] = (wv ? sred[e] : 0.0) + v;
+          }
+      __syncthreads();
+    }
+    for (int e = tid; e < NT * 256; e += 256) {
+      const int l = e & 63, g = (e >> 6) & 3, ct = e >> 8;
+      abr[pass * 16 * P + (4 * g + (l >> 4)) * P + 16 * ct + (l & 15)] = sred[e];
+    }
+    __syncthreads();
+  }
+}
+
+template <int P>
+static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
+                           const double *warm, int kw, double tol, int maxit, int poll, char *ws,
+                           char *fws, double *lam, double *Uk, double *trace_out, int *status,
+                           hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst) {
+  const int m = fb.T;
+  EigWork w = carve(ws, m, nb, P, maxit);
+  const int64_t ldz = (int64_t)nb * P;
+  double *Zc = (double *)fws;
+  double *HZ = Zc + (size_t)m * ldz;
+  double *ab = HZ + (size_t)m * ldz;
+  const size_t lds = (size_t)m * P * 8;
+  hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
+  hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
+  const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
+  double *cur = w.Q, *alt = w.Y;
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
+  {
+    const int64_t n = (int64_t)m * P;
+    dim3 grid((unsigned)((n + 255) / 256), nb);
+    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, (int64_t)0);
+    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
+                       off, lst, w.trace);
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, -1, 1, 0, eta,
+                       off, lst, cur, alt, Zc, ldz, ab, seed);
+  }
+  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
+  int it = 0, last_gemm = -1;
+  for (; it < maxit; ++it) {
+    if (tf) tf(tctx, DFM_KC_GEMM, 1);
+    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+    if (tf) tf(tctx, DFM_KC_GEMM, 0);
+    if (e != hipSuccess) return 1000 + (int)e;
+    last_gemm = it;
+    if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
+    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(256), 0, st, fb, w, m, idx, eta, HZ, ldz, ab, cur, alt);
+    if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
+    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, jacobi_sweeps());
+    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
+    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
+                       it == maxit - 1 ? 1 : 0, eta, off, lst, cur, alt, Zc, ldz, ab, seed);
+    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+    std::swap(cur, alt);
+    if ((it + 1) % poll == 0) {
+      int a = -1;
+      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return 1000 + (int)e;
+      if (a == 0) { ++it; break; }
+    }
+  }
+  g_last_iters = it;
+  g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -875,6 +1430,15 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
                      timer_fn tf, void *tctx, int *off, int *lst) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
+  static const bool legacy = getenv("DFM_FACT_LEGACY") != nullptr;   // development A/B switch
+  const int Pb = p <= 16 ? 16 : 32;
+  if (!legacy && fb.r <= 16 && (size_t)fb.T * Pb * 8 <= (size_t)F2_LDS_MAX) {
+    if (Pb == 16)
+      return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                                 trace_out, status, st, tf, tctx, off, lst);
+    return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                               trace_out, status, st, tf, tctx, off, lst);
+  }
   if (p <= 16)
     return eig_run_fact_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
                               trace_out, status, st, tf, tctx, off, lst);
@@ -1003,7 +1567,7 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
                                                        double *__restrict__ ev) {
   constexpr int S = SPEC_MAX + 1;
   __shared__ double H[SPEC_MAX * S];
-  __shared__ double rc[SPEC_MAX / 2], rs[SPEC_MAX / 2], red[256];
+  __shared__ double rc[SPEC_MAX / 2], rs[SPEC_MAX / 2];
   __shared__ int ra[SPEC_MAX / 2], rbb[SPEC_MAX / 2];
   __shared__ int sdone;
   const int tid = threadIdx.x, rep = blockIdx.x;
@@ -1014,26 +1578,11 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
     H[a * S + c] = (a < m && c < m) ? 0.5 * (g[(int64_t)a * ldg + c] + g[(int64_t)c * ldg + a]) : 0.0;
   }
   __syncthreads();
+  // classic threshold Jacobi (see eig_small_kernel): rotate while |h_ab| >
+  // 4 eps sqrt(|h_aa h_bb|); stop after a sweep that rotates nothing
   for (int sweep = 0; sweep < 80; ++sweep) {
-    double off = 0.0, fro = 0.0;
-    for (int e = tid; e < n * n; e += 256) {
-      const int a = e / n, c = e % n;
-      const double h = H[a * S + c];
-      fro += h * h;
-      if (a != c) off += h * h;
-    }
-    red[tid] = off;
+    if (tid == 0) sdone = 1;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) { if (tid < o) red[tid] += red[tid + o]; __syncthreads(); }
-    off = red[0];
-    __syncthreads();
-    red[tid] = fro;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) { if (tid < o) red[tid] += red[tid + o]; __syncthreads(); }
-    fro = red[0];
-    if (tid == 0) sdone = (off <= 1e-30 * fro) || fro == 0.0;
-    __syncthreads();
-    if (sdone) break;
     for (int r = 0; r < n - 1; ++r) {
       for (int s = tid; s < n / 2; s += 256) {
         const int pa = s, pb = n - 1 - s;
@@ -1041,9 +1590,10 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
         int b = pb == 0 ? 0 : 1 + (pb - 1 + r) % (n - 1);
         if (a > b) { const int t = a; a = b; b = t; }
         double c = 1.0, sn = 0.0;
-        const double hab = H[a * S + b];
-        if (fabs(hab) > 1e-300) {
-          const double zeta = (H[b * S + b] - H[a * S + a]) / (2.0 * hab);
+        const double hab = H[a * S + b], haa = H[a * S + a], hbb = H[b * S + b];
+        if (fabs(hab) > 1e-300 && fabs(hab) > 8.9e-16 * sqrt(fabs(haa) * fabs(hbb))) {
+          sdone = 0;
+          const double zeta = (hbb - haa) / (2.0 * hab);
           const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
           c = 1.0 / sqrt(1.0 + t * t);
           sn = t * c;
@@ -1070,6 +1620,8 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
       }
       __syncthreads();
     }
+    if (sdone) break;
+    __syncthreads();
   }
   // sort descending; the padding index (if any) carries an exact 0 that is dropped
   for (int i = tid; i < n; i += 256) {

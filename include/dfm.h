@@ -73,6 +73,12 @@ int dfm_ctx_synchronize(dfm_ctx *ctx);
  * subspace iterations (default 400), block width (0 = auto). */
 int dfm_ctx_set_eig_params(dfm_ctx *ctx, double tol, int max_iter, int block);
 /* Per-kernel HIP-event timing on the context stream (bench/roofline use). */
+/* Bootstrap calls whose statistics are all eigenvalue functions (V, CRIT,
+   EIGVAL, TRACE) stop the eigensolver when every returned eigenvalue and the
+   residual energy trace - sum(theta) are within `tol` relative by the
+   Kato-Temple bound (default 1e-12); tol <= 0 always uses the eigenvector
+   residual rule of dfm_ctx_set_eig_params. */
+int dfm_ctx_set_value_tol(dfm_ctx *ctx, double tol);
 int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable);
 /* ms accumulated per kernel class (see DFM_KCLASS_* in the implementation);
  * returns the number of classes written into ms_out/launches_out. */
@@ -81,6 +87,11 @@ int dfm_ctx_reset_timing(dfm_ctx *ctx);
 /* Eigensolver statistics since the last reset: batches solved, total and
  * maximum subspace iterations per batch. */
 int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max);
+/* Replicate-iterations of the eigensolver's dominant product (the H.Z GEMM in
+   the factored bootstrap, G.Q otherwise) summed over the calls since the last
+   dfm_ctx_reset_timing: each counts one unconverged replicate in one
+   iteration (2 m^2 P flop).  Instrumentation for the roofline figure. */
+int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters);
 const char *dfm_kernel_class_name(int cls);
 
 /* ------------------------------------------------ principal components

@@ -300,6 +300,36 @@ def test_c3_replicates_match_oracle(dfm, oracle, mode):
 
 
 @pytest.mark.parametrize("mode", ["direct", "factored"])
+def test_c3_value_only_stopping_rule(dfm, oracle, mode):
+    """Eigenvalue-only statistics stop the eigensolver on the Kato-Temple
+    eigenvalue bound (dfm_ctx_set_value_tol): V, criteria, eigenvalues and the
+    trace must still match the oracle within STAT_RTOL at C3 size, and the
+    strict (eigenvector-residual) rule within 1e-11."""
+    y, x, w = panel(oracle, 500, 2000, 8, 23)
+    g = dfm.DynamicFactorModel(y, w, x, 8, "ICp2")
+    g.set_bootstrap_mode(mode)
+    o = oracle.DynamicFactorModel(y, w, x, 8, "ICp2")
+    B = 4
+    idx, eta = oracle.draw_wild(np.random.default_rng(8), B, 500)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.criterion("BIC"), S.trace()] + [S.eigenvalue(j) for j in range(1, 9)]
+    out = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, 8, "ICp2")
+        ref = [oracle.factor_residual_variance(d), d.number_of_factors_criterion_value,
+               oracle.criterion_value("BIC", d), np.sum(xs * xs)] + list(d.eigenvalues[0][:8])
+        assert rel(out[b], ref) < STAT_RTOL
+    ctx = g._ctx
+    ctx.set_value_tol(0.0)
+    try:
+        strict = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    finally:
+        ctx.set_value_tol(1e-12)
+    assert rel(out, strict) < 1e-11
+
+
+@pytest.mark.parametrize("mode", ["direct", "factored"])
 def test_batching_is_bit_identical(dfm, oracle, mode):
     """Per-replicate results do not depend on batch composition — the property
     behind bit-identical 1-GPU vs 8-GPU sharding."""
