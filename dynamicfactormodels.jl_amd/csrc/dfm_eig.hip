@@ -978,7 +978,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
 }
 
 // ================================================= fused factored iteration
-// For T * P * 8 <= F2_LDS_MAX (C3: T = 500, P = 16 -> 64 KB) one iteration of
+// For T <= F2_T_MAX and r <= 16 (C3: T = 500, r = 8) one iteration of
 // the factored solver is four launches instead of five, with no per-row-block
 // partial arrays and no separate convergence pass:
 //   GEMM  HZ = H Z                          (shared H, all unconverged replicates)
@@ -992,7 +992,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
 // (tools/mfma16_layout.hip).  An accumulator register g holds rows
 // 4g .. 4g+3 in exactly the B-operand layout, so Q'Y etc. need no lane movement.
 // Reductions over waves run in a fixed order: bit-reproducible, batch-invariant.
-constexpr int F2_LDS_MAX = 96 * 1024;
+constexpr int F2_T_MAX = 4096;   // dynamic LDS of ap2: 16 T + 4 bytes
 typedef double dv4 __attribute__((ext_vector_type(4)));
 DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
@@ -1034,6 +1034,40 @@ DFM_DEV bool decide_converged(const double *res2, const double *th, const double
   return ok;
 }
 
+// One 16-row tile's operands for y2: F / EL[idx] rows in A-operand layout
+// (row t0 + (lane & 15), factor 4kk + (lane >> 4)), HZ[idx] and Q in the
+// accumulator layout (row t0 + 4g + (lane >> 4), column 16ct + (lane & 15)).
+// Rows >= T load row T-1 and are masked by the consumer.
+template <int P>
+struct Y2Tile {
+  double fA[4], eA[4], hz[P / 16][4], q[P / 16][4];
+};
+template <int P>
+DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, const int *six, const FactBase &fb,
+                     const double *__restrict__ HZ, int64_t ldz, int rep, const double *__restrict__ Qr) {
+  constexpr int NT = P / 16;
+  const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
+  const int ta = min(t0 + li, T - 1);
+  const int ia = six[ta];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int j = min(4 * kk + lk, r - 1);
+    L.fA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.F[(int64_t)ta * r + j] : 0.0;
+    L.eA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.EL[(int64_t)ia * r + j] : 0.0;
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int t = min(t0 + 4 * g + lk, T - 1);
+    const int i = six[t];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      const int c = 16 * ct + li;
+      L.hz[ct][g] = HZ[(int64_t)i * ldz + (int64_t)rep * P + c];
+      L.q[ct][g] = Qr[(int64_t)t * P + c];
+    }
+  }
+}
+
 // y2: one workgroup (4 waves) per replicate; wave w takes 16-row tiles w, w+4, ...
 template <int P>
 __global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
@@ -1048,6 +1082,14 @@ __global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, in
   const int li = lane & 15, lk = lane >> 4;
   __shared__ double sa[16 * P], sb[16 * P];          // a = F'Q, S a + cc  (rows >= r zero)
   __shared__ double red[3 * NT * NT * 256];
+  extern __shared__ double sdyn[];                   // eta (T doubles), idx (T ints)
+  double *set = sdyn;
+  int *six = (int *)(sdyn + T);
+  {
+    const int32_t *ixg = idx + (int64_t)rep * T;
+    const double *etg = eta ? eta + (int64_t)rep * T : nullptr;
+    for (int e = tid; e < T; e += 256) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; }
+  }
   const double *abr = ab + (int64_t)rep * 32 * P;
   for (int e = tid; e < 16 * P; e += 256) sa[e] = abr[e];
   __syncthreads();
@@ -1077,46 +1119,39 @@ __global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, in
       for (int b = 0; b < NT; ++b) acc[m3][a][b] = dv4{0.0, 0.0, 0.0, 0.0};
   const double *Qr = Qc + (int64_t)rep * T * P;
   double *Yr = Yo + (int64_t)rep * T * P;
-  const int32_t *ix = idx + (int64_t)rep * T;
-  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
   const int ntile = (T + 15) >> 4;
+  // software pipeline: the next tile's loads are issued before this tile's MFMAs
+  Y2Tile<P> cur, nxt;
+  y2_load<P>(cur, min(wave, ntile - 1), T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
   for (int tile = wave; tile < ntile; tile += 4) {
+    y2_load<P>(nxt, min(tile + 4, ntile - 1), T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
     const int t0 = tile * 16;
-    const int ta = t0 + li;
-    const bool va = ta < T;
-    const int ia = va ? ix[ta] : 0;
     dv4 yF[NT], yE[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) { yF[ct] = dv4{0.0, 0.0, 0.0, 0.0}; yE[ct] = yF[ct]; }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       if (kk < KR) {
-        const int j = 4 * kk + lk;
-        const double fA = (va && j < r) ? fb.F[(int64_t)ta * r + j] : 0.0;
-        const double eA = (va && j < r) ? fb.EL[(int64_t)ia * r + j] : 0.0;
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-          yF[ct] = mfma16(fA, bB[kk][ct], yF[ct]);
-          yE[ct] = mfma16(eA, bA[kk][ct], yE[ct]);
+          yF[ct] = mfma16(cur.fA[kk], bB[kk][ct], yF[ct]);
+          yE[ct] = mfma16(cur.eA[kk], bA[kk][ct], yE[ct]);
         }
       }
     }
-    double Yv[NT][4], Qv[NT][4];
+    double Yv[NT][4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int t = t0 + 4 * g + lk;
       const bool v = t < T;
-      const int i = v ? ix[t] : 0;
-      const double e = v ? (et ? et[t] : 1.0) : 0.0;
+      const double e = v ? set[t] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
-        const double hz = v ? HZ[(int64_t)i * ldz + (int64_t)rep * P + c] : 0.0;
-        const double y = v ? fma(e, yE[ct][g] + hz, yF[ct][g]) : 0.0;
-        const double q = v ? Qr[(int64_t)t * P + c] : 0.0;
+        const double y = v ? fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]) : 0.0;
         if (v) Yr[(int64_t)t * P + c] = y;
         Yv[ct][g] = y;
-        Qv[ct][g] = q;
+        if (!v) cur.q[ct][g] = 0.0;   // clamped row: no contribution to Q'Y, Q'Q
       }
     }
 #pragma unroll
@@ -1125,10 +1160,11 @@ __global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, in
       for (int a = 0; a < NT; ++a)
 #pragma unroll
         for (int b = 0; b < NT; ++b) {
-          acc[0][a][b] = mfma16(Qv[a][g], Yv[b][g], acc[0][a][b]);
+          acc[0][a][b] = mfma16(cur.q[a][g], Yv[b][g], acc[0][a][b]);
           acc[1][a][b] = mfma16(Yv[a][g], Yv[b][g], acc[1][a][b]);
-          acc[2][a][b] = mfma16(Qv[a][g], Qv[b][g], acc[2][a][b]);
+          acc[2][a][b] = mfma16(cur.q[a][g], cur.q[b][g], acc[2][a][b]);
         }
+    cur = nxt;
   }
   // fixed-order sum over the four waves
   for (int wv = 0; wv < 4; ++wv) {
@@ -1155,8 +1191,44 @@ __global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, in
   }
 }
 
+// One 16-row tile's operands for ap2: Q and Y rows in A-operand layout
+// (row t0 + (lane & 15), column 4kk + (lane >> 4)), F rows for a = F'Qn in
+// A-operand layout per row group g (row t0 + 4g + (lane >> 4), factor lane & 15),
+// and (init) Q in the accumulator layout.  Rows >= T read row T-1 (masked later).
+template <int P>
+struct Ap2Tile {
+  double qa[P / 4], yo[P / 4], fa[4], q[P / 16][4];
+};
+template <int P>
+DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init, const double *__restrict__ Qr,
+                      const double *Yr, const FactBase &fb) {
+  constexpr int NT = P / 16, KP = P / 4;
+  const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
+  const int ta = min(t0 + li, T - 1);
+#pragma unroll
+  for (int kk = 0; kk < KP; ++kk) {
+    L.qa[kk] = init ? 0.0 : Qr[(int64_t)ta * P + 4 * kk + lk];
+    L.yo[kk] = init ? 0.0 : Yr[(int64_t)ta * P + 4 * kk + lk];
+  }
+  const bool rowok = t0 + li < T;
+#pragma unroll
+  for (int kk = 0; kk < KP; ++kk) { L.qa[kk] = rowok ? L.qa[kk] : 0.0; L.yo[kk] = rowok ? L.yo[kk] : 0.0; }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int t = t0 + 4 * g + lk;
+    const int tc = min(t, T - 1);
+    const double f = fb.F[(int64_t)tc * r + min(li, r - 1)];
+    L.fa[g] = (t < T && li < r) ? f : 0.0;
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = init ? Qr[(int64_t)tc * P + 16 * ct + li] : 0.0;
+  }
+}
+
 // ap2: one workgroup per replicate.  init = 1: Qn := Q (the warm start), no
-// Ritz step.  Dynamic LDS: T x P image of eta_t Qn[t][:] for the CSR gather.
+// Ritz step.  Qn goes to global memory (over the Y rows this wave just read)
+// and is gathered back through the CSR after the barrier: same-CU L1, so the
+// workgroup-scope fence of __syncthreads makes it visible.  Dynamic LDS:
+// eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
 template <int P>
 __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
                                                        int it, int init, int last,
@@ -1168,12 +1240,21 @@ __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, i
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
   if (!init && w.done[rep]) return;
-  extern __shared__ double sZ[];   // T x P
+  extern __shared__ double sdyn[];
+  double *set = sdyn;                          // eta_t
+  int *so = (int *)(sdyn + T), *sl = so + T + 1;
   __shared__ double sred[NT * 256];
   __shared__ double sres[4][P];
   __shared__ int s_conv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
   const int li = lane & 15, lk = lane >> 4;
+  {
+    const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+    const int *o = off + (int64_t)rep * (T + 1);
+    const int *L = lst + (int64_t)rep * T;
+    for (int e = tid; e < T; e += 256) { set[e] = et ? et[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
+    if (tid == 0) so[T] = o[T];
+  }
   double *small = w.small + (int64_t)rep * small_stride<P>();
   double bAm[KP][NT], bBm[KP][NT], th[NT];
   bool dd[NT];
@@ -1190,41 +1271,37 @@ __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, i
   }
   const double *Qr = Qc + (int64_t)rep * T * P;
   double *Yr = Yq + (int64_t)rep * T * P;
-  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
   double res2[NT];
   dv4 aacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) { res2[ct] = 0.0; aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; }
   const int ntile = (T + 15) >> 4;
+  // software pipeline: operands of the wave's next tile load during this tile's MFMAs
+  Ap2Tile<P> cur, nxt;
+  ap2_load<P>(cur, min(wave, ntile - 1), T, r, lane, init, Qr, Yr, fb);
   for (int tile = wave; tile < ntile; tile += 4) {
+    ap2_load<P>(nxt, min(tile + 4, ntile - 1), T, r, lane, init, Qr, Yr, fb);
     const int t0 = tile * 16;
     double qv[NT][4];
     if (init) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int t = t0 + 4 * g + lk;
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) qv[ct][g] = t < T ? Qr[(int64_t)t * P + 16 * ct + li] : 0.0;
-      }
+        for (int ct = 0; ct < NT; ++ct) qv[ct][g] = (t0 + 4 * g + lk < T) ? cur.q[ct][g] : 0.0;
     } else {
       dv4 u[NT], ya[NT], qn[NT];
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) { u[ct] = dv4{0.0, 0.0, 0.0, 0.0}; ya[ct] = u[ct]; qn[ct] = u[ct]; }
-      const int ta = t0 + li;
 #pragma unroll
-      for (int kk = 0; kk < KP; ++kk) {
-        const double qa = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
-        const double yo = ta < T ? Yr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+      for (int kk = 0; kk < KP; ++kk)
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-          u[ct] = mfma16(qa, bAm[kk][ct], u[ct]);
-          ya[ct] = mfma16(yo, bAm[kk][ct], ya[ct]);
-          qn[ct] = mfma16(yo, bBm[kk][ct], qn[ct]);
+          u[ct] = mfma16(cur.qa[kk], bAm[kk][ct], u[ct]);
+          ya[ct] = mfma16(cur.yo[kk], bAm[kk][ct], ya[ct]);
+          qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
         }
-      }
-      // every wave reads only its own tile's Y rows, so Qn may overwrite them
-      // once all lanes of the wave have issued those reads
-      __builtin_amdgcn_wave_barrier();
+      // every wave reads only its own tiles' Y rows, and the next tile's rows
+      // were loaded before these stores: Qn may overwrite this tile's Y rows
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int t = t0 + 4 * g + lk;
@@ -1243,17 +1320,10 @@ __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, i
       }
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int t = t0 + 4 * g + lk;
-      const bool v = t < T;
-      const double e = v ? (et ? et[t] : 1.0) : 0.0;
-      const double fa = (v && li < r) ? fb.F[(int64_t)t * r + li] : 0.0;
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct) {
-        if (v) sZ[t * P + 16 * ct + li] = e * qv[ct][g];
-        aacc[ct] = mfma16(fa, qv[ct][g], aacc[ct]);
-      }
-    }
+      for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(cur.fa[g], qv[ct][g], aacc[ct]);
+    cur = nxt;
   }
   // residuals: sum over the 4 row-lanes of a column, then over waves (fixed order)
   if (!init) {
@@ -1291,12 +1361,13 @@ __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, i
       dv4 u[NT];
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) u[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+      double qa[KP];
 #pragma unroll
-      for (int kk = 0; kk < KP; ++kk) {
-        const double qa = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+      for (int kk = 0; kk < KP; ++kk) qa[kk] = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa, bAm[kk][ct], u[ct]);
-      }
+      for (int kk = 0; kk < KP; ++kk)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa[kk], bAm[kk][ct], u[ct]);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int t = t0 + 4 * g + lk;
@@ -1308,33 +1379,60 @@ __global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, i
     return;
   }
   // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
-  const int *o = off + (int64_t)rep * (T + 1);
-  const int *L = lst + (int64_t)rep * T;
+  const double *Qn = init ? Qr : Yr;
   dv4 cacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) cacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
   for (int tile = wave; tile < ntile; tile += 4) {
     const int s0 = tile * 16;
+    // all four row groups' first GU bucket entries are fetched together
+    // (independent loads in flight); longer buckets finish serially
+    constexpr int GU = 3;
+    double z[4][NT];
+    int qn0[4], qn1[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = s0 + 4 * g + lk;
+      qn0[g] = s < T ? so[s] : 0;
+      qn1[g] = s < T ? so[s + 1] : 0;
+    }
+    double val[4][GU][NT], ev[4][GU];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int q = qn0[g] + u;
+        const bool ok = q < qn1[g];
+        const int t = sl[ok ? q : 0];
+        ev[g][u] = ok ? set[t] : 0.0;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) val[g][u][ct] = Qn[(int64_t)t * P + 16 * ct + li];
+      }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < GU; ++u) acc = fma(ev[g][u], val[g][u][ct], acc);
+        z[g][ct] = acc;
+      }
+      for (int q = qn0[g] + GU; q < qn1[g]; ++q) {
+        const int t = sl[q];
+        const double e = set[t];
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) z[g][ct] = fma(e, Qn[(int64_t)t * P + 16 * ct + li], z[g][ct]);
+      }
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int s = s0 + 4 * g + lk;
       const bool v = s < T;
-      double z[NT];
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) z[ct] = 0.0;
-      if (v) {
-        const int q1 = o[s + 1];
-        for (int q = o[s]; q < q1; ++q) {
-          const int t = L[q];
-#pragma unroll
-          for (int ct = 0; ct < NT; ++ct) z[ct] += sZ[t * P + 16 * ct + li];
-        }
-      }
       const double ea = (v && li < r) ? fb.EL[(int64_t)s * r + li] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + 16 * ct + li] = z[ct];
-        cacc[ct] = mfma16(ea, z[ct], cacc[ct]);
+        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + 16 * ct + li] = z[g][ct];
+        cacc[ct] = mfma16(ea, z[g][ct], cacc[ct]);
       }
     }
   }
@@ -1372,7 +1470,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)m * ldz;
   double *ab = HZ + (size_t)m * ldz;
-  const size_t lds = (size_t)m * P * 8;
+  const size_t lds = (size_t)m * 8 + (size_t)(2 * m + 1) * 4;
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
@@ -1396,7 +1494,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(256), 0, st, fb, w, m, idx, eta, HZ, ldz, ab, cur, alt);
+    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(256), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, ab,
+                       cur, alt);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, jacobi_sweeps());
@@ -1432,7 +1531,7 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
   static const bool legacy = getenv("DFM_FACT_LEGACY") != nullptr;   // development A/B switch
   const int Pb = p <= 16 ? 16 : 32;
-  if (!legacy && fb.r <= 16 && (size_t)fb.T * Pb * 8 <= (size_t)F2_LDS_MAX) {
+  if (!legacy && fb.r <= 16 && fb.T <= F2_T_MAX) {
     if (Pb == 16)
       return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
                                  trace_out, status, st, tf, tctx, off, lst);
