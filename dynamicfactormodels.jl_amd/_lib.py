@@ -49,7 +49,12 @@ SIGNATURES = [
     ("dfm_model_fit", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                 c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                 C.c_int, C.POINTER(C.c_void_p)]),
+    ("dfm_model_fit_breaks", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
+                                       c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                       C.c_int, c_int64_p, C.c_int, C.POINTER(C.c_void_p)]),
     ("dfm_model_destroy", C.c_int, [C.c_void_p]),
+    ("dfm_model_blocks", C.c_int, [C.c_void_p]),
+    ("dfm_model_block", C.c_int, [C.c_void_p, C.c_int, c_int64_p, c_int64_p, c_double_p, c_double_p]),
     ("dfm_model_dims", C.c_int, [C.c_void_p, c_int64_p, c_int64_p, c_int64_p]),
     ("dfm_model_scalars", C.c_int, [C.c_void_p, c_int64_p, c_double_p, c_double_p, c_double_p]),
     ("dfm_model_read", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p,

@@ -236,8 +236,22 @@ class DynamicFactorModelResult:
             self.coefficient_covariance.ctypes.data_as(_lib.c_double_p), _lib.ptr(self.residuals),
             F.ctypes.data_as(_lib.c_double_p), L.ctypes.data_as(_lib.c_double_p), None,
             _lib.ptr(self.ic_values) if self.ic_values is not None else None))
-        self.factors = [np.ascontiguousarray(F)]
-        self.loadings = [np.ascontiguousarray(L)]
+        nblk = int(ctx.lib.dfm_model_blocks(handle))
+        if nblk <= 1:
+            self.factors = [np.ascontiguousarray(F)]
+            self.loadings = [np.ascontiguousarray(L)]
+            self.block_eigenvalues = [self.eigenvalues[:rr].copy()]
+        else:   # one (F_j, L_j) per break block, :98-100
+            self.factors, self.loadings, self.block_eigenvalues = [], [], []
+            for j in range(nblk):
+                a, t = C.c_int64(), C.c_int64()
+                ev = np.zeros(rr)
+                Lj = np.zeros((N, rr), order="F")
+                ctx.check(ctx.lib.dfm_model_block(handle, j, C.byref(a), C.byref(t), _lib.ptr(ev),
+                                                  Lj.ctypes.data_as(_lib.c_double_p)))
+                self.factors.append(np.ascontiguousarray(F[a.value:a.value + t.value]))
+                self.loadings.append(np.ascontiguousarray(Lj))
+                self.block_eigenvalues.append(ev)
         self._E = None
 
     @property
@@ -252,8 +266,12 @@ class DynamicFactorModelResult:
         return self._E
 
     @property
+    def F(self) -> np.ndarray:                       # vcat(F_j), D1
+        return np.vstack(self.factors)
+
+    @property
     def design_matrix(self) -> np.ndarray:           # :130-133
-        return np.hstack([self.w, self.factors[0]])
+        return np.hstack([self.w, self.F])
 
     @property
     def handle(self):
@@ -297,8 +315,6 @@ def DynamicFactorModel(y, w, x, number_of_factors: Union[int, str, None] = None,
     if factor_type != "principal components":
         raise NotImplementedError(f"factor_type {factor_type!r}: the reference branch is broken "
                                   "(defect D6) and out of scope")
-    if len(break_indices):
-        raise NotImplementedError("break-aware PCA (SURVEY §8(f) next #3) is not built yet")
     if number_of_factor_lags:
         raise NotImplementedError("factor lags are unfinished in the reference (:35-37)")
     y = _f64(y).ravel()
@@ -321,9 +337,12 @@ def DynamicFactorModel(y, w, x, number_of_factors: Union[int, str, None] = None,
     km = int(kmax) if kmax else 0
     xc, wc = _colmajor(x), _colmajor(w)
     h = C.c_void_p()
-    ctx.check(ctx.lib.dfm_model_fit(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p),
-                                    w.shape[1], T, xc.ctypes.data_as(_lib.c_double_p), T, N, T,
-                                    r, code, km, C.byref(h)))
+    # 1-based break_indices (first rows of blocks 2..), :73 -> 0-based rows
+    brk = np.asarray([int(b) - 1 for b in break_indices], dtype=np.int64)
+    ctx.check(ctx.lib.dfm_model_fit_breaks(
+        ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), w.shape[1], T,
+        xc.ctypes.data_as(_lib.c_double_p), T, N, T, r, code, km,
+        brk.ctypes.data_as(_lib.c_int64_p) if len(brk) else None, len(brk), C.byref(h)))
     res = DynamicFactorModelResult(ctx, h, y, w, x, crit, break_indices)
     res.targeted_predictors = (np.ones(N, dtype=bool) if targeted_predictors is None
                                else np.asarray(targeted_predictors, dtype=bool))
@@ -338,12 +357,15 @@ def calculate_factors(x, factor_type: str = "principal components", targeted_pre
     ctx = ctx or default_context()
     if factor_type != "principal components":
         raise NotImplementedError("only the principal-components branch exists (defect D6)")
-    if len(break_indices):
-        raise NotImplementedError("break-aware PCA is not built yet")
     x = _f64(x, 2)
     T, N = x.shape
     mfn = int(math.ceil(min(T, N) / 2))
     r = mfn if number_of_factors is None else min(int(number_of_factors), mfn)
+    if len(break_indices):
+        # per-block PCA with the full-sample T, N (:72, :98, D7) runs inside the
+        # model-fit entry point; its regression part is not read here
+        d = DynamicFactorModel(np.zeros(T), np.zeros((T, 0)), x, r, break_indices=break_indices, ctx=ctx)
+        return d.factors, d.loadings, r
     ev, F, L, tr = principal_components(x, r, ctx=ctx)
     return [F], [L], r
 

@@ -30,12 +30,14 @@ hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m,
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
 __global__ void colmajor_from_rows_kernel(const double *, int64_t, int, int, double *);
 int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb, const double *Uk,
-                   double *F, double *L, double *colssr, hipStream_t st);
+                   double *F, double *L, double *colssr, hipStream_t st, double Ts = 0, int64_t fstride = 0);
 __global__ void colssr_cols_kernel(const double *, int64_t, int64_t, int, int, const double *,
                                    const double *, double *);
 __global__ void common_residual_kernel(const double *, int64_t, int, int, int, const double *,
                                        const double *, double *, double *);
 __global__ void panel_row_ssq_kernel(const double *, int64_t, int, double *);
+__global__ void col_ssq_kernel(const double *, int64_t, int, int, double *);
+__global__ void block_accum_kernel(const double *, const double *, int, int, double *, double *, int);
 __global__ void ordered_sum_kernel(const double *, int, double *);
 __global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, const int *,
                                const int *, double *,
@@ -117,6 +119,13 @@ struct dfm_model {
   bool fact_ready = false;
   int64_t ldH = 0;
   double *H = nullptr, *EL = nullptr, *S = nullptr, *cF = nullptr, *hd = nullptr;
+  // break blocks (src/DynamicFactorModel.jl:73, :98): first row, rows, Gram
+  // size, per-block eigenvectors (Gram size x r) and loadings (N x r); block 0's
+  // are aliased by Ub and L
+  int nblk = 1;
+  std::vector<int> ba, bt, bm;
+  std::vector<double *> Ubs, Ls;
+  std::vector<std::vector<double>> blam;
 };
 
 static int fail(dfm_ctx *ctx, int code, const char *fmt, ...) {
@@ -337,6 +346,8 @@ int dfm_model_destroy(dfm_model *m) {
   for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->L, m->Ub, m->colssr, m->H, m->EL, m->S,
                     m->cF, m->hd})
     hipFree(p);
+  for (size_t j = 1; j < m->Ubs.size(); ++j) hipFree(m->Ubs[j]);
+  for (size_t j = 1; j < m->Ls.size(); ++j) hipFree(m->Ls[j]);
   hipFree(m->ws);
   hipFree(m->sd_dev);
   hipFree(m->flag_dev);
@@ -349,6 +360,12 @@ int dfm_model_destroy(dfm_model *m) {
 int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                   const double *X, int64_t T64, int64_t N64, int64_t ldx, int r, int crit, int kmax,
                   dfm_model **out) {
+  return dfm_model_fit_breaks(ctx, y, w, q, ldw, X, T64, N64, ldx, r, crit, kmax, nullptr, 0, out);
+}
+
+int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                         const double *X, int64_t T64, int64_t N64, int64_t ldx, int r, int crit,
+                         int kmax, const int64_t *breaks, int nbreaks, dfm_model **out) {
   if (!ctx || !out) return -1;
   *out = nullptr;
   if (!y || !X || T64 < 2 || N64 < 1 || ldx < T64 || q < 0 || (q > 0 && (!w || ldw < T64)))
@@ -356,6 +373,10 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   if (T64 > (1 << 24) || N64 > (1 << 24)) return fail(ctx, -2, "panel too large");
   if (crit < -1 || crit > 6) return fail(ctx, -3, "unknown criterion %d", crit);
   if (r <= 0 && crit < 0) return fail(ctx, -3, "IC sweep needs a criterion");
+  if (nbreaks < 0 || (nbreaks > 0 && !breaks)) return fail(ctx, -2, "dfm_model_fit: bad break list");
+  for (int j = 0; j < nbreaks; ++j)   // src/DynamicFactorModel.jl:73: vcat(1, breaks, T+1)
+    if (breaks[j] <= (j ? breaks[j - 1] : 0) || breaks[j] >= T64)
+      return fail(ctx, -9, "break indices must increase strictly inside 1..T-1 (0-based rows)");
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   const int T = (int)T64, N = (int)N64, m = std::min(T, N);
@@ -363,19 +384,43 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   dfm_model *M = new dfm_model();
   ++ctx->refs;
   M->ctx = ctx; M->T = T; M->N = N; M->q = q; M->crit = crit; M->m = m;
-  M->orient = (N > T) ? 0 : 1;  // src/DynamicFactorModel.jl:77 (T >= N) vs :86 (N > T)
+  // src/DynamicFactorModel.jl:77 (T >= N) vs :86 (N > T), with the FULL-sample
+  // T and N for every break block (:72, defect D7)
+  M->orient = (N > T) ? 0 : 1;
   M->ld = round_up(N, 16);
-  auto bail = [&](int code) { dfm_model_destroy(M); return code; };
-  int rc = 0;
+  const int nblk = nbreaks + 1;
+  M->nblk = nblk;
+  for (int j = 0; j < nblk; ++j) {
+    const int a = j ? (int)breaks[j - 1] : 0, e = j < nbreaks ? (int)breaks[j] : T;
+    M->ba.push_back(a);
+    M->bt.push_back(e - a);
+    M->bm.push_back(M->orient == 0 ? e - a : N);   // size of the block's Gram
+  }
+  const bool nob = nblk == 1;
+  std::vector<double *> Gb(nblk, nullptr), lamd(nblk, nullptr), Ukd(nblk, nullptr);
+  std::vector<double *> tmp;   // freed on every exit path below
+  auto tfree = [&]() {
+    for (int j = 0; j < nblk; ++j) {
+      if (!nob) hipFree(Gb[j]);
+      hipFree(lamd[j]); hipFree(Ukd[j]);
+      Gb[j] = lamd[j] = Ukd[j] = nullptr;
+    }
+    for (double *p : tmp) hipFree(p);
+    tmp.clear();
+  };
+  auto bail = [&](int code) { tfree(); dfm_model_destroy(M); return code; };
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return bail(fail(ctx, 1000 + (int)e_, "HIP %s line %d", hipGetErrorString(e_), __LINE__)); } while (0)
+#define LCK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(ctx, 1000 + (int)e_, "HIP %s line %d", hipGetErrorString(e_), __LINE__); } while (0)
+#define CKB(x) do { int r_ = (x); if (r_) return bail(r_); } while (0)
+#define TALLOC(p, n) do { CK(dalloc(&(p), (n))); tmp.push_back((double *)(p)); } while (0)
   const size_t panel = (size_t)T * M->ld;
   CK(dalloc(&M->Xp, panel));
   CK(dalloc(&M->Cp, panel));
   CK(dalloc(&M->Ep, panel));
   CK(dalloc(&M->y, T));
   CK(dalloc(&M->w, (size_t)T * std::max(q, 1)));
-  double *Xraw = nullptr, *G = nullptr;
-  CK(dalloc(&Xraw, (size_t)T * N));
+  double *Xraw = nullptr;
+  TALLOC(Xraw, (size_t)T * N);
   CK(hipMemcpy2DAsync(Xraw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(M->y, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
   if (q > 0) CK(hipMemcpy2DAsync(M->w, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
@@ -385,67 +430,119 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
                        dim3(256), 0, st, Xraw, (int64_t)T, T, N, M->Xp, M->ld);
   }
   CK(hipGetLastError());
-  CK(dalloc(&G, (size_t)m * m));
-  PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld};
-  {
+  // block j's panel: rows ba[j] .. ba[j] + bt[j] - 1 of X
+  auto block_src = [&](int j) { return PanelSrc{nullptr, M->Xp + (size_t)M->ba[j] * M->ld, nullptr, nullptr, M->ld, 0}; };
+  auto block_gram = [&](int j, double *G) -> hipError_t {
     Scope sc(ctx, DFM_KC_GRAM);
-    CK(launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
-  }
-  // --- how many eigenvalues: the IC sweep needs kmax, PCp needs sigma^2 = V(ceil(m/2))
+    return launch_gram(M->orient, block_src(j), M->bm[j], M->orient == 0 ? N : M->bt[j], M->bt[j], G,
+                       M->bm[j], (int64_t)M->bm[j] * M->bm[j], 1, st);
+  };
+  auto spectrum = [&](const double *G, int mm, std::vector<double> &sp) -> int {
+    double *ev = nullptr;
+    LCK(dalloc(&ev, mm));
+    tmp.push_back(ev);
+    {
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      LCK(launch_spectrum(G, mm, (int64_t)mm * mm, mm, 1, ev, st));
+    }
+    sp.resize(mm);
+    LCK(hipMemcpyAsync(sp.data(), ev, (size_t)mm * 8, hipMemcpyDeviceToHost, st));
+    LCK(hipStreamSynchronize(st));
+    return 0;
+  };
   const bool pcp = crit >= 0 && crit <= 2;
   if (kmax <= 0) kmax = mfn;  // src/DynamicFactorModel.jl:54 (D11)
   kmax = std::min(kmax, mfn);
   M->kmax = kmax;
-  std::vector<double> spec;
-  double trace = 0.0;
+  const double NT = (double)N * (double)T;
+  // --- PCp's sigma^2 = V(ceil(m/2)) of the UNRESTRICTED fit DynamicFactorModel(y, w, x):
+  // full sample, no breaks (src/criteria.jl:18, :23, :28)
+  double *Gfull = nullptr;
+  std::vector<double> spec_full;
   // the sweep reports all 7 criteria: PCp rows need sigma^2 (NaN when the full
   // spectrum is out of reach and the chosen criterion is not a PCp one)
-  const bool need_spec = pcp || (r <= 0 && kmax > 24) || (r <= 0 && m <= spectrum_max());
-  if (need_spec) {
-    if (m > spectrum_max()) {
-      hipFree(Xraw); hipFree(G);
-      return bail(fail(ctx, -30, "PCp criteria / kmax > 24 need the full spectrum; supported for "
-                                 "min(T,N) <= %d (got %d)", spectrum_max(), m));
-    }
-    double *ev = nullptr;
-    CK(dalloc(&ev, m));
-    {
-      Scope sc(ctx, DFM_KC_EIG_OTHER);
-      CK(launch_spectrum(G, m, (int64_t)m * m, m, 1, ev, st));
-    }
-    spec.resize(m);
-    CK(hipMemcpyAsync(spec.data(), ev, (size_t)m * 8, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
-    hipFree(ev);
-    for (double v : spec) trace += v;  // replaced below by the Gram trace
+  const bool full_spec = pcp || (nob && r <= 0 && (kmax > 24 || m <= spectrum_max()));
+  if (full_spec && m > spectrum_max()) {
+    return bail(fail(ctx, -30, "PCp criteria / kmax > 24 need the full spectrum; supported for "
+                               "min(T,N) <= %d (got %d)", spectrum_max(), m));
   }
-  // --- top-k eigenpairs
-  const int k_eig = (r <= 0) ? (need_spec ? 1 : kmax) : std::min(r, mfn);
-  int kk = std::max(k_eig, 1);
-  double *lam_d = nullptr, *Uk = nullptr, *tr_d = nullptr;
+  if (nob || full_spec) {
+    TALLOC(Gfull, (size_t)m * m);
+    PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld, 0};
+    Scope sc(ctx, DFM_KC_GRAM);
+    CK(launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, Gfull, m, (int64_t)m * m, 1, st));
+  }
+  if (full_spec) {
+    CKB(spectrum(Gfull, m, spec_full));
+    double s = 0.0;
+    for (double v : spec_full) s += v;
+    for (int j = 0; j < mfn; ++j) s -= spec_full[j];
+    M->sigma2 = s / NT;
+  }
+  // --- per block: Gram, the eigenvalues the sweep needs, trace
+  std::vector<int> kk(nblk, 0);
+  std::vector<std::vector<double>> bev(nblk), blam(nblk);
+  std::vector<double> btr(nblk, 0.0);
+  double *tr_d = nullptr;
   int *st_d = nullptr;
-  CK(dalloc(&lam_d, kk)); CK(dalloc(&Uk, (size_t)m * kk)); CK(dalloc(&tr_d, 1)); CK(dalloc(&st_d, 1));
-  rc = run_eig(ctx, G, m, 1, kk, nullptr, 0, lam_d, Uk, tr_d, st_d);
-  if (rc) { hipFree(Xraw); hipFree(G); return bail(rc); }
-  std::vector<double> lam(kk);
-  int est = 0;
-  CK(hipMemcpyAsync(lam.data(), lam_d, (size_t)kk * 8, hipMemcpyDeviceToHost, st));
-  CK(hipMemcpyAsync(&trace, tr_d, 8, hipMemcpyDeviceToHost, st));
-  CK(hipMemcpyAsync(&est, st_d, 4, hipMemcpyDeviceToHost, st));
-  CK(hipStreamSynchronize(st));
-  if (est) { hipFree(Xraw); hipFree(G); return bail(fail(ctx, 2, "eigensolver did not converge")); }
-  const double NT = (double)N * (double)T;
-  // eigenvalues used by the sweep: full spectrum when computed, else the top-k
-  const std::vector<double> &ev = need_spec ? spec : lam;
-  if (need_spec) {
-    double s = trace;
-    for (int j = 0; j < mfn; ++j) s -= spec[j];
-    M->sigma2 = s / NT;   // V of DynamicFactorModel(y, w, x), src/criteria.jl:18
+  TALLOC(tr_d, 1);
+  CK(dalloc(&st_d, 1));
+  tmp.push_back((double *)st_d);
+  auto top_eig = [&](int j, int k) -> int {
+    hipFree(lamd[j]); hipFree(Ukd[j]);
+    lamd[j] = Ukd[j] = nullptr;
+    LCK(dalloc(&lamd[j], k)); LCK(dalloc(&Ukd[j], (size_t)M->bm[j] * k));
+    kk[j] = k;
+    int rc2 = run_eig(ctx, Gb[j], M->bm[j], 1, k, nullptr, 0, lamd[j], Ukd[j], tr_d, st_d);
+    if (rc2) return rc2;
+    int est = 0;
+    blam[j].resize(k);
+    LCK(hipMemcpyAsync(blam[j].data(), lamd[j], (size_t)k * 8, hipMemcpyDeviceToHost, st));
+    LCK(hipMemcpyAsync(&btr[j], tr_d, 8, hipMemcpyDeviceToHost, st));
+    LCK(hipMemcpyAsync(&est, st_d, 4, hipMemcpyDeviceToHost, st));
+    LCK(hipStreamSynchronize(st));
+    if (est) return fail(ctx, 2, "eigensolver did not converge");
+    return 0;
+  };
+  const int r_req = (r <= 0) ? kmax : std::min(r, mfn);
+  for (int j = 0; j < nblk; ++j) {
+    // the reference slices F_j[:, 1:k] (:33, :131): a block needs >= k eigenpairs
+    if (M->bm[j] < r_req)
+      CKB(fail(ctx, -9, "break block %d has %d rows: fewer than the %d factors requested", j, M->bt[j], r_req));
+    if (nob) Gb[j] = Gfull;
+    else {
+      CKB(dalloc(&Gb[j], (size_t)M->bm[j] * M->bm[j]) == hipSuccess ? 0 : fail(ctx, 1002, "out of memory"));
+      CKB(block_gram(j, Gb[j]) == hipSuccess ? 0 : fail(ctx, 1001, "block Gram failed"));
+    }
+    if (r <= 0) {   // the sweep's eigenvalues of this block
+      if (nob && full_spec) bev[j] = spec_full;
+      else if (!nob && M->bm[j] <= spectrum_max() && (kmax > 24 || pcp)) {
+        std::vector<double> sp;
+        CKB(spectrum(Gb[j], M->bm[j], sp));
+        bev[j] = sp;
+      } else if (kmax > 24) {
+        CKB(fail(ctx, -30, "kmax > 24 needs the full spectrum of every block; supported for Gram "
+                           "size <= %d (block %d: %d)", spectrum_max(), j, M->bm[j]));
+      }
+      // top-k pairs: the trace, and the sweep's eigenvalues when no spectrum
+      CKB(top_eig(j, bev[j].empty() ? kmax : 1));
+      if (bev[j].empty()) bev[j] = blam[j];
+    } else {
+      CKB(top_eig(j, r_req));
+      bev[j] = blam[j];
+    }
   }
+  double trace = 0.0;
+  for (int j = 0; j < nblk; ++j) trace += btr[j];
+  // eigenvalue i summed over blocks: V(k) = (trace - sum_{i<=k} ev[i]) / (N T)
+  const int n_ev = (int)bev[0].size();
+  std::vector<double> ev(n_ev, 0.0);
+  for (int j = 0; j < nblk; ++j)
+    for (int i = 0; i < n_ev && i < (int)bev[j].size(); ++i) ev[i] += bev[j][i];
   if (r <= 0) {
     M->swept = true;
     M->ic.assign(7 * kmax, 0.0);
-    dfm_ic_sweep(ev.data(), (int)ev.size(), kmax, trace, T, N, need_spec ? M->sigma2 : NAN, M->ic.data());
+    dfm_ic_sweep(ev.data(), (int)ev.size(), kmax, trace, T, N, full_spec ? M->sigma2 : NAN, M->ic.data());
     int best = 0;
     for (int k = 1; k < kmax; ++k)   // first argmin, indmin (src/DynamicFactorModel.jl:65)
       if (M->ic[crit * kmax + k] < M->ic[crit * kmax + best]) best = k;
@@ -453,69 +550,78 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   }
   r = std::min(r, mfn);   // src/DynamicFactorModel.jl:116-119
   M->r = r;
-  if (r > kk) {   // the sweep used the full spectrum: now the r eigenvectors
-    hipFree(lam_d); hipFree(Uk);
-    kk = r;
-    CK(dalloc(&lam_d, kk)); CK(dalloc(&Uk, (size_t)m * kk));
-    rc = run_eig(ctx, G, m, 1, kk, nullptr, 0, lam_d, Uk, tr_d, st_d);
-    if (rc) { hipFree(Xraw); hipFree(G); return bail(rc); }
-    lam.resize(kk);
-    CK(hipMemcpyAsync(lam.data(), lam_d, (size_t)kk * 8, hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(&est, st_d, 4, hipMemcpyDeviceToHost, st));
-    CK(hipStreamSynchronize(st));
-    if (est) { hipFree(Xraw); hipFree(G); return bail(fail(ctx, 2, "eigensolver did not converge")); }
-  }
-  // eigenvalues reported: kmax of the sweep (when it ran) or r
+  for (int j = 0; j < nblk; ++j)
+    if (r > kk[j]) CKB(top_eig(j, r));   // the sweep used spectra: now the r eigenvectors
+  // eigenvalues reported: kmax of the sweep (when it ran) or r; per block summed
   {
     const size_t ne = (size_t)(M->swept ? std::max(kmax, r) : r);
     M->lam.assign(ne, NAN);
     for (size_t j = 0; j < ne && j < ev.size(); ++j) M->lam[j] = ev[j];
+    for (int i = 0; i < r; ++i) {
+      double s = 0.0;
+      for (int j = 0; j < nblk; ++j) s += blam[j][i];
+      M->lam[i] = s;
+    }
+    M->blam.resize(nblk);
+    for (int j = 0; j < nblk; ++j) M->blam[j].assign(blam[j].begin(), blam[j].begin() + r);
   }
-  M->k_eig = kk;
-  // --- factors, loadings for r (first r canonical eigenvectors)
-  CK(dalloc(&M->Ub, (size_t)m * r));
+  M->k_eig = kk[0];
+  // --- factors, loadings per block for r (first r canonical eigenvectors)
   CK(dalloc(&M->F, (size_t)T * r));
-  CK(dalloc(&M->L, (size_t)N * r));
   CK(dalloc(&M->colssr, N));
-  CK(hipMemcpy2DAsync(M->Ub, (size_t)r * 8, Uk, (size_t)kk * 8, (size_t)r * 8, m, hipMemcpyDeviceToDevice, st));
-  {
+  M->Ubs.assign(nblk, nullptr);
+  M->Ls.assign(nblk, nullptr);
+  for (int j = 0; j < nblk; ++j) {
+    const int mj = M->bm[j];
+    CK(dalloc(&M->Ubs[j], (size_t)mj * r));
+    CK(dalloc(&M->Ls[j], (size_t)N * r));
+    if (j == 0) { M->Ub = M->Ubs[0]; M->L = M->Ls[0]; }
+    CK(hipMemcpy2DAsync(M->Ubs[j], (size_t)r * 8, Ukd[j], (size_t)kk[j] * 8, (size_t)r * 8, mj,
+                        hipMemcpyDeviceToDevice, st));
+  }
+  for (int j = 0; j < nblk; ++j) {
     Scope sc(ctx, DFM_KC_FACTORS);
-    if (launch_factors(M->orient, src, T, N, r, 1, M->Ub, M->F, M->L, M->colssr, st))
-      return bail(fail(ctx, -4, "r=%d too large", r));
-    if (M->orient == 1) {
+    if (launch_factors(M->orient, block_src(j), M->bt[j], N, r, 1, M->Ubs[j], M->F + (size_t)M->ba[j] * r,
+                       M->Ls[j], nob ? M->colssr : nullptr, st, (double)T, 0))
+      CKB(fail(ctx, -4, "r=%d too large", r));
+    if (nob && M->orient == 1) {
       double *lr = nullptr;
       CK(dalloc(&lr, r));
-      CK(hipMemcpyAsync(lr, lam_d, (size_t)r * 8, hipMemcpyDeviceToDevice, st));
-      hipLaunchKernelGGL(colssr_cols_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, st, G, m,
+      CK(hipMemcpyAsync(lr, lamd[0], (size_t)r * 8, hipMemcpyDeviceToDevice, st));
+      hipLaunchKernelGGL(colssr_cols_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, st, Gfull, m,
                          (int64_t)m * m, N, r, lr, M->Ub, M->colssr);
       CK(hipStreamSynchronize(st));
       hipFree(lr);
     }
   }
-  {
+  for (int j = 0; j < nblk; ++j) {   // :33 per subperiod
     Scope sc(ctx, DFM_KC_MISC);
-    hipLaunchKernelGGL(common_residual_kernel, dim3((unsigned)((M->ld + 255) / 256), T), dim3(256), 0,
-                       st, M->Xp, M->ld, T, N, r, M->F, M->L, M->Cp, M->Ep);
+    const size_t o = (size_t)M->ba[j] * M->ld;
+    hipLaunchKernelGGL(common_residual_kernel, dim3((unsigned)((M->ld + 255) / 256), M->bt[j]), dim3(256), 0,
+                       st, M->Xp + o, M->ld, M->bt[j], N, r, M->F + (size_t)M->ba[j] * r, M->Ls[j], M->Cp + o,
+                       M->Ep + o);
   }
   CK(hipGetLastError());
+  if (!nob)
+    hipLaunchKernelGGL(col_ssq_kernel, dim3((N + 255) / 256), dim3(256), 0, st, M->Ep, M->ld, T, N, M->colssr);
   // --- V(r) by brute force over the explicit residual panel (src/criteria.jl:5)
   double essq = 0.0;
   {
     double *rows = nullptr, *tot = nullptr;
-    CK(dalloc(&rows, T)); CK(dalloc(&tot, 1));
+    TALLOC(rows, T); TALLOC(tot, 1);
     hipLaunchKernelGGL(panel_row_ssq_kernel, dim3(T), dim3(256), 0, st, M->Ep, M->ld, T, rows);
     hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, st, rows, T, tot);
     CK(hipMemcpyAsync(&essq, tot, 8, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
-    hipFree(rows); hipFree(tot);
   }
-  // --- OLS + HC2 on [w F_r]
+  // --- OLS + HC2 on [w vcat(F_j)] (:40-48, :130-133)
   const int d = q + r;
   if (d > 32) return bail(fail(ctx, -5, "q + r = %d > 32 unsupported", d));
   double *coef = nullptr, *tst = nullptr, *cov = nullptr, *res = nullptr;
   int *ost = nullptr;
-  CK(dalloc(&coef, d)); CK(dalloc(&tst, d)); CK(dalloc(&cov, (size_t)d * d)); CK(dalloc(&res, T));
+  TALLOC(coef, d); TALLOC(tst, d); TALLOC(cov, (size_t)d * d); TALLOC(res, T);
   CK(dalloc(&ost, 1));
+  tmp.push_back((double *)ost);
   {
     Scope sc(ctx, DFM_KC_OLS);
     hipLaunchKernelGGL(ols_hc2_kernel, dim3(1), dim3(256), 0, st, M->y, M->w, q, M->F, T, r, nullptr, nullptr, coef,
@@ -530,8 +636,7 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
   CK(hipMemcpyAsync(M->resid.data(), res, (size_t)T * 8, hipMemcpyDeviceToHost, st));
   CK(hipMemcpyAsync(&ols_bad, ost, 4, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
-  for (double *p : {Xraw, G, lam_d, Uk, tr_d, coef, tst, cov, res}) hipFree(p);
-  hipFree(st_d); hipFree(ost);
+  tfree();
   if (ols_bad) return bail(fail(ctx, 3, "singular design matrix D'D"));
   M->trace = trace;
   M->V = essq / NT;
@@ -547,11 +652,33 @@ int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t
       case 6: M->critval = M->V + r * std::log((double)T) / T; break;
     }
   }
-  for (int j = 0; j < r && j < (int)M->lam.size(); ++j) M->lam[j] = lam[j];
   CK(dalloc(&M->flag_dev, 4));
   *out = M;
   return 0;
+#undef CKB
+#undef LCK
+#undef TALLOC
 #undef CK
+}
+
+int dfm_model_blocks(const dfm_model *m) { return m ? m->nblk : -1; }
+
+int dfm_model_block(const dfm_model *m, int j, int64_t *row0, int64_t *rows, double *eigvals, double *L) {
+  if (!m) return -1;
+  if (j < 0 || j >= m->nblk) return fail(m->ctx, -2, "block %d out of range", j);
+  if (row0) *row0 = m->ba[j];
+  if (rows) *rows = m->bt[j];
+  if (eigvals) std::copy(m->blam[j].begin(), m->blam[j].end(), eigvals);
+  if (L) {
+    dfm_ctx *ctx = m->ctx;
+    hipSetDevice(ctx->device);
+    std::vector<double> tmp((size_t)m->N * m->r);
+    HIPCHK(ctx, hipMemcpyAsync(tmp.data(), m->Ls[j], tmp.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < m->N; ++i)
+      for (int c = 0; c < m->r; ++c) L[(size_t)c * m->N + i] = tmp[(size_t)i * m->r + c];
+  }
+  return 0;
 }
 
 int dfm_model_dims(const dfm_model *m, int64_t *r, int64_t *kmax, int64_t *n_eig) {
@@ -629,7 +756,7 @@ int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
 
 // Per-batch device workspace layout for the bootstrap.
 struct BootWs {
-  double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat;
+  double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat, *blam, *btr;
   int *status, *ost, *off, *lst;
   char *eig, *chow, *fact, *fload;
   size_t eig_bytes, chow_bytes, fact_bytes, fload_bytes;
@@ -649,6 +776,8 @@ static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool c
   w.colssr = (double *)take((size_t)nb * N * 8);
   w.coef = (double *)take((size_t)nb * d * 8);
   w.tstat = (double *)take((size_t)nb * d * 8);
+  w.blam = (double *)take(M->nblk > 1 ? (size_t)nb * r * 8 : 8);   // one break block's lambdas
+  w.btr = (double *)take(M->nblk > 1 ? (size_t)nb * 8 : 8);
   w.status = (int *)take((size_t)nb * 4);
   w.ost = (int *)take((size_t)nb * 4);
   w.eig_bytes = eig_workspace_bytes_padded(m, nb, P, maxit);
@@ -663,6 +792,11 @@ static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool c
   w.lst = (int *)take(fact ? (size_t)nb * T * 4 : 4);
   if (o) *o = w;
   return off;
+}
+
+__global__ void or_flag_kernel(const int *s, int nb, int *flag, int bit) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb && s[i]) atomicOr(flag, bit);
 }
 
 __global__ void or_status_kernel(const int *s1, const int *s2, int nb, int *flag) {
@@ -701,6 +835,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     if (s.kind >= DFM_STAT_LR) {
       if (s.arg0 < r || s.arg0 > T - r) return fail(ctx, -7, "break period %d out of range", s.arg0);
       if (chow && s.arg0 != chow_bp) return fail(ctx, -7, "one break period per call");
+      if (M->nblk > 1) return fail(ctx, -7, "Chow statistics of a model fitted with break_indices are not "
+                                           "supported (the tests read one loadings matrix: defect D1)");
       chow = true; chow_bp = s.arg0;
       if (s.kind <= DFM_STAT_WALD && (s.arg1 < 0 || s.arg1 >= N)) return fail(ctx, -7, "variable index");
     }
@@ -717,7 +853,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
   const int p = eig_block_p(m, r, ctx->block);
   const int P = p <= 16 ? 16 : 32;
-  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32;
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1;
   int64_t nb = M->batch;
   if (nb <= 0) {
     if (fact) {
@@ -744,7 +880,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     HIPCHK(ctx, dalloc(&M->cF, T));
     HIPCHK(ctx, dalloc(&M->hd, T));
     HIPCHK(ctx, hipMemsetAsync(M->H, 0, (size_t)T * M->ldH * 8, st));
-    PanelSrc es{nullptr, M->Ep, nullptr, nullptr, M->ld};
+    PanelSrc es{nullptr, M->Ep, nullptr, nullptr, M->ld, 0};
     {
       Scope sc(ctx, DFM_KC_GRAM);
       HIPCHK(ctx, launch_gram(0, es, T, N, T, M->H, M->ldH, 0, 1, st));
@@ -773,7 +909,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   FactBase fb{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd};
   for (int64_t b0 = 0; b0 < B; b0 += nb) {
     const int n = (int)std::min<int64_t>(nb, B - b0);
-    PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld};
+    PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld, T};
     if (fact) {
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
@@ -783,6 +919,29 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       Scope sc(ctx, DFM_KC_FACTORS);
       rc = fact_loadings(fb, M->Ep, M->ld, N, M->L, w.Uk, et, w.off, w.lst, n, w.F, w.L, w.fload, st);
       if (rc) return fail(ctx, rc, "factored loadings failed");
+    } else if (M->nblk > 1) {
+      // refit per break block (src/bootstrap.jl:36, :48 pass dfm.break_indices):
+      // block j of X*_b is rows a..a+t_j-1 of C + diag(eta_b) E[idx_b, :]
+      for (int j = 0; j < M->nblk; ++j) {
+        const int a = M->ba[j], tj = M->bt[j], mj = M->bm[j];
+        PanelSrc sj{M->Cp + (size_t)a * M->ld, M->Ep, idx + b0 * T + a,
+                    kind == DFM_BOOT_WILD ? eta + b0 * T + a : nullptr, M->ld, T};
+        {
+          Scope sc(ctx, DFM_KC_GRAM);
+          HIPCHK(ctx, launch_gram(M->orient, sj, mj, M->orient == 0 ? N : tj, tj, w.G, mj, (int64_t)mj * mj, n, st));
+        }
+        const int pj = eig_block_p(mj, r, ctx->block);
+        int rc = eig_run(w.G, mj, (int64_t)mj * mj, mj, n, r, pj, M->Ubs[j], r, etol, ctx->maxit, ctx->poll,
+                         w.eig, w.blam, w.Uk, w.btr, w.status, nullptr, st, timer_cb, ctx, b0);
+        if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+        note_iters(ctx);
+        hipLaunchKernelGGL(or_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, n, M->flag_dev, 1);
+        Scope sc(ctx, DFM_KC_FACTORS);
+        launch_factors(M->orient, sj, tj, N, r, n, w.Uk, w.F + (size_t)a * r, w.L, nullptr, st, (double)T,
+                       (int64_t)T * r);
+        hipLaunchKernelGGL(block_accum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.blam, w.btr, n, r,
+                           w.lam, w.trace, j == 0 ? 1 : 0);
+      }
     } else {
       {
         Scope sc(ctx, DFM_KC_GRAM);
@@ -918,7 +1077,7 @@ int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, int64_t ldx
   HIPCHK(ctx, dalloc(&G, (size_t)m * m));
   HIPCHK(ctx, dalloc(&lam, k)); HIPCHK(ctx, dalloc(&Uk, (size_t)m * k)); HIPCHK(ctx, dalloc(&tr, 1));
   HIPCHK(ctx, dalloc(&Fd, (size_t)T * k)); HIPCHK(ctx, dalloc(&Ld, (size_t)N * k)); HIPCHK(ctx, dalloc(&sd, 1));
-  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld};
+  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld, 0};
   {
     Scope sc(ctx, DFM_KC_GRAM);
     HIPCHK(ctx, launch_gram(orient, src, m, orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
@@ -962,7 +1121,7 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
   double *G = nullptr, *ev = nullptr;
   HIPCHK(ctx, dalloc(&G, (size_t)m * m));
   HIPCHK(ctx, dalloc(&ev, m));
-  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld};
+  PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld, 0};
   {
     Scope sc(ctx, DFM_KC_GRAM);
     HIPCHK(ctx, launch_gram(orient, src, m, orient == 0 ? N : T, T, G, m, (int64_t)m * m, 1, st));
@@ -994,7 +1153,7 @@ int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald)
   const size_t bytes = chow_workspace_bytes(M->T, M->N, M->r, 1);
   char *ws = nullptr;
   HIPCHK(ctx, hipMalloc(&ws, bytes));
-  PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld};
+  PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld, 0};
   {
     Scope sc(ctx, DFM_KC_CHOW);
     HIPCHK(ctx, launch_chow(M->orient, src, M->T, M->N, M->r, (int)bp, 1, M->F, M->L, nullptr, nullptr,
@@ -1132,7 +1291,7 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
     if (!H || !zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
     HIPCHK(ctx, hipMemsetAsync(H, 0, (size_t)T * ldH * 8, st));
     HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
-    PanelSrc es{nullptr, dp.P, nullptr, nullptr, dp.ld};
+    PanelSrc es{nullptr, dp.P, nullptr, nullptr, dp.ld, 0};
     {
       Scope sc(ctx, DFM_KC_GRAM);
       HIPCHK(ctx, launch_gram(0, es, T, N, T, H, ldH, 0, 1, st));   // ONE Gram for every window
@@ -1150,7 +1309,7 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
   } else {
     double *G = (double *)dal((size_t)P * N * N * 8), *Ld = (double *)dal((size_t)P * N * kmax * 8);
     if (!G || !Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
-    PanelSrc src{nullptr, dp.P, didx, deta, dp.ld};
+    PanelSrc src{nullptr, dp.P, didx, deta, dp.ld, T};
     {
       Scope sc(ctx, DFM_KC_GRAM);
       HIPCHK(ctx, launch_gram(1, src, N, T, T, G, N, (int64_t)N * N, P, st));

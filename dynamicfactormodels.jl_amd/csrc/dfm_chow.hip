@@ -116,8 +116,8 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
     reinterpret_cast<double *>(&P)[e] = reinterpret_cast<const double *>(prep + rep)[e];
   const double *Fr = F + (int64_t)rep * T * r;
   const double *Zr = Z + (int64_t)rep * T * r;
-  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * T : nullptr;
-  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * T : nullptr;
+  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * src.rs : nullptr;
+  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * src.rs : nullptr;
   const bool ok = i < N;
   auto stage = [&](int t0) {
     for (int e = tid; e < TR * R; e += 256) {

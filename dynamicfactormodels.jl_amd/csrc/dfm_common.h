@@ -11,7 +11,8 @@ namespace dfm {
 //   X*[t, n] = C[t, n] + eta_b[t] * E[idx_b[t], n]
 // C == nullptr -> 0, eta == nullptr -> 1, idx == nullptr -> identity.
 // C and E are row-major T x N with row stride `ld` (elements); idx/eta are
-// B x T row-major.  This is the wild/residual bootstrap of
+// B x rs row-major (rs = T except for a break block, whose idx/eta rows are
+// the block's columns of the full B x T draws).  This is the wild/residual bootstrap of
 // src/bootstrap.jl:44-45 (:24 for the residual form) and, with C = E = X and
 // no idx/eta, the plain panel of principal_components (src/DynamicFactorModel.jl:75).
 struct PanelSrc {
@@ -20,6 +21,7 @@ struct PanelSrc {
   const int32_t *idx;
   const double *eta;
   int64_t ld;
+  int64_t rs;   // elements between consecutive replicates' idx / eta rows
 };
 
 // v_mfma_f64_4x4x4_4b_f64: 4 independent 4x4x4 blocks per instruction

@@ -51,8 +51,8 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
   const bool diag = (I == J);
   const int abase = I * GT, bbase = J * GT;
 
-  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * T : nullptr;
-  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * T : nullptr;
+  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * src.rs : nullptr;
+  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * src.rs : nullptr;
   const int64_t ld = src.ld;
 
   // ---------------- staging state: each thread moves 2 x 16-B chunks per operand

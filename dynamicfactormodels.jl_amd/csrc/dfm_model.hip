@@ -48,19 +48,20 @@ __global__ __launch_bounds__(256) void factors_rows_kernel(PanelSrc src, int T, 
                                                            const double *__restrict__ Uk,
                                                            double *__restrict__ F,
                                                            double *__restrict__ L,
-                                                           double *__restrict__ colssr) {
+                                                           double *__restrict__ colssr, double Ts,
+                                                           int64_t fstride) {
   constexpr int TR = 64;
   __shared__ double sF[TR * KM];
   __shared__ double sE[TR];
   __shared__ int sI[TR];
   const int rep = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
-  const double sT = sqrt((double)T);
+  const double sT = sqrt(Ts);
   const double *U = Uk + (int64_t)rep * T * k;
-  double *Fr = F + (int64_t)rep * T * k;
+  double *Fr = F + (int64_t)rep * fstride;
   if (blockIdx.x == 0)
     for (int e = threadIdx.x; e < T * k; e += 256) Fr[e] = sT * U[e];
-  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * T : nullptr;
-  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * T : nullptr;
+  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * src.rs : nullptr;
+  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * src.rs : nullptr;
   double acc[KM];
 #pragma unroll
   for (int j = 0; j < KM; ++j) acc[j] = 0.0;
@@ -96,8 +97,8 @@ __global__ __launch_bounds__(256) void factors_rows_kernel(PanelSrc src, int T, 
     double *Lr = L + (int64_t)rep * N * k + (int64_t)n * k;
 #pragma unroll
     for (int j = 0; j < KM; ++j)
-      if (j < k) { const double l = acc[j] / T; Lr[j] = l; l2 = fma(l, l, l2); }
-    if (colssr) colssr[(int64_t)rep * N + n] = ss - T * l2;
+      if (j < k) { const double l = acc[j] / Ts; Lr[j] = l; l2 = fma(l, l, l2); }
+    if (colssr) colssr[(int64_t)rep * N + n] = ss - Ts * l2;
   }
 }
 
@@ -107,7 +108,8 @@ template <int KM, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
 __global__ __launch_bounds__(256) void factors_cols_kernel(PanelSrc src, int T, int N, int k,
                                                            const double *__restrict__ Uk,
                                                            double *__restrict__ F,
-                                                           double *__restrict__ L) {
+                                                           double *__restrict__ L,
+                                                           int64_t fstride) {
   const int rep = blockIdx.y, lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   const double sN = sqrt((double)N);
@@ -117,8 +119,8 @@ __global__ __launch_bounds__(256) void factors_cols_kernel(PanelSrc src, int T, 
     for (int e = threadIdx.x; e < N * k; e += 256) Lr[e] = sN * U[e];
   }
   if (t >= T) return;
-  const int er = HAS_IDX ? src.idx[(int64_t)rep * T + t] : t;
-  const double ev = HAS_ETA ? src.eta[(int64_t)rep * T + t] : 1.0;
+  const int er = HAS_IDX ? src.idx[(int64_t)rep * src.rs + t] : t;
+  const double ev = HAS_ETA ? src.eta[(int64_t)rep * src.rs + t] : 1.0;
   double acc[KM];
 #pragma unroll
   for (int j = 0; j < KM; ++j) acc[j] = 0.0;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(256) void factors_cols_kernel(PanelSrc src, int T, 
     for (int j = 0; j < KM; ++j)
       if (j < k) acc[j] = fma(x, U[(int64_t)n * k + j], acc[j]);
   }
-  double *Fr = F + (int64_t)rep * T * k + (int64_t)t * k;
+  double *Fr = F + (int64_t)rep * fstride + (int64_t)t * k;
 #pragma unroll
   for (int j = 0; j < KM; ++j) {
     const double s = wave_sum(acc[j]);
@@ -413,28 +415,62 @@ __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, doubl
 
 template <int KM>
 static void launch_factors_km(int orient, const PanelSrc &src, int T, int N, int k, int nb,
-                              const double *Uk, double *F, double *L, double *colssr, hipStream_t st) {
+                              const double *Uk, double *F, double *L, double *colssr, hipStream_t st,
+                              double Ts, int64_t fs) {
   const bool c = src.C, e = src.eta, x = src.idx;
 #define DFM_FR(C_, E_, X_)                                                                         \
   if (orient == 0)                                                                                 \
     hipLaunchKernelGGL((factors_rows_kernel<KM, C_, E_, X_>), dim3((N + 255) / 256, nb), dim3(256), \
-                       0, st, src, T, N, k, Uk, F, L, colssr);                                     \
+                       0, st, src, T, N, k, Uk, F, L, colssr, Ts, fs);                                     \
   else                                                                                             \
     hipLaunchKernelGGL((factors_cols_kernel<KM, C_, E_, X_>), dim3((T + 3) / 4, nb), dim3(256), 0, \
-                       st, src, T, N, k, Uk, F, L);
+                       st, src, T, N, k, Uk, F, L, fs);
   if (c && e && x) { DFM_FR(true, true, true) }
   else if (c && !e && x) { DFM_FR(true, false, true) }
   else { DFM_FR(false, false, false) }
 #undef DFM_FR
 }
+// T = rows of the panel block; Ts = the T of the sqrt(T) / (1/T) scaling
+// (the full-sample T for a break block, defect D7); F of replicate b starts at
+// F + b * fstride (the block's rows inside a stacked T x k factor matrix).
 int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb,
-                          const double *Uk, double *F, double *L, double *colssr, hipStream_t st) {
-  if (k <= 8) launch_factors_km<8>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
-  else if (k <= 16) launch_factors_km<16>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
-  else if (k <= 32) launch_factors_km<32>(orient, src, T, N, k, nb, Uk, F, L, colssr, st);
+                   const double *Uk, double *F, double *L, double *colssr, hipStream_t st,
+                   double Ts, int64_t fstride) {
+  if (Ts <= 0) Ts = T;
+  if (fstride <= 0) fstride = (int64_t)T * k;
+  if (k <= 8) launch_factors_km<8>(orient, src, T, N, k, nb, Uk, F, L, colssr, st, Ts, fstride);
+  else if (k <= 16) launch_factors_km<16>(orient, src, T, N, k, nb, Uk, F, L, colssr, st, Ts, fstride);
+  else if (k <= 32) launch_factors_km<32>(orient, src, T, N, k, nb, Uk, F, L, colssr, st, Ts, fstride);
   else return -1;
   return 0;
 }
 
+
+
+// ------------------------------------------------------------ break blocks
+// Per-variable ||E_n||^2 of a row-major residual panel, rows summed in order
+// (the per-variable SSR the Chow LR test reads, for a model fitted per break
+// block: src/DynamicFactorModel.jl:33 with break_indices).
+__global__ void col_ssq_kernel(const double *__restrict__ E, int64_t ld, int T, int N,
+                               double *__restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int t = 0; t < T; ++t) { const double v = E[(int64_t)t * ld + n]; s = fma(v, v, s); }
+  out[n] = s;
+}
+
+// Break blocks of a batch of replicates: the criteria read V(k) = (sum_j
+// trace(G_j) - sum_j sum_{i<=k} lambda_{j,i}) / (N T), so the per-block top-r
+// eigenvalues and traces are summed into one (lambda, trace) row per replicate.
+__global__ void block_accum_kernel(const double *__restrict__ lam_b, const double *__restrict__ tr_b,
+                                   int nb, int r, double *__restrict__ lam, double *__restrict__ tr,
+                                   int first) {
+  const int rep = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rep >= nb) return;
+  for (int j = 0; j < r; ++j)
+    lam[(int64_t)rep * r + j] = (first ? 0.0 : lam[(int64_t)rep * r + j]) + lam_b[(int64_t)rep * r + j];
+  tr[rep] = (first ? 0.0 : tr[rep]) + tr_b[rep];
+}
 
 }  // namespace dfm

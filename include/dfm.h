@@ -130,7 +130,27 @@ int dfm_ic_sweep(const double *eigvals, int n_eig, int kmax, double trace_G,
 int dfm_model_fit(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                   const double *X, int64_t T, int64_t N, int64_t ldx,
                   int r, int crit, int kmax, dfm_model **out);
+/* The same with structural breaks (src/DynamicFactorModel.jl:73, :98): the
+ * rows split into blocks at `breaks` (0-based first rows of blocks 2..nbreaks+1,
+ * strictly increasing inside 1..T-1 — the reference's 1-based break_indices
+ * minus 1).  Each block gets its own principal components with the FULL-sample
+ * T, N for branch choice and scaling (:72, defect D7); E = X - vcat(F_j L_j')
+ * (:33); the design matrix stacks the blocks' factors (:131).  The IC sweep
+ * reads V(k) = (sum_j trace G_j - sum_j sum_{i<=k} lambda_{j,i}) / (N T); PCp's
+ * sigma^2 is the no-break unrestricted fit (src/criteria.jl:18).  A block needs
+ * at least r (sweep: kmax) eigenpairs: -9 otherwise (the reference's
+ * F_j[:, 1:r] would raise).  Reported eigenvalue i is sum_j lambda_{j,i};
+ * per-block values and loadings via dfm_model_block.  nbreaks = 0 is
+ * dfm_model_fit. */
+int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                         const double *X, int64_t T, int64_t N, int64_t ldx, int r, int crit,
+                         int kmax, const int64_t *breaks, int nbreaks, dfm_model **out);
 int dfm_model_destroy(dfm_model *m);
+/* Number of break blocks (1 without breaks), and block j's first row, rows,
+ * top-r eigenvalues (r) and loadings L_j (N x r col-major); NULL skips. */
+int dfm_model_blocks(const dfm_model *m);
+int dfm_model_block(const dfm_model *m, int j, int64_t *row0, int64_t *rows, double *eigvals,
+                    double *L);
 /* Sizes of the arrays dfm_model_read fills: r, the IC-sweep kmax (0 when r was
  * given), n_eig = number of eigenvalues returned (max(r, kmax)). */
 int dfm_model_dims(const dfm_model *m, int64_t *r, int64_t *kmax, int64_t *n_eig);
@@ -149,7 +169,11 @@ int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *ts
 /* ------------------------------------------------------------- bootstrap
  * wild_bootstrap (src/bootstrap.jl:41-51) / residual_bootstrap (:21-39):
  * for b < B: X*_b = F_r L_r' + diag(eta_b) E[idx_b, :]  (eta == NULL for
- * RESIDUAL), refit at the model's r and criterion, emit the stats.
+ * RESIDUAL), refit at the model's r and criterion, emit the stats.  A model
+ * fitted with breaks refits per break block (:36, :48 pass break_indices);
+ * the common component is the blockwise vcat(F_j L_j'); the residual
+ * bootstrap's block-wise draws (:23-28) are the caller's idx.  Chow stats
+ * are refused for such models (-7).
  * idx: B x T int32 (row-major, 0-based), eta: B x T.  out: B rows of
  * sum(width(stat)) doubles (row-major). */
 int dfm_bootstrap(dfm_model *m, int kind, int64_t B, const int32_t *idx,

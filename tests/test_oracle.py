@@ -182,3 +182,39 @@ def test_golden_c2_base_reproduces(oracle):
     assert base.number_of_factors == int(g["r"])
     for i in (0, 7, 129):
         assert abs(oracle.LR_test(base, 300, i) - g["base_chow"][i, 0]) < 1e-9 * max(1, abs(g["base_chow"][i, 0]))
+
+
+# ------------------------------------------------------------- break blocks
+@pytest.mark.parametrize("T,N,breaks", [(90, 200, [31, 61]), (160, 40, [81])])
+def test_break_blocks_scaling_and_residual_identity(oracle, T, N, breaks):
+    """src/DynamicFactorModel.jl:72-98 with break_indices: each block's PCA
+    uses the FULL-sample T, N (D7): F_j'F_j/T = I (N > T) or L_j'L_j/N = I
+    (T >= N); the block common component is the projection of X_j on its top-r
+    eigenspace, so ||E||^2 = sum_j (trace G_j - sum_{i<=r} lambda_{j,i})."""
+    y, x, w = _panel(oracle, T, N, 2, 11, model="Breitung_Eickmeier_2011", b=0.7)
+    r = 2
+    d = oracle.DynamicFactorModel(y, w, x, r, "", breaks)
+    b = [1] + breaks + [T + 1]
+    assert [F.shape[0] for F in d.factors] == [b[i] - b[i - 1] for i in range(1, len(b))]
+    energy = 0.0
+    for j, (F, L, ev) in enumerate(zip(d.factors, d.loadings, d.eigenvalues)):
+        xj = x[b[j] - 1:b[j + 1] - 1]
+        if N > T:
+            assert np.allclose(F.T @ F / T, np.eye(F.shape[1]), atol=1e-11)
+        else:
+            assert np.allclose(L.T @ L / N, np.eye(N), atol=1e-11)
+        P = F[:, :r] @ L[:, :r].T
+        assert np.allclose(P, xj - d.factor_residuals[b[j] - 1:b[j + 1] - 1], atol=1e-10)
+        energy += np.sum(xj ** 2) - np.sum(ev[:r])
+    assert abs(np.sum(d.factor_residuals ** 2) - energy) < 1e-9 * np.sum(x ** 2)
+    # the design matrix stacks the blocks' factors (:131)
+    assert d.design_matrix.shape == (T, 1 + r)
+    assert np.array_equal(d.design_matrix[:, 1:], np.vstack([F[:, :r] for F in d.factors]))
+
+
+def test_break_residual_draws_stay_in_block(oracle):
+    """src/bootstrap.jl:23-28: DiscreteUniform(from, to) per break block."""
+    idx = oracle.draw_residual(np.random.default_rng(0), 50, 30, [11, 21])
+    assert np.all((idx[:, :10] >= 0) & (idx[:, :10] < 10))
+    assert np.all((idx[:, 10:20] >= 10) & (idx[:, 10:20] < 20))
+    assert np.all((idx[:, 20:] >= 20) & (idx[:, 20:] < 30))
