@@ -28,7 +28,7 @@ from typing import List, Optional, Sequence, Union
 import numpy as np
 
 from . import _lib
-from .host import draw_residual, draw_wild, t_quantile
+from .host import draw_residual, draw_wild, glmnet_default_folds, t_quantile
 
 CRITERIA = ("PCp1", "PCp2", "PCp3", "ICp1", "ICp2", "ICp3", "BIC")
 _CRIT_CODE = {n: i for i, n in enumerate(CRITERIA)}
@@ -498,13 +498,18 @@ def Wald_test(dfm, break_period: int, variable_index: int) -> float:
 
 # ------------------------------------------------------- targeted predictors
 def targeted_predictors(y, w, x, thresholding: str = "hard", mode: str = "joint",
-                        *, return_tstats: bool = False, ctx: Optional[Context] = None):
-    """``src/targeted_predictors.jl:1-37``: boolean mask of the x columns whose
-    |t| exceeds t_{0.975}.  mode="joint" is the reference (needs q + N < T);
-    mode="per_candidate" is the Bai–Ng (2008) extension (defect D8)."""
+                        *, return_tstats: bool = False, folds=None,
+                        rng: Optional[np.random.Generator] = None, nlambda: int = 100,
+                        lambda_min_ratio: Optional[float] = None, return_path: bool = False,
+                        ctx: Optional[Context] = None):
+    """``src/targeted_predictors.jl:1-37``: boolean mask of the x columns.
+    Hard (``:9-30``): |t| exceeds t_{0.975}; mode="joint" is the reference
+    (needs q + N < T), mode="per_candidate" the Bai–Ng (2008) extension (D8).
+    Soft (``:31-36``): nonzero lasso coefficient at the glmnetcv-optimal
+    lambda; ``folds`` (T ids 1..K) default to GLMNet.jl's shuffled
+    assignment drawn from ``rng``; ``return_path`` adds the CV path."""
     if thresholding == "soft":
-        raise NotImplementedError("soft thresholding (glmnet lasso-CV) is SURVEY §8(f) next #2; "
-                                  "the reference's GLMNet call is not even imported (defect D5)")
+        return _targeted_soft(y, w, x, folds, rng, nlambda, lambda_min_ratio, return_path, ctx)
     if thresholding != "hard":
         raise ValueError(thresholding)
     ctx = ctx or default_context()
@@ -523,6 +528,36 @@ def targeted_predictors(y, w, x, thresholding: str = "hard", mode: str = "joint"
                                         xc.ctypes.data_as(_lib.c_double_p), T, N, T, m, cv,
                                         _lib.ptr(ts), mask.ctypes.data_as(_lib.c_uint8_p)))
     return (mask.astype(bool), ts) if return_tstats else mask.astype(bool)
+
+
+def _targeted_soft(y, w, x, folds, rng, nlambda, lambda_min_ratio, return_path, ctx):
+    ctx = ctx or default_context()
+    y = _f64(y).ravel()
+    w = _f64(w, 2)
+    x = _f64(x, 2)
+    T, N = x.shape
+    q = w.shape[1]
+    if folds is None:
+        folds = glmnet_default_folds(T, rng or np.random.default_rng())
+    folds = np.ascontiguousarray(folds, dtype=np.int32)
+    if folds.shape != (T,):
+        raise ValueError("folds must hold one fold id per row")
+    L, best, a0 = C.c_int(), C.c_int(), C.c_double()
+    lam, ml = np.zeros(nlambda), np.zeros(nlambda)
+    beta = np.zeros(q + N)
+    mask = np.zeros(N, dtype=np.uint8)
+    xc, wc = _colmajor(x), _colmajor(w)
+    ctx.check(ctx.lib.dfm_targeted_soft(
+        ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T, xc.ctypes.data_as(_lib.c_double_p),
+        T, N, T, folds.ctypes.data_as(_lib.c_int32_p), int(nlambda),
+        float(lambda_min_ratio) if lambda_min_ratio else 0.0, C.byref(L), C.byref(best),
+        _lib.ptr(lam), _lib.ptr(ml), _lib.ptr(beta), C.byref(a0), mask.ctypes.data_as(_lib.c_uint8_p)))
+    out = mask.astype(bool)
+    if not return_path:
+        return out
+    n = L.value
+    return out, {"lambda": lam[:n], "meanloss": ml[:n], "best": best.value, "beta": beta,
+                 "a0": a0.value, "folds": folds}
 
 
 # ---------------------------------------------------------- expanding windows

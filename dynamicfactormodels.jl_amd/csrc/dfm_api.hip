@@ -182,6 +182,12 @@ struct Scope {
   ~Scope() { timer_cb(c, cls, 0); }
 };
 
+namespace dfm {
+int ctx_fail(dfm_ctx *ctx, int code, const char *msg) { return fail(ctx, code, "%s", msg); }
+hipStream_t ctx_stream(dfm_ctx *ctx) { return ctx->stream; }
+int ctx_device(dfm_ctx *ctx) { return ctx->device; }
+}  // namespace dfm
+
 static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 static int ceil_half(int m) { return (m + 1) / 2; }
 
@@ -817,7 +823,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   if (B == 0) return 0;
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
-  const int m = M->m, r = M->r, T = M->T, N = M->N, q = M->q, d = q + r;
+  const int m = M->m, r = M->r, T = M->T, N = M->N, q = M->q;
   // stat descriptors
   std::vector<StatDesc> sd(ns);
   int64_t width = 0;

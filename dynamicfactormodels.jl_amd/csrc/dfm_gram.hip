@@ -191,12 +191,14 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
     else if (c && !e && x) DFM_GRAM_L(ORIENT_ROWS, true, false, true);
     else if (!c && !e && !x) DFM_GRAM_L(ORIENT_ROWS, false, false, false);
     else if (!c && e && x) DFM_GRAM_L(ORIENT_ROWS, false, true, true);
+    else if (!c && !e && x) DFM_GRAM_L(ORIENT_ROWS, false, false, true);
     else return hipErrorInvalidValue;
   } else {
     if (c && e && x) DFM_GRAM_L(ORIENT_COLS, true, true, true);
     else if (c && !e && x) DFM_GRAM_L(ORIENT_COLS, true, false, true);
     else if (!c && !e && !x) DFM_GRAM_L(ORIENT_COLS, false, false, false);
     else if (!c && e && x) DFM_GRAM_L(ORIENT_COLS, false, true, true);
+    else if (!c && !e && x) DFM_GRAM_L(ORIENT_COLS, false, false, true);
     else return hipErrorInvalidValue;
   }
 #undef DFM_GRAM_L

@@ -1,0 +1,431 @@
+// dfm_soft.hip — soft-threshold targeted predictors: the glmnetcv lasso path.
+//
+// Replaces src/targeted_predictors.jl:31-36 (GLMNet.glmnetcv(Z, y) on
+// Z = [w x], keep the x columns whose coefficient at the CV-optimal lambda is
+// nonzero).  GLMNet is never imported by the reference (defect D5); the
+// algorithm is glmnet's gaussian lasso (Friedman, Hastie & Tibshirani 2010),
+// the same restatement the parity tests' CPU checker holds: standardised coordinate descent with covariance
+// updates on the active set, KKT scan appending violators in index order,
+// warm starts along the lambda grid, early path exit on the full fit.
+//
+// Device work per call, K folds + the full fit = K + 1 "problems":
+//   soft_stats_kernel   per (problem, column): training-row mean / population
+//                       sd / constant flag (two passes), the standardised
+//                       panel of every problem stacked in one tall panel, and
+//                       c = Zs'ys / n                          (HBM-bound)
+//   gram_kernel (K1)    G_f = Zs_f' Zs_f over each problem's training rows,
+//                       gathered by row index (zero row pads ragged folds):
+//                       (K+1) p^2 n MACs on MFMA              (MFMA-bound)
+//   lasso_path_kernel   one workgroup per problem: the whole lambda path in
+//                       one launch; g_A updates against an LDS-cached G_AA
+//                       (latency-bound: sequential coordinate updates)
+//   soft_loss_kernel    hold-out SSE per (fold, lambda)        (HBM-bound)
+#include "dfm_common.h"
+#include "../../include/dfm.h"
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace dfm {
+hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
+                       int64_t strideG, int nrep, hipStream_t st);
+__global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
+
+constexpr int LS_AMAX = 1024;   // active-set capacity (glmnet's pmax analogue)
+constexpr int LS_GC = 64;       // G_AA cached in LDS while the active set is this small
+
+// y mean / population sd over each problem's training rows (fold != f; f = 0: all).
+__global__ void soft_ystats_kernel(const double *__restrict__ y, const int32_t *__restrict__ fold, int n,
+                                   int nprob, double *__restrict__ ystat) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nprob) return;
+  double s = 0.0;
+  int nf = 0;
+  for (int i = 0; i < n; ++i)
+    if (fold[i] != f) { s += y[i]; ++nf; }
+  const double yb = s / nf;
+  double v = 0.0;
+  for (int i = 0; i < n; ++i)
+    if (fold[i] != f) { const double d = y[i] - yb; v = fma(d, d, v); }
+  ystat[3 * f + 0] = yb;
+  ystat[3 * f + 1] = sqrt(v / nf);
+  ystat[3 * f + 2] = (double)nf;
+}
+
+// Column statistics and the standardised stacked panel.  Problem f's rows
+// occupy rows f*(n+1) .. f*(n+1)+n of Zs (row n of each block stays zero:
+// the pad target of the ragged training-row gather).  Every row of a block
+// is standardised with the problem's training statistics (hold-out rows are
+// read by the loss kernel).
+__global__ void soft_stats_kernel(const double *__restrict__ Z, int64_t ld, int n, int p,
+                                  const double *__restrict__ y, const int32_t *__restrict__ fold,
+                                  const double *__restrict__ ystat, double *__restrict__ Zs,
+                                  double *__restrict__ mu, double *__restrict__ sd,
+                                  uint8_t *__restrict__ ju, double *__restrict__ c) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y;
+  if (j >= p) return;
+  const double nf = ystat[3 * f + 2], yb = ystat[3 * f + 0], ys = ystat[3 * f + 1];
+  double s = 0.0, lo = INFINITY, hi = -INFINITY;
+  for (int i = 0; i < n; ++i)
+    if (fold[i] != f) {
+      const double v = Z[(int64_t)i * ld + j];
+      s += v; lo = fmin(lo, v); hi = fmax(hi, v);
+    }
+  const double m = s / nf;
+  double v2 = 0.0;
+  for (int i = 0; i < n; ++i)
+    if (fold[i] != f) { const double d = Z[(int64_t)i * ld + j] - m; v2 = fma(d, d, v2); }
+  const bool keep = hi > lo;                    // glmnet chkvars: constant columns excluded
+  const double sdv = keep ? sqrt(v2 / nf) : 1.0;
+  double cy = 0.0;
+  double *Zf = Zs + (int64_t)f * (n + 1) * ld;
+  for (int i = 0; i < n; ++i) {
+    const double z = keep ? (Z[(int64_t)i * ld + j] - m) / sdv : 0.0;
+    Zf[(int64_t)i * ld + j] = z;
+    if (fold[i] != f) cy = fma(z, (y[i] - yb) / ys, cy);
+  }
+  mu[(int64_t)f * p + j] = m;
+  sd[(int64_t)f * p + j] = sdv;
+  ju[(int64_t)f * p + j] = keep ? 1 : 0;
+  c[(int64_t)f * p + j] = cy / nf;
+}
+
+// G_f /= n_f (the Gram kernel leaves Zs_f' Zs_f)
+__global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64_t count,
+                                  const double *__restrict__ ystat) {
+  const int f = blockIdx.y;
+  const double inv = 1.0 / ystat[3 * f + 2];
+  double *Gf = G + (int64_t)f * strideG;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (int64_t)gridDim.x * blockDim.x)
+    Gf[e] *= inv;
+}
+
+// One workgroup per problem: the lasso path over lambdas alm[0..nlam-1]
+// (standardised units), warm-started, by coordinate descent on the active
+// set.  Per pass thread 0 walks the active list in entry order (the serial
+// dependency of coordinate descent), every coordinate change is broadcast
+// and applied to g_A by all threads; after a converged pass the non-active
+// gradients are refreshed with the pass's accumulated changes (rows of G for
+// the active variables, coalesced along j) and the KKT scan appends every
+// violator |g_j| > lambda in index order.  status: 0 ok, 1 no convergence,
+// 2 active set over LS_AMAX.
+__global__ __launch_bounds__(256) void lasso_path_kernel(
+    const double *__restrict__ Gall, int64_t strideG, int p, const double *__restrict__ call,
+    const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early,
+    double thr, int maxit, double *__restrict__ gws, int *__restrict__ actws, double *__restrict__ bpath,
+    double *__restrict__ rsq_out, int *__restrict__ nlam_out, int *__restrict__ status) {
+  const int f = prob0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double *G = Gall + (int64_t)f * strideG;
+  const double *c = call + (int64_t)f * p;
+  const uint8_t *ju = juall + (int64_t)f * p;
+  const double *alm = almall + (int64_t)f * nlam;
+  double *g = gws + (int64_t)f * p;
+  int *act = actws + (int64_t)f * p;
+  double *bp = bpath + (int64_t)f * nlam * p;
+  __shared__ int ia[LS_AMAX];
+  __shared__ double bA[LS_AMAX], gA[LS_AMAX], dA[LS_AMAX];
+  __shared__ double GC[LS_GC * LS_GC];
+  __shared__ double s_d, s_red[4];
+  __shared__ int s_flag, s_cnt[4];
+  for (int j = tid; j < p; j += 256) { g[j] = c[j]; act[j] = 0; }
+  __syncthreads();
+  int na = 0, L = nlam, st = 0;
+  double rsq_prev = 0.0;
+  for (int m = 0; m < nlam && !st; ++m) {
+    const double lam = alm[m];
+    for (;;) {
+      // ---- passes over the active set until max delta^2 < thr
+      int it = 0;
+      for (; it < maxit; ++it) {
+        double dlx = 0.0;
+        for (int k = 0; k < na; ++k) {
+          if (tid == 0) {
+            const double u = gA[k] + bA[k], v = fabs(u) - lam;
+            const double nb = v > 0.0 ? copysign(v, u) : 0.0;
+            const double d = nb - bA[k];
+            if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
+            s_d = d;
+          }
+          __syncthreads();
+          const double d = s_d;
+          if (d != 0.0) {
+            if (na <= LS_GC) {
+              for (int t = tid; t < na; t += 256) gA[t] -= GC[k * LS_GC + t] * d;
+            } else {
+              const double *Gk = G + (int64_t)ia[k] * p;
+              for (int t = tid; t < na; t += 256) gA[t] -= Gk[ia[t]] * d;
+            }
+          }
+          __syncthreads();
+        }
+        if (tid == 0) s_flag = dlx < thr;
+        __syncthreads();
+        const bool done = s_flag;
+        __syncthreads();
+        if (done) break;
+      }
+      if (it == maxit) { st = 1; break; }
+      // ---- refresh the non-active gradients with this round's changes
+      for (int j = tid; j < p; j += 256) {
+        if (act[j]) continue;
+        double s = 0.0;
+        for (int t = 0; t < na; ++t) s = fma(G[(int64_t)ia[t] * p + j], dA[t], s);
+        g[j] -= s;
+      }
+      __syncthreads();
+      for (int t = tid; t < na; t += 256) dA[t] = 0.0;
+      // ---- KKT scan: append violators in index order
+      const int na0 = na;
+      int base = na;
+      for (int j0 = 0; j0 < p; j0 += 256) {
+        const int j = j0 + tid;
+        const bool v = j < p && ju[j] && !act[j] && fabs(g[j]) > lam;
+        const unsigned long long bal = __ballot(v);
+        if (lane == 0) s_cnt[wave] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int w2 = 0; w2 < wave; ++w2) off += s_cnt[w2];
+        const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        if (v) {
+          const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+          if (pos < LS_AMAX) { ia[pos] = j; bA[pos] = 0.0; gA[pos] = g[j]; dA[pos] = 0.0; act[j] = 1; }
+        }
+        base += tot;
+        __syncthreads();
+      }
+      if (base > LS_AMAX) { st = 2; break; }
+      na = base;
+      if (na == na0) break;
+      if (na <= LS_GC)   // G_AA entries of the new variables (G symmetric)
+        for (int e = tid; e < (na - na0) * na; e += 256) {
+          const int k = na0 + e / na, t = e % na;
+          const double v = G[(int64_t)ia[k] * p + ia[t]];
+          GC[k * LS_GC + t] = v;
+          GC[t * LS_GC + k] = v;
+        }
+      __syncthreads();
+    }
+    if (st) break;
+    // ---- record: dense beta_m, R^2 = beta'(c + g)
+    double part = 0.0;
+    for (int t = tid; t < na; t += 256) part = fma(bA[t], c[ia[t]] + gA[t], part);
+    part = wave_sum(part);
+    if (lane == 0) s_red[wave] = part;
+    double *bm = bp + (int64_t)m * p;
+    for (int j = tid; j < p; j += 256) bm[j] = 0.0;
+    __syncthreads();
+    for (int t = tid; t < na; t += 256) bm[ia[t]] = bA[t];
+    const double rsq = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    if (tid == 0) rsq_out[(int64_t)f * nlam + m] = rsq;
+    __syncthreads();
+    if (early && m + 1 >= min(5, nlam) && (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999)) { L = m + 1; break; }
+    rsq_prev = rsq;
+  }
+  if (tid == 0) { nlam_out[f] = L; status[f] = st; }
+}
+
+// Hold-out SSE of fold f (problem f >= 1) at lambda m: one workgroup per (m, f).
+__global__ __launch_bounds__(256) void soft_loss_kernel(const double *__restrict__ Zs, int64_t ld, int n, int p,
+                                                        const double *__restrict__ y,
+                                                        const int32_t *__restrict__ fold,
+                                                        const double *__restrict__ ystat,
+                                                        const double *__restrict__ bpath, int nlam,
+                                                        double *__restrict__ sse) {
+  const int m = blockIdx.x, f = blockIdx.y + 1, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double red[4];
+  const double *b = bpath + ((int64_t)f * nlam + m) * p;
+  const double *Zf = Zs + (int64_t)f * (n + 1) * ld;
+  const double yb = ystat[3 * f], ys = ystat[3 * f + 1];
+  double acc = 0.0;
+  for (int i = 0; i < n; ++i) {
+    if (fold[i] != f) continue;
+    double s = 0.0;
+    for (int j = tid; j < p; j += 256) s = fma(b[j], Zf[(int64_t)i * ld + j], s);
+    s = wave_sum(s);
+    __syncthreads();
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    const double e = y[i] - (yb + ys * ((red[0] + red[1]) + (red[2] + red[3])));
+    acc = fma(e, e, acc);
+  }
+  if (tid == 0) sse[(int64_t)(f - 1) * nlam + m] = acc;
+}
+
+}  // namespace dfm
+
+using namespace dfm;
+
+// Context internals shared with dfm_api.hip (error text, stream, device).
+namespace dfm {
+int ctx_fail(dfm_ctx *ctx, int code, const char *msg);
+hipStream_t ctx_stream(dfm_ctx *ctx);
+int ctx_device(dfm_ctx *ctx);
+}  // namespace dfm
+
+extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                                 const double *X, int64_t T64, int64_t N64, int64_t ldx,
+                                 const int32_t *folds, int nlambda, double lmr, int *nlam_out,
+                                 int *best_out, double *lambda_out, double *meanloss_out,
+                                 double *beta_out, double *a0_out, uint8_t *mask) {
+  if (!ctx) return -1;
+  auto fail = [&](int code, const char *msg) { return ctx_fail(ctx, code, msg); };
+  if (!y || !X || !folds || T64 < 3 || N64 < 1 || q < 0 || ldx < T64 || (q > 0 && (!w || ldw < T64)))
+    return fail(-2, "dfm_targeted_soft: bad arguments");
+  if (nlambda < 2 || nlambda > 1000) return fail(-2, "dfm_targeted_soft: nlambda must be in 2..1000");
+  const int n = (int)T64, N = (int)N64, p = q + N;
+  int K = 0;
+  std::vector<int> hold(n + 2, 0);
+  for (int i = 0; i < n; ++i) {
+    if (folds[i] < 1 || folds[i] > n) return fail(-2, "dfm_targeted_soft: fold ids must be 1..K");
+    K = std::max(K, folds[i]);
+    hold[folds[i]]++;
+  }
+  if (K < 2) return fail(-2, "dfm_targeted_soft: need at least 2 folds");
+  for (int f = 1; f <= K; ++f)
+    if (hold[f] == 0 || hold[f] > n - 2) return fail(-2, "dfm_targeted_soft: every fold id 1..K needs rows");
+  const int nprob = K + 1;
+  const int64_t ld = (p + 15) / 16 * 16;
+  const int64_t strideG = (int64_t)p * p;
+  const double gbytes = (double)nprob * strideG * 8;
+  if (gbytes > 64e9) return fail(-2, "dfm_targeted_soft: (K+1) p^2 Gram workspace above 64 GB");
+  if (lmr <= 0) lmr = n < p ? 1e-2 : 1e-4;   // GLMNet.jl lambda_min_ratio default
+  hipSetDevice(ctx_device(ctx));
+  hipStream_t st = ctx_stream(ctx);
+  // ---- device buffers
+  std::vector<void *> bufs;
+  bool oom = false;
+  auto alloc = [&](size_t bytes) -> void * {
+    void *p_ = nullptr;
+    if (hipMalloc(&p_, std::max<size_t>(bytes, 8)) != hipSuccess) { oom = true; return nullptr; }
+    bufs.push_back(p_);
+    return p_;
+  };
+  auto cleanup = [&]() { hipStreamSynchronize(st); for (void *b : bufs) hipFree(b); bufs.clear(); };
+  double *Zraw = (double *)alloc((size_t)n * p * 8);
+  double *Zp = (double *)alloc((size_t)n * ld * 8);
+  double *Zs = (double *)alloc((size_t)nprob * (n + 1) * ld * 8);
+  double *yd = (double *)alloc((size_t)n * 8);
+  int32_t *fd = (int32_t *)alloc((size_t)n * 4);
+  int32_t *tidx = (int32_t *)alloc((size_t)nprob * n * 4);
+  double *ystat = (double *)alloc((size_t)nprob * 3 * 8);
+  double *mu = (double *)alloc((size_t)nprob * p * 8), *sd = (double *)alloc((size_t)nprob * p * 8);
+  double *cc = (double *)alloc((size_t)nprob * p * 8);
+  uint8_t *ju = (uint8_t *)alloc((size_t)nprob * p);
+  double *G = (double *)alloc((size_t)nprob * strideG * 8);
+  double *alm = (double *)alloc((size_t)nprob * nlambda * 8);
+  double *gws = (double *)alloc((size_t)nprob * p * 8);
+  int *actws = (int *)alloc((size_t)nprob * p * 4);
+  double *bpath = (double *)alloc((size_t)nprob * nlambda * p * 8);
+  double *rsq = (double *)alloc((size_t)nprob * nlambda * 8);
+  int *nl = (int *)alloc((size_t)nprob * 4), *sts = (int *)alloc((size_t)nprob * 4);
+  double *sse = (double *)alloc((size_t)K * nlambda * 8);
+  if (oom) { cleanup(); return fail(1002, "dfm_targeted_soft: out of device memory"); }
+  // ---- inputs: Z = [w x] column-major on the host side of the copy
+  hipError_t e = hipSuccess;
+  if (q > 0) e = hipMemcpy2DAsync(Zraw, (size_t)n * 8, w, (size_t)ldw * 8, (size_t)n * 8, q, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpy2DAsync(Zraw + (size_t)q * n, (size_t)n * 8, X, (size_t)ldx * 8, (size_t)n * 8, N,
+                         hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(yd, y, (size_t)n * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(fd, folds, (size_t)n * 4, hipMemcpyHostToDevice, st);
+  // training-row lists per problem, padded with the block's zero row n
+  std::vector<int32_t> tl((size_t)nprob * n);
+  for (int f = 0; f < nprob; ++f) {
+    int c = 0;
+    for (int i = 0; i < n; ++i)
+      if (folds[i] != f) tl[(size_t)f * n + c++] = f * (n + 1) + i;
+    for (; c < n; ++c) tl[(size_t)f * n + c] = f * (n + 1) + n;
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(tidx, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(Zs, 0, (size_t)nprob * (n + 1) * ld * 8, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
+  hipLaunchKernelGGL(panel_from_colmajor_kernel, dim3((unsigned)((ld + 31) / 32), (n + 31) / 32), dim3(256), 0, st,
+                     Zraw, (int64_t)n, n, p, Zp, ld);
+  hipLaunchKernelGGL(soft_ystats_kernel, dim3(1), dim3(64), 0, st, yd, fd, n, nprob, ystat);
+  hipLaunchKernelGGL(soft_stats_kernel, dim3((p + 255) / 256, nprob), dim3(256), 0, st, Zp, ld, n, p, yd, fd,
+                     ystat, Zs, mu, sd, ju, cc);
+  // ---- standardised Grams of every problem on MFMA: G_f = Zs_f' Zs_f / n_f
+  PanelSrc src{nullptr, Zs, tidx, nullptr, ld, (int64_t)n};
+  e = launch_gram(1, src, p, n, n, G, p, strideG, nprob, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: Gram launch failed"); }
+  hipLaunchKernelGGL(soft_scale_kernel, dim3(2048, nprob), dim3(256), 0, st, G, strideG, strideG, ystat);
+  // ---- lambda grid of the full fit: lambda_max = max_j |c_j| over non-constant columns
+  std::vector<double> hc(p), hys(3 * nprob);
+  std::vector<uint8_t> hju(p);
+  e = hipMemcpyAsync(hc.data(), cc, (size_t)p * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hju.data(), ju, (size_t)p, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hys.data(), ystat, hys.size() * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: stats failed"); }
+  double lam_max = 0.0;
+  for (int j = 0; j < p; ++j)
+    if (hju[j]) lam_max = std::max(lam_max, std::fabs(hc[j]));
+  if (!(lam_max > 0.0) || !(hys[1] > 0.0)) { cleanup(); return fail(-2, "dfm_targeted_soft: degenerate y or Z"); }
+  const double alf = std::pow(lmr, 1.0 / (nlambda - 1));
+  std::vector<double> halm((size_t)nprob * nlambda);
+  for (int m = 0; m < nlambda; ++m) halm[m] = lam_max * std::pow(alf, (double)m);
+  const double thr = 1e-7;   // glmnet's default convergence threshold
+  const int maxit = 100000;
+  e = hipMemcpyAsync(alm, halm.data(), (size_t)nlambda * 8, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
+  // ---- full-sample path (early exit decides the path length L)
+  hipLaunchKernelGGL(lasso_path_kernel, dim3(1), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1, thr,
+                     maxit, gws, actws, bpath, rsq, nl, sts);
+  int L = 0, s0 = 0;
+  e = hipMemcpyAsync(&L, nl, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(&s0, sts, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: path kernel failed"); }
+  if (s0) { cleanup(); return fail(2, s0 == 1 ? "lasso coordinate descent did not converge"
+                                               : "lasso active set above 1024 variables"); }
+  // ---- fold paths on the same lambdas in original units: alm_f = alm_0 ys_0 / ys_f.
+  // The fold launch runs with nlam = L: problem f's lambdas at alm + f L, its
+  // path rows at bpath + f L p (problem 0's rows 0..L-1 stay below f L p).
+  std::vector<double> falm((size_t)nprob * L);
+  for (int f = 1; f < nprob; ++f)
+    for (int m = 0; m < L; ++m) falm[(size_t)f * L + m] = halm[m] * hys[1] / hys[3 * f + 1];
+  e = hipMemcpyAsync(alm + L, falm.data() + L, (size_t)K * L * 8, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
+  hipLaunchKernelGGL(lasso_path_kernel, dim3(K), dim3(256), 0, st, G, strideG, p, cc, ju, alm, L, 1, 0, thr,
+                     maxit, gws, actws, bpath, rsq, nl, sts);
+  hipLaunchKernelGGL(soft_loss_kernel, dim3(L, K), dim3(256), 0, st, Zs, ld, n, p, yd, fd, ystat, bpath, L, sse);
+  std::vector<int> hst(nprob);
+  std::vector<double> hsse((size_t)K * L), hb(p), hmu(p), hsd(p);
+  e = hipMemcpyAsync(hst.data(), sts, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hsse.data(), sse, hsse.size() * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: fold kernels failed"); }
+  for (int f = 1; f < nprob; ++f)
+    if (hst[f]) { cleanup(); return fail(2, "lasso coordinate descent failed on a fold"); }
+  // ---- meanloss = sum_f SSE_f / n (fold-size-weighted hold-out MSE), first argmin
+  std::vector<double> ml(L, 0.0);
+  for (int f = 0; f < K; ++f)
+    for (int m = 0; m < L; ++m) ml[m] += hsse[(size_t)f * L + m];
+  int best = 0;
+  for (int m = 0; m < L; ++m) {
+    ml[m] /= n;
+    if (ml[m] < ml[best]) best = m;
+  }
+  e = hipMemcpyAsync(hb.data(), bpath + (size_t)best * p, (size_t)p * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hmu.data(), mu, (size_t)p * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hsd.data(), sd, (size_t)p * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  cleanup();
+  if (e != hipSuccess) return fail(1000 + (int)e, "dfm_targeted_soft: read-back failed");
+  const double yb = hys[0], ys = hys[1];
+  double a0 = yb;
+  for (int j = 0; j < p; ++j) {
+    const double bo = hb[j] * ys / hsd[j];
+    if (beta_out) beta_out[j] = bo;
+    a0 -= bo * hmu[j];
+    if (j >= q && mask) mask[j - q] = hb[j] != 0.0 ? 1 : 0;
+  }
+  if (a0_out) *a0_out = a0;
+  if (nlam_out) *nlam_out = L;
+  if (best_out) *best_out = best;
+  for (int m = 0; m < L; ++m) {
+    if (lambda_out) lambda_out[m] = halm[m] * ys;
+    if (meanloss_out) meanloss_out[m] = ml[m];
+  }
+  return 0;
+}

@@ -82,6 +82,18 @@ def draw_residual(rng: np.random.Generator, B: int, T: int, break_indices: Seque
     return idx
 
 
+def glmnet_default_folds(n: int, rng: np.random.Generator, nfolds: int | None = None) -> np.ndarray:
+    """GLMNet.jl's default fold assignment for glmnetcv (used by
+    ``src/targeted_predictors.jl:33``): nfolds = min(10, n ÷ 3),
+    shuffle([repeat(1:nfolds, outer=n ÷ nfolds); 1:(n % nfolds)]) — 1-based
+    ids, drawn on the host like the bootstrap indices."""
+    k = nfolds or min(10, n // 3)
+    q, rem = divmod(n, k)
+    f = np.concatenate([np.tile(np.arange(1, k + 1), q), np.arange(1, rem + 1)]).astype(np.int32)
+    rng.shuffle(f)
+    return f
+
+
 def t_quantile(p: float, df: float) -> float:
     """``quantile(TDist(df), p)`` (``src/targeted_predictors.jl:27``)."""
     from scipy import stats

@@ -222,6 +222,25 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
                       const double *X, int64_t T, int64_t N, int64_t ldx, int mode,
                       double crit_value, double *tstat, uint8_t *mask);
 
+/* targeted_predictors(..., thresholding="soft") (src/targeted_predictors.jl:31-36):
+ * GLMNet.glmnetcv(Z = [w x], y), gaussian lasso (alpha = 1) with standardised
+ * columns and an intercept; keep the x columns with a nonzero coefficient at
+ * the CV-optimal lambda.  GLMNet is never imported by the reference (D5): the
+ * algorithm is glmnet's published coordinate descent (covariance updates on
+ * the active set, threshold 1e-7, warm starts over `nlambda` log-spaced
+ * lambdas from lambda_max down to lambda_min_ratio * lambda_max (<= 0: 1e-2 if
+ * T < q + N else 1e-4), early path exit on the full fit after 5 lambdas when
+ * R^2 gains < 1e-5 relative or R^2 > 0.999).  folds: T fold ids 1..K (host-drawn, as the
+ * bootstrap draws).  Outputs: path length L, best (0-based argmin of the
+ * fold-size-weighted hold-out MSE), lambda (L, original units), meanloss (L),
+ * beta (q + N, original scale, at best), intercept a0, mask (N, 0/1).  Any
+ * output pointer may be NULL. */
+int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                      const double *X, int64_t T, int64_t N, int64_t ldx, const int32_t *folds,
+                      int nlambda, double lambda_min_ratio, int *nlam_out, int *best_out,
+                      double *lambda_out, double *meanloss_out, double *beta_out, double *a0_out,
+                      uint8_t *mask);
+
 #ifdef __cplusplus
 }
 #endif

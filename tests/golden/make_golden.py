@@ -83,8 +83,41 @@ def tp():
                         y2=y2, w2=w2, x2=x2, t_cand=tc, m_cand=mc)
 
 
+def c4_inputs():
+    """C4 panel (regenerated, not stored: 16 MB): Bai-Ng DGP T=400, N=5000,
+    r=5, y = f beta + eps, normalised x, w = 1, GLMNet.jl default folds."""
+    rng = np.random.default_rng(20261015 + 4)
+    T, N = 400, 5000
+    y, x, *_ = O.factor_model_DGP(T, N, 5, rng)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    folds = O.glmnet_default_folds(T, np.random.default_rng(404))
+    return y, w, x, folds
+
+
+def soft():
+    """Targeted predictors (soft, glmnetcv lasso): a small panel with its
+    inputs, and the full C4 panel (T=400, N=5000) as outputs + input digest."""
+    rng = np.random.default_rng(20261015 + 5)
+    y, x, *_ = O.factor_model_DGP(120, 300, 3, rng)
+    x = O.normalize(x)
+    w = np.ones((120, 1))
+    folds = O.glmnet_default_folds(120, np.random.default_rng(5))
+    mask, res = O.targeted_predictors_soft(y, w, x, folds)
+    y4, w4, x4, f4 = c4_inputs()
+    mask4, res4 = O.targeted_predictors_soft(y4, w4, x4, f4)
+    np.savez_compressed(
+        os.path.join(HERE, "tp_soft.npz"), y=y, w=w, x=x, folds=folds, mask=mask,
+        lam=res["lambda"], meanloss=res["meanloss"], best=res["best"], beta=res["betas"][res["best"]],
+        a0=res["a0"][res["best"]],
+        c4_digest=np.array([x4.sum(), np.abs(x4).sum(), y4.sum(), f4.sum()]), c4_mask=mask4,
+        c4_lam=res4["lambda"], c4_meanloss=res4["meanloss"], c4_best=res4["best"],
+        c4_beta=res4["betas"][res4["best"]])
+
+
 if __name__ == "__main__":
     c1()
     c2()
     tp()
+    soft()
     print("golden fixtures written to", HERE)

