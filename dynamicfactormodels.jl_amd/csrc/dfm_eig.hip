@@ -867,6 +867,8 @@ __global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, in
   emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
 }
 
+hipError_t launch_gemm_loadings(const double *E, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
+                                int r, const double *Lb, const double *M1, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1);
@@ -1598,10 +1600,19 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
   const int T = fb.T, r = fb.r;
   const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
   double *ZF = (double *)ws;
-  double *GL = ZF + (size_t)T * ldzf;
+  double *GL = ZF + (size_t)((T + 15) / 16 * 16) * ldzf;
   double *M1 = GL + (size_t)N * ldzf;
+  // ZF rows T..round_up(T,16) are the zero k-padding the LDS-DMA GEMM reads
+  const int Tp = (T + 15) / 16 * 16;
+  hipMemsetAsync(ZF + (size_t)T * ldzf, 0, (size_t)(Tp - T) * ldzf * 8, st);
   hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, ldzf, M1);
-  hipError_t e = launch_gemm(true, Ep, ld, ZF, ldzf, GL, ldzf, N, (int)ldzf, T, st);
+  hipError_t e;
+  if (ldzf == (int64_t)nb * r && ld % 2 == 0) {
+    // GEMM with the finish fused in its epilogue (no E'ZF round trip through HBM)
+    e = launch_gemm_loadings(Ep, ld, ZF, ldzf, N, nb * r, T, r, Lb, M1, Lout, st);
+    return e == hipSuccess ? 0 : 1000 + (int)e;
+  }
+  e = launch_gemm(true, Ep, ld, ZF, ldzf, GL, ldzf, N, (int)ldzf, T, st);
   if (e != hipSuccess) return 1000 + (int)e;
   hipLaunchKernelGGL(boot_lfinish_kernel, dim3((unsigned)(((int64_t)N * r + 255) / 256), nb), dim3(256), 0, st,
                      Lb, N, r, T, M1, GL, ldzf, Lout);
@@ -1610,7 +1621,8 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
 }
 size_t fact_loadings_bytes(int T, int N, int r, int nb) {
   const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
-  return ((size_t)T * ldzf + (size_t)N * ldzf + (size_t)nb * r * r) * 8 + 1024;
+  const int Tp = (T + 15) / 16 * 16;
+  return ((size_t)Tp * ldzf + (size_t)N * ldzf + (size_t)nb * r * r) * 8 + 1024;
 }
 
 // ---- model-level precompute: EL = E L (T x r), S = L'L, cF, hd

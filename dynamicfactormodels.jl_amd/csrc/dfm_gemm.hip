@@ -13,6 +13,7 @@
 // blocks of one column block are issued to one XCD so a B tile is fetched
 // from HBM once and re-read from that XCD's L2.
 #include "dfm_common.h"
+#include <cstdlib>
 
 namespace dfm {
 
@@ -171,15 +172,260 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const double *__restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// gemmh_kernel: C = A B for the eigen-iteration product H.Z, staged by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR staging, no ds_write pass) through a
+// 4-deep ring of 16-deep stages, two stages in flight across each barrier:
+// every wave waits only for its own DMAs of the stage about to be read
+// (counted vmcnt, never 0 inside the loop), then ONE raw s_barrier orders
+// them for every reader and retires the ring slot being refilled (read one
+// iteration earlier).  All LDS is one __shared__ array (a second object makes
+// hipcc drain vmcnt before ds_reads).  LDS images as dfm_gram.hip's 16-deep
+// ones; DMA writes are lane-linear, so the XOR swizzle is applied to the
+// per-lane SOURCE address.  Out-of-range rows/columns read clamped (finite)
+// data that only reaches discarded outputs; the k tail reads A's zero
+// padding (requirement: lda >= round_up(K, 16), A[i][K..lda) = 0).
+namespace {
+constexpr int G2_KS = 16, G2_STAGE = 2 * GT * G2_KS;   // doubles per stage (A + B)
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+DFM_DEV int g2_offA(int a, int kc) { return a * G2_KS + (kc ^ (((a >> 1) & 1) << 3)); }   // [a][k]
+DFM_DEV int g2_offB(int kc, int a) { return kc * GT + (a ^ ((kc & 7) << 2)); }           // [k][a]
+}  // namespace
+
+// Per-lane DMA sources, fixed for the whole K loop: A chunk rows 8c..8c+7
+// (lane pair lane & 7), B chunk k-rows 2c, 2c+1 (lane pair lane & 31), with
+// the LDS images' XOR swizzle applied to the source column.
+struct G2Src {
+  int64_t a[2], b[2];   // element offsets at k0 = 0
+  int kb[2];            // B k-row within the stage
+};
+DFM_DEV G2Src g2_sources(int64_t lda, int64_t ldb, int abase, int bbase, int M, int Nc, int wave, int lane) {
+  G2Src s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 2 * wave + h;
+    const int a = 8 * c + (lane >> 3);
+    const int ka = (2 * (lane & 7)) ^ (((a >> 1) & 1) << 3);
+    s.a[h] = (int64_t)min(abase + a, M - 1) * lda + ka;
+    const int kc = 2 * c + (lane >> 5);
+    s.kb[h] = kc;
+    s.b[h] = (int64_t)kc * ldb + min(bbase + ((2 * (lane & 31)) ^ ((kc & 7) << 2)), Nc - 2);
+  }
+  return s;
+}
+DFM_DEV void g2_issue(double *stage, const double *__restrict__ A, const double *__restrict__ B, int64_t ldb,
+                      const G2Src &src, int k0, int K) {
+  double *la = stage, *lb = stage + GT * G2_KS;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c_off = (2 * (threadIdx.x >> 6) + h) * 128;
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(A + src.a[h] + k0), (lds_void_t *)(la + c_off), 16, 0, 0);
+    // k rows past K (last stage only) re-read row K-1: finite, multiplied by A's zero k-padding
+    const int64_t over = (int64_t)max(0, k0 + src.kb[h] - (K - 1)) * ldb;
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(B + src.b[h] + (int64_t)k0 * ldb - over),
+                                     (lds_void_t *)(lb + c_off), 16, 0, 0);
+  }
+}
+
+template <int NBUF, int MINB, bool PRIO>
+__global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__restrict__ A, int64_t lda,
+                                                       const double *__restrict__ B, int64_t ldb,
+                                                       double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
+                                                       int nrb, int ncb, const int *__restrict__ col_done,
+                                                       int col_group) {
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
+  constexpr int AHEAD = NBUF - 2;   // stages in flight across a barrier
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+  const int rb = j % nrb, cb = (j / nrb) * 8 + xcd;
+  if (cb >= ncb) return;
+  const int abase = rb * GT, bbase = cb * GT;
+  if (col_done) {
+    bool all = true;
+    const int r0 = bbase / col_group, r1 = min(Nc - 1, bbase + GT - 1) / col_group;
+    for (int q = r0; q <= r1; ++q) all = all && col_done[q];
+    if (all) return;
+  }
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int nst = (K + G2_KS - 1) / G2_KS;
+  const G2Src src = g2_sources(lda, ldb, abase, bbase, M, Nc, wave, lane);
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) g2_issue(lds + (s % NBUF) * G2_STAGE, A, B, ldb, src, s * G2_KS, K);
+  for (int s = 0; s < nst; ++s) {
+    const int ahead = min(AHEAD, nst - 1 - s);   // later stages already issued (4 DMAs each per wave)
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NBUF - 1 < nst)   // ring slot (s-1)%NBUF: its readers all passed this barrier
+      g2_issue(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, A, B, ldb, src, (s + NBUF - 1) * G2_KS, K);
+    const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    double af[8], bf[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = la[g2_offA(wr * 32 + 4 * f + fi, fkc)];
+      bf[f] = lb[g2_offB(fkc, wc * 32 + 4 * f + fi)];
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2],
+                   a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int row = abase + wr * 32 + 4 * fa + oi;
+      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+      if (row < M && col < Nc) C[(int64_t)row * ldc + col] = v;
+    }
+}
+
+// the production configuration
+#define gemmh_kernel gemmh_kernel_t<4, 2, false>
+
+// ---------------------------------------------------------------------------
+// Loadings GEMM of the factored bootstrap with its finish fused in the
+// epilogue:  L*[rep][n][j] = ( (E' ZF)[n][rep r + j] + sum_i Lb[n][i] M1[rep][i][j] ) / T
+// (src/DynamicFactorModel.jl:90 for every replicate: L* = X*' F* / T with
+// X*' F* = L (F'F*) + E' P' D F*).  A^T operand E (K = T rows x lda) and B
+// operand ZF (Kpad x ldb, rows K..round_up(K,16) zero) both staged by LDS-DMA
+// into [k][a] images (4-deep ring as gemmh_kernel).  Grid: the row blocks
+// (64 variables) are spread over the XCDs — XCD x owns row blocks x, x+8, ...
+// whose E slabs (64 x T x 8 B each) stay in its L2 — and every XCD walks the
+// column blocks in the same order, so a ZF tile is fetched from HBM once and
+// served to the other XCDs from the Infinity Cache.
+DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda, const double *__restrict__ B,
+                        int64_t ldb, int k0, int abase, int bbase, int M, int Nc, int K, int wave, int lane) {
+  double *la = stage, *lb = stage + GT * G2_KS;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 2 * wave + h;
+    const int kc = 2 * c + (lane >> 5);
+    const int sw = (2 * (lane & 31)) ^ ((kc & 7) << 2);
+    const int ra = min(k0 + kc, K - 1);             // rows past K: finite, times B's zero rows
+    const int ca = min(abase + sw, (int)lda - 2);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(A + (int64_t)ra * lda + ca), (lds_void_t *)(la + c * 128), 16,
+                                     0, 0);
+    const int cb = min(bbase + sw, Nc - 2);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(B + (int64_t)(k0 + kc) * ldb + cb), (lds_void_t *)(lb + c * 128),
+                                     16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
+                                                               const double *__restrict__ B, int64_t ldb, int M,
+                                                               int Nc, int K, int nrb, int ncb, int r, double invT,
+                                                               const double *__restrict__ Lb,
+                                                               const double *__restrict__ M1,
+                                                               double *__restrict__ Lout) {
+  constexpr int NBUF = 4;
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nrb8 = (nrb + 7) / 8;
+  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+  const int rb = (j % nrb8) * 8 + xcd, cb = j / nrb8;
+  if (rb >= nrb || cb >= ncb) return;
+  const int abase = rb * GT, bbase = cb * GT;
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int nst = (K + G2_KS - 1) / G2_KS;
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s)
+    g2_issue_t(lds + (s % NBUF) * G2_STAGE, A, lda, B, ldb, s * G2_KS, abase, bbase, M, Nc, K, wave, lane);
+  for (int s = 0; s < nst; ++s) {
+    const int ahead = min(NBUF - 2, nst - 1 - s);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NBUF - 1 < nst)
+      g2_issue_t(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, A, lda, B, ldb, (s + NBUF - 1) * G2_KS, abase, bbase, M,
+                 Nc, K, wave, lane);
+    const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    double af[8], bf[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = la[g2_offB(fkc, wr * 32 + 4 * f + fi)];
+      bf[f] = lb[g2_offB(fkc, wc * 32 + 4 * f + fi)];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2],
+                   a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int n = abase + wr * 32 + 4 * fa + oi;
+      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+      if (n < M && col < Nc) {
+        const int rep = col / r, jj = col - rep * r;
+        const double *m1 = M1 + (int64_t)rep * r * r + jj;
+        double w = v;
+        for (int i = 0; i < r; ++i) w = fma(Lb[(int64_t)n * r + i], m1[i * r], w);
+        Lout[((int64_t)rep * M + n) * r + jj] = w * invT;
+      }
+    }
+}
+
+hipError_t launch_gemm_loadings(const double *E, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
+                                int r, const double *Lb, const double *M1, double *Lout, hipStream_t st) {
+  const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
+  const int nrb8 = (nrb + 7) / 8;
+  hipLaunchKernelGGL(gemm_loadings_kernel, dim3(8 * nrb8 * ncb), dim3(256), 0, st, E, lda, ZF, ldb, N, Nc, K, nrb,
+                     ncb, r, 1.0 / K, Lb, M1, Lout);
+  return hipGetLastError();
+}
+
+static int gemm_variant() {
+  static const int v = [] { const char *e = getenv("DFM_GEMM"); return e ? atoi(e) : 2; }();
+  return v;
+}
+
 // Requirements: lda, ldb even (16-B aligned pairs); B/A padding beyond the
-// logical size is never read (masked).
+// logical size is never read (masked).  The LDS-DMA kernel additionally
+// needs Nc even and A's zero k-padding (lda >= round_up(K, 16)); otherwise
+// the register-staged kernel runs.
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1) {
   const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
-  if (a_trans)
+  if (!a_trans && gemm_variant() == 2 && lda >= (K + G2_KS - 1) / G2_KS * G2_KS && Nc % 2 == 0 && Nc >= 2)
+    hipLaunchKernelGGL(gemmh_kernel, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb, col_done,
+                       col_group);
+  else if (a_trans)
     hipLaunchKernelGGL(gemm_kernel<true>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
                        col_done, col_group);
   else
