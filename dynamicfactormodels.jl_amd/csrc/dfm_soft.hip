@@ -32,7 +32,7 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
 
 constexpr int LS_AMAX = 1024;   // active-set capacity (glmnet's pmax analogue)
-constexpr int LS_GC = 64;       // G_AA cached in LDS while the active set is this small
+constexpr int LS_GC = 112;      // G_AA cached in LDS while the active set is this small (98 KB)
 
 // y mean / population sd over each problem's training rows (fold != f; f = 0: all).
 __global__ void soft_ystats_kernel(const double *__restrict__ y, const int32_t *__restrict__ fold, int n,
@@ -107,8 +107,11 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 // and applied to g_A by all threads; after a converged pass the non-active
 // gradients are refreshed with the pass's accumulated changes (rows of G for
 // the active variables, coalesced along j) and the KKT scan appends every
-// violator |g_j| > lambda in index order.  status: 0 ok, 1 no convergence,
-// 2 active set over LS_AMAX.
+// violator |g_j| > lambda in index order.  status[f]: 0 ok, 1 no convergence,
+// 2 active set over LS_AMAX; status[nprob + f]: the lambda index of the failure.
+// early = 1: problem 0 (the full fit) applies glmnet's early path exit and
+// publishes its path length in nlam_out[0] (zeroed before the launch); the
+// other problems stop when they reach it.
 __global__ __launch_bounds__(256) void lasso_path_kernel(
     const double *__restrict__ Gall, int64_t strideG, int p, const double *__restrict__ call,
     const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early,
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
   __shared__ int s_flag, s_cnt[4];
   for (int j = tid; j < p; j += 256) { g[j] = c[j]; act[j] = 0; }
   __syncthreads();
-  int na = 0, L = nlam, st = 0;
+  int na = 0, L = nlam, st = 0, fail_m = nlam;
   double rsq_prev = 0.0;
   for (int m = 0; m < nlam && !st; ++m) {
     const double lam = alm[m];
@@ -164,13 +167,31 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
         __syncthreads();
         if (done) break;
       }
-      if (it == maxit) { st = 1; break; }
-      // ---- refresh the non-active gradients with this round's changes
-      for (int j = tid; j < p; j += 256) {
-        if (act[j]) continue;
-        double s = 0.0;
-        for (int t = 0; t < na; ++t) s = fma(G[(int64_t)ia[t] * p + j], dA[t], s);
-        g[j] -= s;
+      if (it == maxit) { st = 1; fail_m = m; break; }
+      // ---- refresh the non-active gradients with this round's changes:
+      // row-outer, so each thread keeps SEG loads in flight (one per owned j)
+      // instead of one dependent load per FMA; rows with no change skipped
+      // (adding 0 * G leaves the sum unchanged), t ascending as before
+      constexpr int SEG = 8;
+      for (int j0 = 0; j0 < p; j0 += 256 * SEG) {
+        double acc[SEG];
+#pragma unroll
+        for (int u = 0; u < SEG; ++u) acc[u] = 0.0;
+        for (int t = 0; t < na; ++t) {
+          const double dt = dA[t];
+          if (dt == 0.0) continue;
+          const double *Gt = G + (int64_t)ia[t] * p;
+#pragma unroll
+          for (int u = 0; u < SEG; ++u) {
+            const int j = j0 + tid + 256 * u;
+            if (j < p) acc[u] = fma(Gt[j], dt, acc[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < SEG; ++u) {
+          const int j = j0 + tid + 256 * u;
+          if (j < p && !act[j]) g[j] -= acc[u];
+        }
       }
       __syncthreads();
       for (int t = tid; t < na; t += 256) dA[t] = 0.0;
@@ -193,7 +214,7 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
         base += tot;
         __syncthreads();
       }
-      if (base > LS_AMAX) { st = 2; break; }
+      if (base > LS_AMAX) { st = 2; fail_m = m; break; }
       na = base;
       if (na == na0) break;
       if (na <= LS_GC)   // G_AA entries of the new variables (G symmetric)
@@ -218,10 +239,24 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
     const double rsq = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     if (tid == 0) rsq_out[(int64_t)f * nlam + m] = rsq;
     __syncthreads();
-    if (early && m + 1 >= min(5, nlam) && (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999)) { L = m + 1; break; }
+    if (early && f == 0 && m + 1 >= min(5, nlam) && (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999)) {
+      L = m + 1;
+      break;
+    }
     rsq_prev = rsq;
+    // folds stop once the full fit (running concurrently) has published a
+    // path length they have reached
+    if (early && f > 0) {
+      const int Lp = __hip_atomic_load(nlam_out, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (Lp > 0 && m + 1 >= Lp) { L = m + 1; break; }
+    }
   }
-  if (tid == 0) { nlam_out[f] = L; status[f] = st; }
+  if (tid == 0) {
+    status[f] = st;
+    status[gridDim.x + prob0 + f] = st ? fail_m : nlam;   // lambda index of a failure
+    if (f == 0) __hip_atomic_store(nlam_out, L, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else nlam_out[f] = L;
+  }
 }
 
 // Hold-out SSE of fold f (problem f >= 1) at lambda m: one workgroup per (m, f).
@@ -317,7 +352,7 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   int *actws = (int *)alloc((size_t)nprob * p * 4);
   double *bpath = (double *)alloc((size_t)nprob * nlambda * p * 8);
   double *rsq = (double *)alloc((size_t)nprob * nlambda * 8);
-  int *nl = (int *)alloc((size_t)nprob * 4), *sts = (int *)alloc((size_t)nprob * 4);
+  int *nl = (int *)alloc((size_t)nprob * 4), *sts = (int *)alloc((size_t)nprob * 8);
   double *sse = (double *)alloc((size_t)K * nlambda * 8);
   if (oom) { cleanup(); return fail(1002, "dfm_targeted_soft: out of device memory"); }
   // ---- inputs: Z = [w x] column-major on the host side of the copy
@@ -368,39 +403,39 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   const int maxit = 100000;
   e = hipMemcpyAsync(alm, halm.data(), (size_t)nlambda * 8, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
-  // ---- full-sample path (early exit decides the path length L)
-  hipLaunchKernelGGL(lasso_path_kernel, dim3(1), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1, thr,
-                     maxit, gws, actws, bpath, rsq, nl, sts);
-  int L = 0, s0 = 0;
-  e = hipMemcpyAsync(&L, nl, 4, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(&s0, sts, 4, hipMemcpyDeviceToHost, st);
+  // ---- every problem's path in ONE launch (one workgroup each).  The full
+  // fit (problem 0) exits early at L; the folds use the same lambdas in
+  // original units, alm_f = alm_0 ys_0 / ys_f, and run the whole grid (user
+  // lambdas: no early exit) — their first L path points are the ones used,
+  // so they need not wait for L.
+  for (int f = 1; f < nprob; ++f)
+    for (int m = 0; m < nlambda; ++m) halm[(size_t)f * nlambda + m] = halm[m] * hys[1] / hys[3 * f + 1];
+  e = hipMemcpyAsync(alm, halm.data(), halm.size() * 8, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
+  e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: memset failed"); }
+  hipLaunchKernelGGL(lasso_path_kernel, dim3(nprob), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1,
+                     thr, maxit, gws, actws, bpath, rsq, nl, sts);
+  std::vector<int> hnl(nprob), hst(2 * nprob);
+  e = hipMemcpyAsync(hnl.data(), nl, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), sts, (size_t)nprob * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: path kernel failed"); }
-  if (s0) { cleanup(); return fail(2, s0 == 1 ? "lasso coordinate descent did not converge"
-                                               : "lasso active set above 1024 variables"); }
-  // ---- fold paths on the same lambdas in original units: alm_f = alm_0 ys_0 / ys_f.
-  // The fold launch runs with nlam = L: problem f's lambdas at alm + f L, its
-  // path rows at bpath + f L p (problem 0's rows 0..L-1 stay below f L p).
-  std::vector<double> falm((size_t)nprob * L);
-  for (int f = 1; f < nprob; ++f)
-    for (int m = 0; m < L; ++m) falm[(size_t)f * L + m] = halm[m] * hys[1] / hys[3 * f + 1];
-  e = hipMemcpyAsync(alm + L, falm.data() + L, (size_t)K * L * 8, hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
-  hipLaunchKernelGGL(lasso_path_kernel, dim3(K), dim3(256), 0, st, G, strideG, p, cc, ju, alm, L, 1, 0, thr,
-                     maxit, gws, actws, bpath, rsq, nl, sts);
-  hipLaunchKernelGGL(soft_loss_kernel, dim3(L, K), dim3(256), 0, st, Zs, ld, n, p, yd, fd, ystat, bpath, L, sse);
-  std::vector<int> hst(nprob);
-  std::vector<double> hsse((size_t)K * L), hb(p), hmu(p), hsd(p);
-  e = hipMemcpyAsync(hst.data(), sts, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(hsse.data(), sse, hsse.size() * 8, hipMemcpyDeviceToHost, st);
+  const int L = hnl[0];
+  for (int f = 0; f < nprob; ++f)   // a fold's failure past L concerns lambdas the CV never reads
+    if (hst[f] && (f == 0 || hst[nprob + f] < L))
+      { cleanup(); return fail(2, hst[f] == 1 ? "lasso coordinate descent did not converge"
+                                              : "lasso active set above 1024 variables"); }
+  hipLaunchKernelGGL(soft_loss_kernel, dim3(L, K), dim3(256), 0, st, Zs, ld, n, p, yd, fd, ystat, bpath, nlambda,
+                     sse);
+  std::vector<double> hsse((size_t)K * nlambda), hb(p), hmu(p), hsd(p);
+  e = hipMemcpyAsync(hsse.data(), sse, hsse.size() * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: fold kernels failed"); }
-  for (int f = 1; f < nprob; ++f)
-    if (hst[f]) { cleanup(); return fail(2, "lasso coordinate descent failed on a fold"); }
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: loss kernel failed"); }
   // ---- meanloss = sum_f SSE_f / n (fold-size-weighted hold-out MSE), first argmin
   std::vector<double> ml(L, 0.0);
   for (int f = 0; f < K; ++f)
-    for (int m = 0; m < L; ++m) ml[m] += hsse[(size_t)f * L + m];
+    for (int m = 0; m < L; ++m) ml[m] += hsse[(size_t)f * nlambda + m];
   int best = 0;
   for (int m = 0; m < L; ++m) {
     ml[m] /= n;
