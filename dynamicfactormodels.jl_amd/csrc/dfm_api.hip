@@ -39,9 +39,9 @@ __global__ void panel_row_ssq_kernel(const double *, int64_t, int, double *);
 __global__ void col_ssq_kernel(const double *, int64_t, int, int, double *);
 __global__ void block_accum_kernel(const double *, const double *, int, int, double *, double *, int);
 __global__ void ordered_sum_kernel(const double *, int, double *);
-__global__ void ols_hc2_kernel(const double *, const double *, int, const double *, int, int, const int *,
-                               const int *, double *,
-                               double *, double *, double *, int *);
+hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, int q, const double *F, int Tphys,
+                      int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
+                      double *resid_out, int *status);
 struct StatDesc { int kind, arg0, arg1, off; };
 __global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *,
                              const double *, const double *, const StatDesc *, int, double *, int64_t);
@@ -630,7 +630,7 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   tmp.push_back((double *)ost);
   {
     Scope sc(ctx, DFM_KC_OLS);
-    hipLaunchKernelGGL(ols_hc2_kernel, dim3(1), dim3(256), 0, st, M->y, M->w, q, M->F, T, r, nullptr, nullptr, coef,
+    launch_ols(1, st, M->y, M->w, q, M->F, T, r, nullptr, nullptr, coef,
                        tst, cov, res, ost);
   }
   CK(hipGetLastError());
@@ -962,7 +962,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     }
     {
       Scope sc(ctx, DFM_KC_OLS);
-      hipLaunchKernelGGL(ols_hc2_kernel, dim3(n), dim3(256), 0, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
+      launch_ols(n, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
                          w.tstat, nullptr, nullptr, w.ost);
     }
     {
@@ -1357,7 +1357,7 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
   HIPCHK(ctx, hipMemcpyAsync(dkr, hkr.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
   {
     Scope sc(ctx, DFM_KC_OLS);
-    hipLaunchKernelGGL(ols_hc2_kernel, dim3(P), dim3(256), 0, st, dy, dw, q, F, T, kmax, dTn, dkr, coef, tst,
+    launch_ols(P, st, dy, dw, q, F, T, kmax, dTn, dkr, coef, tst,
                        nullptr, nullptr, ost);
   }
   if (coef_out) HIPCHK(ctx, hipMemcpyAsync(coef_out, coef, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));

@@ -531,32 +531,49 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
 template <int P>
 __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
                                                         double *__restrict__ Uk, int *__restrict__ status) {
-  __shared__ double sv[256];
-  __shared__ int si[256];
+  // one pass over U: each thread keeps the running max |U[r][j]| (first row
+  // on ties) of its rows for every column j, then one tree reduction over the
+  // block for all columns at once (smaller row index wins ties: same pick as
+  // a serial scan)
+  __shared__ double sv[P][256];
+  __shared__ int si[P][256];
   __shared__ double ssign[P];
   const int tid = threadIdx.x, rep = blockIdx.x;
   const double *Ur = w.U + (int64_t)rep * m * P;
   const double *theta = w.small + (int64_t)rep * small_stride<P>() + 2 * P * P;
-  for (int j = 0; j < k; ++j) {
-    double best = -1.0;
-    int bi = 0;
-    for (int r = tid; r < m; r += 256) {
-      const double a = fabs(Ur[(int64_t)r * P + j]);
-      if (a > best) { best = a; bi = r; }
+  double best[P];
+  int bi[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) { best[j] = -1.0; bi[j] = 0; }
+  for (int r = tid; r < m; r += 256) {
+    double v[P];
+#pragma unroll
+    for (int j = 0; j < P; j += 2) {
+      const double2 x = *reinterpret_cast<const double2 *>(Ur + (int64_t)r * P + j);
+      v[j] = x.x; v[j + 1] = x.y;
     }
-    sv[tid] = best; si[tid] = bi;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) {
-        const double a = sv[tid + o];
-        const int ai = si[tid + o];
-        if (a > sv[tid] || (a == sv[tid] && ai < si[tid])) { sv[tid] = a; si[tid] = ai; }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const double a = fabs(v[j]);
+      if (j < k && a > best[j]) { best[j] = a; bi[j] = r; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < P; ++j) { sv[j][tid] = best[j]; si[j][tid] = bi[j]; }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o)
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (j >= k) continue;
+        const double a = sv[j][tid + o];
+        const int ai = si[j][tid + o];
+        if (a > sv[j][tid] || (a == sv[j][tid] && ai < si[j][tid])) { sv[j][tid] = a; si[j][tid] = ai; }
       }
-      __syncthreads();
-    }
-    if (tid == 0) ssign[j] = Ur[(int64_t)si[0] * P + j] < 0.0 ? -1.0 : 1.0;
     __syncthreads();
   }
+  if (tid < k) ssign[tid] = Ur[(int64_t)si[tid][0] * P + tid] < 0.0 ? -1.0 : 1.0;
+  __syncthreads();
   if (tid < k) lam[(int64_t)rep * k + tid] = theta[tid];
   if (tid == 0) status[rep] = w.done[rep] ? 0 : 1;
   for (int64_t e = tid; e < (int64_t)m * k; e += 256) {

@@ -204,7 +204,8 @@ constexpr int OLS_TR = 128;
 // Per-replicate sample sizes Tn[rep] (rows 0..Tn-1 used) and factor counts
 // kr[rep] <= kF are optional (expanding windows, src/utils.jl:59-65); F rows
 // have stride kF, coefficient rows stride q + kF (unused tail = NaN).
-__global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__ y,
+template <int DMAX>
+__global__ __launch_bounds__(256) void ols_hc2_kernel_t(const double *__restrict__ y,
                                                       const double *__restrict__ w, int q,
                                                       const double *__restrict__ F, int Tphys, int kF,
                                                       const int *__restrict__ Tn,
@@ -214,12 +215,12 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__
                                                       double *__restrict__ cov_out,
                                                       double *__restrict__ resid_out,
                                                       int *__restrict__ status) {
-  constexpr int S = OLS_DMAX + 1;
+  constexpr int S = DMAX + 1;
   __shared__ double sD[OLS_TR * S];
   __shared__ double sy[OLS_TR], ssig[OLS_TR];
-  __shared__ double M[OLS_DMAX * S], Li[OLS_DMAX * S], Inv[OLS_DMAX * S], Meat[OLS_DMAX * S],
-      Tmp[OLS_DMAX * S];
-  __shared__ double sb[OLS_DMAX], sDy[OLS_DMAX];
+  __shared__ double M[DMAX * S], Li[DMAX * S], Inv[DMAX * S], Meat[DMAX * S],
+      Tmp[DMAX * S];
+  __shared__ double sb[DMAX], sDy[DMAX];
   __shared__ int sbad;
   const int tid = threadIdx.x, rep = blockIdx.x;
   const int T = Tn ? Tn[rep] : Tphys;
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__
   if (tid == 0) sbad = 0;
   __syncthreads();
   // Cholesky D'D = L L' (all threads step through j), then Inv = L^-T L^-1
-  for (int e = tid; e < OLS_DMAX * S; e += 256) Li[e] = 0.0;
+  for (int e = tid; e < DMAX * S; e += 256) Li[e] = 0.0;
   __syncthreads();
   for (int j = 0; j < d; ++j) {
     if (tid == 0) {
@@ -364,6 +365,20 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel(const double *__restrict__
   if (cov_out)
     for (int e = tid; e < d * d; e += 256) cov_out[(int64_t)rep * d * d + (e % d) * d + e / d] = M[(e / d) * S + e % d];
   if (tid == 0 && status) status[rep] = sbad ? 2 : 0;
+}
+
+// LDS sized to the design width: d <= 16 (every bootstrap fit at r <= 15
+// with one regressor) fits 5 workgroups per CU instead of 2.
+hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, int q, const double *F, int Tphys,
+                      int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
+                      double *resid_out, int *status) {
+  if (q + kF <= 16)
+    hipLaunchKernelGGL(ols_hc2_kernel_t<16>, dim3(nb), dim3(256), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef, tstat,
+                       cov_out, resid_out, status);
+  else
+    hipLaunchKernelGGL(ols_hc2_kernel_t<OLS_DMAX>, dim3(nb), dim3(256), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef,
+                       tstat, cov_out, resid_out, status);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- stats
