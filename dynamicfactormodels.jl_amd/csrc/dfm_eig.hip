@@ -1590,11 +1590,22 @@ __global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double 
     }
     ZF[(int64_t)sI * ldzf + (int64_t)rep * r + j] = z;
   }
-  for (int e = tid; e < r * r; e += 256) {
-    const int i = e / r, j = e % r;
+  // M1 = F' F*: 4 row-interleaved partial sums per entry (four independent
+  // chains of T/4 instead of one of T), combined in a fixed order
+  __shared__ double m1p[4][256];
+  const int part = tid >> 6;
+  for (int e0 = 0; e0 < r * r; e0 += 64) {
+    const int e = e0 + (tid & 63);
     double acc = 0.0;
-    for (int t = 0; t < T; ++t) acc = fma(fb.F[(int64_t)t * r + i], sT * U[(int64_t)t * r + j], acc);
-    M1[(int64_t)rep * r * r + e] = acc;
+    if (e < r * r) {
+      const int i = e / r, j = e % r;
+      for (int t = part; t < T; t += 4) acc = fma(fb.F[(int64_t)t * r + i], sT * U[(int64_t)t * r + j], acc);
+    }
+    m1p[part][tid & 63] = acc;
+    __syncthreads();
+    if (tid < 64 && e < r * r)
+      M1[(int64_t)rep * r * r + e] = (m1p[0][tid] + m1p[1][tid]) + (m1p[2][tid] + m1p[3][tid]);
+    __syncthreads();
   }
 }
 
