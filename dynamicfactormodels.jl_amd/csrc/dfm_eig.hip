@@ -1089,7 +1089,9 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
 
 // y2: one workgroup (4 waves) per replicate; wave w takes 16-row tiles w, w+4, ...
 template <int P>
-__global__ __launch_bounds__(256) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
+// 3 workgroups per CU (~147 VGPRs, no spills): these per-replicate passes are
+// HBM-latency-bound, so occupancy buys bandwidth (2 -> 3 WGs/CU: y2 -20 %)
+__global__ __launch_bounds__(256, 3) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
                                                       const double *__restrict__ eta,
                                                       const double *__restrict__ HZ, int64_t ldz,
                                                       const double *__restrict__ ab,
@@ -1249,7 +1251,8 @@ DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init,
 // workgroup-scope fence of __syncthreads makes it visible.  Dynamic LDS:
 // eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
 template <int P>
-__global__ __launch_bounds__(256) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
+// 3 workgroups per CU (see boot_y2_kernel)
+__global__ __launch_bounds__(256, 3) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
                                                        int it, int init, int last,
                                                        const double *__restrict__ eta,
                                                        const int *__restrict__ off, const int *__restrict__ lst,
