@@ -248,7 +248,13 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
 template <int P>
 struct SmallLds {
   static constexpr int S = P + 1;
-  double Hq[P * S], Yq[P * S], Qq[P * S], L[P * S], Li[P * S], W[P * S], V[P * S], A[P * S];
+  // A is first written after the last read of H~ (the sorted Ritz values),
+  // and the Cholesky factor L is dead while the Jacobi vectors V live:
+  // aliasing them cuts the image from 8 to 6 P x (P+1) matrices (more
+  // workgroups per CU for this latency-bound kernel)
+  union { double Hq[P * S]; double A[P * S]; };
+  union { double L[P * S]; double V[P * S]; };
+  double Yq[P * S], Qq[P * S], Li[P * S], W[P * S];
   double rc[P / 2], rs[P / 2];
   double dinv[P];   // 1 / L[j][j] of the last Cholesky (1 for dead pivots)
   int ra[P / 2], rb[P / 2], perm[P];
