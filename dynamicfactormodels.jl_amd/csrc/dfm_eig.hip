@@ -1095,9 +1095,11 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
 
 // y2: one workgroup (4 waves) per replicate; wave w takes 16-row tiles w, w+4, ...
 template <int P>
-// 3 workgroups per CU (~147 VGPRs, no spills): these per-replicate passes are
-// HBM-latency-bound, so occupancy buys bandwidth (2 -> 3 WGs/CU: y2 -20 %)
-__global__ __launch_bounds__(256, 3) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
+// 4 workgroups per CU (~113 VGPRs, no spills; a tile is loaded at the top of
+// its own iteration, no register prefetch of the next): these per-replicate
+// passes are HBM-latency-bound, and resident waves buy more bandwidth than
+// per-wave prefetch did (2 -> 4 WGs/CU: y2 -24 %, ap2 -13 %)
+__global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
                                                       const double *__restrict__ eta,
                                                       const double *__restrict__ HZ, int64_t ldz,
                                                       const double *__restrict__ ab,
@@ -1147,11 +1149,10 @@ __global__ __launch_bounds__(256, 3) void boot_y2_kernel(FactBase fb, EigWork w,
   const double *Qr = Qc + (int64_t)rep * T * P;
   double *Yr = Yo + (int64_t)rep * T * P;
   const int ntile = (T + 15) >> 4;
-  // software pipeline: the next tile's loads are issued before this tile's MFMAs
-  Y2Tile<P> cur, nxt;
-  y2_load<P>(cur, min(wave, ntile - 1), T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
+  // each tile's operands load at the top of its iteration (occupancy hides the latency)
+  Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += 4) {
-    y2_load<P>(nxt, min(tile + 4, ntile - 1), T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1191,7 +1192,6 @@ __global__ __launch_bounds__(256, 3) void boot_y2_kernel(FactBase fb, EigWork w,
           acc[1][a][b] = mfma16(Yv[a][g], Yv[b][g], acc[1][a][b]);
           acc[2][a][b] = mfma16(cur.q[a][g], cur.q[b][g], acc[2][a][b]);
         }
-    cur = nxt;
   }
   // fixed-order sum over the four waves
   for (int wv = 0; wv < 4; ++wv) {
@@ -1257,8 +1257,8 @@ DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init,
 // workgroup-scope fence of __syncthreads makes it visible.  Dynamic LDS:
 // eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
 template <int P>
-// 3 workgroups per CU (see boot_y2_kernel)
-__global__ __launch_bounds__(256, 3) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
+// 4 workgroups per CU (see boot_y2_kernel)
+__global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
                                                        int it, int init, int last,
                                                        const double *__restrict__ eta,
                                                        const int *__restrict__ off, const int *__restrict__ lst,
@@ -1304,11 +1304,10 @@ __global__ __launch_bounds__(256, 3) void boot_ap2_kernel(FactBase fb, EigWork w
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) { res2[ct] = 0.0; aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; }
   const int ntile = (T + 15) >> 4;
-  // software pipeline: operands of the wave's next tile load during this tile's MFMAs
-  Ap2Tile<P> cur, nxt;
-  ap2_load<P>(cur, min(wave, ntile - 1), T, r, lane, init, Qr, Yr, fb);
+  // each tile's operands load at the top of its iteration (occupancy hides the latency)
+  Ap2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += 4) {
-    ap2_load<P>(nxt, min(tile + 4, ntile - 1), T, r, lane, init, Qr, Yr, fb);
+    ap2_load<P>(cur, tile, T, r, lane, init, Qr, Yr, fb);
     const int t0 = tile * 16;
     double qv[NT][4];
     if (init) {
@@ -1328,8 +1327,8 @@ __global__ __launch_bounds__(256, 3) void boot_ap2_kernel(FactBase fb, EigWork w
           ya[ct] = mfma16(cur.yo[kk], bAm[kk][ct], ya[ct]);
           qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
         }
-      // every wave reads only its own tiles' Y rows, and the next tile's rows
-      // were loaded before these stores: Qn may overwrite this tile's Y rows
+      // every wave reads only its own tiles' Y rows, loaded (above) before
+      // these stores: Qn may overwrite this tile's Y rows
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int t = t0 + 4 * g + lk;
@@ -1351,7 +1350,6 @@ __global__ __launch_bounds__(256, 3) void boot_ap2_kernel(FactBase fb, EigWork w
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(cur.fa[g], qv[ct][g], aacc[ct]);
-    cur = nxt;
   }
   // residuals: sum over the 4 row-lanes of a column, then over waves (fixed order)
   if (!init) {
