@@ -890,8 +890,8 @@ __global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, in
   emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
 }
 
-hipError_t launch_gemm_loadings(const double *E, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, const double *Lb, const double *M1, double *Lout, hipStream_t st);
+hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
+                                int r, double invT, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1);
@@ -1610,8 +1610,12 @@ __global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double 
     }
     m1p[part][tid & 63] = acc;
     __syncthreads();
-    if (tid < 64 && e < r * r)
-      M1[(int64_t)rep * r * r + e] = (m1p[0][tid] + m1p[1][tid]) + (m1p[2][tid] + m1p[3][tid]);
+    if (tid < 64 && e < r * r) {
+      const double v = (m1p[0][tid] + m1p[1][tid]) + (m1p[2][tid] + m1p[3][tid]);
+      M1[(int64_t)rep * r * r + e] = v;
+      // the same block as k-rows T..T+r-1 of the loadings GEMM's B operand
+      ZF[(int64_t)(T + e / r) * ldzf + (int64_t)rep * r + e % r] = v;
+    }
     __syncthreads();
   }
 }
@@ -1629,22 +1633,35 @@ __global__ void boot_lfinish_kernel(const double *__restrict__ Lb, int N, int r,
   Lout[(int64_t)rep * N * r + e] = v / T;
 }
 
+// rows T.. of [E; L'; 0]: row T+i = column i of L (i < r), then zero rows
+__global__ void eaug_tail_kernel(const double *__restrict__ Lb, int N, int r, int64_t ld, double *__restrict__ tail) {
+  const int i = blockIdx.y;
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= ld) return;
+  tail[(int64_t)i * ld + n] = (i < r && n < N) ? Lb[n * r + i] : 0.0;
+}
+
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
                   const double *Uk, const double *eta, const int *off, const int *lst, int nb,
                   double *Fout, double *Lout, char *ws, hipStream_t st) {
   const int T = fb.T, r = fb.r;
   const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
+  // ZF: Kp rows — F-scatter rows 0..T-1, the M1 = F'F* blocks as rows
+  // T..T+r-1 (written by boot_zf), zero rows up to Kp (the GEMM's k padding)
+  const int Kp = (T + r + 15) / 16 * 16;
   double *ZF = (double *)ws;
-  double *GL = ZF + (size_t)((T + 15) / 16 * 16) * ldzf;
+  double *GL = ZF + (size_t)Kp * ldzf;
   double *M1 = GL + (size_t)N * ldzf;
-  // ZF rows T..round_up(T,16) are the zero k-padding the LDS-DMA GEMM reads
-  const int Tp = (T + 15) / 16 * 16;
-  hipMemsetAsync(ZF + (size_t)T * ldzf, 0, (size_t)(Tp - T) * ldzf * 8, st);
+  double *Eaug = M1 + (size_t)nb * r * r;   // [E; L'; 0]: Kp x ld
+  hipMemsetAsync(ZF + (size_t)T * ldzf, 0, (size_t)(Kp - T) * ldzf * 8, st);
   hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, ldzf, M1);
   hipError_t e;
   if (ldzf == (int64_t)nb * r && ld % 2 == 0) {
-    // GEMM with the finish fused in its epilogue (no E'ZF round trip through HBM)
-    e = launch_gemm_loadings(Ep, ld, ZF, ldzf, N, nb * r, T, r, Lb, M1, Lout, st);
+    // one GEMM of depth T + r does the whole finish (see gemm_loadings_kernel)
+    hipMemcpy2DAsync(Eaug, (size_t)ld * 8, Ep, (size_t)ld * 8, (size_t)ld * 8, T, hipMemcpyDeviceToDevice, st);
+    hipLaunchKernelGGL(eaug_tail_kernel, dim3((unsigned)((ld + 255) / 256), Kp - T), dim3(256), 0, st, Lb, N, r, ld,
+                       Eaug + (size_t)T * ld);
+    e = launch_gemm_loadings(Eaug, ld, ZF, ldzf, N, nb * r, T + r, r, 1.0 / T, Lout, st);
     return e == hipSuccess ? 0 : 1000 + (int)e;
   }
   e = launch_gemm(true, Ep, ld, ZF, ldzf, GL, ldzf, N, (int)ldzf, T, st);
@@ -1656,8 +1673,9 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
 }
 size_t fact_loadings_bytes(int T, int N, int r, int nb) {
   const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
-  const int Tp = (T + 15) / 16 * 16;
-  return ((size_t)Tp * ldzf + (size_t)N * ldzf + (size_t)nb * r * r) * 8 + 1024;
+  const int Kp = (T + r + 15) / 16 * 16;
+  const int64_t ld = ((int64_t)N + 15) / 16 * 16;
+  return ((size_t)Kp * ldzf + (size_t)N * ldzf + (size_t)nb * r * r + (size_t)Kp * ld) * 8 + 1024;
 }
 
 // ---- model-level precompute: EL = E L (T x r), S = L'L, cF, hd

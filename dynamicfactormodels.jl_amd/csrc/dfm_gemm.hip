@@ -301,16 +301,19 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 #define gemmh_kernel gemmh_kernel_t<4, 2, false>
 
 // ---------------------------------------------------------------------------
-// Loadings GEMM of the factored bootstrap with its finish fused in the
-// epilogue:  L*[rep][n][j] = ( (E' ZF)[n][rep r + j] + sum_i Lb[n][i] M1[rep][i][j] ) / T
+// Loadings GEMM of the factored bootstrap:
+//   L*[rep][n][j] = ( [E' | L] [ZF ; M1] )[n][rep r + j] / T
 // (src/DynamicFactorModel.jl:90 for every replicate: L* = X*' F* / T with
-// X*' F* = L (F'F*) + E' P' D F*).  A^T operand E (K = T rows x lda) and B
-// operand ZF (Kpad x ldb, rows K..round_up(K,16) zero) both staged by LDS-DMA
-// into [k][a] images (4-deep ring as gemmh_kernel).  Grid: the row blocks
-// (64 variables) are spread over the XCDs — XCD x owns row blocks x, x+8, ...
-// whose E slabs (64 x T x 8 B each) stay in its L2 — and every XCD walks the
-// column blocks in the same order, so a ZF tile is fetched from HBM once and
-// served to the other XCDs from the Infinity Cache.
+// X*' F* = E' P' D F* + L (F'F*)): the r x r blocks M1 = F'F* sit under ZF
+// as r extra k-rows and L' under E, so the whole finish is K = T + r MFMA
+// depth (+1.6 %) and the epilogue a plain scaled store.  A^T operand
+// [E; L'] (Kpad x lda) and B operand [ZF; M1; 0] (Kpad x ldb, Kpad =
+// round_up(T + r, 16), zero rows past T + r) staged by LDS-DMA into [k][a]
+// images (4-deep ring as gemmh_kernel).  Grid: the row blocks (64 variables)
+// are spread over the XCDs — XCD x owns row blocks x, x+8, ... whose E slabs
+// (64 x T x 8 B each) stay in its L2 — and every XCD walks the column blocks
+// in the same order, so a ZF tile is fetched from HBM once and served to the
+// other XCDs from the Infinity Cache.
 DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda, const double *__restrict__ B,
                         int64_t ldb, int k0, int abase, int bbase, int M, int Nc, int K, int wave, int lane) {
   double *la = stage, *lb = stage + GT * G2_KS;
@@ -332,8 +335,6 @@ DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda
 __global__ __launch_bounds__(256, 2) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
                                                                const double *__restrict__ B, int64_t ldb, int M,
                                                                int Nc, int K, int nrb, int ncb, int r, double invT,
-                                                               const double *__restrict__ Lb,
-                                                               const double *__restrict__ M1,
                                                                double *__restrict__ Lout) {
   constexpr int NBUF = 4;
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
@@ -390,20 +391,17 @@ __global__ __launch_bounds__(256, 2) void gemm_loadings_kernel(const double *__r
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
       if (n < M && col < Nc) {
         const int rep = col / r, jj = col - rep * r;
-        const double *m1 = M1 + (int64_t)rep * r * r + jj;
-        double w = v;
-        for (int i = 0; i < r; ++i) w = fma(Lb[(int64_t)n * r + i], m1[i * r], w);
-        Lout[((int64_t)rep * M + n) * r + jj] = w * invT;
+        Lout[((int64_t)rep * M + n) * r + jj] = v * invT;
       }
     }
 }
 
-hipError_t launch_gemm_loadings(const double *E, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, const double *Lb, const double *M1, double *Lout, hipStream_t st) {
+hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
+                                int r, double invT, double *Lout, hipStream_t st) {
   const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int nrb8 = (nrb + 7) / 8;
-  hipLaunchKernelGGL(gemm_loadings_kernel, dim3(8 * nrb8 * ncb), dim3(256), 0, st, E, lda, ZF, ldb, N, Nc, K, nrb,
-                     ncb, r, 1.0 / K, Lb, M1, Lout);
+  hipLaunchKernelGGL(gemm_loadings_kernel, dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N, Nc, K, nrb,
+                     ncb, r, invT, Lout);
   return hipGetLastError();
 }
 
