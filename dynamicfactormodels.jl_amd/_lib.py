@@ -70,6 +70,9 @@ SIGNATURES = [
     ("dfm_windows", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
                               C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
                               c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("dfm_windows_forecast", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
+                                       C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
+                                       c_double_p, c_double_p]),
     ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                     C.c_double, c_double_p, c_uint8_p]),

@@ -590,9 +590,37 @@ def pseudo_out_of_sample_refits(y, w, x, criterion: str = "ICp2", num_prediction
             "criterion_value": cv, "eigenvalues": ev, "coefficients": coef, "t_stats": ts}
 
 
-def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions: int = 200):
-    """``src/utils.jl:54-72``.  The refits are built (pseudo_out_of_sample_refits);
-    the forecast step calls ``predict`` -> ``get_factors``, which reads the
-    non-existent field ``dfm.rotation`` (defect D4), so it is not reproduced."""
-    raise NotImplementedError("predict/get_factors is broken in the reference (defect D4); "
-                              "use pseudo_out_of_sample_refits for the refit loop")
+def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions: int = 200,
+                                   kmax: Optional[int] = None, ctx: Optional[Context] = None):
+    """``src/utils.jl:54-72``: one-step-ahead pseudo out-of-sample forecasts.
+    For date_index = T-P+1..T the model is refit on rows 1..date_index-1 and
+    row date_index is predicted with ``predict`` (``src/DynamicFactorModel.jl:152``)
+    through ``get_factors`` repaired (defect D4: the local rotation of ``:126``).
+    ``model`` is ``DynamicFactorModel`` with a criterion name as its first extra
+    argument (the IC-sweep constructor, ``:53``).  Returns (predictions,
+    true_values)."""
+    if model is not DynamicFactorModel or not model_args or not isinstance(model_args[0], str):
+        raise NotImplementedError("the device path refits DynamicFactorModel(y, w, x, criterion) per window")
+    ctx = ctx or default_context()
+    crit = model_args[0]
+    y = _f64(y).ravel()
+    w = _f64(w, 2)
+    x = _f64(x, 2)
+    T, N = x.shape
+    q, P = w.shape[1], int(num_predictions)
+    m = min(T - P, N)
+    km = int(kmax) if kmax else int(math.ceil(m / 2))
+    km = min(km, int(math.ceil(m / 2)))
+    r = np.zeros(P, dtype=np.int64)
+    pred, true = np.zeros(P), np.zeros(P)
+    xc, wc = _colmajor(x), _colmajor(w)
+    ctx.check(ctx.lib.dfm_windows_forecast(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T,
+                                           xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[crit], km,
+                                           r.ctypes.data_as(_lib.c_int64_p), _lib.ptr(pred), _lib.ptr(true)))
+    return pred, true
+
+
+def MSE(y, predictions) -> float:
+    """``src/utils.jl:75``: sum((y - predictions).^2) / length(y) (host arithmetic)."""
+    y = np.asarray(y, dtype=np.float64)
+    return float(np.sum((y - np.asarray(predictions)) ** 2) / y.size)

@@ -1238,10 +1238,106 @@ __global__ void window_scale_kernel(const double *__restrict__ Uk, int T, int k,
   F[(int64_t)rep * T * k + e] = t < n ? sqrt((double)n) * Uk[(int64_t)rep * T * k + e] : 0.0;
 }
 
+// ---- forecast step of pseudo_out_of_sample_forecasts (src/utils.jl:54-72)
+// with get_factors repaired (defect D4: the local rotation = L (L'L)^-1 of
+// src/DynamicFactorModel.jl:126, L = block 1's full loadings).  For the
+// window's first r columns rotation is L_j n / lambda_j (N > T: L'L =
+// Lambda / n) or L_j / N (T >= N: L'L = N I), so with the new row
+// x~ = (x_n - mean(X_w)) / std(X_w) (scalar moments of all window entries,
+// Julia 0.3 mean/std of a matrix):
+//   N > T : F_new_j = sum_{s<n} (x~ . x_s) F_j[s] / lambda_j,
+//           x~ . x_s = (H[n][s] - mean * rowsum_s) / std   (H = X X', prefix Gram)
+//   T >= N: F_new_j = x~ . V_j / sqrt(N)
+// and the forecast is [w_n F_new] beta (src/DynamicFactorModel.jl:152-155).
+__global__ void panel_row_sums_kernel(const double *__restrict__ P, int64_t ld, int N, double *__restrict__ rs,
+                                      double *__restrict__ ss) {
+  __shared__ double r1[256], r2[256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int c = tid; c < N; c += 256) { const double v = P[(int64_t)t * ld + c]; a += v; b = fma(v, v, b); }
+  r1[tid] = a; r2[tid] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) { r1[tid] += r1[tid + o]; r2[tid] += r2[tid + o]; }
+    __syncthreads();
+  }
+  if (tid == 0) { rs[t] = r1[0]; ss[t] = r2[0]; }
+}
+
+__global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp, int64_t ld, int T, int N, int n0,
+                                       int q, int kmax, const double *__restrict__ H, int64_t ldH,
+                                       const double *__restrict__ F, const double *__restrict__ Uk,
+                                       const double *__restrict__ lam, const double *__restrict__ rs,
+                                       const double *__restrict__ ss, const int *__restrict__ kr,
+                                       const double *__restrict__ coef, const double *__restrict__ y,
+                                       const double *__restrict__ w, double *__restrict__ pred,
+                                       double *__restrict__ truev) {
+  __shared__ double red[256];
+  __shared__ double smom[2];
+  const int wi = blockIdx.x, tid = threadIdx.x, n = n0 + wi, r = kr[wi], d = q + kmax;
+  if (tid == 0) {   // scalar moments of the window's n x N entries (fixed order)
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < n; ++s) { a += rs[s]; b += ss[s]; }
+    const double cnt = (double)n * N, mu = a / cnt;
+    smom[0] = mu;
+    smom[1] = sqrt((b - cnt * mu * mu) / (cnt - 1.0));
+  }
+  __syncthreads();
+  const double mu = smom[0], sd = smom[1];
+  double yhat = 0.0;
+  for (int j = 0; j < r; ++j) {
+    double part = 0.0;
+    if (orient == 0) {
+      const double *Hn = H + (int64_t)n * ldH;
+      const double *Fw = F + (int64_t)wi * T * kmax;
+      for (int s = tid; s < n; s += 256) part = fma((Hn[s] - mu * rs[s]) / sd, Fw[(int64_t)s * kmax + j], part);
+    } else {
+      const double *xn = Xp + (int64_t)n * ld;
+      const double *V = Uk + (int64_t)wi * N * kmax;
+      for (int c = tid; c < N; c += 256) part = fma((xn[c] - mu) / sd, V[(int64_t)c * kmax + j], part);
+    }
+    red[tid] = part;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (tid < o) red[tid] += red[tid + o];
+      __syncthreads();
+    }
+    const double fnew = orient == 0 ? red[0] / lam[(int64_t)wi * kmax + j] : red[0] / sqrt((double)N);
+    yhat = fma(fnew, coef[(int64_t)wi * d + q + j], yhat);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    for (int i = 0; i < q; ++i) yhat = fma(w[(int64_t)i * T + n], coef[(int64_t)wi * d + i], yhat);
+    pred[wi] = yhat;
+    truev[wi] = y[n];
+  }
+}
+
+static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
+                        int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
+                        double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
+                        double *pred_out, double *true_out);
+
 extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                            const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
                            int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                            double *coef_out, double *tstat_out) {
+  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, V_out, crit_out, eig_out,
+                      coef_out, tstat_out, nullptr, nullptr);
+}
+
+extern "C" int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                                    const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
+                                    int kmax, int64_t *r_out, double *pred_out, double *true_out) {
+  if (!pred_out || !true_out) return fail(ctx, -2, "dfm_windows_forecast: output pointers required");
+  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, pred_out, true_out);
+}
+
+static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
+                        int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
+                        double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
+                        double *pred_out, double *true_out) {
   if (!ctx) return -1;
   const int T = (int)T64, N = (int)N64;
   if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
@@ -1289,9 +1385,12 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
   HIPCHK(ctx, hipMemcpyAsync(deta, heta.data(), heta.size() * 8, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
   if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  double *H = nullptr;
+  int64_t ldH = 0;
   if (orient == 0) {
-    const int64_t ldH = round_up(T, 16);
-    double *H = (double *)dal((size_t)T * ldH * 8), *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
+    ldH = round_up(T, 16);
+    H = (double *)dal((size_t)T * ldH * 8);
+    double *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
     char *fws = (char *)dal(fact_workspace_bytes(T, P, Pb));
     int *off = (int *)dal((size_t)P * (T + 1) * 4), *lst = (int *)dal((size_t)P * T * 4);
     if (!H || !zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
@@ -1362,6 +1461,18 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
   }
   if (coef_out) HIPCHK(ctx, hipMemcpyAsync(coef_out, coef, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
   if (tstat_out) HIPCHK(ctx, hipMemcpyAsync(tstat_out, tst, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
+  if (pred_out) {   // forecast step: predict row n = n0 + w from window w's fit
+    double *rs = (double *)dal((size_t)T * 8), *ss = (double *)dal((size_t)T * 8);
+    double *dp_ = (double *)dal((size_t)P * 8), *dt_ = (double *)dal((size_t)P * 8);
+    if (!rs || !ss || !dp_ || !dt_) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    Scope sc(ctx, DFM_KC_MISC);
+    hipLaunchKernelGGL(panel_row_sums_kernel, dim3(T), dim3(256), 0, st, dp.P, dp.ld, N, rs, ss);
+    hipLaunchKernelGGL(window_forecast_kernel, dim3(P), dim3(256), 0, st, orient, dp.P, dp.ld, T, N, n0, q, kmax, H,
+                       ldH, F, Uk, lam, rs, ss, dkr, coef, dy, dw, dp_, dt_);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(pred_out, dp_, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(true_out, dt_, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+  }
   HIPCHK(ctx, hipStreamSynchronize(st));
   return 0;
 }

@@ -205,12 +205,21 @@ int dfm_chow_all(dfm_model *m, int64_t bp, double *LR, double *LM, double *Wald)
  * N > T uses the prefix-Gram identity (one Gram for all windows).
  * Outputs per window: r (P), V(r) (P), criterion value (P), eigenvalues
  * (P x kmax, row-major), OLS coefficients and HC2 t-stats (P x (q + kmax),
- * row-major, NaN past q + r).  The forecast step itself is not built: the
- * reference's predict/get_factors read a non-existent field (defect D4). */
+ * row-major, NaN past q + r).  The forecast step: dfm_windows_forecast. */
 int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                 const double *X, int64_t T, int64_t N, int64_t ldx, int P, int crit,
                 int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                 double *coef_out, double *tstat_out);
+
+/* pseudo_out_of_sample_forecasts (src/utils.jl:54-72) in full: the refits of
+ * dfm_windows, then window w predicts row n = T-P+w from its own fit:
+ * predict (src/DynamicFactorModel.jl:152-155) with get_factors repaired
+ * (defect D4: rotation = L (L'L)^-1 of :126, L = the window's loadings; the
+ * new row normalised by the scalar mean / sample std of the window's X).
+ * Outputs per window: r (P), prediction (P), true value y[n] (P). */
+int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                         const double *X, int64_t T, int64_t N, int64_t ldx, int P, int crit,
+                         int kmax, int64_t *r_out, double *pred_out, double *true_out);
 
 /* --------------------------------------------------- targeted predictors
  * targeted_predictors(..., thresholding="hard") (src/targeted_predictors.jl:9-30).

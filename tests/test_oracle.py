@@ -276,3 +276,18 @@ def test_golden_soft_reproduces(oracle):
     mask, res = oracle.targeted_predictors_soft(g["y"], g["w"], g["x"], g["folds"])
     assert np.array_equal(mask, g["mask"]) and res["best"] == int(g["best"])
     assert np.allclose(res["meanloss"], g["meanloss"], rtol=1e-10, atol=0)
+
+
+# ----------------------------------------------------- forecasts (D4 repaired)
+def test_repaired_get_factors_reproduces_in_sample_factors(oracle):
+    """get_factors(dfm, x) of the training rows themselves, with the scalar
+    normalisation undone, reproduces the fitted factors: rotation = L (L'L)^-1
+    is the least-squares inverse of x = F L' on the factor space."""
+    for T, N in [(80, 150), (150, 40)]:
+        y, x, w = _panel(oracle, T, N, 3, 31)
+        d = oracle.DynamicFactorModel(y, w, x, 3)
+        L = d.loadings[0]
+        rot = L @ np.linalg.inv(L.T @ L)
+        assert np.allclose((x @ rot)[:, :3], d.F, atol=1e-8 * np.abs(d.F).max())
+        xs_new = x[:2] * x.std(ddof=1) + x.mean()        # de-normalised by the scalar moments
+        assert np.allclose(oracle.get_factors(d, xs_new), d.F[:2], atol=1e-8 * np.abs(d.F).max())
