@@ -24,7 +24,19 @@ int eig_block_p(int m, int k, int req);
 extern int g_last_iters;
 extern int64_t g_last_rep_iters;
 int spectrum_max();
-hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+int spectrum_any_max();
+int64_t spectrum_work(int m, int nb);
+int dense_eig_max();
+int launch_factors_wide(int orient, const double *X, int64_t ld, int T, int N, int k, const double *Uk,
+                        double *F, double *L, double *colssr, hipStream_t st, double Ts);
+int64_t ols_wide_work(int T, int d);
+hipError_t launch_ols_wide(const double *y, const double *w, int q, const double *F, int T, int k, double *coef,
+                           double *tstat, double *cov_out, double *resid_out, int *status, double *work,
+                           hipStream_t st);
+int64_t dense_eig_work(int m, int k);
+hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
+                            double *work, hipStream_t st);
+hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev, double *work,
                            hipStream_t st);
 // dfm_model.hip
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
@@ -294,7 +306,7 @@ int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters) {
 const char *dfm_kernel_class_name(int cls) {
   return (cls >= 0 && cls < DFM_KC_COUNT) ? kclass_names[cls] : "?";
 }
-int dfm_full_spectrum_max(void) { return spectrum_max(); }
+int dfm_full_spectrum_max(void) { return spectrum_any_max(); }
 
 int dfm_ic_sweep(const double *eig, int n_eig, int kmax, double trace, int64_t T, int64_t N,
                  double sigma2, double *out) {
@@ -330,6 +342,21 @@ int dfm_ic_sweep(const double *eig, int n_eig, int kmax, double trace, int64_t T
 static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const double *warm, int kw,
                    double *lam, double *Uk, double *trace, int *status_dev) {
   const int p = eig_block_p(m, k, ctx->block);
+  if ((p > 32 || p < k) && nb == 1 && m >= 2 && m <= dense_eig_max()) {
+    // k beyond the subspace block: tridiagonalisation + inverse iteration (dfm_spec.hip)
+    double *wk = nullptr;
+    HIPCHK(ctx, hipMalloc(&wk, (size_t)dense_eig_work(m, k) * 8));
+    hipError_t e;
+    {
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      e = launch_dense_eig(G, m, m, k, lam, Uk, trace, wk, ctx->stream);
+    }
+    if (e == hipSuccess && status_dev) e = hipMemsetAsync(status_dev, 0, sizeof(int), ctx->stream);
+    hipStreamSynchronize(ctx->stream);
+    hipFree(wk);
+    if (e != hipSuccess) return fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));
+    return 0;
+  }
   if (p > 32 || p < k) return fail(ctx, -20, "eigensolver block %d unsupported for k=%d m=%d", p, k, m);
   const int P = p <= 16 ? 16 : 32;
   const size_t bytes = eig_workspace_bytes_padded(m, nb, P, ctx->maxit);
@@ -447,9 +474,14 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
     double *ev = nullptr;
     LCK(dalloc(&ev, mm));
     tmp.push_back(ev);
+    double *wk = nullptr;
+    if (spectrum_work(mm, 1) > 0) {
+      LCK(dalloc(&wk, (size_t)spectrum_work(mm, 1)));
+      tmp.push_back(wk);
+    }
     {
       Scope sc(ctx, DFM_KC_EIG_OTHER);
-      LCK(launch_spectrum(G, mm, (int64_t)mm * mm, mm, 1, ev, st));
+      LCK(launch_spectrum(G, mm, (int64_t)mm * mm, mm, 1, ev, wk, st));
     }
     sp.resize(mm);
     LCK(hipMemcpyAsync(sp.data(), ev, (size_t)mm * 8, hipMemcpyDeviceToHost, st));
@@ -468,9 +500,9 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   // the sweep reports all 7 criteria: PCp rows need sigma^2 (NaN when the full
   // spectrum is out of reach and the chosen criterion is not a PCp one)
   const bool full_spec = pcp || (nob && r <= 0 && (kmax > 24 || m <= spectrum_max()));
-  if (full_spec && m > spectrum_max()) {
+  if (full_spec && m > spectrum_any_max()) {
     return bail(fail(ctx, -30, "PCp criteria / kmax > 24 need the full spectrum; supported for "
-                               "min(T,N) <= %d (got %d)", spectrum_max(), m));
+                               "min(T,N) <= %d (got %d)", spectrum_any_max(), m));
   }
   if (nob || full_spec) {
     TALLOC(Gfull, (size_t)m * m);
@@ -522,13 +554,13 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
     }
     if (r <= 0) {   // the sweep's eigenvalues of this block
       if (nob && full_spec) bev[j] = spec_full;
-      else if (!nob && M->bm[j] <= spectrum_max() && (kmax > 24 || pcp)) {
+      else if (!nob && M->bm[j] <= spectrum_any_max() && (kmax > 24 || pcp)) {
         std::vector<double> sp;
         CKB(spectrum(Gb[j], M->bm[j], sp));
         bev[j] = sp;
       } else if (kmax > 24) {
         CKB(fail(ctx, -30, "kmax > 24 needs the full spectrum of every block; supported for Gram "
-                           "size <= %d (block %d: %d)", spectrum_max(), j, M->bm[j]));
+                           "size <= %d (block %d: %d)", spectrum_any_max(), j, M->bm[j]));
       }
       // top-k pairs: the trace, and the sweep's eigenvalues when no spectrum
       CKB(top_eig(j, bev[j].empty() ? kmax : 1));
@@ -587,9 +619,15 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   }
   for (int j = 0; j < nblk; ++j) {
     Scope sc(ctx, DFM_KC_FACTORS);
-    if (launch_factors(M->orient, block_src(j), M->bt[j], N, r, 1, M->Ubs[j], M->F + (size_t)M->ba[j] * r,
-                       M->Ls[j], nob ? M->colssr : nullptr, st, (double)T, 0))
-      CKB(fail(ctx, -4, "r=%d too large", r));
+    if (r <= 32) {
+      if (launch_factors(M->orient, block_src(j), M->bt[j], N, r, 1, M->Ubs[j], M->F + (size_t)M->ba[j] * r,
+                         M->Ls[j], nob ? M->colssr : nullptr, st, (double)T, 0))
+        CKB(fail(ctx, -4, "r=%d too large", r));
+    } else if (launch_factors_wide(M->orient, M->Xp + (size_t)M->ba[j] * M->ld, M->ld, M->bt[j], N, r, M->Ubs[j],
+                                   M->F + (size_t)M->ba[j] * r, M->Ls[j], nob ? M->colssr : nullptr, st,
+                                   (double)T)) {
+      CKB(fail(ctx, 1001, "factor kernels failed"));
+    }
     if (nob && M->orient == 1) {
       double *lr = nullptr;
       CK(dalloc(&lr, r));
@@ -622,16 +660,21 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   }
   // --- OLS + HC2 on [w vcat(F_j)] (:40-48, :130-133)
   const int d = q + r;
-  if (d > 32) return bail(fail(ctx, -5, "q + r = %d > 32 unsupported", d));
+  if (d > T) return bail(fail(ctx, -5, "q + r = %d regressors exceed the %d observations", d, T));
   double *coef = nullptr, *tst = nullptr, *cov = nullptr, *res = nullptr;
   int *ost = nullptr;
   TALLOC(coef, d); TALLOC(tst, d); TALLOC(cov, (size_t)d * d); TALLOC(res, T);
   CK(dalloc(&ost, 1));
   tmp.push_back((double *)ost);
-  {
+  if (d <= 32) {
     Scope sc(ctx, DFM_KC_OLS);
     launch_ols(1, st, M->y, M->w, q, M->F, T, r, nullptr, nullptr, coef,
                        tst, cov, res, ost);
+  } else {   // wide design: GEMM-built OLS (dfm_wide.hip)
+    double *wk = nullptr;
+    TALLOC(wk, (size_t)ols_wide_work(T, d));
+    Scope sc(ctx, DFM_KC_OLS);
+    CK(launch_ols_wide(M->y, M->w, q, M->F, T, r, coef, tst, cov, res, ost, wk, st));
   }
   CK(hipGetLastError());
   M->coef.resize(d); M->tstat.resize(d); M->cov.resize((size_t)d * d); M->resid.resize(T);
@@ -1041,6 +1084,10 @@ int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const d
 
 // --------------------------------------------------------- stand-alone entry points
 namespace {
+struct DevBuf {
+  double *p = nullptr;
+  ~DevBuf() { hipFree(p); }
+};
 struct DevPanel {
   double *raw = nullptr, *P = nullptr;
   int64_t ld = 0;
@@ -1092,7 +1139,9 @@ int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, int64_t ldx
   int est = 0;
   if (!rc) {
     Scope sc(ctx, DFM_KC_FACTORS);
-    if (launch_factors(orient, src, T, N, k, 1, Uk, Fd, Ld, nullptr, st)) rc = fail(ctx, -4, "k too large");
+    if (k <= 32 ? launch_factors(orient, src, T, N, k, 1, Uk, Fd, Ld, nullptr, st)
+                : launch_factors_wide(orient, dp.P, dp.ld, T, N, k, Uk, Fd, Ld, nullptr, st, (double)T))
+      rc = fail(ctx, 1001, "factor kernels failed");
   }
   std::vector<double> hF((size_t)T * k), hL((size_t)N * k);
   if (!rc) {
@@ -1117,16 +1166,18 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
   if (!ctx) return -1;
   if (!X || !eigvals_m || T64 < 1 || N64 < 1 || ldx < T64) return fail(ctx, -2, "bad arguments");
   const int T = (int)T64, N = (int)N64, m = std::min(T, N);
-  if (m > spectrum_max()) return fail(ctx, -30, "full spectrum supported for min(T,N) <= %d", spectrum_max());
+  if (m > spectrum_any_max()) return fail(ctx, -30, "full spectrum supported for min(T,N) <= %d", spectrum_any_max());
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   DevPanel dp;
   int rc = upload_panel(ctx, X, T, N, ldx, dp);
   if (rc) return rc;
   const int orient = (N > T) ? 0 : 1;
-  double *G = nullptr, *ev = nullptr;
-  HIPCHK(ctx, dalloc(&G, (size_t)m * m));
-  HIPCHK(ctx, dalloc(&ev, m));
+  DevBuf Gb, evb, wk;
+  HIPCHK(ctx, dalloc(&Gb.p, (size_t)m * m));
+  HIPCHK(ctx, dalloc(&evb.p, m));
+  double *G = Gb.p, *ev = evb.p;
+  if (spectrum_work(m, 1) > 0) HIPCHK(ctx, dalloc(&wk.p, (size_t)spectrum_work(m, 1)));
   PanelSrc src{nullptr, dp.P, nullptr, nullptr, dp.ld, 0};
   {
     Scope sc(ctx, DFM_KC_GRAM);
@@ -1134,7 +1185,7 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
   }
   {
     Scope sc(ctx, DFM_KC_EIG_OTHER);
-    HIPCHK(ctx, launch_spectrum(G, m, (int64_t)m * m, m, 1, ev, st));
+    HIPCHK(ctx, launch_spectrum(G, m, (int64_t)m * m, m, 1, ev, wk.p, st));
   }
   HIPCHK(ctx, hipMemcpyAsync(eigvals_m, ev, (size_t)m * 8, hipMemcpyDeviceToHost, st));
   if (trace_G) {
@@ -1146,7 +1197,6 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
     *trace_G = s;
   }
   HIPCHK(ctx, hipStreamSynchronize(st));
-  hipFree(G); hipFree(ev);
   return 0;
 }
 

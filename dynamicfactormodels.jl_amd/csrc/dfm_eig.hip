@@ -1800,8 +1800,8 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
 }
 
 int spectrum_max() { return SPEC_MAX; }
-hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
-                           hipStream_t st) {
+hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+                                  hipStream_t st) {
   if (m > SPEC_MAX || m < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(spectrum_kernel, dim3(nb), dim3(256), 0, st, G, ldg, strideG, m, ev);
   return hipGetLastError();

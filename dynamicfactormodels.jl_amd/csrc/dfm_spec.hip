@@ -1,0 +1,402 @@
+// dfm_spec.hip — the full spectrum (all eigenvalues) of symmetric m x m Grams
+// of any size, for what the reference gets from the full `eig` of
+// src/DynamicFactorModel.jl:78 / :87 and then reads past the top r:
+//   * the PCp criteria's sigma^2 = V(ceil(m/2)) of the unrestricted fit
+//     (src/criteria.jl:18, :23, :28), i.e. the tail sum of the spectrum;
+//   * IC sweeps with kmax > 24 (src/DynamicFactorModel.jl:54, kmax = ceil(m/2)).
+// m <= SPEC_MAX goes to the LDS-resident Jacobi kernel of dfm_eig.hip.
+// Larger m: Householder tridiagonalisation (one workgroup per matrix, the
+// trailing matrix in HBM, ONE read+write pass per reflector: the previous
+// reflector's rank-2 update is applied lazily in the same pass that forms the
+// next symmetric product), then Sturm-count bisection on the tridiagonal,
+// one thread per eigenvalue.  Both are backward stable: eigenvalues to
+// O(eps ||G||), as LAPACK's dsyevr the reference reaches.
+#include "dfm_common.h"
+
+namespace dfm {
+
+hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+                                  hipStream_t st);
+int spectrum_max();
+
+constexpr int TRI_THREADS = 512;
+constexpr int TRI_WAVES = TRI_THREADS / 64;
+constexpr int SPEC_ANY_MAX = 4096;   // 4 LDS vectors of m doubles
+
+DFM_DEV double block_sum(double v, double *red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < TRI_WAVES; ++i) s += red[i];
+  return s;
+}
+
+// Householder reduction G = Q T Q' (LAPACK dsytd2 semantics, lower form).
+// Work S: m x m per matrix, row-major upper triangle (S[a][b], b >= a), so
+// that column k of the lower triangle — the reflector's source — is the
+// contiguous row k.  Outputs d (m) and e (m-1, stored with stride m); with
+// tout != nullptr also the reflectors for the eigenvector back-transform:
+// v_k over S[k][k+1..m-1] (v_k[k+1] = 1, stored) and tau_k in tout[k].
+__global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__restrict__ G, int64_t ldg,
+                                                              int64_t strideG, int m,
+                                                              double *__restrict__ Sw,
+                                                              double *__restrict__ dout,
+                                                              double *__restrict__ eout,
+                                                              double *__restrict__ tout) {
+  extern __shared__ double sm[];
+  double *vp = sm, *wp = sm + m, *v = sm + 2 * m, *p = sm + 3 * m;
+  __shared__ double red[TRI_WAVES];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int rep = blockIdx.x;
+  const double *g = G + (int64_t)rep * strideG;
+  double *S = Sw + (int64_t)rep * m * m;
+  double *d = dout + (int64_t)rep * m, *e = eout + (int64_t)rep * m;
+  for (int a = wv; a < m; a += TRI_WAVES)
+    for (int b = a + lane; b < m; b += 64) S[(int64_t)a * m + b] = 0.5 * (g[(int64_t)a * ldg + b] + g[(int64_t)b * ldg + a]);
+  for (int i = tid; i < m; i += TRI_THREADS) { vp[i] = 0.0; wp[i] = 0.0; }
+  __syncthreads();
+  for (int k = 0; k < m; ++k) {
+    // 1. column k with the pending update (vp, wp) of reflector k-1 applied
+    const double vpk = vp[k], wpk = wp[k];
+    const double *Sk = S + (int64_t)k * m;
+    double ss = 0.0;
+    for (int i = k + tid; i < m; i += TRI_THREADS) {
+      const double c = Sk[i] - vpk * wp[i] - wpk * vp[i];
+      v[i] = c;
+      if (i > k + 1) ss += c * c;
+    }
+    const double xn2 = block_sum(ss, red);   // (syncs: v[] visible)
+    const double dk = v[k];
+    double tau = 0.0, scale = 0.0;
+    if (k + 1 < m) {
+      const double alpha = v[k + 1];
+      double beta = alpha;
+      if (xn2 > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+        tau = (beta - alpha) / beta;
+        scale = 1.0 / (alpha - beta);
+      }
+      if (tid == 0) e[k] = beta;
+    }
+    if (tid == 0) d[k] = dk;
+    __syncthreads();
+    for (int i = k + 1 + tid; i < m; i += TRI_THREADS) {
+      const double vi = (i == k + 1) ? 1.0 : (tau != 0.0 ? v[i] * scale : 0.0);
+      v[i] = vi;
+      p[i] = 0.0;
+      if (tout) S[(int64_t)k * m + i] = vi;   // row k is consumed: keep the reflector there
+    }
+    if (tout && tid == 0) tout[(int64_t)rep * m + k] = tau;
+    __syncthreads();
+    if (k + 1 >= m) break;
+    // 2. one pass over the trailing triangle: apply the pending rank-2 update,
+    //    store, and accumulate p = A v (row part by wave reduction, the
+    //    mirrored column part by LDS atomics)
+    const bool refl = tau != 0.0;
+    for (int a = k + 1 + wv; a < m; a += TRI_WAVES) {
+      const double vpa = vp[a], wpa = wp[a], va = v[a];
+      double *Sa = S + (int64_t)a * m;
+      double acc = 0.0;
+      int b = a + lane;
+      for (; b + 192 < m; b += 256) {
+        double s0 = Sa[b], s1 = Sa[b + 64], s2 = Sa[b + 128], s3 = Sa[b + 192];
+        s0 -= vpa * wp[b] + wpa * vp[b];
+        s1 -= vpa * wp[b + 64] + wpa * vp[b + 64];
+        s2 -= vpa * wp[b + 128] + wpa * vp[b + 128];
+        s3 -= vpa * wp[b + 192] + wpa * vp[b + 192];
+        Sa[b] = s0; Sa[b + 64] = s1; Sa[b + 128] = s2; Sa[b + 192] = s3;
+        if (refl) {
+          acc += s0 * v[b] + s1 * v[b + 64] + s2 * v[b + 128] + s3 * v[b + 192];
+          if (b > a) atomicAdd(&p[b], s0 * va);
+          atomicAdd(&p[b + 64], s1 * va);
+          atomicAdd(&p[b + 128], s2 * va);
+          atomicAdd(&p[b + 192], s3 * va);
+        }
+      }
+      for (; b < m; b += 64) {
+        const double s = Sa[b] - (vpa * wp[b] + wpa * vp[b]);
+        Sa[b] = s;
+        if (refl) {
+          acc += s * v[b];
+          if (b > a) atomicAdd(&p[b], s * va);
+        }
+      }
+      if (refl) {
+        acc = wave_sum(acc);
+        if (lane == 0) atomicAdd(&p[a], acc);
+      }
+    }
+    __syncthreads();
+    // 3. w = tau p - (tau^2/2)(p'v) v becomes the pending update
+    double pv = 0.0;
+    for (int i = k + 1 + tid; i < m; i += TRI_THREADS) pv += p[i] * v[i];
+    pv = block_sum(pv, red) * tau;
+    for (int i = k + 1 + tid; i < m; i += TRI_THREADS) {
+      const double pi = tau * p[i];
+      wp[i] = pi - 0.5 * tau * pv * v[i];
+      vp[i] = v[i];
+    }
+    __syncthreads();
+  }
+}
+
+// Eigenvalue j (descending) of the symmetric tridiagonal (d, e) by bisection
+// on the Sturm count (LAPACK dlaebz's recurrence with its pivmin guard).
+__global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ din,
+                                                     const double *__restrict__ ein, int m, int nev,
+                                                     double *__restrict__ ev) {
+  extern __shared__ double sm[];
+  double *d = sm, *e2 = sm + m;
+  __shared__ double bnd[2];
+  const int tid = threadIdx.x, rep = blockIdx.y;
+  const double *dg = din + (int64_t)rep * m, *eg = ein + (int64_t)rep * m;
+  for (int i = tid; i < m; i += 256) {
+    d[i] = dg[i];
+    e2[i] = (i + 1 < m) ? eg[i] * eg[i] : 0.0;
+  }
+  __syncthreads();
+  if (tid == 0) {   // Gershgorin interval, pivmin
+    double lo = 1e308, hi = -1e308, emax = 0.0;
+    for (int i = 0; i < m; ++i) {
+      const double r = (i > 0 ? fabs(eg[i - 1]) : 0.0) + (i + 1 < m ? fabs(eg[i]) : 0.0);
+      lo = fmin(lo, d[i] - r);
+      hi = fmax(hi, d[i] + r);
+      if (i + 1 < m) emax = fmax(emax, e2[i]);
+    }
+    const double nrm = fmax(fabs(lo), fabs(hi));
+    lo -= 2.2e-16 * nrm * m + 1e-300;
+    hi += 2.2e-16 * nrm * m + 1e-300;
+    bnd[0] = lo; bnd[1] = hi;
+    e2[m] = fmax(2.2e-308, emax * 2.2e-308);   // pivmin (slot m: LDS holds 2m+1)
+  }
+  __syncthreads();
+  const int j = blockIdx.x * 256 + tid;
+  if (j >= nev) return;
+  const double pivmin = e2[m];
+  const int kth = m - 1 - j;   // ascending index of eigenvalue j (descending)
+  double lo = bnd[0], hi = bnd[1];
+  // absolute accuracy eps * ||T||: what the reduction itself guarantees
+  const double tol = 2.2e-16 * fmax(fabs(lo), fabs(hi));
+  for (int it = 0; it < 160; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (hi - lo <= tol + 4.0 * pivmin || mid <= lo || mid >= hi) break;
+    // number of eigenvalues < mid
+    int cnt = 0;
+    double q = d[0] - mid;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < m; ++i) {
+      q = d[i] - mid - e2[i - 1] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    if (cnt > kth) hi = mid; else lo = mid;
+  }
+  ev[(int64_t)rep * nev + j] = 0.5 * (lo + hi);
+}
+
+int64_t spectrum_work(int m, int nb) {
+  if (m <= spectrum_max()) return 0;
+  return (int64_t)nb * m * m + 2 * (int64_t)nb * m;
+}
+int spectrum_any_max() { return SPEC_ANY_MAX; }
+
+// All m eigenvalues (descending) of nb symmetric matrices G + rep * strideG.
+// work: spectrum_work(m, nb) doubles (none for m <= SPEC_MAX).
+hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+                           double *work, hipStream_t st) {
+  if (m < 1 || nb < 1) return hipErrorInvalidValue;
+  if (m <= spectrum_max()) return launch_spectrum_jacobi(G, ldg, strideG, m, nb, ev, st);
+  if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
+  double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
+  hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
+                     strideG, m, S, d, e, (double *)nullptr);
+  hipLaunchKernelGGL(bisect_kernel, dim3((m + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
+                     d, e, m, m, ev);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------ dense top-k eigenpairs
+// For k beyond the subspace eigensolver's block (k > 24; the reference's r
+// may be anything up to ceil(m/2), src/DynamicFactorModel.jl:101, :116-119):
+// tridiagonalise (reflectors kept), bisect the top k eigenvalues, inverse
+// iteration on the tridiagonal (LAPACK dstein's scheme: partial-pivoting LU
+// of T - lambda I, perturbed tiny pivots, vectors of one cluster
+// re-orthogonalised), then U = H_0 H_1 ... Z.
+constexpr int SPEC_VEC_MAX = 2560;   // 7 LDS vectors of m doubles in stein_kernel
+
+__global__ __launch_bounds__(256) void stein_kernel(const double *__restrict__ dg, const double *__restrict__ eg,
+                                                    const double *__restrict__ ev, int m, int k,
+                                                    double *__restrict__ Zt) {
+  extern __shared__ double sm[];
+  double *d = sm, *e = sm + m, *ua = sm + 2 * m, *ub = sm + 3 * m, *uc = sm + 4 * m, *ud = sm + 5 * m,
+         *x = sm + 6 * m;
+  __shared__ double red[4];
+  __shared__ unsigned char piv[SPEC_VEC_MAX];
+  __shared__ double tnorm;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < m; i += 256) { d[i] = dg[i]; e[i] = (i + 1 < m) ? eg[i] : 0.0; }
+  __syncthreads();
+  if (tid == 0) {
+    double nrm = 0.0;
+    for (int i = 0; i < m; ++i) nrm = fmax(nrm, fabs(d[i]) + fabs(e[i]) + (i > 0 ? fabs(e[i - 1]) : 0.0));
+    tnorm = nrm;
+  }
+  __syncthreads();
+  const double nrm = tnorm, ortol = 1e-3 * nrm, pertol = 10.0 * 2.2e-16 * nrm, tiny = 2.2e-16 * nrm;
+  auto bsum = [&](double v) -> double {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  int c0 = 0;          // first vector of the current cluster
+  double xprev = 0.0;
+  for (int j = 0; j < k; ++j) {
+    double xj = ev[j];
+    if (j > 0 && ev[j - 1] - ev[j] > ortol) c0 = j;
+    if (j > c0 && xj >= xprev - pertol) xj = xprev - pertol;   // separate (near-)equal shifts
+    xprev = xj;
+    if (tid == 0) {   // partial-pivoting LU of T - xj I: U has two superdiagonals (ua, ub, ud)
+      for (int i = 0; i < m; ++i) { ua[i] = d[i] - xj; ub[i] = e[i]; uc[i] = e[i]; ud[i] = 0.0; }
+      for (int i = 0; i + 1 < m; ++i) {
+        if (fabs(ua[i]) >= fabs(uc[i])) {
+          if (fabs(ua[i]) < tiny) ua[i] = copysign(tiny, ua[i]);
+          const double mult = uc[i] / ua[i];
+          uc[i] = mult;
+          ua[i + 1] -= mult * ub[i];
+          piv[i] = 0;
+        } else {
+          const double mult = ua[i] / uc[i];
+          ua[i] = uc[i];
+          const double t = ua[i + 1];
+          ua[i + 1] = ub[i] - mult * t;
+          if (i + 2 < m) { ud[i] = ub[i + 1]; ub[i + 1] = -mult * ud[i]; }
+          ub[i] = t;
+          uc[i] = mult;
+          piv[i] = 1;
+        }
+      }
+      for (int i = 0; i < m; ++i)
+        if (fabs(ua[i]) < tiny) ua[i] = copysign(tiny, ua[i]);
+    }
+    for (int i = tid; i < m; i += 256) x[i] = hash_unit(0x5eed, (uint64_t)j, (uint64_t)i);
+    __syncthreads();
+    for (int it = 0; it < 3; ++it) {
+      if (tid == 0) {   // solve (T - xj I) y = x in place
+        for (int i = 0; i + 1 < m; ++i) {
+          if (piv[i]) { const double t = x[i]; x[i] = x[i + 1]; x[i + 1] = t - uc[i] * x[i]; }
+          else x[i + 1] -= uc[i] * x[i];
+        }
+        x[m - 1] /= ua[m - 1];
+        if (m > 1) x[m - 2] = (x[m - 2] - ub[m - 2] * x[m - 1]) / ua[m - 2];
+        for (int i = m - 3; i >= 0; --i) x[i] = (x[i] - ub[i] * x[i + 1] - ud[i] * x[i + 2]) / ua[i];
+      }
+      __syncthreads();
+      // scale, then re-orthogonalise against the cluster's earlier vectors (MGS)
+      double mx = 0.0;
+      for (int i = tid; i < m; i += 256) mx += x[i] * x[i];
+      const double sc = 1.0 / sqrt(bsum(mx));
+      for (int i = tid; i < m; i += 256) x[i] *= sc;
+      __syncthreads();
+      for (int jj = c0; jj < j; ++jj) {
+        const double *z = Zt + (int64_t)jj * m;
+        double s = 0.0;
+        for (int i = tid; i < m; i += 256) s += z[i] * x[i];
+        s = bsum(s);
+        for (int i = tid; i < m; i += 256) x[i] -= s * z[i];
+        __syncthreads();
+      }
+      double nn = 0.0;
+      for (int i = tid; i < m; i += 256) nn += x[i] * x[i];
+      const double sc2 = 1.0 / sqrt(bsum(nn));
+      for (int i = tid; i < m; i += 256) x[i] *= sc2;
+      __syncthreads();
+    }
+    for (int i = tid; i < m; i += 256) Zt[(int64_t)j * m + i] = x[i];
+    __syncthreads();
+  }
+}
+
+// U(:, j) = H_0 H_1 ... H_{m-3} z_j, one workgroup per vector; then the sign
+// convention of eig_final_kernel (largest |entry|, first on ties, positive)
+// and the m x k row-major layout of the subspace eigensolver's output.
+__global__ __launch_bounds__(256) void backtransform_kernel(const double *__restrict__ S,
+                                                            const double *__restrict__ taus,
+                                                            const double *__restrict__ Zt, int m, int k,
+                                                            double *__restrict__ Uk) {
+  extern __shared__ double x[];
+  __shared__ double red[4];
+  __shared__ int redi[4];
+  const int tid = threadIdx.x, j = blockIdx.x;
+  for (int i = tid; i < m; i += 256) x[i] = Zt[(int64_t)j * m + i];
+  __syncthreads();
+  for (int q = m - 3; q >= 0; --q) {
+    const double tau = taus[q];
+    if (tau == 0.0) continue;
+    const double *v = S + (int64_t)q * m;
+    double s = 0.0;
+    for (int i = q + 1 + tid; i < m; i += 256) s += v[i] * x[i];
+    s = wave_sum(s);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    s = tau * (red[0] + red[1] + red[2] + red[3]);
+    for (int i = q + 1 + tid; i < m; i += 256) x[i] -= s * v[i];
+    __syncthreads();
+  }
+  double best = -1.0;
+  int bi = 0;
+  for (int i = tid; i < m; i += 256)
+    if (fabs(x[i]) > best) { best = fabs(x[i]); bi = i; }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ob = __shfl_xor(best, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if ((tid & 63) == 0) { red[tid >> 6] = best; redi[tid >> 6] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (red[w] > red[0] || (red[w] == red[0] && redi[w] < redi[0])) { red[0] = red[w]; redi[0] = redi[w]; }
+  }
+  __syncthreads();
+  const double sg = x[redi[0]] < 0.0 ? -1.0 : 1.0;
+  for (int i = tid; i < m; i += 256) Uk[(int64_t)i * k + j] = sg * x[i];
+}
+
+__global__ void diag_sum_kernel(const double *__restrict__ G, int64_t ldg, int m, double *__restrict__ tr) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < m; i += 256) s += G[(int64_t)i * ldg + i];
+  s = wave_sum(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *tr = red[0] + red[1] + red[2] + red[3];
+}
+
+int dense_eig_max() { return SPEC_VEC_MAX; }
+int64_t dense_eig_work(int m, int k) { return (int64_t)m * m + 4 * (int64_t)m + (int64_t)k * m; }
+
+// Top-k eigenpairs of ONE symmetric m x m matrix (lam: k, Uk: m x k
+// row-major, trace: 1), work: dense_eig_work(m, k) doubles.
+hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
+                            double *work, hipStream_t st) {
+  if (m < 2 || m > SPEC_VEC_MAX || k < 1 || k > m || !work) return hipErrorInvalidValue;
+  double *S = work, *d = S + (int64_t)m * m, *e = d + m, *taus = e + m, *Zt = taus + m;
+  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
+                     (int64_t)0, m, S, d, e, taus);
+  hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, 1), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
+                     d, e, m, k, lam);
+  hipLaunchKernelGGL(stein_kernel, dim3(1), dim3(256), (size_t)7 * m * sizeof(double), st, d, e, lam, m, k, Zt);
+  hipLaunchKernelGGL(backtransform_kernel, dim3(k), dim3(256), (size_t)m * sizeof(double), st, S, taus, Zt, m, k,
+                     Uk);
+  if (trace) hipLaunchKernelGGL(diag_sum_kernel, dim3(1), dim3(256), 0, st, G, ldg, m, trace);
+  return hipGetLastError();
+}
+
+}  // namespace dfm

@@ -1,0 +1,118 @@
+"""GPU parity for the full spectrum of Grams of any size (dfm_spec.hip:
+Householder tridiagonalisation + Sturm bisection above the Jacobi kernel's
+140): the full `eig` of src/DynamicFactorModel.jl:78 / :87, read past the top
+r by the PCp criteria's sigma^2 (src/criteria.jl:18, :23, :28) and by IC
+sweeps with kmax > 24 (src/DynamicFactorModel.jl:54)."""
+import numpy as np
+import pytest
+import scipy.linalg
+
+from test_gpu_parity import panel, STAT_RTOL, assert_fit_matches, max_sin_angle, signs, rel, ANGLE_TOL
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("T,N", [(400, 300), (250, 900), (141, 500), (900, 141), (1100, 1300)])
+def test_gram_spectrum_any_size(dfm, oracle, T, N):
+    _, x, _ = panel(oracle, T, N, 4, 7000 + T)
+    G = x.T @ x if T >= N else x @ x.T
+    ref = scipy.linalg.eigh(G, eigvals_only=True, driver="evr")[::-1]
+    ev, tr = dfm.gram_spectrum(x)
+    assert ev.shape == (min(T, N),)
+    assert np.all(np.diff(ev) <= 0)
+    # backward stable: every eigenvalue to O(eps ||G||), tail sums to far better than STAT_RTOL
+    assert np.max(np.abs(ev - ref)) <= 1e-12 * ref[0] * np.sqrt(min(T, N))
+    h = -(-min(T, N) // 2)
+    assert abs(ev[h:].sum() - ref[h:].sum()) <= 1e-11 * ref.sum()
+
+
+def test_spectrum_of_exact_rank_gram(dfm):
+    """Rank-deficient Gram: the zero eigenvalues come out at O(eps ||G||)."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((300, 6)) @ rng.standard_normal((6, 200))
+    ev, _ = dfm.gram_spectrum(x)
+    ref = np.linalg.eigvalsh(x.T @ x)[::-1]
+    assert np.max(np.abs(ev - ref)) <= 1e-11 * ref[0]
+    assert np.max(np.abs(ev[6:])) <= 1e-11 * ref[0]
+
+
+@pytest.mark.parametrize("T,N,r,crit", [(300, 200, 3, "PCp2"), (180, 600, 4, "PCp1"), (500, 2000, 8, "PCp3")])
+def test_pcp_fit_beyond_jacobi_size(dfm, oracle, T, N, r, crit):
+    y, x, w = panel(oracle, T, N, r, 7100 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, crit)
+    o = oracle.DynamicFactorModel(y, w, x, r, crit)
+    assert abs(g.number_of_factors_criterion_value - o.number_of_factors_criterion_value) <= \
+        STAT_RTOL * abs(o.number_of_factors_criterion_value)
+
+
+@pytest.mark.parametrize("T,N,crit", [(300, 200, "ICp2"), (160, 400, "PCp2")])
+def test_default_kmax_sweep_beyond_jacobi_size(dfm, oracle, T, N, crit):
+    """kmax = ceil(m/2) > 24: the sweep reads the full spectrum."""
+    y, x, w = panel(oracle, T, N, 3, 7200 + T)
+    d = dfm.DynamicFactorModel(y, w, x, crit)
+    o = oracle.DynamicFactorModel_ic(y, w, x, crit)
+    assert d.number_of_factors == o.number_of_factors
+    assert abs(d.number_of_factors_criterion_value - o.number_of_factors_criterion_value) <= \
+        STAT_RTOL * abs(o.number_of_factors_criterion_value)
+
+
+def test_pcp_sweep_with_large_break_blocks(dfm, oracle):
+    y, x, w = panel(oracle, 420, 180, 3, 7300)
+    d = dfm.DynamicFactorModel(y, w, x, "PCp2", break_indices=[210], kmax=8)
+    o = oracle.DynamicFactorModel_ic(y, w, x, "PCp2", kmax=8, break_indices=[210])
+    assert d.number_of_factors == o.number_of_factors
+    assert abs(d.number_of_factors_criterion_value - o.number_of_factors_criterion_value) <= \
+        STAT_RTOL * abs(o.number_of_factors_criterion_value)
+
+
+# ------------------------------------------- top-k eigenpairs with k > 24
+@pytest.mark.parametrize("T,N,r,crit", [(200, 160, 30, "ICp2"), (120, 400, 41, "BIC"), (600, 2000, 36, "ICp1"),
+                                        (70, 60, 30, "ICp3")])
+def test_fit_with_many_factors(dfm, oracle, T, N, r, crit):
+    """r beyond the subspace eigensolver's block: the dense path (reference
+    allows any r <= ceil(m/2), src/DynamicFactorModel.jl:116-119)."""
+    y, x, w = panel(oracle, T, N, 3, 7400 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, crit)
+    o = oracle.DynamicFactorModel(y, w, x, r, crit)
+    assert_fit_matches(g, o, oracle)
+
+
+def test_principal_components_many(dfm, oracle):
+    for T, N in [(300, 180), (150, 500)]:
+        _, x, _ = panel(oracle, T, N, 4, 7500 + T)
+        ev, F, L, tr = dfm.principal_components(x, 60)
+        Fo, Lo, wo = oracle.principal_components(x, T, N)
+        assert rel(ev, wo[:60]) < STAT_RTOL
+        assert max_sin_angle(F, Fo[:, :60]) < ANGLE_TOL
+        assert rel(L * signs(F, Fo[:, :60]), Lo[:, :60]) < 1e-8
+        assert np.allclose(F.T @ F / (T if N > T else 1.0), np.eye(60) if N > T else F.T @ F, atol=1e-10 * T)
+
+
+def test_default_constructor_reference_test_shape(dfm, oracle):
+    """The reference's own test (test/DynamicFactorModel.jl:6-24): w = [1, 4
+    lags of y], the 3-argument constructor, r = ceil(min(T,N)/2) (D2) — here
+    T = 200, N = 130 -> r = 65, q + r = 70 regressors."""
+    rng = np.random.default_rng(77)
+    y0, x0, *_ = oracle.factor_model_DGP(204, 130, 4, rng)
+    x = oracle.normalize(x0)[4:]
+    lags = np.column_stack([y0[4 - k:-k] for k in range(1, 5)])
+    w = np.hstack([np.ones((200, 1)), lags])
+    y = y0[4:]
+    g = dfm.DynamicFactorModel(y, w, x)
+    o = oracle.DynamicFactorModel(y, w, x)
+    assert g.number_of_factors == o.number_of_factors == 65
+    assert_fit_matches(g, o, oracle, q=5)
+    # the reference test's quantity: sum(model.factor_residuals.^2)
+    assert abs(np.sum(g.factor_residuals ** 2) - np.sum(o.factor_residuals ** 2)) <= \
+        1e-10 * np.sum(o.factor_residuals ** 2)
+
+
+def test_many_factors_with_breaks(dfm, oracle):
+    """Per-block dense eigenpairs + wide factors + wide OLS (D7, D13 as in test_gpu_breaks)."""
+    y, x, w = panel(oracle, 240, 90, 3, 7600)
+    g = dfm.DynamicFactorModel(y, w, x, 35, "ICp2", break_indices=[121])
+    o = oracle.DynamicFactorModel(y, w, x, 35, "ICp2", break_indices=[121])
+    assert g.number_of_factors == o.number_of_factors == 35
+    assert abs(g.V - oracle.factor_residual_variance(o)) <= STAT_RTOL * oracle.factor_residual_variance(o)
+    assert rel(g.t_stats[:1], o.t_stats[:1]) < 1e-9
+    assert np.max(np.abs(g.factor_residuals - o.factor_residuals)) < 1e-9 * np.max(np.abs(o.factor_residuals))
