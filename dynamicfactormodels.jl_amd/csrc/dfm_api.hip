@@ -55,8 +55,9 @@ hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, 
                       int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
                       double *resid_out, int *status);
 struct StatDesc { int kind, arg0, arg1, off; };
-__global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *,
+__global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *, const double *,
                              const double *, const double *, const StatDesc *, int, double *, int64_t);
+__global__ void tail_sigma2_kernel(const double *, int, int, int, double, double *);
 // dfm_chow.hip
 hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
                        const double *F, const double *Lm, double *LR, double *LM, double *Wald,
@@ -336,6 +337,12 @@ int dfm_ic_sweep(const double *eig, int n_eig, int kmax, double trace, int64_t T
 }
 
 }  // extern "C"
+
+// device buffer freed on every return path
+struct DevBuf {
+  double *p = nullptr;
+  ~DevBuf() { hipFree(p); }
+};
 
 // ---------------------------------------------------------------- internals
 // Top-k eigen-decomposition of nb Grams + trace; G workspace provided.
@@ -870,7 +877,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   // stat descriptors
   std::vector<StatDesc> sd(ns);
   int64_t width = 0;
-  bool chow = false;
+  bool chow = false, pcp = false;
   int chow_bp = -1;
   for (int i = 0; i < ns; ++i) {
     const dfm_stat s = stats[i];
@@ -878,8 +885,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     if (s.kind == DFM_STAT_CRIT) {
       const int c = s.arg0 >= 0 ? s.arg0 : M->crit;
       if (c < 0 || c > 6) return fail(ctx, -6, "criterion stat without a criterion");
-      if (c <= 2) return fail(ctx, -31, "PCp criteria inside the bootstrap need a per-replicate "
-                                        "unrestricted fit (not supported yet)");
+      if (c <= 2) pcp = true;
     }
     if (s.kind >= DFM_STAT_LR) {
       if (s.arg0 < r || s.arg0 > T - r) return fail(ctx, -7, "break period %d out of range", s.arg0);
@@ -902,7 +908,11 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
   const int p = eig_block_p(m, r, ctx->block);
   const int P = p <= 16 ? 16 : 32;
-  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1;
+  // PCp reads each replicate's full spectrum, so its Gram is formed: direct path
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1 && !pcp;
+  if (pcp && m > spectrum_any_max())
+    return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
+                          "supported for min(T,N) <= %d", spectrum_any_max());
   int64_t nb = M->batch;
   if (nb <= 0) {
     if (fact) {
@@ -912,7 +922,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       const double per = (double)boot_ws_bytes(M, 1024, P, ctx->maxit, chow, true, nullptr, nullptr) / 1024.0;
       nb = (int64_t)std::max(1.0, std::min(16384.0, std::floor(16e9 / per)));
     } else {
-      const double gbytes = (double)m * m * 8;
+      const double gbytes = (double)m * m * 8 * (pcp ? 3 : 1);
       nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
     }
     // equal batches (no small tail batch running the iterations half-empty)
@@ -955,6 +965,15 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   HIPCHK(ctx, hipMemsetAsync(M->flag_dev, 0, 4, st));
   BootWs w;
   boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, &w, M->ws);
+  // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
+  // src/criteria.jl:18), its spectrum, sigma^2 per replicate
+  DevBuf pG, pEv, pWk, pSig;
+  if (pcp) {
+    HIPCHK(ctx, dalloc(&pG.p, (size_t)nb * m * m));
+    HIPCHK(ctx, dalloc(&pEv.p, (size_t)nb * m));
+    HIPCHK(ctx, dalloc(&pSig.p, (size_t)nb));
+    if (spectrum_work(m, (int)nb) > 0) HIPCHK(ctx, dalloc(&pWk.p, (size_t)spectrum_work(m, (int)nb)));
+  }
   FactBase fb{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd};
   for (int64_t b0 = 0; b0 < B; b0 += nb) {
     const int n = (int)std::min<int64_t>(nb, B - b0);
@@ -1008,12 +1027,24 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       launch_ols(n, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
                          w.tstat, nullptr, nullptr, w.ost);
     }
+    if (pcp) {
+      const double *Gp = w.G;
+      if (M->nblk > 1) {   // the blocks' Grams are not the full-sample one
+        Scope sc(ctx, DFM_KC_GRAM);
+        HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, pG.p, m, (int64_t)m * m, n, st));
+        Gp = pG.p;
+      }
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      HIPCHK(ctx, launch_spectrum(Gp, m, (int64_t)m * m, m, n, pEv.p, pWk.p, st));
+      hipLaunchKernelGGL(tail_sigma2_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pEv.p, m, (m + 1) / 2, n,
+                         (double)N * (double)T, pSig.p);
+    }
     {
       Scope sc(ctx, DFM_KC_STATS);
       if (ns)
         hipLaunchKernelGGL(stats_kernel, dim3((n + 127) / 128), dim3(128), 0, st, n, T, N, r, q,
-                           M->crit, M->sigma2, w.lam, w.trace, w.coef, w.tstat, M->sd_dev, ns,
-                           out + b0 * width, width);
+                           M->crit, M->sigma2, pcp ? pSig.p : nullptr, w.lam, w.trace, w.coef, w.tstat,
+                           M->sd_dev, ns, out + b0 * width, width);
       hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
                          n, M->flag_dev);
     }
@@ -1084,10 +1115,6 @@ int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const d
 
 // --------------------------------------------------------- stand-alone entry points
 namespace {
-struct DevBuf {
-  double *p = nullptr;
-  ~DevBuf() { hipFree(p); }
-};
 struct DevPanel {
   double *raw = nullptr, *P = nullptr;
   int64_t ld = 0;

@@ -400,8 +400,21 @@ DFM_DEV double criterion_dev(int code, double V, int k, int T, int N, double sig
 
 struct StatDesc { int kind, arg0, arg1, off; };
 
+// PCp's sigma^2 of each replicate's unrestricted fit (src/criteria.jl:18):
+// V(h) = sum_{j >= h} lambda_j / (N T), h = ceil(m/2), from its full spectrum
+// (descending), summed in a fixed order.
+__global__ void tail_sigma2_kernel(const double *__restrict__ ev, int m, int h, int nb, double NT,
+                                   double *__restrict__ sig2) {
+  const int rep = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rep >= nb) return;
+  double s = 0.0;
+  for (int j = m - 1; j >= h; --j) s += ev[(int64_t)rep * m + j];
+  sig2[rep] = s / NT;
+}
+
 // One thread per replicate.  out row stride = width.
 __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, double sigma2,
+                             const double *__restrict__ sig2v,
                              const double *__restrict__ lam, const double *__restrict__ trace,
                              const double *__restrict__ coef, const double *__restrict__ tstat,
                              const StatDesc *__restrict__ sd, int ns, double *__restrict__ out,
@@ -417,7 +430,7 @@ __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, doubl
     double v = NAN;
     switch (st.kind) {
       case 0: v = V; break;
-      case 1: v = criterion_dev(st.arg0 >= 0 ? st.arg0 : crit, V, r, T, N, sigma2); break;
+      case 1: v = criterion_dev(st.arg0 >= 0 ? st.arg0 : crit, V, r, T, N, sig2v ? sig2v[rep] : sigma2); break;
       case 2: v = st.arg0 < r ? lam[(int64_t)rep * r + st.arg0] : NAN; break;
       case 3: v = st.arg0 < d ? coef[(int64_t)rep * d + st.arg0] : NAN; break;
       case 4: v = st.arg0 < d ? tstat[(int64_t)rep * d + st.arg0] : NAN; break;

@@ -388,8 +388,6 @@ def test_errors_are_reported(dfm, oracle):
     y, x, w = panel(oracle, 50, 20, 2, 21)
     g = dfm.DynamicFactorModel(y, w, x, 2, "PCp2")
     idx, eta = oracle.draw_wild(np.random.default_rng(0), 2, 50)
-    with pytest.raises(dfm.DFMError):      # PCp inside a replicate: not built yet
-        dfm.wild_bootstrap(g, 2, dfm.Stat.criterion(), idx=idx, eta=eta)
     with pytest.raises(dfm.DFMError):      # break period leaves < r rows
         dfm.chow_all(g, 1)
     with pytest.raises(dfm.DFMError):      # D8: joint thresholding singular

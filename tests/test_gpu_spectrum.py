@@ -116,3 +116,27 @@ def test_many_factors_with_breaks(dfm, oracle):
     assert abs(g.V - oracle.factor_residual_variance(o)) <= STAT_RTOL * oracle.factor_residual_variance(o)
     assert rel(g.t_stats[:1], o.t_stats[:1]) < 1e-9
     assert np.max(np.abs(g.factor_residuals - o.factor_residuals)) < 1e-9 * np.max(np.abs(o.factor_residuals))
+
+
+# ------------------------------------------------ PCp inside the bootstrap
+@pytest.mark.parametrize("T,N,r,crit,mode,breaks", [
+    (120, 60, 3, "PCp2", "auto", ()),          # m = 60: Jacobi spectrum per replicate
+    (60, 150, 2, "PCp1", "factored", ()),       # N > T: the PCp stat forces the direct Gram
+    (300, 180, 3, "PCp3", "auto", ()),          # m = 180: tridiagonal + bisection per replicate
+    (160, 70, 2, "PCp2", "auto", (81,)),        # break blocks: sigma^2 from the full-sample Gram
+])
+def test_pcp_criterion_in_replicates(dfm, oracle, T, N, r, crit, mode, breaks):
+    y, x, w = panel(oracle, T, N, r, 7700 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, crit, break_indices=breaks)
+    g.set_bootstrap_mode(mode)
+    o = oracle.DynamicFactorModel(y, w, x, r, crit, break_indices=breaks)
+    B = 4
+    idx, eta = oracle.draw_wild(np.random.default_rng(9), B, T)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, B, [S.criterion(), S.criterion("PCp1"), S.V()], idx=idx, eta=eta)
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, r, crit, break_indices=breaks)
+        ref = [d.number_of_factors_criterion_value, oracle.criterion_value("PCp1", d),
+               oracle.factor_residual_variance(d)]
+        assert rel(out[b], ref) < STAT_RTOL
