@@ -36,6 +36,8 @@ hipError_t launch_ols_wide(const double *y, const double *w, int q, const double
 int64_t dense_eig_work(int m, int k);
 hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
                             double *work, hipStream_t st);
+hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
+                               double *ev, double *work, hipStream_t st);
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev, double *work,
                            hipStream_t st);
 // dfm_model.hip
@@ -1420,8 +1422,8 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
       !r_out)
     return fail(ctx, -2, "dfm_windows: bad arguments");
-  if (crit < 3 || crit > 6)
-    return fail(ctx, -31, "dfm_windows: criterion must be ICp1-3 or BIC (PCp needs each window's full spectrum)");
+  if (crit < 0 || crit > 6) return fail(ctx, -31, "dfm_windows: unknown criterion %d", crit);
+  const bool pcp = crit <= 2;
   const int n0 = T - P;
   const int orient = (N > T) ? 0 : 1;
   if (orient == 1 && N > n0) return fail(ctx, -2, "dfm_windows: windows straddle the T >= N / N > T branches");
@@ -1435,6 +1437,9 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   int rc = upload_panel(ctx, X, T, N, ldx, dp);
   if (rc) return rc;
   const int m = orient == 0 ? T : N;
+  if (pcp && (orient == 0 ? T - 1 : N) > spectrum_any_max())
+    return fail(ctx, -31, "dfm_windows: PCp needs each window's full spectrum: supported for min(T,N) <= %d",
+                spectrum_any_max());
   const int p = eig_block_p(m, kmax, ctx->block);
   if (p > 32) return fail(ctx, -20, "block too wide");
   const int Pb = p <= 16 ? 16 : 32;
@@ -1462,8 +1467,9 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   HIPCHK(ctx, hipMemcpyAsync(deta, heta.data(), heta.size() * 8, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
   if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
-  double *H = nullptr;
+  double *H = nullptr, *pev = nullptr;   // pev: per-window full spectra (PCp), row stride pst
   int64_t ldH = 0;
+  int pst = 0;
   if (orient == 0) {
     ldH = round_up(T, 16);
     H = (double *)dal((size_t)T * ldH * 8);
@@ -1482,6 +1488,15 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     if (rc) return fail(ctx, rc, "precompute");
     HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
     FactBase fb{T, 0, ldH, zero, zero, zero, H, zero, hd};
+    if (pcp) {   // window w's Gram: the leading (n0 + w) x (n0 + w) block of H
+      const int mx = T - 1;
+      pev = (double *)dal((size_t)P * mx * 8);
+      double *pwk = spectrum_work(mx, P) > 0 ? (double *)dal((size_t)spectrum_work(mx, P) * 8) : nullptr;
+      if (!pev || (spectrum_work(mx, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      HIPCHK(ctx, launch_spectrum_var(H, ldH, 0, mx, n0, 1, P, pev, pwk, st));
+      pst = mx;
+    }
     rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
                           lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
     if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
@@ -1495,6 +1510,14 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     {
       Scope sc(ctx, DFM_KC_GRAM);
       HIPCHK(ctx, launch_gram(1, src, N, T, T, G, N, (int64_t)N * N, P, st));
+    }
+    if (pcp) {
+      pev = (double *)dal((size_t)P * N * 8);
+      double *pwk = spectrum_work(N, P) > 0 ? (double *)dal((size_t)spectrum_work(N, P) * 8) : nullptr;
+      if (!pev || (spectrum_work(N, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      HIPCHK(ctx, launch_spectrum(G, N, (int64_t)N * N, N, P, pev, pwk, st));
+      pst = N;
     }
     rc = eig_run(G, N, (int64_t)N * N, N, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, lam, Uk,
                  tr, stt, nullptr, st, timer_cb, ctx, 0);
@@ -1511,10 +1534,23 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   HIPCHK(ctx, hipStreamSynchronize(st));
   for (int wi = 0; wi < P; ++wi)
     if (hs[wi]) return fail(ctx, 2, "eigensolver did not converge for window %d", wi);
+  std::vector<double> hev;
+  if (pcp) {
+    hev.resize((size_t)P * pst);
+    HIPCHK(ctx, hipMemcpyAsync(hev.data(), pev, hev.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+  }
   std::vector<double> ic(7 * (size_t)kmax);
   for (int wi = 0; wi < P; ++wi) {
     const int n = n0 + wi;
-    dfm_ic_sweep(&hl[(size_t)wi * kmax], kmax, kmax, ht[wi], n, N, NAN, ic.data());
+    double s2 = NAN;
+    if (pcp) {   // src/criteria.jl:18: V(ceil(m_w/2)) of the window's unrestricted fit = spectral tail
+      const int mw = std::min(n, N), h = (mw + 1) / 2;
+      double s = 0.0;
+      for (int j = mw - 1; j >= h; --j) s += hev[(size_t)wi * pst + j];
+      s2 = s / ((double)N * n);
+    }
+    dfm_ic_sweep(&hl[(size_t)wi * kmax], kmax, kmax, ht[wi], n, N, s2, ic.data());
     int best = 0;
     for (int k = 1; k < kmax; ++k)
       if (ic[(size_t)crit * kmax + k] < ic[(size_t)crit * kmax + best]) best = k;

@@ -1726,8 +1726,10 @@ int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const dou
 // the PCp criteria's unrestricted sigma^2 = V(ceil(m/2)) (src/criteria.jl:18)
 // and for full IC sweeps (k up to ceil(m/2), src/DynamicFactorModel.jl:54).
 constexpr int SPEC_MAX = 140;
+// Matrix rep has size m0 + dm * rep (expanding windows share one prefix Gram);
+// ev rows have stride mst.
 __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict__ G, int64_t ldg,
-                                                       int64_t strideG, int m,
+                                                       int64_t strideG, int mst, int m0, int dm,
                                                        double *__restrict__ ev) {
   constexpr int S = SPEC_MAX + 1;
   __shared__ double H[SPEC_MAX * S];
@@ -1736,6 +1738,7 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
   __shared__ int sdone;
   const int tid = threadIdx.x, rep = blockIdx.x;
   const double *g = G + (int64_t)rep * strideG;
+  const int m = m0 + dm * rep;
   const int n = m + (m & 1);
   for (int e = tid; e < n * n; e += 256) {
     const int a = e / n, c = e % n;
@@ -1795,15 +1798,15 @@ __global__ __launch_bounds__(256) void spectrum_kernel(const double *__restrict_
       const double u = H[j * S + j];
       if (u > v || (u == v && j < i)) ++rank;
     }
-    if (rank < m) ev[(int64_t)rep * m + rank] = v;
+    if (rank < m) ev[(int64_t)rep * mst + rank] = v;
   }
 }
 
 int spectrum_max() { return SPEC_MAX; }
-hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
-                                  hipStream_t st) {
-  if (m > SPEC_MAX || m < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spectrum_kernel, dim3(nb), dim3(256), 0, st, G, ldg, strideG, m, ev);
+hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
+                                  double *ev, hipStream_t st) {
+  if (m > SPEC_MAX || m0 < 1 || m0 + dm * (nb - 1) > m) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spectrum_kernel, dim3(nb), dim3(256), 0, st, G, ldg, strideG, m, m0, dm, ev);
   return hipGetLastError();
 }
 

@@ -15,8 +15,8 @@
 
 namespace dfm {
 
-hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
-                                  hipStream_t st);
+hipError_t launch_spectrum_jacobi(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
+                                  double *ev, hipStream_t st);
 int spectrum_max();
 
 constexpr int TRI_THREADS = 512;
@@ -42,19 +42,20 @@ DFM_DEV double block_sum(double v, double *red) {
 // tout != nullptr also the reflectors for the eigenvector back-transform:
 // v_k over S[k][k+1..m-1] (v_k[k+1] = 1, stored) and tau_k in tout[k].
 __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__restrict__ G, int64_t ldg,
-                                                              int64_t strideG, int m,
+                                                              int64_t strideG, int mst, int m0, int dm,
                                                               double *__restrict__ Sw,
                                                               double *__restrict__ dout,
                                                               double *__restrict__ eout,
                                                               double *__restrict__ tout) {
   extern __shared__ double sm[];
-  double *vp = sm, *wp = sm + m, *v = sm + 2 * m, *p = sm + 3 * m;
+  double *vp = sm, *wp = sm + mst, *v = sm + 2 * mst, *p = sm + 3 * mst;
   __shared__ double red[TRI_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int rep = blockIdx.x;
   const double *g = G + (int64_t)rep * strideG;
-  double *S = Sw + (int64_t)rep * m * m;
-  double *d = dout + (int64_t)rep * m, *e = eout + (int64_t)rep * m;
+  const int m = m0 + dm * rep;   // this matrix's size; buffers have stride mst
+  double *S = Sw + (int64_t)rep * mst * mst;
+  double *d = dout + (int64_t)rep * mst, *e = eout + (int64_t)rep * mst;
   for (int a = wv; a < m; a += TRI_WAVES)
     for (int b = a + lane; b < m; b += 64) S[(int64_t)a * m + b] = 0.5 * (g[(int64_t)a * ldg + b] + g[(int64_t)b * ldg + a]);
   for (int i = tid; i < m; i += TRI_THREADS) { vp[i] = 0.0; wp[i] = 0.0; }
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
       p[i] = 0.0;
       if (tout) S[(int64_t)k * m + i] = vi;   // row k is consumed: keep the reflector there
     }
-    if (tout && tid == 0) tout[(int64_t)rep * m + k] = tau;
+    if (tout && tid == 0) tout[(int64_t)rep * mst + k] = tau;
     __syncthreads();
     if (k + 1 >= m) break;
     // 2. one pass over the trailing triangle: apply the pending rank-2 update,
@@ -147,13 +148,15 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
 // Eigenvalue j (descending) of the symmetric tridiagonal (d, e) by bisection
 // on the Sturm count (LAPACK dlaebz's recurrence with its pivmin guard).
 __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ din,
-                                                     const double *__restrict__ ein, int m, int nev,
-                                                     double *__restrict__ ev) {
+                                                     const double *__restrict__ ein, int mst, int m0, int dm,
+                                                     int nev, double *__restrict__ ev) {
   extern __shared__ double sm[];
+  const int tid = threadIdx.x, rep = blockIdx.y;
+  const int m = m0 + dm * rep;   // nev == 0: all m of this matrix
+  if (nev <= 0) nev = m;
   double *d = sm, *e2 = sm + m;
   __shared__ double bnd[2];
-  const int tid = threadIdx.x, rep = blockIdx.y;
-  const double *dg = din + (int64_t)rep * m, *eg = ein + (int64_t)rep * m;
+  const double *dg = din + (int64_t)rep * mst, *eg = ein + (int64_t)rep * mst;
   for (int i = tid; i < m; i += 256) {
     d[i] = dg[i];
     e2[i] = (i + 1 < m) ? eg[i] * eg[i] : 0.0;
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
     }
     if (cnt > kth) hi = mid; else lo = mid;
   }
-  ev[(int64_t)rep * nev + j] = 0.5 * (lo + hi);
+  ev[(int64_t)rep * (dm ? mst : nev) + j] = 0.5 * (lo + hi);
 }
 
 int64_t spectrum_work(int m, int nb) {
@@ -205,19 +208,24 @@ int64_t spectrum_work(int m, int nb) {
 }
 int spectrum_any_max() { return SPEC_ANY_MAX; }
 
-// All m eigenvalues (descending) of nb symmetric matrices G + rep * strideG.
+// All eigenvalues (descending) of nb symmetric matrices G + rep * strideG;
+// matrix rep has size m0 + dm * rep <= m (dm = 0: all m x m), ev rows stride m.
 // work: spectrum_work(m, nb) doubles (none for m <= SPEC_MAX).
-hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
-                           double *work, hipStream_t st) {
-  if (m < 1 || nb < 1) return hipErrorInvalidValue;
-  if (m <= spectrum_max()) return launch_spectrum_jacobi(G, ldg, strideG, m, nb, ev, st);
+hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
+                               double *ev, double *work, hipStream_t st) {
+  if (m0 < 1 || nb < 1 || dm < 0 || m0 + (int64_t)dm * (nb - 1) > m) return hipErrorInvalidValue;
+  if (m <= spectrum_max()) return launch_spectrum_jacobi(G, ldg, strideG, m, m0, dm, nb, ev, st);
   if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
   hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
-                     strideG, m, S, d, e, (double *)nullptr);
+                     strideG, m, m0, dm, S, d, e, (double *)nullptr);
   hipLaunchKernelGGL(bisect_kernel, dim3((m + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
-                     d, e, m, m, ev);
+                     d, e, m, m0, dm, 0, ev);
   return hipGetLastError();
+}
+hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
+                           double *work, hipStream_t st) {
+  return launch_spectrum_var(G, ldg, strideG, m, m, 0, nb, ev, work, st);
 }
 
 // ------------------------------------------------ dense top-k eigenpairs
@@ -389,9 +397,9 @@ hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *
   if (m < 2 || m > SPEC_VEC_MAX || k < 1 || k > m || !work) return hipErrorInvalidValue;
   double *S = work, *d = S + (int64_t)m * m, *e = d + m, *taus = e + m, *Zt = taus + m;
   hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
-                     (int64_t)0, m, S, d, e, taus);
+                     (int64_t)0, m, m, 0, S, d, e, taus);
   hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, 1), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
-                     d, e, m, k, lam);
+                     d, e, m, m, 0, k, lam);
   hipLaunchKernelGGL(stein_kernel, dim3(1), dim3(256), (size_t)7 * m * sizeof(double), st, d, e, lam, m, k, Zt);
   hipLaunchKernelGGL(backtransform_kernel, dim3(k), dim3(256), (size_t)m * sizeof(double), st, S, taus, Zt, m, k,
                      Uk);

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 FCST_RTOL = 1e-9
 
 
-@pytest.mark.parametrize("T,N,P,crit", [(90, 160, 8, "ICp2"), (140, 40, 10, "BIC"), (120, 300, 6, "ICp1")])
+@pytest.mark.parametrize("T,N,P,crit", [(90, 160, 8, "ICp2"), (140, 40, 10, "BIC"), (120, 300, 6, "ICp1"),
+                                        (90, 160, 8, "PCp2"), (140, 40, 10, "PCp1"), (260, 400, 5, "PCp3")])
 def test_forecasts_match_oracle(dfm, oracle, T, N, P, crit):
     y, x, w = panel(oracle, T, N, 3, 4000 + T)
     kmax = 6

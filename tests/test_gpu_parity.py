@@ -365,7 +365,8 @@ def test_direct_and_factored_agree(dfm, oracle):
     assert rel(b[:, 4:], a[:, 4:]) < 1e-9
 
 
-@pytest.mark.parametrize("T,N,P,crit", [(60, 150, 6, "ICp2"), (90, 30, 5, "BIC"), (41, 300, 3, "ICp1")])
+@pytest.mark.parametrize("T,N,P,crit", [(60, 150, 6, "ICp2"), (90, 30, 5, "BIC"), (41, 300, 3, "ICp1"),
+                                        (60, 150, 6, "PCp2"), (200, 160, 4, "PCp1")])
 def test_expanding_window_refits(dfm, oracle, T, N, P, crit):
     """src/utils.jl:54-72 refit loop: each window = IC-sweep constructor on rows
     1..date_index-1 (N > T via the prefix-Gram identity)."""
