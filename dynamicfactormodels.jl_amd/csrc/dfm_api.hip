@@ -35,7 +35,7 @@ hipError_t launch_ols_wide(const double *y, const double *w, int q, const double
                            hipStream_t st);
 int64_t dense_eig_work(int m, int k);
 hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
-                            double *work, hipStream_t st);
+                            int *status, double *work, hipStream_t st);
 hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
                                double *ev, double *work, hipStream_t st);
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev, double *work,
@@ -358,9 +358,8 @@ static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const do
     hipError_t e;
     {
       Scope sc(ctx, DFM_KC_EIG_OTHER);
-      e = launch_dense_eig(G, m, m, k, lam, Uk, trace, wk, ctx->stream);
+      e = launch_dense_eig(G, m, m, k, lam, Uk, trace, status_dev, wk, ctx->stream);
     }
-    if (e == hipSuccess && status_dev) e = hipMemsetAsync(status_dev, 0, sizeof(int), ctx->stream);
     hipStreamSynchronize(ctx->stream);
     hipFree(wk);
     if (e != hipSuccess) return fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));

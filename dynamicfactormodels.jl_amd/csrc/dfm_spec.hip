@@ -12,6 +12,7 @@
 // one thread per eigenvalue.  Both are backward stable: eigenvalues to
 // O(eps ||G||), as LAPACK's dsyevr the reference reaches.
 #include "dfm_common.h"
+#include <algorithm>
 
 namespace dfm {
 
@@ -231,104 +232,151 @@ hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m,
 // ------------------------------------------------ dense top-k eigenpairs
 // For k beyond the subspace eigensolver's block (k > 24; the reference's r
 // may be anything up to ceil(m/2), src/DynamicFactorModel.jl:101, :116-119):
-// tridiagonalise (reflectors kept), bisect the top k eigenvalues, inverse
-// iteration on the tridiagonal (LAPACK dstein's scheme: partial-pivoting LU
-// of T - lambda I, perturbed tiny pivots, vectors of one cluster
-// re-orthogonalised), then U = H_0 H_1 ... Z.
-constexpr int SPEC_VEC_MAX = 2560;   // 7 LDS vectors of m doubles in stein_kernel
+// tridiagonalise (reflectors kept), bisect the top k eigenvalues, then
+//  1. inverse iteration on the tridiagonal, ONE THREAD PER EIGENVECTOR (LAPACK
+//     dstein's partial-pivoting LU of T - sigma I with perturbed tiny pivots;
+//     near-equal shifts separated by 10 eps ||T||; distinct pseudo-random
+//     starts, so a (near-)degenerate cluster yields independent vectors of its
+//     invariant subspace), LU and vectors interleaved [i * k + j] so a wave's
+//     serial recurrences read coalesced rows;
+//  2. orthonormalisation in eigenvalue order by block classical Gram-Schmidt
+//     with re-orthogonalisation (BCGS2) and CholQR2 inside 32-column blocks,
+//     all as strided GEMMs: every overlap it removes is O(eps ||T|| / gap), the
+//     accuracy any backward-stable solver has;
+//  3. U = H_0 H_1 ... H_{m-3} Z.
+constexpr int SPEC_VEC_MAX = 4096;
+constexpr int OB = 32;   // orthonormalisation block
 
-__global__ __launch_bounds__(256) void stein_kernel(const double *__restrict__ dg, const double *__restrict__ eg,
-                                                    const double *__restrict__ ev, int m, int k,
-                                                    double *__restrict__ Zt) {
-  extern __shared__ double sm[];
-  double *d = sm, *e = sm + m, *ua = sm + 2 * m, *ub = sm + 3 * m, *uc = sm + 4 * m, *ud = sm + 5 * m,
-         *x = sm + 6 * m;
-  __shared__ double red[4];
-  __shared__ unsigned char piv[SPEC_VEC_MAX];
-  __shared__ double tnorm;
+hipError_t gemm_strided(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
+                        const double *B, int64_t sBr, int64_t sBc, double beta, double *C, int64_t sCr,
+                        int64_t sCc, hipStream_t st);
+
+// ||T||_inf, and the shifts: sigma_j = lambda_j, pushed down so consecutive
+// shifts differ by >= 10 eps ||T|| (dstein's perturbation of close shifts)
+__global__ void stein_shifts_kernel(const double *__restrict__ d, const double *__restrict__ e, int m,
+                                    const double *__restrict__ lam, int k, double *__restrict__ sig,
+                                    double *__restrict__ tn) {
+  if (threadIdx.x != 0) return;
+  double nrm = 0.0;
+  for (int i = 0; i < m; ++i)
+    nrm = fmax(nrm, fabs(d[i]) + (i + 1 < m ? fabs(e[i]) : 0.0) + (i > 0 ? fabs(e[i - 1]) : 0.0));
+  const double pertol = 10.0 * 2.2e-16 * nrm;
+  double prev = 0.0;
+  for (int j = 0; j < k; ++j) {
+    double x = lam[j];
+    if (j > 0 && x > prev - pertol) x = prev - pertol;
+    sig[j] = x;
+    prev = x;
+  }
+  *tn = nrm;
+}
+
+__global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d, const double *__restrict__ e,
+                                                   int m, int k, const double *__restrict__ sig,
+                                                   const double *__restrict__ tn, double *__restrict__ ua,
+                                                   double *__restrict__ ub, double *__restrict__ uc,
+                                                   double *__restrict__ ud, unsigned char *__restrict__ piv,
+                                                   double *__restrict__ Z) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= k) return;
+  const double xj = sig[j], tiny = 2.2e-16 * *tn;
+#define IX(i) ((int64_t)(i) * k + j)
+  for (int i = 0; i < m; ++i) { ua[IX(i)] = d[i] - xj; ub[IX(i)] = (i + 1 < m) ? e[i] : 0.0; ud[IX(i)] = 0.0; }
+  for (int i = 0; i + 1 < m; ++i) {
+    const double a = ua[IX(i)], c = e[i];
+    if (fabs(a) >= fabs(c)) {
+      const double aa = fabs(a) < tiny ? copysign(tiny, a) : a;
+      const double mult = c / aa;
+      ua[IX(i)] = aa;
+      uc[IX(i)] = mult;
+      ua[IX(i + 1)] -= mult * ub[IX(i)];
+      piv[IX(i)] = 0;
+    } else {
+      const double mult = a / c;
+      const double t = ua[IX(i + 1)];
+      ua[IX(i)] = c;
+      ua[IX(i + 1)] = ub[IX(i)] - mult * t;
+      if (i + 2 < m) { const double b1 = ub[IX(i + 1)]; ud[IX(i)] = b1; ub[IX(i + 1)] = -mult * b1; }
+      ub[IX(i)] = t;
+      uc[IX(i)] = mult;
+      piv[IX(i)] = 1;
+    }
+  }
+  for (int i = 0; i < m; ++i) {
+    const double a = ua[IX(i)];
+    if (fabs(a) < tiny) ua[IX(i)] = copysign(tiny, a);
+  }
+  double nn = 0.0;
+  for (int i = 0; i < m; ++i) { const double v = hash_unit(0x5eed, (uint64_t)j, (uint64_t)i); Z[IX(i)] = v; nn += v * v; }
+  double sc = 1.0 / sqrt(nn);
+  for (int it = 0; it < 3; ++it) {
+    // forward: the row interchanges and multipliers of L
+    double xi = Z[IX(0)] * sc;
+    for (int i = 0; i + 1 < m; ++i) {
+      const double xn = Z[IX(i + 1)] * sc;
+      double a, b;
+      if (piv[IX(i)]) { a = xn; b = xi - uc[IX(i)] * xn; }
+      else { a = xi; b = xn - uc[IX(i)] * xi; }
+      Z[IX(i)] = a;
+      xi = b;
+    }
+    Z[IX(m - 1)] = xi;
+    // back substitution with U (diagonal ua, superdiagonals ub, ud)
+    double x1 = Z[IX(m - 1)] / ua[IX(m - 1)], x2 = 0.0;
+    Z[IX(m - 1)] = x1;
+    nn = x1 * x1;
+    for (int i = m - 2; i >= 0; --i) {
+      const double x0 = (Z[IX(i)] - ub[IX(i)] * x1 - ud[IX(i)] * x2) / ua[IX(i)];
+      Z[IX(i)] = x0;
+      nn += x0 * x0;
+      x2 = x1; x1 = x0;
+    }
+    sc = 1.0 / sqrt(nn);
+  }
+  for (int i = 0; i < m; ++i) Z[IX(i)] *= sc;
+#undef IX
+}
+
+// CholQR step on a b-column block: W = R'R (Cholesky, b <= OB), Rinv = R^-1.
+__global__ void small_chol_inv_kernel(const double *__restrict__ W, int b, double *__restrict__ Rinv,
+                                      int *__restrict__ status) {
+  __shared__ double R[OB][OB + 1], X[OB][OB + 1];
   const int tid = threadIdx.x;
-  for (int i = tid; i < m; i += 256) { d[i] = dg[i]; e[i] = (i + 1 < m) ? eg[i] : 0.0; }
+  for (int e = tid; e < OB * OB; e += blockDim.x) {
+    const int a = e / OB, c = e % OB;
+    R[a][c] = (a < b && c < b) ? W[a * b + c] : 0.0;
+    X[a][c] = 0.0;
+  }
   __syncthreads();
   if (tid == 0) {
-    double nrm = 0.0;
-    for (int i = 0; i < m; ++i) nrm = fmax(nrm, fabs(d[i]) + fabs(e[i]) + (i > 0 ? fabs(e[i - 1]) : 0.0));
-    tnorm = nrm;
+    int bad = 0;
+    for (int j = 0; j < b; ++j) {   // upper R: W = R'R
+      double s = R[j][j];
+      for (int p = 0; p < j; ++p) s -= R[p][j] * R[p][j];
+      if (!(s > 0.0)) { bad = 1; s = 1.0; }
+      R[j][j] = sqrt(s);
+      for (int c = j + 1; c < b; ++c) {
+        double t = R[j][c];
+        for (int p = 0; p < j; ++p) t -= R[p][j] * R[p][c];
+        R[j][c] = t / R[j][j];
+      }
+    }
+    for (int c = 0; c < b; ++c)   // X = R^-1 (upper), column by column
+      for (int i = c; i >= 0; --i) {
+        double t = (i == c) ? 1.0 : 0.0;
+        for (int p = i + 1; p <= c; ++p) t -= R[i][p] * X[p][c];
+        X[i][c] = t / R[i][i];
+      }
+    if (bad) *status = 1;
   }
   __syncthreads();
-  const double nrm = tnorm, ortol = 1e-3 * nrm, pertol = 10.0 * 2.2e-16 * nrm, tiny = 2.2e-16 * nrm;
-  auto bsum = [&](double v) -> double {
-    v = wave_sum(v);
-    __syncthreads();
-    if ((tid & 63) == 0) red[tid >> 6] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-  };
-  int c0 = 0;          // first vector of the current cluster
-  double xprev = 0.0;
-  for (int j = 0; j < k; ++j) {
-    double xj = ev[j];
-    if (j > 0 && ev[j - 1] - ev[j] > ortol) c0 = j;
-    if (j > c0 && xj >= xprev - pertol) xj = xprev - pertol;   // separate (near-)equal shifts
-    xprev = xj;
-    if (tid == 0) {   // partial-pivoting LU of T - xj I: U has two superdiagonals (ua, ub, ud)
-      for (int i = 0; i < m; ++i) { ua[i] = d[i] - xj; ub[i] = e[i]; uc[i] = e[i]; ud[i] = 0.0; }
-      for (int i = 0; i + 1 < m; ++i) {
-        if (fabs(ua[i]) >= fabs(uc[i])) {
-          if (fabs(ua[i]) < tiny) ua[i] = copysign(tiny, ua[i]);
-          const double mult = uc[i] / ua[i];
-          uc[i] = mult;
-          ua[i + 1] -= mult * ub[i];
-          piv[i] = 0;
-        } else {
-          const double mult = ua[i] / uc[i];
-          ua[i] = uc[i];
-          const double t = ua[i + 1];
-          ua[i + 1] = ub[i] - mult * t;
-          if (i + 2 < m) { ud[i] = ub[i + 1]; ub[i + 1] = -mult * ud[i]; }
-          ub[i] = t;
-          uc[i] = mult;
-          piv[i] = 1;
-        }
-      }
-      for (int i = 0; i < m; ++i)
-        if (fabs(ua[i]) < tiny) ua[i] = copysign(tiny, ua[i]);
-    }
-    for (int i = tid; i < m; i += 256) x[i] = hash_unit(0x5eed, (uint64_t)j, (uint64_t)i);
-    __syncthreads();
-    for (int it = 0; it < 3; ++it) {
-      if (tid == 0) {   // solve (T - xj I) y = x in place
-        for (int i = 0; i + 1 < m; ++i) {
-          if (piv[i]) { const double t = x[i]; x[i] = x[i + 1]; x[i + 1] = t - uc[i] * x[i]; }
-          else x[i + 1] -= uc[i] * x[i];
-        }
-        x[m - 1] /= ua[m - 1];
-        if (m > 1) x[m - 2] = (x[m - 2] - ub[m - 2] * x[m - 1]) / ua[m - 2];
-        for (int i = m - 3; i >= 0; --i) x[i] = (x[i] - ub[i] * x[i + 1] - ud[i] * x[i + 2]) / ua[i];
-      }
-      __syncthreads();
-      // scale, then re-orthogonalise against the cluster's earlier vectors (MGS)
-      double mx = 0.0;
-      for (int i = tid; i < m; i += 256) mx += x[i] * x[i];
-      const double sc = 1.0 / sqrt(bsum(mx));
-      for (int i = tid; i < m; i += 256) x[i] *= sc;
-      __syncthreads();
-      for (int jj = c0; jj < j; ++jj) {
-        const double *z = Zt + (int64_t)jj * m;
-        double s = 0.0;
-        for (int i = tid; i < m; i += 256) s += z[i] * x[i];
-        s = bsum(s);
-        for (int i = tid; i < m; i += 256) x[i] -= s * z[i];
-        __syncthreads();
-      }
-      double nn = 0.0;
-      for (int i = tid; i < m; i += 256) nn += x[i] * x[i];
-      const double sc2 = 1.0 / sqrt(bsum(nn));
-      for (int i = tid; i < m; i += 256) x[i] *= sc2;
-      __syncthreads();
-    }
-    for (int i = tid; i < m; i += 256) Zt[(int64_t)j * m + i] = x[i];
-    __syncthreads();
-  }
+  for (int e = tid; e < b * b; e += blockDim.x) Rinv[e] = X[e / b][e % b];
+}
+
+__global__ void copy_cols_kernel(const double *__restrict__ src, int b, int m, double *__restrict__ Z, int k,
+                                 int j0) {
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)m * b; e += (int64_t)gridDim.x * 256)
+    Z[(e / b) * k + j0 + e % b] = src[e];
 }
 
 // U(:, j) = H_0 H_1 ... H_{m-3} z_j, one workgroup per vector; then the sign
@@ -336,13 +384,13 @@ __global__ __launch_bounds__(256) void stein_kernel(const double *__restrict__ d
 // and the m x k row-major layout of the subspace eigensolver's output.
 __global__ __launch_bounds__(256) void backtransform_kernel(const double *__restrict__ S,
                                                             const double *__restrict__ taus,
-                                                            const double *__restrict__ Zt, int m, int k,
+                                                            const double *__restrict__ Z, int m, int k,
                                                             double *__restrict__ Uk) {
   extern __shared__ double x[];
   __shared__ double red[4];
   __shared__ int redi[4];
   const int tid = threadIdx.x, j = blockIdx.x;
-  for (int i = tid; i < m; i += 256) x[i] = Zt[(int64_t)j * m + i];
+  for (int i = tid; i < m; i += 256) x[i] = Z[(int64_t)i * k + j];
   __syncthreads();
   for (int q = m - 3; q >= 0; --q) {
     const double tau = taus[q];
@@ -388,20 +436,48 @@ __global__ void diag_sum_kernel(const double *__restrict__ G, int64_t ldg, int m
 }
 
 int dense_eig_max() { return SPEC_VEC_MAX; }
-int64_t dense_eig_work(int m, int k) { return (int64_t)m * m + 4 * (int64_t)m + (int64_t)k * m; }
+int64_t dense_eig_work(int m, int k) {
+  return (int64_t)m * m + 4 * (int64_t)m + 5 * (int64_t)m * k + ((int64_t)m * k + 7) / 8 + 2 * (int64_t)k + 8 +
+         (int64_t)k * OB + 2 * OB * OB + (int64_t)m * OB;
+}
 
 // Top-k eigenpairs of ONE symmetric m x m matrix (lam: k, Uk: m x k
-// row-major, trace: 1), work: dense_eig_work(m, k) doubles.
+// row-major, trace: 1, status: 1 if an orthonormalisation block was
+// numerically rank deficient), work: dense_eig_work(m, k) doubles.
 hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
-                            double *work, hipStream_t st) {
+                            int *status, double *work, hipStream_t st) {
   if (m < 2 || m > SPEC_VEC_MAX || k < 1 || k > m || !work) return hipErrorInvalidValue;
-  double *S = work, *d = S + (int64_t)m * m, *e = d + m, *taus = e + m, *Zt = taus + m;
+  const int64_t mk = (int64_t)m * k;
+  double *S = work, *d = S + (int64_t)m * m, *e = d + m, *taus = e + m, *tn = taus + m;
+  double *ua = tn + 8, *ub = ua + mk, *uc = ub + mk, *ud = uc + mk, *Z = ud + mk;
+  unsigned char *piv = (unsigned char *)(Z + mk);
+  double *sig = Z + mk + (mk + 7) / 8, *Sm = sig + 2 * k, *W = Sm + (int64_t)k * OB, *Ri = W + OB * OB,
+         *Tmp = Ri + OB * OB;
   hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
                      (int64_t)0, m, m, 0, S, d, e, taus);
   hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, 1), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
                      d, e, m, m, 0, k, lam);
-  hipLaunchKernelGGL(stein_kernel, dim3(1), dim3(256), (size_t)7 * m * sizeof(double), st, d, e, lam, m, k, Zt);
-  hipLaunchKernelGGL(backtransform_kernel, dim3(k), dim3(256), (size_t)m * sizeof(double), st, S, taus, Zt, m, k,
+  hipLaunchKernelGGL(stein_shifts_kernel, dim3(1), dim3(64), 0, st, d, e, m, lam, k, sig, tn);
+  hipLaunchKernelGGL(invit_kernel, dim3((k + 63) / 64), dim3(64), 0, st, d, e, m, k, sig, tn, ua, ub, uc, ud, piv, Z);
+  hipError_t er = hipMemsetAsync(status, 0, sizeof(int), st);
+  if (er != hipSuccess) return er;
+  // BCGS2 + CholQR2 in eigenvalue order; Z(i, j) = Z[i * k + j]
+  for (int j0 = 0; j0 < k; j0 += OB) {
+    const int b = std::min(OB, k - j0);
+    double *Bj = Z + j0;
+    for (int pass = 0; pass < 2 && j0 > 0; ++pass) {
+      if ((er = gemm_strided(j0, b, m, 1.0, Z, 1, k, Bj, k, 1, 0.0, Sm, b, 1, st)) != hipSuccess) return er;
+      if ((er = gemm_strided(m, b, j0, -1.0, Z, k, 1, Sm, b, 1, 1.0, Bj, k, 1, st)) != hipSuccess) return er;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      if ((er = gemm_strided(b, b, m, 1.0, Bj, 1, k, Bj, k, 1, 0.0, W, b, 1, st)) != hipSuccess) return er;
+      hipLaunchKernelGGL(small_chol_inv_kernel, dim3(1), dim3(64), 0, st, W, b, Ri, status);
+      if ((er = gemm_strided(m, b, b, 1.0, Bj, k, 1, Ri, b, 1, 0.0, Tmp, b, 1, st)) != hipSuccess) return er;
+      hipLaunchKernelGGL(copy_cols_kernel, dim3(std::min(1024, (m * b + 255) / 256)), dim3(256), 0, st, Tmp, b, m, Z,
+                         k, j0);
+    }
+  }
+  hipLaunchKernelGGL(backtransform_kernel, dim3(k), dim3(256), (size_t)m * sizeof(double), st, S, taus, Z, m, k,
                      Uk);
   if (trace) hipLaunchKernelGGL(diag_sum_kernel, dim3(1), dim3(256), 0, st, G, ldg, m, trace);
   return hipGetLastError();

@@ -18,7 +18,7 @@ namespace dfm {
 __global__ __launch_bounds__(256) void gemm_strided_kernel(int M, int Nc, int K, double alpha,
                                                            const double *__restrict__ A, int64_t sAr, int64_t sAc,
                                                            const double *__restrict__ B, int64_t sBr, int64_t sBc,
-                                                           double *__restrict__ C, int64_t sCr, int64_t sCc) {
+                                                           double beta, double *C, int64_t sCr, int64_t sCc) {
   __shared__ double As[16][65], Bs[16][65];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
@@ -52,14 +52,25 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(int M, int Nc, int K,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int gm = m0 + ty + 16 * i, gn = n0 + tx + 16 * j;
-      if (gm < M && gn < Nc) C[(int64_t)gm * sCr + (int64_t)gn * sCc] = alpha * acc[i][j];
+      if (gm < M && gn < Nc) {
+        double *c = C + (int64_t)gm * sCr + (int64_t)gn * sCc;
+        *c = beta == 0.0 ? alpha * acc[i][j] : fma(alpha, acc[i][j], beta * *c);
+      }
     }
 }
 
+// C = alpha A B + beta C (beta == 0: C not read).  C may share an allocation
+// with A or B when the elements touched are disjoint.
+hipError_t gemm_strided(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
+                        const double *B, int64_t sBr, int64_t sBc, double beta, double *C, int64_t sCr,
+                        int64_t sCc, hipStream_t st) {
+  hipLaunchKernelGGL(gemm_strided_kernel, dim3((Nc + 63) / 64, (M + 63) / 64), dim3(256), 0, st, M, Nc, K, alpha, A,
+                     sAr, sAc, B, sBr, sBc, beta, C, sCr, sCc);
+  return hipGetLastError();
+}
 static void gemm_s(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc, const double *B,
                    int64_t sBr, int64_t sBc, double *C, int64_t sCr, int64_t sCc, hipStream_t st) {
-  hipLaunchKernelGGL(gemm_strided_kernel, dim3((Nc + 63) / 64, (M + 63) / 64), dim3(256), 0, st, M, Nc, K, alpha, A,
-                     sAr, sAc, B, sBr, sBc, C, sCr, sCc);
+  gemm_strided(M, Nc, K, alpha, A, sAr, sAc, B, sBr, sBc, 0.0, C, sCr, sCc, st);
 }
 
 __global__ void scale_copy_kernel(const double *__restrict__ x, int64_t n, double s, double *__restrict__ y) {
