@@ -203,8 +203,11 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
   ev[(int64_t)rep * (dm ? mst : nev) + j] = 0.5 * (lo + hi);
 }
 
+// Jacobi (LDS-resident, 1 WG per CU) only for small matrices: from m ~ 40 on
+// the tridiagonal path's O(m) barriers beat Jacobi's O(sweeps * m).
+constexpr int JACOBI_MAX = 32;
 int64_t spectrum_work(int m, int nb) {
-  if (m <= spectrum_max()) return 0;
+  if (m <= JACOBI_MAX) return 0;
   return (int64_t)nb * m * m + 2 * (int64_t)nb * m;
 }
 int spectrum_any_max() { return SPEC_ANY_MAX; }
@@ -215,7 +218,7 @@ int spectrum_any_max() { return SPEC_ANY_MAX; }
 hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
                                double *ev, double *work, hipStream_t st) {
   if (m0 < 1 || nb < 1 || dm < 0 || m0 + (int64_t)dm * (nb - 1) > m) return hipErrorInvalidValue;
-  if (m <= spectrum_max()) return launch_spectrum_jacobi(G, ldg, strideG, m, m0, dm, nb, ev, st);
+  if (m <= JACOBI_MAX) return launch_spectrum_jacobi(G, ldg, strideG, m, m0, dm, nb, ev, st);
   if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
   hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
