@@ -28,7 +28,12 @@ int spectrum_any_max();
 int64_t spectrum_work(int m, int nb);
 int dense_eig_max();
 int launch_factors_wide(int orient, const double *X, int64_t ld, int T, int N, int k, const double *Uk,
-                        double *F, double *L, double *colssr, hipStream_t st, double Ts);
+                        double *F, double *L, double *colssr, hipStream_t st, double Ts, int nb = 1, int64_t sX = 0,
+                        int64_t fstride = 0);
+hipError_t launch_materialize(const PanelSrc &src, int T, int N, int64_t ld, int nb, double *X, hipStream_t st);
+hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
+                                   int k, const int *Tn, double *coef, double *tstat, double *cov_out,
+                                   double *resid_out, int *status, double *work, hipStream_t st);
 int64_t ols_wide_work(int T, int d);
 hipError_t launch_ols_wide(const double *y, const double *w, int q, const double *F, int T, int k, double *coef,
                            double *tstat, double *cov_out, double *resid_out, int *status, double *work,
@@ -36,6 +41,9 @@ hipError_t launch_ols_wide(const double *y, const double *w, int q, const double
 int64_t dense_eig_work(int m, int k);
 hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
                             int *status, double *work, hipStream_t st);
+hipError_t launch_dense_eig_batched(const double *G, int64_t ldg, int64_t strideG, int m, int mv0, int dmv, int nb,
+                                    int k, double *lam, double *Uk, double *trace, int *status, double *work,
+                                    hipStream_t st);
 hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, int m, int m0, int dm, int nb,
                                double *ev, double *work, hipStream_t st);
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev, double *work,
@@ -908,9 +916,16 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
                                   stats[i].kind == DFM_STAT_EIGVAL || stats[i].kind == DFM_STAT_TRACE);
   const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
   const int p = eig_block_p(m, r, ctx->block);
-  const int P = p <= 16 ? 16 : 32;
+  // r beyond the subspace eigensolver's block: dense batched eigenpairs,
+  // materialised replicate panels for the factor GEMMs, GEMM-built OLS
+  const bool wide = p > 32 || p < r;
+  const int P = (p <= 16 || wide) ? 16 : 32;
+  if (wide && (M->m > dense_eig_max()))
+    return fail(ctx, -20, "bootstrap at r=%d > 24 needs min(T,N) <= %d", r, dense_eig_max());
+  if (wide && chow && r > 16)
+    return fail(ctx, -7, "Chow statistics inside the bootstrap support r <= 16 (got %d)", r);
   // PCp reads each replicate's full spectrum, so its Gram is formed: direct path
-  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1 && !pcp;
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1 && !pcp && !wide;
   if (pcp && m > spectrum_any_max())
     return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
                           "supported for min(T,N) <= %d", spectrum_any_max());
@@ -923,8 +938,10 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       const double per = (double)boot_ws_bytes(M, 1024, P, ctx->maxit, chow, true, nullptr, nullptr) / 1024.0;
       nb = (int64_t)std::max(1.0, std::min(16384.0, std::floor(16e9 / per)));
     } else {
-      const double gbytes = (double)m * m * 8 * (pcp ? 3 : 1);
-      nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor(1.5e9 / gbytes)));
+      double gbytes = (double)m * m * 8 * (pcp ? 3 : 1);
+      if (wide)
+        gbytes += 8.0 * ((double)dense_eig_work(m, r) + (double)T * M->ld + (double)ols_wide_work(T, q + r));
+      nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor((wide ? 4e9 : 1.5e9) / gbytes)));
     }
     // equal batches (no small tail batch running the iterations half-empty)
     const int64_t nbat = (B + nb - 1) / nb;
@@ -968,7 +985,41 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, &w, M->ws);
   // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
   // src/criteria.jl:18), its spectrum, sigma^2 per replicate
-  DevBuf pG, pEv, pWk, pSig;
+  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls;
+  if (wide) {
+    HIPCHK(ctx, dalloc(&wDe.p, (size_t)nb * dense_eig_work(m, r)));
+    if (r > 32) HIPCHK(ctx, dalloc(&wX.p, (size_t)nb * T * M->ld));
+    if (q + r > 32) HIPCHK(ctx, dalloc(&wOls.p, (size_t)nb * ols_wide_work(T, q + r)));
+  }
+  // top-r eigenpairs of n Grams (stride mm*mm): subspace iteration or dense
+  auto eig_any = [&](const double *G, int mm, int n, const double *warm, double *lam, double *Uk, double *tr,
+                     int64_t b0) -> int {
+    if (!wide) {
+      const int pj = eig_block_p(mm, r, ctx->block);
+      int rc = eig_run(G, mm, (int64_t)mm * mm, mm, n, r, pj, warm, r, etol, ctx->maxit, ctx->poll, w.eig, lam, Uk,
+                       tr, w.status, nullptr, st, timer_cb, ctx, b0);
+      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      note_iters(ctx);
+      return 0;
+    }
+    Scope sc(ctx, DFM_KC_EIG_OTHER);
+    hipError_t e = launch_dense_eig_batched(G, mm, (int64_t)mm * mm, mm, mm, 0, n, r, lam, Uk, tr, w.status, wDe.p,
+                                            st);
+    return e == hipSuccess ? 0 : fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));
+  };
+  // factors of n replicate panels (rows T_rows of src) into F (+ row offset)
+  auto factors_any = [&](const PanelSrc &ps, int Trows, int n, double *Fo, const double *Uk) -> int {
+    Scope sc(ctx, DFM_KC_FACTORS);
+    if (r <= 32) {
+      launch_factors(M->orient, ps, Trows, N, r, n, Uk, Fo, w.L, nullptr, st, (double)T, (int64_t)T * r);
+      return 0;
+    }
+    HIPCHK(ctx, launch_materialize(ps, Trows, N, M->ld, n, wX.p, st));
+    if (launch_factors_wide(M->orient, wX.p, M->ld, Trows, N, r, Uk, Fo, w.L, nullptr, st, (double)T, n,
+                            (int64_t)Trows * M->ld, (int64_t)T * r))
+      return fail(ctx, 1001, "factor kernels failed");
+    return 0;
+  };
   if (pcp) {
     HIPCHK(ctx, dalloc(&pG.p, (size_t)nb * m * m));
     HIPCHK(ctx, dalloc(&pEv.p, (size_t)nb * m));
@@ -999,15 +1050,10 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
           Scope sc(ctx, DFM_KC_GRAM);
           HIPCHK(ctx, launch_gram(M->orient, sj, mj, M->orient == 0 ? N : tj, tj, w.G, mj, (int64_t)mj * mj, n, st));
         }
-        const int pj = eig_block_p(mj, r, ctx->block);
-        int rc = eig_run(w.G, mj, (int64_t)mj * mj, mj, n, r, pj, M->Ubs[j], r, etol, ctx->maxit, ctx->poll,
-                         w.eig, w.blam, w.Uk, w.btr, w.status, nullptr, st, timer_cb, ctx, b0);
-        if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-        note_iters(ctx);
+        int rc = eig_any(w.G, mj, n, M->Ubs[j], w.blam, w.Uk, w.btr, b0);
+        if (rc) return rc;
         hipLaunchKernelGGL(or_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, n, M->flag_dev, 1);
-        Scope sc(ctx, DFM_KC_FACTORS);
-        launch_factors(M->orient, sj, tj, N, r, n, w.Uk, w.F + (size_t)a * r, w.L, nullptr, st, (double)T,
-                       (int64_t)T * r);
+        if ((rc = factors_any(sj, tj, n, w.F + (size_t)a * r, w.Uk))) return rc;
         hipLaunchKernelGGL(block_accum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.blam, w.btr, n, r,
                            w.lam, w.trace, j == 0 ? 1 : 0);
       }
@@ -1016,17 +1062,18 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
         Scope sc(ctx, DFM_KC_GRAM);
         HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
       }
-      int rc = eig_run(w.G, m, (int64_t)m * m, m, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
-                       w.eig, w.lam, w.Uk, w.trace, w.status, nullptr, st, timer_cb, ctx, b0);
-      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-      note_iters(ctx);
-      Scope sc(ctx, DFM_KC_FACTORS);
-      launch_factors(M->orient, src, T, N, r, n, w.Uk, w.F, w.L, nullptr, st);
+      int rc = eig_any(w.G, m, n, M->Ub, w.lam, w.Uk, w.trace, b0);
+      if (rc) return rc;
+      if ((rc = factors_any(src, T, n, w.F, w.Uk))) return rc;
     }
-    {
+    if (q + r <= 32) {
       Scope sc(ctx, DFM_KC_OLS);
       launch_ols(n, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
                          w.tstat, nullptr, nullptr, w.ost);
+    } else {
+      Scope sc(ctx, DFM_KC_OLS);
+      HIPCHK(ctx, launch_ols_wide_batched(n, M->y, M->w, q, w.F, T, r, r, nullptr, w.coef, w.tstat, nullptr, nullptr,
+                                          w.ost, wOls.p, st));
     }
     if (pcp) {
       const double *Gp = w.G;

@@ -43,7 +43,7 @@ DFM_DEV double block_sum(double v, double *red) {
 // tout != nullptr also the reflectors for the eigenvector back-transform:
 // v_k over S[k][k+1..m-1] (v_k[k+1] = 1, stored) and tau_k in tout[k].
 __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__restrict__ G, int64_t ldg,
-                                                              int64_t strideG, int mst, int m0, int dm,
+                                                              int64_t strideG, int mst, int m0, int dm, int pad,
                                                               double *__restrict__ Sw,
                                                               double *__restrict__ dout,
                                                               double *__restrict__ eout,
@@ -54,11 +54,14 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int rep = blockIdx.x;
   const double *g = G + (int64_t)rep * strideG;
-  const int m = m0 + dm * rep;   // this matrix's size; buffers have stride mst
+  // this matrix's size m0 + dm * rep (buffers have stride mst); pad: the
+  // matrix is the leading (m0 + dm * rep) block zero-padded to mst x mst
+  const int mv = m0 + dm * rep, m = pad ? mst : mv;
   double *S = Sw + (int64_t)rep * mst * mst;
   double *d = dout + (int64_t)rep * mst, *e = eout + (int64_t)rep * mst;
   for (int a = wv; a < m; a += TRI_WAVES)
-    for (int b = a + lane; b < m; b += 64) S[(int64_t)a * m + b] = 0.5 * (g[(int64_t)a * ldg + b] + g[(int64_t)b * ldg + a]);
+    for (int b = a + lane; b < m; b += 64)
+      S[(int64_t)a * m + b] = (a < mv && b < mv) ? 0.5 * (g[(int64_t)a * ldg + b] + g[(int64_t)b * ldg + a]) : 0.0;
   for (int i = tid; i < m; i += TRI_THREADS) { vp[i] = 0.0; wp[i] = 0.0; }
   __syncthreads();
   for (int k = 0; k < m; ++k) {
@@ -222,7 +225,7 @@ hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, in
   if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
   hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
-                     strideG, m, m0, dm, S, d, e, (double *)nullptr);
+                     strideG, m, m0, dm, 0, S, d, e, (double *)nullptr);
   hipLaunchKernelGGL(bisect_kernel, dim3((m + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
                      d, e, m, m0, dm, 0, ev);
   return hipGetLastError();
@@ -250,16 +253,19 @@ hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m,
 constexpr int SPEC_VEC_MAX = 4096;
 constexpr int OB = 32;   // orthonormalisation block
 
-hipError_t gemm_strided(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
-                        const double *B, int64_t sBr, int64_t sBc, double beta, double *C, int64_t sCr,
-                        int64_t sCc, hipStream_t st);
+hipError_t gemm_batched(int nb, int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
+                        int64_t sAb, const double *B, int64_t sBr, int64_t sBc, int64_t sBb, double beta, double *C,
+                        int64_t sCr, int64_t sCc, int64_t sCb, hipStream_t st);
 
 // ||T||_inf, and the shifts: sigma_j = lambda_j, pushed down so consecutive
 // shifts differ by >= 10 eps ||T|| (dstein's perturbation of close shifts)
-__global__ void stein_shifts_kernel(const double *__restrict__ d, const double *__restrict__ e, int m,
-                                    const double *__restrict__ lam, int k, double *__restrict__ sig,
-                                    double *__restrict__ tn) {
+__global__ void stein_shifts_kernel(const double *__restrict__ db, const double *__restrict__ eb, int m,
+                                    const double *__restrict__ lamb, int k, double *__restrict__ sigb,
+                                    double *__restrict__ tnb) {
   if (threadIdx.x != 0) return;
+  const int rep = blockIdx.x;
+  const double *d = db + (int64_t)rep * m, *e = eb + (int64_t)rep * m, *lam = lamb + (int64_t)rep * k;
+  double *sig = sigb + (int64_t)rep * k, *tn = tnb + rep;
   double nrm = 0.0;
   for (int i = 0; i < m; ++i)
     nrm = fmax(nrm, fabs(d[i]) + (i + 1 < m ? fabs(e[i]) : 0.0) + (i > 0 ? fabs(e[i - 1]) : 0.0));
@@ -274,14 +280,19 @@ __global__ void stein_shifts_kernel(const double *__restrict__ d, const double *
   *tn = nrm;
 }
 
-__global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d, const double *__restrict__ e,
-                                                   int m, int k, const double *__restrict__ sig,
-                                                   const double *__restrict__ tn, double *__restrict__ ua,
-                                                   double *__restrict__ ub, double *__restrict__ uc,
-                                                   double *__restrict__ ud, unsigned char *__restrict__ piv,
-                                                   double *__restrict__ Z) {
-  const int j = blockIdx.x * 64 + threadIdx.x;
+__global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ db, const double *__restrict__ eb,
+                                                   int m, int k, const double *__restrict__ sigb,
+                                                   const double *__restrict__ tnb, double *__restrict__ uab,
+                                                   double *__restrict__ ubb, double *__restrict__ ucb,
+                                                   double *__restrict__ udb, unsigned char *__restrict__ pivb,
+                                                   double *__restrict__ Zb) {
+  const int j = blockIdx.x * 64 + threadIdx.x, rep = blockIdx.y;
   if (j >= k) return;
+  const int64_t mk = (int64_t)m * k;
+  const double *d = db + (int64_t)rep * m, *e = eb + (int64_t)rep * m, *sig = sigb + (int64_t)rep * k,
+               *tn = tnb + rep;
+  double *ua = uab + rep * mk, *ub = ubb + rep * mk, *uc = ucb + rep * mk, *ud = udb + rep * mk, *Z = Zb + rep * mk;
+  unsigned char *piv = pivb + rep * mk;
   const double xj = sig[j], tiny = 2.2e-16 * *tn;
 #define IX(i) ((int64_t)(i) * k + j)
   for (int i = 0; i < m; ++i) { ua[IX(i)] = d[i] - xj; ub[IX(i)] = (i + 1 < m) ? e[i] : 0.0; ud[IX(i)] = 0.0; }
@@ -341,10 +352,12 @@ __global__ __launch_bounds__(64) void invit_kernel(const double *__restrict__ d,
 }
 
 // CholQR step on a b-column block: W = R'R (Cholesky, b <= OB), Rinv = R^-1.
-__global__ void small_chol_inv_kernel(const double *__restrict__ W, int b, double *__restrict__ Rinv,
+__global__ void small_chol_inv_kernel(const double *__restrict__ Wb, int b, double *__restrict__ Rinvb,
                                       int *__restrict__ status) {
   __shared__ double R[OB][OB + 1], X[OB][OB + 1];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, rep = blockIdx.x;
+  const double *W = Wb + (int64_t)rep * OB * OB;
+  double *Rinv = Rinvb + (int64_t)rep * OB * OB;
   for (int e = tid; e < OB * OB; e += blockDim.x) {
     const int a = e / OB, c = e % OB;
     R[a][c] = (a < b && c < b) ? W[a * b + c] : 0.0;
@@ -370,14 +383,17 @@ __global__ void small_chol_inv_kernel(const double *__restrict__ W, int b, doubl
         for (int p = i + 1; p <= c; ++p) t -= R[i][p] * X[p][c];
         X[i][c] = t / R[i][i];
       }
-    if (bad) *status = 1;
+    if (bad) status[rep] = 1;
   }
   __syncthreads();
   for (int e = tid; e < b * b; e += blockDim.x) Rinv[e] = X[e / b][e % b];
 }
 
-__global__ void copy_cols_kernel(const double *__restrict__ src, int b, int m, double *__restrict__ Z, int k,
+__global__ void copy_cols_kernel(const double *__restrict__ srcb, int b, int m, double *__restrict__ Zb, int k,
                                  int j0) {
+  const int rep = blockIdx.y;
+  const double *src = srcb + (int64_t)rep * m * OB;
+  double *Z = Zb + (int64_t)rep * m * k;
   for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)m * b; e += (int64_t)gridDim.x * 256)
     Z[(e / b) * k + j0 + e % b] = src[e];
 }
@@ -385,14 +401,17 @@ __global__ void copy_cols_kernel(const double *__restrict__ src, int b, int m, d
 // U(:, j) = H_0 H_1 ... H_{m-3} z_j, one workgroup per vector; then the sign
 // convention of eig_final_kernel (largest |entry|, first on ties, positive)
 // and the m x k row-major layout of the subspace eigensolver's output.
-__global__ __launch_bounds__(256) void backtransform_kernel(const double *__restrict__ S,
-                                                            const double *__restrict__ taus,
+__global__ __launch_bounds__(256) void backtransform_kernel(const double *S, const double *taus,
                                                             const double *__restrict__ Z, int m, int k,
                                                             double *__restrict__ Uk) {
   extern __shared__ double x[];
   __shared__ double red[4];
   __shared__ int redi[4];
-  const int tid = threadIdx.x, j = blockIdx.x;
+  const int tid = threadIdx.x, j = blockIdx.x, rep = blockIdx.y;
+  S += (int64_t)rep * m * m;
+  taus += (int64_t)rep * m;
+  Z += (int64_t)rep * m * k;
+  Uk += (int64_t)rep * m * k;
   for (int i = tid; i < m; i += 256) x[i] = Z[(int64_t)i * k + j];
   __syncthreads();
   for (int q = m - 3; q >= 0; --q) {
@@ -428,7 +447,11 @@ __global__ __launch_bounds__(256) void backtransform_kernel(const double *__rest
   for (int i = tid; i < m; i += 256) Uk[(int64_t)i * k + j] = sg * x[i];
 }
 
-__global__ void diag_sum_kernel(const double *__restrict__ G, int64_t ldg, int m, double *__restrict__ tr) {
+__global__ void diag_sum_kernel(const double *__restrict__ G, int64_t ldg, int64_t strideG, int m0, int dm,
+                                double *__restrict__ trb) {
+  const int rep = blockIdx.x, m = m0 + dm * rep;
+  G += (int64_t)rep * strideG;
+  double *tr = trb + rep;
   double s = 0.0;
   for (int i = threadIdx.x; i < m; i += 256) s += G[(int64_t)i * ldg + i];
   s = wave_sum(s);
@@ -439,51 +462,67 @@ __global__ void diag_sum_kernel(const double *__restrict__ G, int64_t ldg, int m
 }
 
 int dense_eig_max() { return SPEC_VEC_MAX; }
-int64_t dense_eig_work(int m, int k) {
-  return (int64_t)m * m + 4 * (int64_t)m + 5 * (int64_t)m * k + ((int64_t)m * k + 7) / 8 + 2 * (int64_t)k + 8 +
+int64_t dense_eig_work(int m, int k) {   // per matrix
+  return (int64_t)m * m + 3 * (int64_t)m + 8 + 5 * (int64_t)m * k + ((int64_t)m * k + 7) / 8 + 2 * (int64_t)k +
          (int64_t)k * OB + 2 * OB * OB + (int64_t)m * OB;
 }
 
-// Top-k eigenpairs of ONE symmetric m x m matrix (lam: k, Uk: m x k
-// row-major, trace: 1, status: 1 if an orthonormalisation block was
-// numerically rank deficient), work: dense_eig_work(m, k) doubles.
-hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
-                            int *status, double *work, hipStream_t st) {
-  if (m < 2 || m > SPEC_VEC_MAX || k < 1 || k > m || !work) return hipErrorInvalidValue;
+// Top-k eigenpairs of nb symmetric matrices G + rep * strideG, each the
+// leading (mv0 + dmv * rep) block zero-padded to m x m (dmv = 0, mv0 = m: plain
+// m x m).  lam: nb x k, Uk: nb x m x k (row-major m x k each), trace: nb (of
+// the valid block), status: nb (1 = an orthonormalisation block numerically
+// rank deficient).  work: nb * dense_eig_work(m, k) doubles.
+hipError_t launch_dense_eig_batched(const double *G, int64_t ldg, int64_t strideG, int m, int mv0, int dmv, int nb,
+                                    int k, double *lam, double *Uk, double *trace, int *status, double *work,
+                                    hipStream_t st) {
+  if (m < 2 || m > SPEC_VEC_MAX || k < 1 || k > m || nb < 1 || !work || !status) return hipErrorInvalidValue;
   const int64_t mk = (int64_t)m * k;
-  double *S = work, *d = S + (int64_t)m * m, *e = d + m, *taus = e + m, *tn = taus + m;
-  double *ua = tn + 8, *ub = ua + mk, *uc = ub + mk, *ud = uc + mk, *Z = ud + mk;
-  unsigned char *piv = (unsigned char *)(Z + mk);
-  double *sig = Z + mk + (mk + 7) / 8, *Sm = sig + 2 * k, *W = Sm + (int64_t)k * OB, *Ri = W + OB * OB,
-         *Tmp = Ri + OB * OB;
-  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
-                     (int64_t)0, m, m, 0, S, d, e, taus);
-  hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, 1), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
+  double *S = work, *d = S + nb * (int64_t)m * m, *e = d + (int64_t)nb * m, *taus = e + (int64_t)nb * m;
+  double *tn = taus + (int64_t)nb * m, *ua = tn + 8 * (int64_t)nb, *ub = ua + nb * mk, *uc = ub + nb * mk;
+  double *ud = uc + nb * mk, *Z = ud + nb * mk;
+  unsigned char *piv = (unsigned char *)(Z + nb * mk);
+  double *sig = Z + nb * mk + (nb * mk + 7) / 8, *Sm = sig + 2 * (int64_t)nb * k, *W = Sm + (int64_t)nb * k * OB;
+  double *Ri = W + (int64_t)nb * OB * OB, *Tmp = Ri + (int64_t)nb * OB * OB;
+  const int pad = (dmv != 0 || mv0 != m) ? 1 : 0;
+  hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
+                     strideG, m, mv0, dmv, pad, S, d, e, taus);
+  hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
                      d, e, m, m, 0, k, lam);
-  hipLaunchKernelGGL(stein_shifts_kernel, dim3(1), dim3(64), 0, st, d, e, m, lam, k, sig, tn);
-  hipLaunchKernelGGL(invit_kernel, dim3((k + 63) / 64), dim3(64), 0, st, d, e, m, k, sig, tn, ua, ub, uc, ud, piv, Z);
-  hipError_t er = hipMemsetAsync(status, 0, sizeof(int), st);
+  hipLaunchKernelGGL(stein_shifts_kernel, dim3(nb), dim3(64), 0, st, d, e, m, lam, k, sig, tn);
+  hipLaunchKernelGGL(invit_kernel, dim3((k + 63) / 64, nb), dim3(64), 0, st, d, e, m, k, sig, tn, ua, ub, uc, ud, piv,
+                     Z);
+  hipError_t er = hipMemsetAsync(status, 0, sizeof(int) * nb, st);
   if (er != hipSuccess) return er;
   // BCGS2 + CholQR2 in eigenvalue order; Z(i, j) = Z[i * k + j]
+  const int64_t sS = (int64_t)k * OB, sW = OB * OB, sT = (int64_t)m * OB;
   for (int j0 = 0; j0 < k; j0 += OB) {
     const int b = std::min(OB, k - j0);
     double *Bj = Z + j0;
     for (int pass = 0; pass < 2 && j0 > 0; ++pass) {
-      if ((er = gemm_strided(j0, b, m, 1.0, Z, 1, k, Bj, k, 1, 0.0, Sm, b, 1, st)) != hipSuccess) return er;
-      if ((er = gemm_strided(m, b, j0, -1.0, Z, k, 1, Sm, b, 1, 1.0, Bj, k, 1, st)) != hipSuccess) return er;
+      if ((er = gemm_batched(nb, j0, b, m, 1.0, Z, 1, k, mk, Bj, k, 1, mk, 0.0, Sm, b, 1, sS, st)) != hipSuccess)
+        return er;
+      if ((er = gemm_batched(nb, m, b, j0, -1.0, Z, k, 1, mk, Sm, b, 1, sS, 1.0, Bj, k, 1, mk, st)) != hipSuccess)
+        return er;
     }
     for (int pass = 0; pass < 2; ++pass) {
-      if ((er = gemm_strided(b, b, m, 1.0, Bj, 1, k, Bj, k, 1, 0.0, W, b, 1, st)) != hipSuccess) return er;
-      hipLaunchKernelGGL(small_chol_inv_kernel, dim3(1), dim3(64), 0, st, W, b, Ri, status);
-      if ((er = gemm_strided(m, b, b, 1.0, Bj, k, 1, Ri, b, 1, 0.0, Tmp, b, 1, st)) != hipSuccess) return er;
-      hipLaunchKernelGGL(copy_cols_kernel, dim3(std::min(1024, (m * b + 255) / 256)), dim3(256), 0, st, Tmp, b, m, Z,
-                         k, j0);
+      if ((er = gemm_batched(nb, b, b, m, 1.0, Bj, 1, k, mk, Bj, k, 1, mk, 0.0, W, b, 1, sW, st)) != hipSuccess)
+        return er;
+      hipLaunchKernelGGL(small_chol_inv_kernel, dim3(nb), dim3(64), 0, st, W, b, Ri, status);
+      if ((er = gemm_batched(nb, m, b, b, 1.0, Bj, k, 1, mk, Ri, b, 1, sW, 0.0, Tmp, b, 1, sT, st)) != hipSuccess)
+        return er;
+      hipLaunchKernelGGL(copy_cols_kernel, dim3(std::min(1024, (m * b + 255) / 256), nb), dim3(256), 0, st, Tmp, b, m,
+                         Z, k, j0);
     }
   }
-  hipLaunchKernelGGL(backtransform_kernel, dim3(k), dim3(256), (size_t)m * sizeof(double), st, S, taus, Z, m, k,
+  hipLaunchKernelGGL(backtransform_kernel, dim3(k, nb), dim3(256), (size_t)m * sizeof(double), st, S, taus, Z, m, k,
                      Uk);
-  if (trace) hipLaunchKernelGGL(diag_sum_kernel, dim3(1), dim3(256), 0, st, G, ldg, m, trace);
+  if (trace)
+    hipLaunchKernelGGL(diag_sum_kernel, dim3(nb), dim3(256), 0, st, G, ldg, strideG, mv0, dmv, trace);
   return hipGetLastError();
+}
+hipError_t launch_dense_eig(const double *G, int64_t ldg, int m, int k, double *lam, double *Uk, double *trace,
+                            int *status, double *work, hipStream_t st) {
+  return launch_dense_eig_batched(G, ldg, 0, m, m, 0, 1, k, lam, Uk, trace, status, work, st);
 }
 
 }  // namespace dfm

@@ -18,9 +18,13 @@ namespace dfm {
 __global__ __launch_bounds__(256) void gemm_strided_kernel(int M, int Nc, int K, double alpha,
                                                            const double *__restrict__ A, int64_t sAr, int64_t sAc,
                                                            const double *__restrict__ B, int64_t sBr, int64_t sBc,
-                                                           double beta, double *C, int64_t sCr, int64_t sCc) {
+                                                           double beta, double *C, int64_t sCr, int64_t sCc,
+                                                           int64_t sAb, int64_t sBb, int64_t sCb) {
   __shared__ double As[16][65], Bs[16][65];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  A += blockIdx.z * sAb;
+  B += blockIdx.z * sBb;
+  C += blockIdx.z * sCb;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   double acc[4][4] = {};
   for (int k0 = 0; k0 < K; k0 += 16) {
@@ -61,12 +65,19 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(int M, int Nc, int K,
 
 // C = alpha A B + beta C (beta == 0: C not read).  C may share an allocation
 // with A or B when the elements touched are disjoint.
+// Batched: problem z reads A + z sAb, B + z sBb, writes C + z sCb.
+hipError_t gemm_batched(int nb, int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
+                        int64_t sAb, const double *B, int64_t sBr, int64_t sBc, int64_t sBb, double beta, double *C,
+                        int64_t sCr, int64_t sCc, int64_t sCb, hipStream_t st) {
+  if (nb < 1 || M < 1 || Nc < 1) return hipSuccess;
+  hipLaunchKernelGGL(gemm_strided_kernel, dim3((Nc + 63) / 64, (M + 63) / 64, nb), dim3(256), 0, st, M, Nc, K, alpha,
+                     A, sAr, sAc, B, sBr, sBc, beta, C, sCr, sCc, sAb, sBb, sCb);
+  return hipGetLastError();
+}
 hipError_t gemm_strided(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc,
                         const double *B, int64_t sBr, int64_t sBc, double beta, double *C, int64_t sCr,
                         int64_t sCc, hipStream_t st) {
-  hipLaunchKernelGGL(gemm_strided_kernel, dim3((Nc + 63) / 64, (M + 63) / 64), dim3(256), 0, st, M, Nc, K, alpha, A,
-                     sAr, sAc, B, sBr, sBc, beta, C, sCr, sCc);
-  return hipGetLastError();
+  return gemm_batched(1, M, Nc, K, alpha, A, sAr, sAc, 0, B, sBr, sBc, 0, beta, C, sCr, sCc, 0, st);
 }
 static void gemm_s(int M, int Nc, int K, double alpha, const double *A, int64_t sAr, int64_t sAc, const double *B,
                    int64_t sBr, int64_t sBc, double *C, int64_t sCr, int64_t sCc, hipStream_t st) {
@@ -75,6 +86,13 @@ static void gemm_s(int M, int Nc, int K, double alpha, const double *A, int64_t 
 
 __global__ void scale_copy_kernel(const double *__restrict__ x, int64_t n, double s, double *__restrict__ y) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = s * x[i];
+}
+// y[rep][i] = s x[rep][i] for strided batches (rows of n elements)
+__global__ void scale_copy_batched_kernel(const double *__restrict__ x, int64_t sx, int64_t n, double s,
+                                          double *__restrict__ y, int64_t sy) {
+  const int rep = blockIdx.y;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    y[rep * sy + i] = s * x[rep * sx + i];
 }
 
 // per-variable SSR of the factor residual, N > T branch: ||x_n||^2 - Ts ||l_n||^2
@@ -95,46 +113,78 @@ __global__ void col_ssq_plain_kernel(const double *__restrict__ P, int64_t ld, i
   out[n] = s;
 }
 
-// Factors and loadings of one block at any k (the layouts of launch_factors):
-// orient 0 (N > T): F = sqrt(Ts) U, L = X' F / Ts; orient 1: L = sqrt(N) V,
-// F = X V / sqrt(N).  X: row-major T x ld panel.
+// X*_rep = C + eta_rep * E[idx_rep] (rows 0..T-1 of the PanelSrc), T x ld per replicate
+__global__ void materialize_kernel(PanelSrc src, int T, int N, int64_t ld, double *__restrict__ X) {
+  const int rep = blockIdx.z, t = blockIdx.y;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= ld) return;
+  double v = 0.0;
+  if (n < N) {
+    const int er = src.idx ? src.idx[(int64_t)rep * src.rs + t] : t;
+    const double ev = src.eta ? src.eta[(int64_t)rep * src.rs + t] : 1.0;
+    v = src.E[(int64_t)er * src.ld + n] * ev;
+    if (src.C) v += src.C[(int64_t)t * src.ld + n];
+  }
+  X[((int64_t)rep * T + t) * ld + n] = v;
+}
+hipError_t launch_materialize(const PanelSrc &src, int T, int N, int64_t ld, int nb, double *X, hipStream_t st) {
+  hipLaunchKernelGGL(materialize_kernel, dim3((unsigned)((ld + 255) / 256), T, nb), dim3(256), 0, st, src, T, N, ld,
+                     X);
+  return hipGetLastError();
+}
+
+// Factors and loadings of one block at any k (the layouts of launch_factors),
+// for nb panels X + rep * sX (row-major T x ld): orient 0 (N > T): F = sqrt(Ts) U,
+// L = X' F / Ts; orient 1: L = sqrt(N) V, F = X V / sqrt(N).  U/V of replicate
+// rep at Uk + rep * m * k, F at F + rep * fstride, L at L + rep * N * k.
 int launch_factors_wide(int orient, const double *X, int64_t ld, int T, int N, int k, const double *Uk,
-                        double *F, double *L, double *colssr, hipStream_t st, double Ts) {
+                        double *F, double *L, double *colssr, hipStream_t st, double Ts, int nb, int64_t sX,
+                        int64_t fstride) {
   if (Ts <= 0) Ts = T;
+  if (fstride <= 0) fstride = (int64_t)T * k;
+  const int64_t sL = (int64_t)N * k;
   if (orient == 0) {
-    hipLaunchKernelGGL(scale_copy_kernel, dim3(std::min<int64_t>(1024, ((int64_t)T * k + 255) / 256)), dim3(256),
-                       0, st, Uk, (int64_t)T * k, sqrt(Ts), F);
-    gemm_s(N, k, T, 1.0 / Ts, X, 1, ld, F, k, 1, L, k, 1, st);
-    if (colssr) {
+    const int64_t sU = (int64_t)T * k;
+    hipLaunchKernelGGL(scale_copy_batched_kernel, dim3((unsigned)std::min<int64_t>(1024, (sU + 255) / 256), nb),
+                       dim3(256), 0, st, Uk, sU, sU, sqrt(Ts), F, fstride);
+    gemm_batched(nb, N, k, T, 1.0 / Ts, X, 1, ld, sX, F, k, 1, fstride, 0.0, L, k, 1, sL, st);
+    if (colssr && nb == 1) {
       hipLaunchKernelGGL(col_ssq_plain_kernel, dim3((N + 255) / 256), dim3(256), 0, st, X, ld, T, N, colssr);
       hipLaunchKernelGGL(colssr_rows_fix_kernel, dim3((N + 255) / 256), dim3(256), 0, st, N, k, Ts, L, colssr);
     }
   } else {
-    hipLaunchKernelGGL(scale_copy_kernel, dim3(std::min<int64_t>(1024, ((int64_t)N * k + 255) / 256)), dim3(256),
-                       0, st, Uk, (int64_t)N * k, sqrt((double)N), L);
-    gemm_s(T, k, N, 1.0 / sqrt((double)N), X, ld, 1, Uk, k, 1, F, k, 1, st);
+    hipLaunchKernelGGL(scale_copy_batched_kernel, dim3((unsigned)std::min<int64_t>(1024, (sL + 255) / 256), nb),
+                       dim3(256), 0, st, Uk, sL, sL, sqrt((double)N), L, sL);
+    gemm_batched(nb, T, k, N, 1.0 / sqrt((double)N), X, ld, 1, sX, Uk, k, 1, sL, 0.0, F, k, 1, fstride, st);
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 // ------------------------------------------------------------- wide OLS
-// D = [w F] (T x d, row-major), F row-major T x k, w column-major (ld T).
-__global__ void design_kernel(const double *__restrict__ w, int q, const double *__restrict__ F, int T, int k,
-                              double *__restrict__ D) {
-  const int d = q + k;
+// D = [w F] (T x d, row-major) per replicate; F of replicate rep at
+// F + rep * Tphys * kF (row stride kF, first k columns used), rows t >= Tn[rep]
+// zeroed (expanding windows) — they then drop out of D'D, D'y and the meat.
+__global__ void design_kernel(const double *__restrict__ w, int q, const double *__restrict__ F, int T, int kF,
+                              int k, const int *__restrict__ Tn, double *__restrict__ D) {
+  const int d = q + k, rep = blockIdx.y;
+  const int Tr = Tn ? Tn[rep] : T;
+  const double *Fr = F + (int64_t)rep * T * kF;
+  double *Dr = D + (int64_t)rep * T * d;
   for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)T * d; e += (int64_t)gridDim.x * 256) {
     const int t = (int)(e / d), c = (int)(e % d);
-    D[e] = c < q ? w[(int64_t)c * T + t] : F[(int64_t)t * k + (c - q)];
+    Dr[e] = t >= Tr ? 0.0 : (c < q ? w[(int64_t)c * T + t] : Fr[(int64_t)t * kF + (c - q)]);
   }
 }
 
 // In-place Cholesky of the row-major d x d M (lower), then Linv = L^-1
-// (rows of Linv' per thread: Lt[c][i] = Linv[i][c]).  One workgroup.
-__global__ __launch_bounds__(1024) void chol_inv_kernel(double *__restrict__ M, int d, double *__restrict__ Lt,
+// (rows of Linv' per thread: Lt[c][i] = Linv[i][c]).  One workgroup per
+// replicate (blockIdx.x).
+__global__ __launch_bounds__(1024) void chol_inv_kernel(double *__restrict__ Mb, int d, double *__restrict__ Ltb,
                                                         int *__restrict__ status) {
   __shared__ int bad;
   __shared__ double piv;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, rep = blockIdx.x;
+  double *M = Mb + (int64_t)rep * d * d, *Lt = Ltb + (int64_t)rep * d * d;
   if (tid == 0) bad = 0;
   __syncthreads();
   for (int j = 0; j < d; ++j) {
@@ -173,60 +223,81 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(double *__restrict__ M, 
       x[i] = s / Li[i];
     }
   }
-  if (tid == 0) *status = bad ? 2 : 0;
+  if (tid == 0 && status) status[rep] = bad ? 2 : 0;
 }
 
 // Per row t (one wave): fit, leverage h_t = sum_c H1[t][c] D[t][c] with
 // H1 = D inv(D'D), u_t, sigma2_t = u_t^2 / (1 - h_t), Ds = sigma2_t * D[t].
-__global__ void hc2_rows_kernel(const double *__restrict__ D, const double *__restrict__ H1,
-                                const double *__restrict__ y, const double *__restrict__ beta, int T, int d,
-                                double *__restrict__ Ds, double *__restrict__ resid) {
-  const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ void hc2_rows_kernel(const double *__restrict__ Db, const double *__restrict__ H1b,
+                                const double *__restrict__ y, const double *__restrict__ betab, int T, int d,
+                                const int *__restrict__ Tn, double *__restrict__ Dsb, double *__restrict__ resid) {
+  const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6), rep = blockIdx.y;
   if (t >= T) return;
-  const double *Dt = D + (int64_t)t * d, *Ht = H1 + (int64_t)t * d;
+  const int64_t o = ((int64_t)rep * T + t) * d;
+  const double *Dt = Db + o, *Ht = H1b + o, *beta = betab + (int64_t)rep * d;
+  const bool in = !Tn || t < Tn[rep];
   double fit = 0.0, h = 0.0;
   for (int c = lane; c < d; c += 64) { fit = fma(Dt[c], beta[c], fit); h = fma(Ht[c], Dt[c], h); }
   fit = wave_sum(fit);
   h = wave_sum(h);
-  const double u = y[t] - fit, s2 = u * u / (1.0 - h);
-  if (lane == 0 && resid) resid[t] = u;
-  for (int c = lane; c < d; c += 64) Ds[(int64_t)t * d + c] = s2 * Dt[c];
+  const double u = y[t] - fit, s2 = in ? u * u / (1.0 - h) : 0.0;
+  if (lane == 0 && resid && in) resid[(int64_t)rep * T + t] = u;
+  for (int c = lane; c < d; c += 64) Dsb[o + c] = s2 * Dt[c];
 }
 
-__global__ void ols_finish_kernel(const double *__restrict__ beta, const double *__restrict__ Sig, int d,
+// coef / t rows of stride dstr (NaN past d), optional covariance (nb == 1)
+__global__ void ols_finish_kernel(const double *__restrict__ betab, const double *__restrict__ Sigb, int d, int dstr,
                                   double *__restrict__ coef, double *__restrict__ tstat, double *__restrict__ cov) {
+  const int rep = blockIdx.y;
+  const double *beta = betab + (int64_t)rep * d, *Sig = Sigb + (int64_t)rep * d * d;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < d * d; e += gridDim.x * 256) {
     const int a = e / d, c = e % d;
     if (cov) cov[(int64_t)c * d + a] = Sig[e];
-    if (a == c) { coef[a] = beta[a]; tstat[a] = beta[a] / sqrt(Sig[e]); }
+    if (a == c) {
+      coef[(int64_t)rep * dstr + a] = beta[a];
+      tstat[(int64_t)rep * dstr + a] = beta[a] / sqrt(Sig[e]);
+    }
+  }
+  for (int a = d + blockIdx.x * 256 + threadIdx.x; a < dstr; a += gridDim.x * 256) {
+    coef[(int64_t)rep * dstr + a] = NAN;
+    tstat[(int64_t)rep * dstr + a] = NAN;
   }
 }
 
 int64_t ols_wide_work(int T, int d) { return 3 * (int64_t)T * d + 6 * (int64_t)d * d + 2 * (int64_t)d; }
 
-// src/DynamicFactorModel.jl:40-48 for one fit of any width d = q + k.
+// src/DynamicFactorModel.jl:40-48 for nb fits of any width d = q + k: F of
+// replicate rep at F + rep * T * kF (first k of kF columns), optional sample
+// sizes Tn; coef / tstat rows of stride q + kF; work: nb * ols_wide_work(T, d).
+hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
+                                   int k, const int *Tn, double *coef, double *tstat, double *cov_out,
+                                   double *resid_out, int *status, double *work, hipStream_t st) {
+  const int d = q + k, dstr = q + kF;
+  const int64_t Td = (int64_t)T * d, dd = (int64_t)d * d;
+  double *D = work, *H1 = D + nb * Td, *Ds = H1 + nb * Td, *DtD = Ds + nb * Td;
+  double *Lt = DtD + nb * dd, *Inv = Lt + nb * dd, *Meat = Inv + nb * dd;
+  double *Tmp = Meat + nb * dd, *Sig = Tmp + nb * dd, *Dty = Sig + nb * dd, *beta = Dty + (int64_t)nb * d;
+  hipLaunchKernelGGL(design_kernel, dim3((unsigned)std::min<int64_t>(1024, (Td + 255) / 256), nb), dim3(256), 0, st,
+                     w, q, F, T, kF, k, Tn, D);
+  gemm_batched(nb, d, d, T, 1.0, D, 1, d, Td, D, d, 1, Td, 0.0, DtD, d, 1, dd, st);       // D'D
+  gemm_batched(nb, d, 1, T, 1.0, D, 1, d, Td, y, 1, 0, 0, 0.0, Dty, 1, 0, d, st);         // D'y
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(nb), dim3(1024), 0, st, DtD, d, Lt, status);
+  gemm_batched(nb, d, d, d, 1.0, Lt, d, 1, dd, Lt, 1, d, dd, 0.0, Inv, d, 1, dd, st);      // Linv' Linv
+  gemm_batched(nb, d, 1, d, 1.0, Inv, d, 1, dd, Dty, 1, 0, d, 0.0, beta, 1, 0, d, st);     // beta
+  gemm_batched(nb, T, d, d, 1.0, D, d, 1, Td, Inv, d, 1, dd, 0.0, H1, d, 1, Td, st);       // D inv(D'D)
+  hipLaunchKernelGGL(hc2_rows_kernel, dim3((T + 3) / 4, nb), dim3(256), 0, st, D, H1, y, beta, T, d, Tn, Ds,
+                     resid_out);
+  gemm_batched(nb, d, d, T, 1.0, D, 1, d, Td, Ds, d, 1, Td, 0.0, Meat, d, 1, dd, st);     // sum sigma2_t d_t d_t'
+  gemm_batched(nb, d, d, d, 1.0, Meat, d, 1, dd, Inv, d, 1, dd, 0.0, Tmp, d, 1, dd, st);
+  gemm_batched(nb, d, d, d, 1.0, Inv, d, 1, dd, Tmp, d, 1, dd, 0.0, Sig, d, 1, dd, st);
+  hipLaunchKernelGGL(ols_finish_kernel, dim3((unsigned)std::min<int64_t>(64, (dd + 255) / 256), nb), dim3(256), 0,
+                     st, beta, Sig, d, dstr, coef, tstat, nb == 1 ? cov_out : nullptr);
+  return hipGetLastError();
+}
 hipError_t launch_ols_wide(const double *y, const double *w, int q, const double *F, int T, int k, double *coef,
                            double *tstat, double *cov_out, double *resid_out, int *status, double *work,
                            hipStream_t st) {
-  const int d = q + k;
-  double *D = work, *H1 = D + (int64_t)T * d, *Ds = H1 + (int64_t)T * d, *DtD = Ds + (int64_t)T * d;
-  double *Lt = DtD + (int64_t)d * d, *Inv = Lt + (int64_t)d * d, *Meat = Inv + (int64_t)d * d;
-  double *Tmp = Meat + (int64_t)d * d, *Sig = Tmp + (int64_t)d * d, *Dty = Sig + (int64_t)d * d, *beta = Dty + d;
-  hipLaunchKernelGGL(design_kernel, dim3(std::min<int64_t>(2048, ((int64_t)T * d + 255) / 256)), dim3(256), 0, st,
-                     w, q, F, T, k, D);
-  gemm_s(d, d, T, 1.0, D, 1, d, D, d, 1, DtD, d, 1, st);        // D'D
-  gemm_s(d, 1, T, 1.0, D, 1, d, y, 1, 0, Dty, 1, 0, st);       // D'y
-  hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(1024), 0, st, DtD, d, Lt, status);
-  gemm_s(d, d, d, 1.0, Lt, d, 1, Lt, 1, d, Inv, d, 1, st);      // inv(D'D) = Linv' Linv  (Lt[c][i] = Linv[i][c])
-  gemm_s(d, 1, d, 1.0, Inv, d, 1, Dty, 1, 0, beta, 1, 0, st);  // beta
-  gemm_s(T, d, d, 1.0, D, d, 1, Inv, d, 1, H1, d, 1, st);       // D inv(D'D)
-  hipLaunchKernelGGL(hc2_rows_kernel, dim3((T + 3) / 4), dim3(256), 0, st, D, H1, y, beta, T, d, Ds, resid_out);
-  gemm_s(d, d, T, 1.0, D, 1, d, Ds, d, 1, Meat, d, 1, st);      // sum_t sigma2_t d_t d_t'
-  gemm_s(d, d, d, 1.0, Meat, d, 1, Inv, d, 1, Tmp, d, 1, st);
-  gemm_s(d, d, d, 1.0, Inv, d, 1, Tmp, d, 1, Sig, d, 1, st);
-  hipLaunchKernelGGL(ols_finish_kernel, dim3(std::min(1024, (d * d + 255) / 256)), dim3(256), 0, st, beta, Sig, d,
-                     coef, tstat, cov_out);
-  return hipGetLastError();
+  return launch_ols_wide_batched(1, y, w, q, F, T, k, k, nullptr, coef, tstat, cov_out, resid_out, status, work, st);
 }
 
 }  // namespace dfm

@@ -140,3 +140,29 @@ def test_pcp_criterion_in_replicates(dfm, oracle, T, N, r, crit, mode, breaks):
         ref = [d.number_of_factors_criterion_value, oracle.criterion_value("PCp1", d),
                oracle.factor_residual_variance(d)]
         assert rel(out[b], ref) < STAT_RTOL
+
+
+# ------------------------------------------- bootstrap at r > 24 (dense batch)
+@pytest.mark.parametrize("T,N,r,crit,breaks", [
+    (150, 70, 30, "ICp2", ()),        # T >= N: r <= 32 factor kernels, q + r <= 32 OLS
+    (90, 200, 40, "BIC", ()),         # N > T: wide factors (materialised X*) and wide OLS
+    (200, 130, 65, "PCp2", ()),       # the default r = ceil(m/2) of the reference's test shape, PCp
+    (160, 60, 27, "ICp1", (81,)),     # break blocks, per-block dense eigenpairs
+])
+def test_bootstrap_many_factors(dfm, oracle, T, N, r, crit, breaks):
+    y, x, w = panel(oracle, T, N, 3, 7800 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, crit, break_indices=breaks)
+    o = oracle.DynamicFactorModel(y, w, x, r, crit, break_indices=breaks)
+    B = 3
+    idx, eta = oracle.draw_wild(np.random.default_rng(21), B, T)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, B, [S.V(), S.criterion(), S.eigenvalue(1), S.eigenvalue(r), S.trace(),
+                                    S.coefficient(1), S.t_stat(1)], idx=idx, eta=eta)
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, r, crit, break_indices=breaks)
+        ref = [oracle.factor_residual_variance(d), d.number_of_factors_criterion_value,
+               sum(e[0] for e in d.eigenvalues), sum(e[r - 1] for e in d.eigenvalues), np.sum(xs * xs),
+               d.coefficients[0], d.t_stats[0]]
+        assert rel(out[b, :5], ref[:5]) < STAT_RTOL
+        assert rel(out[b, 5:], ref[5:]) < 1e-8
