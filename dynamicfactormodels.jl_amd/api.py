@@ -561,6 +561,13 @@ def _targeted_soft(y, w, x, folds, rng, nlambda, lambda_min_ratio, return_path, 
 
 
 # ---------------------------------------------------------- expanding windows
+def _window_kmax(T: int, N: int, kmax) -> int:
+    """Row width of the windows' eigenvalue / coefficient outputs: the last
+    (widest) window's sweep bound, ceil(min(T-1, N)/2) capped by kmax."""
+    kd = int(math.ceil(min(T - 1, N) / 2))
+    return min(int(kmax), kd) if kmax else kd
+
+
 def pseudo_out_of_sample_refits(y, w, x, criterion: str = "ICp2", num_predictions: int = 200,
                                 kmax: Optional[int] = None, *, ctx: Optional[Context] = None):
     """The refit loop of ``pseudo_out_of_sample_forecasts`` (``src/utils.jl:54-72``):
@@ -574,16 +581,15 @@ def pseudo_out_of_sample_refits(y, w, x, criterion: str = "ICp2", num_prediction
     x = _f64(x, 2)
     T, N = x.shape
     q, P = w.shape[1], int(num_predictions)
-    m = min(T - P, N)
-    km = int(kmax) if kmax else int(math.ceil(m / 2))
-    km = min(km, int(math.ceil(m / 2)))
+    km = _window_kmax(T, N, kmax)
     r = np.zeros(P, dtype=np.int64)
     V, cv = np.zeros(P), np.zeros(P)
     ev = np.zeros((P, km))
     coef, ts = np.zeros((P, q + km)), np.zeros((P, q + km))
     xc, wc = _colmajor(x), _colmajor(w)
     ctx.check(ctx.lib.dfm_windows(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T,
-                                  xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[criterion], km,
+                                  xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[criterion],
+                                  int(kmax) if kmax else 0,
                                   r.ctypes.data_as(_lib.c_int64_p), _lib.ptr(V), _lib.ptr(cv), _lib.ptr(ev),
                                   _lib.ptr(coef), _lib.ptr(ts)))
     return {"window_rows": np.arange(T - P, T), "number_of_factors": r, "V": V,
@@ -608,14 +614,12 @@ def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions:
     x = _f64(x, 2)
     T, N = x.shape
     q, P = w.shape[1], int(num_predictions)
-    m = min(T - P, N)
-    km = int(kmax) if kmax else int(math.ceil(m / 2))
-    km = min(km, int(math.ceil(m / 2)))
     r = np.zeros(P, dtype=np.int64)
     pred, true = np.zeros(P), np.zeros(P)
     xc, wc = _colmajor(x), _colmajor(w)
     ctx.check(ctx.lib.dfm_windows_forecast(ctx.h, _lib.ptr(y), wc.ctypes.data_as(_lib.c_double_p), q, T,
-                                           xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[crit], km,
+                                           xc.ctypes.data_as(_lib.c_double_p), T, N, T, P, _CRIT_CODE[crit],
+                                           int(kmax) if kmax else 0,
                                            r.ctypes.data_as(_lib.c_int64_p), _lib.ptr(pred), _lib.ptr(true)))
     return pred, true
 

@@ -1442,6 +1442,7 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
                         int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
                         double *pred_out, double *true_out);
+#define LCKW(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(ctx, 1000 + (int)e_, "%s", hipGetErrorString(e_)); } while (0)
 
 extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                            const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
@@ -1473,22 +1474,30 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   const int n0 = T - P;
   const int orient = (N > T) ? 0 : 1;
   if (orient == 1 && N > n0) return fail(ctx, -2, "dfm_windows: windows straddle the T >= N / N > T branches");
-  const int mmin = std::min(n0, N);
-  if (kmax <= 0) kmax = (mmin + 1) / 2;
-  kmax = std::min(kmax, (mmin + 1) / 2);
-  if (kmax > 24 || q + kmax > 32) return fail(ctx, -20, "dfm_windows: kmax %d unsupported (<= 24)", kmax);
+  // window w sweeps k = 1..kmax_w, kmax_w = ceil(m_w / 2) (the IC-sweep
+  // constructor's default, src/DynamicFactorModel.jl:54) capped by the
+  // caller's kmax (D11); m_w = min(n0 + w, N) grows with the window
+  const int kreq = kmax;
+  auto kmax_w = [&](int wi) {
+    const int kd = (std::min(n0 + wi, N) + 1) / 2;
+    return kreq > 0 ? std::min(kreq, kd) : kd;
+  };
+  kmax = kmax_w(P - 1);   // the widest window's: row stride of eig_out / coef_out
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
+  const int m = orient == 0 ? T : N;
+  // kmax beyond the subspace block (or a design wider than 32): each window's
+  // sweep reads its full spectrum, the r_w eigenvectors come from the dense
+  // batched eigensolver (prefix blocks of H zero-padded to T x T for N > T)
+  const int p = eig_block_p(m, kmax, ctx->block);
+  const bool wide = p > 32 || p < kmax || q + kmax > 32;
+  if ((pcp || wide) && m > std::min(spectrum_any_max(), dense_eig_max()))
+    return fail(ctx, -31, "dfm_windows: PCp / kmax > 24 need each window's full spectrum: supported for "
+                          "min(T,N) <= %d", std::min(spectrum_any_max(), dense_eig_max()));
+  const int Pb = (p <= 16 || wide) ? 16 : 32;
   DevPanel dp;
   int rc = upload_panel(ctx, X, T, N, ldx, dp);
   if (rc) return rc;
-  const int m = orient == 0 ? T : N;
-  if (pcp && (orient == 0 ? T - 1 : N) > spectrum_any_max())
-    return fail(ctx, -31, "dfm_windows: PCp needs each window's full spectrum: supported for min(T,N) <= %d",
-                spectrum_any_max());
-  const int p = eig_block_p(m, kmax, ctx->block);
-  if (p > 32) return fail(ctx, -20, "block too wide");
-  const int Pb = p <= 16 ? 16 : 32;
   // host draws: identity + masks
   std::vector<int32_t> hidx((size_t)P * T);
   std::vector<double> heta((size_t)P * T);
@@ -1501,91 +1510,101 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   int32_t *didx = (int32_t *)dal(hidx.size() * 4);
   double *deta = (double *)dal(heta.size() * 8);
   double *dy = (double *)dal((size_t)T * 8), *dw = (double *)dal((size_t)T * std::max(q, 1) * 8);
-  double *lam = (double *)dal((size_t)P * kmax * 8), *Uk = (double *)dal((size_t)P * m * kmax * 8);
-  double *tr = (double *)dal((size_t)P * 8), *F = (double *)dal((size_t)P * T * kmax * 8);
-  double *coef = (double *)dal((size_t)P * (q + kmax) * 8), *tst = (double *)dal((size_t)P * (q + kmax) * 8);
+  double *tr = (double *)dal((size_t)P * 8);
   int *stt = (int *)dal((size_t)P * 4), *ost = (int *)dal((size_t)P * 4);
   int *dTn = (int *)dal((size_t)P * 4), *dkr = (int *)dal((size_t)P * 4);
-  char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
-  if (!didx || !deta || !dy || !dw || !lam || !Uk || !tr || !F || !coef || !tst || !stt || !ost || !dTn || !dkr || !ews)
+  if (!didx || !deta || !dy || !dw || !tr || !stt || !ost || !dTn || !dkr)
     return fail(ctx, 1002, "dfm_windows: out of device memory");
   HIPCHK(ctx, hipMemcpyAsync(didx, hidx.data(), hidx.size() * 4, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(deta, heta.data(), heta.size() * 8, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
   if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
-  double *H = nullptr, *pev = nullptr;   // pev: per-window full spectra (PCp), row stride pst
+  PanelSrc msrc{nullptr, dp.P, didx, deta, dp.ld, T};   // window w = rows < n0 + w of X
+  // ---- the windows' Grams: N > T one prefix Gram H; T >= N per-window G
+  double *H = nullptr, *G = nullptr;
   int64_t ldH = 0;
-  int pst = 0;
   if (orient == 0) {
     ldH = round_up(T, 16);
     H = (double *)dal((size_t)T * ldH * 8);
-    double *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
-    char *fws = (char *)dal(fact_workspace_bytes(T, P, Pb));
-    int *off = (int *)dal((size_t)P * (T + 1) * 4), *lst = (int *)dal((size_t)P * T * 4);
-    if (!H || !zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    if (!H) return fail(ctx, 1002, "dfm_windows: out of device memory");
     HIPCHK(ctx, hipMemsetAsync(H, 0, (size_t)T * ldH * 8, st));
-    HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
     PanelSrc es{nullptr, dp.P, nullptr, nullptr, dp.ld, 0};
-    {
-      Scope sc(ctx, DFM_KC_GRAM);
-      HIPCHK(ctx, launch_gram(0, es, T, N, T, H, ldH, 0, 1, st));   // ONE Gram for every window
-    }
-    rc = fact_precompute(dp.P, dp.ld, T, N, 0, nullptr, nullptr, H, ldH, zero, zero, zero, hd, st);
-    if (rc) return fail(ctx, rc, "precompute");
-    HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
-    FactBase fb{T, 0, ldH, zero, zero, zero, H, zero, hd};
-    if (pcp) {   // window w's Gram: the leading (n0 + w) x (n0 + w) block of H
-      const int mx = T - 1;
-      pev = (double *)dal((size_t)P * mx * 8);
-      double *pwk = spectrum_work(mx, P) > 0 ? (double *)dal((size_t)spectrum_work(mx, P) * 8) : nullptr;
-      if (!pev || (spectrum_work(mx, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
-      Scope sc(ctx, DFM_KC_EIG_OTHER);
-      HIPCHK(ctx, launch_spectrum_var(H, ldH, 0, mx, n0, 1, P, pev, pwk, st));
-      pst = mx;
-    }
-    rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
-                          lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
-    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-    Scope sc(ctx, DFM_KC_FACTORS);
-    hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kmax + 255) / 256), P), dim3(256), 0, st,
-                       Uk, T, kmax, n0, F);
+    Scope sc(ctx, DFM_KC_GRAM);
+    HIPCHK(ctx, launch_gram(0, es, T, N, T, H, ldH, 0, 1, st));   // ONE Gram for every window
   } else {
-    double *G = (double *)dal((size_t)P * N * N * 8), *Ld = (double *)dal((size_t)P * N * kmax * 8);
-    if (!G || !Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
-    PanelSrc src{nullptr, dp.P, didx, deta, dp.ld, T};
-    {
-      Scope sc(ctx, DFM_KC_GRAM);
-      HIPCHK(ctx, launch_gram(1, src, N, T, T, G, N, (int64_t)N * N, P, st));
-    }
-    if (pcp) {
-      pev = (double *)dal((size_t)P * N * 8);
-      double *pwk = spectrum_work(N, P) > 0 ? (double *)dal((size_t)spectrum_work(N, P) * 8) : nullptr;
-      if (!pev || (spectrum_work(N, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
-      Scope sc(ctx, DFM_KC_EIG_OTHER);
-      HIPCHK(ctx, launch_spectrum(G, N, (int64_t)N * N, N, P, pev, pwk, st));
-      pst = N;
-    }
-    rc = eig_run(G, N, (int64_t)N * N, N, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, lam, Uk,
-                 tr, stt, nullptr, st, timer_cb, ctx, 0);
-    if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-    Scope sc(ctx, DFM_KC_FACTORS);
-    launch_factors(1, src, T, N, kmax, P, Uk, F, Ld, nullptr, st);
+    G = (double *)dal((size_t)P * N * N * 8);
+    if (!G) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    Scope sc(ctx, DFM_KC_GRAM);
+    HIPCHK(ctx, launch_gram(1, msrc, N, T, T, G, N, (int64_t)N * N, P, st));
   }
-  // IC sweep per window on the host (arithmetic only), then OLS with each r_w
-  std::vector<double> hl((size_t)P * kmax), ht(P);
-  std::vector<int> hs(P);
-  HIPCHK(ctx, hipMemcpyAsync(hl.data(), lam, hl.size() * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(ht.data(), tr, (size_t)P * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hs.data(), stt, (size_t)P * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
-  for (int wi = 0; wi < P; ++wi)
-    if (hs[wi]) return fail(ctx, 2, "eigensolver did not converge for window %d", wi);
+  // ---- full spectra (PCp's sigma^2, and the whole sweep when wide)
+  double *pev = nullptr;   // P x pst
+  const int pst = orient == 0 ? T - 1 : N;
+  if (pcp || wide) {
+    pev = (double *)dal((size_t)P * pst * 8);
+    double *pwk = spectrum_work(pst, P) > 0 ? (double *)dal((size_t)spectrum_work(pst, P) * 8) : nullptr;
+    if (!pev || (spectrum_work(pst, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    Scope sc(ctx, DFM_KC_EIG_OTHER);
+    if (orient == 0) HIPCHK(ctx, launch_spectrum_var(H, ldH, 0, pst, n0, 1, P, pev, pwk, st));
+    else HIPCHK(ctx, launch_spectrum(G, N, (int64_t)N * N, N, P, pev, pwk, st));
+  }
   std::vector<double> hev;
-  if (pcp) {
+  if (pev) {
     hev.resize((size_t)P * pst);
     HIPCHK(ctx, hipMemcpyAsync(hev.data(), pev, hev.size() * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
   }
+  // ---- narrow: top-kmax pairs of every window by the batched subspace solver
+  int kv = kmax;   // eigenvectors kept per window (stride of F, Uk, lam, coef)
+  double *lam = nullptr, *Uk = nullptr, *F = nullptr;
+  std::vector<double> hl((size_t)P * kmax), ht(P);
+  if (!wide) {
+    lam = (double *)dal((size_t)P * kmax * 8); Uk = (double *)dal((size_t)P * m * kmax * 8);
+    F = (double *)dal((size_t)P * T * kmax * 8);
+    char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
+    if (!lam || !Uk || !F || !ews) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    if (orient == 0) {
+      double *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
+      char *fws = (char *)dal(fact_workspace_bytes(T, P, Pb));
+      int *off = (int *)dal((size_t)P * (T + 1) * 4), *lst = (int *)dal((size_t)P * T * 4);
+      if (!zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
+      rc = fact_precompute(dp.P, dp.ld, T, N, 0, nullptr, nullptr, H, ldH, zero, zero, zero, hd, st);
+      if (rc) return fail(ctx, rc, "precompute");
+      HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
+      FactBase fb{T, 0, ldH, zero, zero, zero, H, zero, hd};
+      rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
+                            lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
+      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      Scope sc(ctx, DFM_KC_FACTORS);
+      hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kmax + 255) / 256), P), dim3(256), 0,
+                         st, Uk, T, kmax, n0, F);
+    } else {
+      double *Ld = (double *)dal((size_t)P * N * kmax * 8);
+      if (!Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      rc = eig_run(G, N, (int64_t)N * N, N, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, lam, Uk,
+                   tr, stt, nullptr, st, timer_cb, ctx, 0);
+      if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      Scope sc(ctx, DFM_KC_FACTORS);
+      launch_factors(1, msrc, T, N, kmax, P, Uk, F, Ld, nullptr, st);
+    }
+    std::vector<int> hs(P);
+    HIPCHK(ctx, hipMemcpyAsync(hl.data(), lam, hl.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(ht.data(), tr, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hs.data(), stt, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (int wi = 0; wi < P; ++wi)
+      if (hs[wi]) return fail(ctx, 2, "eigensolver did not converge for window %d", wi);
+  } else {
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (int wi = 0; wi < P; ++wi) {   // eigenvalues and trace from the window's spectrum
+      const int mw = orient == 0 ? n0 + wi : N;
+      double s = 0.0;
+      for (int j = mw - 1; j >= 0; --j) s += hev[(size_t)wi * pst + j];
+      ht[wi] = s;
+      for (int j = 0; j < kmax; ++j) hl[(size_t)wi * kmax + j] = hev[(size_t)wi * pst + j];
+    }
+  }
+  // ---- IC sweep per window on the host (arithmetic only)
   std::vector<double> ic(7 * (size_t)kmax);
   for (int wi = 0; wi < P; ++wi) {
     const int n = n0 + wi;
@@ -1596,14 +1615,15 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
       for (int j = mw - 1; j >= h; --j) s += hev[(size_t)wi * pst + j];
       s2 = s / ((double)N * n);
     }
-    dfm_ic_sweep(&hl[(size_t)wi * kmax], kmax, kmax, ht[wi], n, N, s2, ic.data());
+    const int kw = kmax_w(wi);
+    dfm_ic_sweep(&hl[(size_t)wi * kmax], kw, kw, ht[wi], n, N, s2, ic.data());
     int best = 0;
-    for (int k = 1; k < kmax; ++k)
-      if (ic[(size_t)crit * kmax + k] < ic[(size_t)crit * kmax + best]) best = k;
+    for (int k = 1; k < kw; ++k)
+      if (ic[(size_t)crit * kw + k] < ic[(size_t)crit * kw + best]) best = k;
     hTn[wi] = n;
     hkr[wi] = best + 1;
     r_out[wi] = best + 1;
-    if (crit_out) crit_out[wi] = ic[(size_t)crit * kmax + best];
+    if (crit_out) crit_out[wi] = ic[(size_t)crit * kw + best];
     if (V_out) {
       double sacc = ht[wi];
       for (int j = 0; j <= best; ++j) sacc -= hl[(size_t)wi * kmax + j];
@@ -1613,20 +1633,87 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   if (eig_out) std::copy(hl.begin(), hl.end(), eig_out);
   HIPCHK(ctx, hipMemcpyAsync(dTn, hTn.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(dkr, hkr.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
-  {
-    Scope sc(ctx, DFM_KC_OLS);
-    launch_ols(P, st, dy, dw, q, F, T, kmax, dTn, dkr, coef, tst,
-                       nullptr, nullptr, ost);
+  // ---- wide: the r_w eigenvectors (kv = max_w r_w) and factors of every window
+  if (wide) {
+    kv = *std::max_element(hkr.begin(), hkr.end());
+    lam = (double *)dal((size_t)P * kv * 8); Uk = (double *)dal((size_t)P * m * kv * 8);
+    F = (double *)dal((size_t)P * T * kv * 8);
+    double *dwk = (double *)dal((size_t)P * dense_eig_work(m, kv) * 8);
+    if (!lam || !Uk || !F || !dwk) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    hipError_t e;
+    {
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      e = orient == 0 ? launch_dense_eig_batched(H, ldH, 0, T, n0, 1, P, kv, lam, Uk, tr, stt, dwk, st)
+                      : launch_dense_eig_batched(G, N, (int64_t)N * N, N, N, 0, P, kv, lam, Uk, tr, stt, dwk, st);
+    }
+    if (e != hipSuccess) return fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));
+    Scope sc(ctx, DFM_KC_FACTORS);
+    if (orient == 0) {
+      hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kv + 255) / 256), P), dim3(256), 0, st,
+                         Uk, T, kv, n0, F);
+    } else {
+      double *Ld = (double *)dal((size_t)P * N * kv * 8);
+      if (!Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      if (kv <= 32) {
+        launch_factors(1, msrc, T, N, kv, P, Uk, F, Ld, nullptr, st);
+      } else {
+        double *Xw = (double *)dal((size_t)P * T * dp.ld * 8);
+        if (!Xw) return fail(ctx, 1002, "dfm_windows: out of device memory");
+        HIPCHK(ctx, launch_materialize(msrc, T, N, dp.ld, P, Xw, st));
+        if (launch_factors_wide(1, Xw, dp.ld, T, N, kv, Uk, F, Ld, nullptr, st, (double)T, P, (int64_t)T * dp.ld,
+                                (int64_t)T * kv))
+          return fail(ctx, 1001, "factor kernels failed");
+      }
+    }
   }
-  if (coef_out) HIPCHK(ctx, hipMemcpyAsync(coef_out, coef, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
-  if (tstat_out) HIPCHK(ctx, hipMemcpyAsync(tstat_out, tst, (size_t)P * (q + kmax) * 8, hipMemcpyDeviceToHost, st));
+  // ---- OLS + HC2 of every window on [w F_{r_w}] over its rows
+  const int dv = q + kv;
+  double *coef = (double *)dal((size_t)P * dv * 8), *tst = (double *)dal((size_t)P * dv * 8);
+  if (!coef || !tst) return fail(ctx, 1002, "dfm_windows: out of device memory");
+  if (dv <= 32) {
+    Scope sc(ctx, DFM_KC_OLS);
+    launch_ols(P, st, dy, dw, q, F, T, kv, dTn, dkr, coef, tst, nullptr, nullptr, ost);
+  } else {   // per window: its own width q + r_w
+    const int dmax = q + kv;
+    double *owk = (double *)dal((size_t)ols_wide_work(T, dmax) * 8);
+    if (!owk) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    Scope sc(ctx, DFM_KC_OLS);
+    for (int wi = 0; wi < P; ++wi)
+      HIPCHK(ctx, launch_ols_wide_batched(1, dy, dw, q, F + (size_t)wi * T * kv, T, kv, hkr[wi], dTn + wi,
+                                          coef + (size_t)wi * dv, tst + (size_t)wi * dv, nullptr, nullptr, ost + wi,
+                                          owk, st));
+  }
+  {
+    std::vector<int> ho(P);
+    HIPCHK(ctx, hipMemcpyAsync(ho.data(), ost, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+    std::vector<int> hs2(P, 0);
+    if (wide) HIPCHK(ctx, hipMemcpyAsync(hs2.data(), stt, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (int wi = 0; wi < P; ++wi) {
+      if (hs2[wi]) return fail(ctx, 2, "dense eigensolver: window %d lost orthogonality", wi);
+      if (ho[wi]) return fail(ctx, 3, "singular design matrix in window %d", wi);
+    }
+  }
+  // outputs keep the q + kmax row stride of the header (NaN past q + r_w)
+  auto restride = [&](const double *dsrc, double *out) -> int {
+    std::vector<double> h((size_t)P * dv);
+    LCKW(hipMemcpyAsync(h.data(), dsrc, h.size() * 8, hipMemcpyDeviceToHost, st));
+    LCKW(hipStreamSynchronize(st));
+    const int dk = q + kmax;
+    for (int wi = 0; wi < P; ++wi)
+      for (int c = 0; c < dk; ++c)
+        out[(size_t)wi * dk + c] = (c < dv && c < q + hkr[wi]) ? h[(size_t)wi * dv + c] : NAN;
+    return 0;
+  };
+  if (coef_out && (rc = restride(coef, coef_out))) return rc;
+  if (tstat_out && (rc = restride(tst, tstat_out))) return rc;
   if (pred_out) {   // forecast step: predict row n = n0 + w from window w's fit
     double *rs = (double *)dal((size_t)T * 8), *ss = (double *)dal((size_t)T * 8);
     double *dp_ = (double *)dal((size_t)P * 8), *dt_ = (double *)dal((size_t)P * 8);
     if (!rs || !ss || !dp_ || !dt_) return fail(ctx, 1002, "dfm_windows: out of device memory");
     Scope sc(ctx, DFM_KC_MISC);
     hipLaunchKernelGGL(panel_row_sums_kernel, dim3(T), dim3(256), 0, st, dp.P, dp.ld, N, rs, ss);
-    hipLaunchKernelGGL(window_forecast_kernel, dim3(P), dim3(256), 0, st, orient, dp.P, dp.ld, T, N, n0, q, kmax, H,
+    hipLaunchKernelGGL(window_forecast_kernel, dim3(P), dim3(256), 0, st, orient, dp.P, dp.ld, T, N, n0, q, kv, H,
                        ldH, F, Uk, lam, rs, ss, dkr, coef, dy, dw, dp_, dt_);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(pred_out, dp_, (size_t)P * 8, hipMemcpyDeviceToHost, st));

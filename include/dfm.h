@@ -201,11 +201,14 @@ int dfm_chow_all(dfm_model *m, int64_t bp, double *LR, double *LM, double *Wald)
 /* ---------------------------------------------------- expanding windows
  * The refits of pseudo_out_of_sample_forecasts (src/utils.jl:54-72): window
  * w = 0..P-1 refits the IC-sweep constructor (src/DynamicFactorModel.jl:53)
- * on rows 0..T-P+w-1 with criterion crit (ICp1-3 or BIC) over k = 1..kmax.
- * N > T uses the prefix-Gram identity (one Gram for all windows).
- * Outputs per window: r (P), V(r) (P), criterion value (P), eigenvalues
- * (P x kmax, row-major), OLS coefficients and HC2 t-stats (P x (q + kmax),
- * row-major, NaN past q + r).  The forecast step: dfm_windows_forecast. */
+ * on rows 0..T-P+w-1 with criterion crit (any of the 7) over k = 1..kmax_w,
+ * kmax_w = ceil(min(T-P+w, N)/2) (the constructor's default, :54), capped by
+ * kmax when kmax > 0 (D11).  N > T uses the prefix-Gram identity (one Gram for
+ * all windows).  Outputs per window: r (P), V(r) (P), criterion value (P),
+ * eigenvalues (P x K, row-major), OLS coefficients and HC2 t-stats
+ * (P x (q + K), row-major, NaN past q + r), K = kmax_{P-1} =
+ * min(kmax, ceil(min(T-1, N)/2)) (kmax <= 0: no cap).  The forecast step:
+ * dfm_windows_forecast. */
 int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                 const double *X, int64_t T, int64_t N, int64_t ldx, int P, int crit,
                 int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,

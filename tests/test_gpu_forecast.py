@@ -36,3 +36,14 @@ def test_forecast_with_extra_regressor(dfm, oracle):
     po, to, _ = oracle.pseudo_out_of_sample_forecasts(
         lambda yy, ww, xx: oracle.DynamicFactorModel_ic(yy, ww, xx, "ICp2", kmax=5), y, w, x, P)
     assert np.max(np.abs(pred - po)) <= FCST_RTOL * np.max(np.abs(po))
+
+
+@pytest.mark.parametrize("T,N,P,crit", [(70, 160, 4, "ICp2"), (150, 60, 5, "PCp2")])
+def test_forecasts_default_kmax(dfm, oracle, T, N, P, crit):
+    """model_args = (criterion,) only: every window sweeps to its own ceil(m_w/2)."""
+    y, x, w = panel(oracle, T, N, 3, 4500 + T)
+    pred, true = dfm.pseudo_out_of_sample_forecasts(dfm.DynamicFactorModel, y, w, x, crit, num_predictions=P)
+    po, to, _ = oracle.pseudo_out_of_sample_forecasts(
+        lambda yy, ww, xx: oracle.DynamicFactorModel_ic(yy, ww, xx, crit), y, w, x, P)
+    assert np.array_equal(true, to)
+    assert np.max(np.abs(pred - po)) <= FCST_RTOL * np.max(np.abs(po))

@@ -365,13 +365,16 @@ def test_direct_and_factored_agree(dfm, oracle):
     assert rel(b[:, 4:], a[:, 4:]) < 1e-9
 
 
-@pytest.mark.parametrize("T,N,P,crit", [(60, 150, 6, "ICp2"), (90, 30, 5, "BIC"), (41, 300, 3, "ICp1"),
-                                        (60, 150, 6, "PCp2"), (200, 160, 4, "PCp1")])
-def test_expanding_window_refits(dfm, oracle, T, N, P, crit):
+@pytest.mark.parametrize("T,N,P,crit,kmax", [
+    (60, 150, 6, "ICp2", 6), (90, 30, 5, "BIC", 6), (41, 300, 3, "ICp1", 6),
+    (60, 150, 6, "PCp2", 6), (200, 160, 4, "PCp1", 6),
+    # the constructor's default kmax_w = ceil(m_w/2) per window (:54): 28..30
+    # for N > T (full spectra + dense eigenpairs), 20 / 35 for T >= N
+    (60, 150, 5, "ICp2", None), (140, 40, 6, "BIC", None), (200, 70, 4, "PCp2", None)])
+def test_expanding_window_refits(dfm, oracle, T, N, P, crit, kmax):
     """src/utils.jl:54-72 refit loop: each window = IC-sweep constructor on rows
     1..date_index-1 (N > T via the prefix-Gram identity)."""
     y, x, w = panel(oracle, T, N, 3, 3000 + T)
-    kmax = 6
     out = dfm.pseudo_out_of_sample_refits(y, w, x, crit, num_predictions=P, kmax=kmax)
     fits = oracle.expanding_window_refits(y, w, x, P, lambda yy, ww, xx: oracle.DynamicFactorModel_ic(
         yy, ww, xx, crit, kmax=kmax))
