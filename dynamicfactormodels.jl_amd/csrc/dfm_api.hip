@@ -31,6 +31,10 @@ int launch_factors_wide(int orient, const double *X, int64_t ld, int T, int N, i
                         double *F, double *L, double *colssr, hipStream_t st, double Ts, int nb = 1, int64_t sX = 0,
                         int64_t fstride = 0);
 hipError_t launch_materialize(const PanelSrc &src, int T, int N, int64_t ld, int nb, double *X, hipStream_t st);
+int64_t chow_wide_work(int T, int N, int r);
+hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, const double *E, int T, int N, int r,
+                            int bp, const double *F, int64_t sF, const double *L, int64_t sL, double *LR, double *LM,
+                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st);
 hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
                                    int k, const int *Tn, double *coef, double *tstat, double *cov_out,
                                    double *resid_out, int *status, double *work, hipStream_t st);
@@ -922,8 +926,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   const int P = (p <= 16 || wide) ? 16 : 32;
   if (wide && (M->m > dense_eig_max()))
     return fail(ctx, -20, "bootstrap at r=%d > 24 needs min(T,N) <= %d", r, dense_eig_max());
-  if (wide && chow && r > 16)
-    return fail(ctx, -7, "Chow statistics inside the bootstrap support r <= 16 (got %d)", r);
+  const bool chow_wide = chow && r > 16;   // GEMM-built Chow tests on materialised replicates
   // PCp reads each replicate's full spectrum, so its Gram is formed: direct path
   const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1 && !pcp && !wide;
   if (pcp && m > spectrum_any_max())
@@ -941,6 +944,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       double gbytes = (double)m * m * 8 * (pcp ? 3 : 1);
       if (wide)
         gbytes += 8.0 * ((double)dense_eig_work(m, r) + (double)T * M->ld + (double)ols_wide_work(T, q + r));
+      if (chow_wide) gbytes += 8.0 * ((double)chow_wide_work(T, N, r) + (double)T * M->ld + 3.0 * N);
       nb = (int64_t)std::max(1.0, std::min(4096.0, std::floor((wide ? 4e9 : 1.5e9) / gbytes)));
     }
     // equal batches (no small tail batch running the iterations half-empty)
@@ -967,7 +971,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     HIPCHK(ctx, hipStreamSynchronize(st));
     M->fact_ready = true;
   }
-  const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, nullptr, nullptr);
+  const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, nullptr, nullptr);
   if (need > M->ws_bytes) {
     hipFree(M->ws);
     M->ws = nullptr; M->ws_bytes = 0;
@@ -982,14 +986,18 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   if (ns) HIPCHK(ctx, hipMemcpyAsync(M->sd_dev, sd.data(), ns * sizeof(StatDesc), hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemsetAsync(M->flag_dev, 0, 4, st));
   BootWs w;
-  boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow, fact, &w, M->ws);
+  boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, &w, M->ws);
   // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
   // src/criteria.jl:18), its spectrum, sigma^2 per replicate
-  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls;
+  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc;
   if (wide) {
     HIPCHK(ctx, dalloc(&wDe.p, (size_t)nb * dense_eig_work(m, r)));
-    if (r > 32) HIPCHK(ctx, dalloc(&wX.p, (size_t)nb * T * M->ld));
     if (q + r > 32) HIPCHK(ctx, dalloc(&wOls.p, (size_t)nb * ols_wide_work(T, q + r)));
+  }
+  if (r > 32 || chow_wide) HIPCHK(ctx, dalloc(&wX.p, (size_t)nb * T * M->ld));
+  if (chow_wide) {
+    HIPCHK(ctx, dalloc(&wCh.p, (size_t)nb * chow_wide_work(T, N, r)));
+    HIPCHK(ctx, dalloc(&wSc.p, (size_t)3 * nb * N));
   }
   // top-r eigenpairs of n Grams (stride mm*mm): subspace iteration or dense
   auto eig_any = [&](const double *G, int mm, int n, const double *warm, double *lam, double *Uk, double *tr,
@@ -1112,15 +1120,23 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       }
       // single-variable Chow stats are served by a full pass too (cheap); they
       // are copied out of a scratch row afterwards.
-      HIPCHK(ctx, launch_chow(M->orient, src, T, N, r, chow_bp, n, w.F, w.L, LR, LM, WD, ostride,
-                              w.chow, w.chow_bytes, st));
+      const double *scr;
+      if (!chow_wide) {
+        HIPCHK(ctx, launch_chow(M->orient, src, T, N, r, chow_bp, n, w.F, w.L, LR, LM, WD, ostride,
+                                w.chow, w.chow_bytes, st));
+        // scratch rows live at the end of the chow workspace: [3][nb][N]
+        scr = (const double *)(w.chow + w.chow_bytes) - (size_t)3 * n * N;   // launch_chow's [3][n][N]
+      } else {
+        if (r <= 32) HIPCHK(ctx, launch_materialize(src, T, N, M->ld, n, wX.p, st));   // (r > 32: factors_any did)
+        HIPCHK(ctx, launch_chow_wide(n, wX.p, M->ld, (int64_t)T * M->ld, nullptr, T, N, r, chow_bp, w.F,
+                                     (int64_t)T * r, w.L, (int64_t)N * r, LR, LM, WD, ostride, wSc.p, wCh.p, st));
+        scr = wSc.p;
+      }
       for (int i = 0; i < ns; ++i) {
         if (sd[i].kind < DFM_STAT_LR || sd[i].kind > DFM_STAT_WALD) continue;
-        // scratch rows live at the end of the chow workspace: [3][nb][N]
-        const double *scr = (const double *)(w.chow + w.chow_bytes) - (size_t)3 * nb * N;
         const int which = sd[i].kind - DFM_STAT_LR;
         HIPCHK(ctx, hipMemcpy2DAsync(out + b0 * width + sd[i].off, (size_t)width * 8,
-                                     scr + ((size_t)which * nb) * N + sd[i].arg1, (size_t)N * 8, 8, n,
+                                     scr + ((size_t)which * n) * N + sd[i].arg1, (size_t)N * 8, 8, n,
                                      hipMemcpyDeviceToDevice, st));
       }
     }
@@ -1281,6 +1297,21 @@ int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald)
   if (bp < M->r || bp > M->T - M->r) return fail(ctx, -7, "break period %lld out of range", (long long)bp);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
+  if (M->r > 16) {   // any r: the GEMM-built tests (dfm_wide.hip)
+    DevBuf wk, sc3;
+    HIPCHK(ctx, dalloc(&wk.p, (size_t)chow_wide_work(M->T, M->N, M->r)));
+    HIPCHK(ctx, dalloc(&sc3.p, (size_t)3 * M->N));
+    {
+      Scope sc(ctx, DFM_KC_CHOW);
+      HIPCHK(ctx, launch_chow_wide(1, M->Xp, M->ld, 0, M->Ep, M->T, M->N, M->r, (int)bp, M->F, 0, M->L, 0, nullptr,
+                                   nullptr, nullptr, M->N, sc3.p, wk.p, st));
+    }
+    double *outs[3] = {LR, LM, Wald};
+    for (int i = 0; i < 3; ++i)
+      if (outs[i]) HIPCHK(ctx, hipMemcpyAsync(outs[i], sc3.p + (size_t)i * M->N, (size_t)M->N * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    return 0;
+  }
   const size_t bytes = chow_workspace_bytes(M->T, M->N, M->r, 1);
   char *ws = nullptr;
   HIPCHK(ctx, hipMalloc(&ws, bytes));

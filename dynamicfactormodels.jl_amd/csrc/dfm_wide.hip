@@ -300,4 +300,152 @@ hipError_t launch_ols_wide(const double *y, const double *w, int q, const double
   return launch_ols_wide_batched(1, y, w, q, F, T, k, k, nullptr, coef, tstat, cov_out, resid_out, status, work, st);
 }
 
+// ------------------------------------------------------------ wide Chow
+// LR / LM / Wald for every variable at any r (src/chowtest.jl:4-42), for nb
+// panels, built from strided GEMMs; every residual is formed explicitly, as
+// the reference's projections do (no ||x||^2 - b'A^-1 b cancellation):
+//   LR   : T (ln ||E_i||^2 - ln(SSR1_i + SSR2_i)), SSR_j from x_i on F_j (:4-23)
+//   LM   : T (1 - ||M_D E_i||^2 / ||E_i||^2), D = [F, F o d]           (:35-42)
+//   Wald : b2' [Q2 (sum_t u_ti^2 d_t d_t') Q2']^-1 b2, Q2 = rows r..2r-1 of
+//          inv(D'D): the HC0 block = sum_t u_ti^2 g_t g_t', g_t = Q2 d_t, all
+//          variables at once as (U o U)' [g_t (x) g_t]                  (:25-33)
+__global__ void copy_panel_kernel(const double *__restrict__ X, int64_t ld, int64_t sX, int T, int N,
+                                  double *__restrict__ Y) {
+  const int rep = blockIdx.y;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)T * N; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e / N), n = (int)(e % N);
+    Y[(int64_t)rep * T * N + e] = X[rep * sX + (int64_t)t * ld + n];
+  }
+}
+__global__ void col_ssq_batched_kernel(const double *__restrict__ Y, int T, int N, double *__restrict__ out) {
+  const int rep = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const double *Yr = Y + (int64_t)rep * T * N;
+  double s = 0.0;
+  for (int t = 0; t < T; ++t) { const double v = Yr[(int64_t)t * N + n]; s = fma(v, v, s); }
+  out[(int64_t)rep * N + n] = s;
+}
+__global__ void chow_design_kernel(const double *__restrict__ F, int64_t sF, int T, int r, int bp,
+                                   double *__restrict__ D) {
+  const int rep = blockIdx.y;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)T * 2 * r; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e / (2 * r)), c = (int)(e % (2 * r));
+    const double f = F[rep * sF + (int64_t)t * r + (c < r ? c : c - r)];
+    D[(int64_t)rep * T * 2 * r + e] = (c < r || t >= bp) ? f : 0.0;
+  }
+}
+__global__ void square_kernel(double *__restrict__ U, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) U[i] *= U[i];
+}
+__global__ void outer_rows_kernel(const double *__restrict__ Gm, int T, int r, double *__restrict__ Pm) {
+  const int rep = blockIdx.y;
+  const int64_t rr = (int64_t)r * r;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < (int64_t)T * rr; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e / rr), a = (int)((e % rr) / r), b = (int)(e % r);
+    const double *g = Gm + ((int64_t)rep * T + t) * r;
+    Pm[(int64_t)rep * T * rr + e] = g[a] * g[b];
+  }
+}
+// per (replicate, variable): LR, LM and the Wald quadratic form ||Linv b2||^2
+__global__ void chow_finish_kernel(int nb, int T, int N, int r, const double *__restrict__ eE,
+                                   const double *__restrict__ ssr, const double *__restrict__ vv,
+                                   const double *__restrict__ Bx, const double *__restrict__ Lt,
+                                   const int *__restrict__ cst, double *__restrict__ LR, double *__restrict__ LM,
+                                   double *__restrict__ WD, int64_t ostr, double *__restrict__ scr) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (int64_t)nb * N) return;
+  const int rep = (int)(g / N), i = (int)(g % N);
+  const double e2 = eE[g];
+  const double lr = T * (log(e2) - log(ssr[g]));
+  const double lm = T * (1.0 - vv[g] / e2);
+  const double *b2 = Bx + (int64_t)rep * 2 * r * N + (int64_t)r * N + i;   // rows r..2r-1, column i
+  const double *Li = Lt + g * r * r;                                        // Lt[p][a] = Linv[a][p]
+  double wd = 0.0;
+  for (int a = 0; a < r; ++a) {
+    double z = 0.0;
+    for (int p = 0; p <= a; ++p) z = fma(Li[(int64_t)p * r + a], b2[(int64_t)p * N], z);
+    wd = fma(z, z, wd);
+  }
+  if (cst[g]) wd = NAN;
+  if (LR) LR[rep * ostr + i] = lr;
+  if (LM) LM[rep * ostr + i] = lm;
+  if (WD) WD[rep * ostr + i] = wd;
+  if (scr) {
+    scr[g] = lr;
+    scr[(int64_t)nb * N + g] = lm;
+    scr[2 * (int64_t)nb * N + g] = wd;
+  }
+}
+
+int64_t chow_wide_work(int T, int N, int r) {   // doubles per panel
+  const int64_t TN = (int64_t)T * N, rN = (int64_t)r * N, rr = (int64_t)r * r;
+  return 2 * TN + 3 * (int64_t)N + 6 * rr + 2 * rN + 2 * (int64_t)T * r + 12 * rr + 6 * rN + (int64_t)T * r +
+         (int64_t)T * rr + 2 * (int64_t)N * rr + 8 + 2 * (int64_t)N;
+}
+
+// nb panels X + rep sX (T x ld row-major), factors F + rep sF (T x r), loadings
+// L + rep sL (N x r); E (the factor residuals, same layout as X) or nullptr
+// (then E = X - F L').  Outputs: rows rep * ostr of LR / LM / WD (any may be
+// null) and, if scr != nullptr, [3][nb][N] scratch rows.
+hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, const double *E, int T, int N, int r,
+                            int bp, const double *F, int64_t sF, const double *L, int64_t sL, double *LR, double *LM,
+                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st) {
+  const int64_t TN = (int64_t)T * N, rN = (int64_t)r * N, rr = (int64_t)r * r, r2 = 2 * (int64_t)r;
+  double *Eb = work, *R = Eb + nb * TN, *eE = R + nb * TN, *ssr = eE + (int64_t)nb * N, *vv = ssr + (int64_t)nb * N;
+  double *A1 = vv + (int64_t)nb * N, *A2 = A1 + nb * rr, *Lt1 = A2 + nb * rr, *Lt2 = Lt1 + nb * rr;
+  double *A1i = Lt2 + nb * rr, *A2i = A1i + nb * rr, *B1 = A2i + nb * rr, *C1 = B1 + nb * rN;
+  double *D = C1 + nb * rN, *DtD = D + nb * r2 * T, *LtD = DtD + nb * 4 * rr, *Di = LtD + nb * 4 * rr;
+  double *G = Di + nb * 4 * rr, *G2 = G + nb * r2 * N, *Bx = G2 + nb * r2 * N, *Gm = Bx + nb * r2 * N;
+  double *Pm = Gm + (int64_t)nb * T * r, *Sig = Pm + nb * (int64_t)T * rr, *LtS = Sig + nb * (int64_t)N * rr;
+  int *cst = (int *)(LtS + nb * (int64_t)N * rr);
+  const dim3 g1((unsigned)std::min<int64_t>(1024, (TN + 255) / 256), nb);
+  hipError_t e;
+#define GB(...) if ((e = gemm_batched(__VA_ARGS__)) != hipSuccess) return e
+  // ||E_i||^2
+  hipLaunchKernelGGL(copy_panel_kernel, g1, dim3(256), 0, st, E ? E : X, ld, sX, T, N, Eb);
+  if (!E) GB(nb, T, N, r, -1.0, F, r, 1, sF, L, 1, r, sL, 1.0, Eb, N, 1, TN, st);
+  hipLaunchKernelGGL(col_ssq_batched_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, st, Eb, T, N, eE);
+  // LR: x_i on F within each subperiod, residuals explicit
+  hipLaunchKernelGGL(copy_panel_kernel, g1, dim3(256), 0, st, X, ld, sX, T, N, R);
+  const int rows[2] = {bp, T - bp}, row0[2] = {0, bp};
+  double *Aj[2] = {A1, A2}, *Ltj[2] = {Lt1, Lt2}, *Aij[2] = {A1i, A2i};
+  for (int j = 0; j < 2; ++j) {
+    const double *Fj = F + (int64_t)row0[j] * r;
+    GB(nb, r, r, rows[j], 1.0, Fj, 1, r, sF, Fj, r, 1, sF, 0.0, Aj[j], r, 1, rr, st);
+    hipLaunchKernelGGL(chol_inv_kernel, dim3(nb), dim3(1024), 0, st, Aj[j], r, Ltj[j], (int *)nullptr);
+    GB(nb, r, r, r, 1.0, Ltj[j], r, 1, rr, Ltj[j], 1, r, rr, 0.0, Aij[j], r, 1, rr, st);
+    GB(nb, r, N, rows[j], 1.0, Fj, 1, r, sF, X + (int64_t)row0[j] * ld, ld, 1, sX, 0.0, B1, N, 1, rN, st);
+    GB(nb, r, N, r, 1.0, Aij[j], r, 1, rr, B1, N, 1, rN, 0.0, C1, N, 1, rN, st);
+    GB(nb, rows[j], N, r, -1.0, Fj, r, 1, sF, C1, N, 1, rN, 1.0, R + (int64_t)row0[j] * N, N, 1, TN, st);
+  }
+  hipLaunchKernelGGL(col_ssq_batched_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, st, R, T, N, ssr);
+  // D = [F, F o d], inv(D'D)
+  hipLaunchKernelGGL(chow_design_kernel, dim3((unsigned)std::min<int64_t>(1024, (T * r2 + 255) / 256), nb), dim3(256),
+                     0, st, F, sF, T, r, bp, D);
+  GB(nb, 2 * r, 2 * r, T, 1.0, D, 1, r2, r2 * T, D, r2, 1, r2 * T, 0.0, DtD, r2, 1, 4 * rr, st);
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(nb), dim3(1024), 0, st, DtD, 2 * r, LtD, (int *)nullptr);
+  GB(nb, 2 * r, 2 * r, 2 * r, 1.0, LtD, r2, 1, 4 * rr, LtD, 1, r2, 4 * rr, 0.0, Di, r2, 1, 4 * rr, st);
+  // LM: v = E - D inv(D'D) D'E
+  GB(nb, 2 * r, N, T, 1.0, D, 1, r2, r2 * T, Eb, N, 1, TN, 0.0, G, N, 1, r2 * N, st);
+  GB(nb, 2 * r, N, 2 * r, 1.0, Di, r2, 1, 4 * rr, G, N, 1, r2 * N, 0.0, G2, N, 1, r2 * N, st);
+  GB(nb, T, N, 2 * r, -1.0, D, r2, 1, r2 * T, G2, N, 1, r2 * N, 1.0, Eb, N, 1, TN, st);   // Eb := V
+  hipLaunchKernelGGL(col_ssq_batched_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, st, Eb, T, N, vv);
+  // Wald: beta = inv(D'D) D'x, U = X - D beta, HC0 block of every variable
+  GB(nb, 2 * r, N, T, 1.0, D, 1, r2, r2 * T, X, ld, 1, sX, 0.0, G, N, 1, r2 * N, st);
+  GB(nb, 2 * r, N, 2 * r, 1.0, Di, r2, 1, 4 * rr, G, N, 1, r2 * N, 0.0, Bx, N, 1, r2 * N, st);
+  hipLaunchKernelGGL(copy_panel_kernel, g1, dim3(256), 0, st, X, ld, sX, T, N, R);
+  GB(nb, T, N, 2 * r, -1.0, D, r2, 1, r2 * T, Bx, N, 1, r2 * N, 1.0, R, N, 1, TN, st);    // R := U
+  hipLaunchKernelGGL(square_kernel, dim3((unsigned)std::min<int64_t>(2048, (nb * TN + 255) / 256)), dim3(256), 0, st, R,
+                     nb * TN);
+  GB(nb, T, r, 2 * r, 1.0, D, r2, 1, r2 * T, Di + r * r2, 1, r2, 4 * rr, 0.0, Gm, r, 1, (int64_t)T * r, st);
+  hipLaunchKernelGGL(outer_rows_kernel, dim3((unsigned)std::min<int64_t>(2048, (T * rr + 255) / 256), nb), dim3(256),
+                     0, st, Gm, T, r, Pm);
+  GB(nb, N, (int)rr, T, 1.0, R, 1, N, TN, Pm, rr, 1, (int64_t)T * rr, 0.0, Sig, rr, 1, (int64_t)N * rr, st);
+  hipLaunchKernelGGL(chol_inv_kernel, dim3(nb * N), dim3(1024), 0, st, Sig, r, LtS, cst);
+  hipLaunchKernelGGL(chow_finish_kernel, dim3((unsigned)(((int64_t)nb * N + 255) / 256)), dim3(256), 0, st, nb, T, N,
+                     r, eE, ssr, vv, Bx, LtS, cst, LR, LM, WD, ostr, scr);
+#undef GB
+  return hipGetLastError();
+}
+
 }  // namespace dfm

@@ -166,3 +166,42 @@ def test_bootstrap_many_factors(dfm, oracle, T, N, r, crit, breaks):
                d.coefficients[0], d.t_stats[0]]
         assert rel(out[b, :5], ref[:5]) < STAT_RTOL
         assert rel(out[b, 5:], ref[5:]) < 1e-8
+
+
+# ------------------------------------------------ Chow tests at r > 16
+@pytest.mark.parametrize("T,N,r", [(160, 40, 20), (90, 150, 18)])
+def test_chow_all_many_factors(dfm, oracle, T, N, r):
+    y, x, w = panel(oracle, T, N, 2, 7900 + T, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, r)
+    o = oracle.DynamicFactorModel(y, w, x, r)
+    bp = T // 2
+    LR, LM, WD = dfm.chow_all(g, bp)
+    nv = min(N, 12)
+    ref = np.array([[oracle.LR_test(o, bp, i), oracle.LM_test(o, bp, i), oracle.Wald_test(o, bp, i)]
+                    for i in range(nv)])
+    # LR / LM are differences (of log SSRs, of 1 - R^2) from r = 18-20 column
+    # projections on 45-80 rows: both sides carry cond(F_j'F_j) eps -> 1e-8
+    assert rel(LR[:nv], ref[:, 0]) < 1e-8
+    assert rel(LM[:nv], ref[:, 1]) < 1e-8
+    assert rel(WD[:nv], ref[:, 2]) < 1e-8
+
+
+@pytest.mark.parametrize("r", [2, 20])
+def test_bootstrap_chow_batched(dfm, oracle, r):
+    """r = 2 (fused Chow kernels) and r = 20 (GEMM-built Chow on materialised
+    replicates), several batches with a short tail batch, all-variable and
+    single-variable forms."""
+    T, N = 150, 40
+    y, x, w = panel(oracle, T, N, 2, 7950, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, r)
+    g.set_batch(2)
+    o = oracle.DynamicFactorModel(y, w, x, r)
+    B, bp, i0 = 5, 70, 3
+    idx, eta = oracle.draw_wild(np.random.default_rng(6), B, T)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, B, [S.LR_all(bp), S.LM(bp, i0 + 1), S.Wald(bp, i0 + 1)], idx=idx, eta=eta)
+    for b in range(B):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]], r)
+        assert rel(out[b, :8], [oracle.LR_test(d, bp, i) for i in range(8)]) < 1e-9
+        assert rel(out[b, N], oracle.LM_test(d, bp, i0)) < 1e-9
+        assert rel(out[b, N + 1], oracle.Wald_test(d, bp, i0)) < 1e-8
