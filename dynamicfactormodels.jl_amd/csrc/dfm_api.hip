@@ -37,7 +37,11 @@ hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, con
                             double *WD, int64_t ostr, double *scr, double *work, hipStream_t st);
 hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
                                    int k, const int *Tn, double *coef, double *tstat, double *cov_out,
-                                   double *resid_out, int *status, double *work, hipStream_t st);
+                                   double *resid_out, int *status, double *work, hipStream_t st, int hc0 = 0);
+hipError_t launch_targeted_joint_wide(const double *y, const double *w, int q, const double *X, int64_t ld, int T,
+                                      int N, double cv, double *tx, uint8_t *mask, int *status, double *work,
+                                      hipStream_t st);
+int64_t targeted_joint_wide_work(int T, int q, int N, int64_t ld);
 int64_t ols_wide_work(int T, int d);
 hipError_t launch_ols_wide(const double *y, const double *w, int q, const double *F, int T, int k, double *coef,
                            double *tstat, double *cov_out, double *resid_out, int *status, double *work,
@@ -1340,7 +1344,7 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
   const int T = (int)T64, N = (int)N64;
   if (mode == DFM_TP_JOINT && q + N >= T)
     return fail(ctx, 3, "joint hard thresholding is singular for q + N >= T (defect D8); use PER_CANDIDATE");
-  if (mode == DFM_TP_JOINT && q + N > 64) return fail(ctx, -32, "JOINT mode supports q + N <= 64");
+
   if (mode == DFM_TP_PER_CANDIDATE && (q < 1 || q > 16)) return fail(ctx, -32, "PER_CANDIDATE needs 1 <= q <= 16");
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
@@ -1358,7 +1362,12 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
   HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
   if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
-  {
+  if (mode == DFM_TP_JOINT && q + N > 64) {   // any width: GEMM-built OLS with HC0 (dfm_wide.hip)
+    DevBuf wk;
+    HIPCHK(ctx, dalloc(&wk.p, (size_t)targeted_joint_wide_work(T, q, N, dp.ld)));
+    Scope sc(ctx, DFM_KC_MISC);
+    HIPCHK(ctx, launch_targeted_joint_wide(dy, dw, q, dp.P, dp.ld, T, N, crit_value, dt, dm, bad, wk.p, st));
+  } else {
     Scope sc(ctx, DFM_KC_MISC);
     HIPCHK(ctx, launch_targeted(mode, dy, dw, q, dp.P, dp.ld, T, N, crit_value, dt, dm, ws, wsb, st, bad));
   }

@@ -230,14 +230,15 @@ __global__ __launch_bounds__(1024) void chol_inv_kernel(double *__restrict__ Mb,
 // H1 = D inv(D'D), u_t, sigma2_t = u_t^2 / (1 - h_t), Ds = sigma2_t * D[t].
 __global__ void hc2_rows_kernel(const double *__restrict__ Db, const double *__restrict__ H1b,
                                 const double *__restrict__ y, const double *__restrict__ betab, int T, int d,
-                                const int *__restrict__ Tn, double *__restrict__ Dsb, double *__restrict__ resid) {
+                                const int *__restrict__ Tn, double *__restrict__ Dsb, double *__restrict__ resid,
+                                int hc0) {
   const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6), rep = blockIdx.y;
   if (t >= T) return;
   const int64_t o = ((int64_t)rep * T + t) * d;
   const double *Dt = Db + o, *Ht = H1b + o, *beta = betab + (int64_t)rep * d;
   const bool in = !Tn || t < Tn[rep];
   double fit = 0.0, h = 0.0;
-  for (int c = lane; c < d; c += 64) { fit = fma(Dt[c], beta[c], fit); h = fma(Ht[c], Dt[c], h); }
+  for (int c = lane; c < d; c += 64) { fit = fma(Dt[c], beta[c], fit); if (!hc0) h = fma(Ht[c], Dt[c], h); }
   fit = wave_sum(fit);
   h = wave_sum(h);
   const double u = y[t] - fit, s2 = in ? u * u / (1.0 - h) : 0.0;
@@ -247,7 +248,8 @@ __global__ void hc2_rows_kernel(const double *__restrict__ Db, const double *__r
 
 // coef / t rows of stride dstr (NaN past d), optional covariance (nb == 1)
 __global__ void ols_finish_kernel(const double *__restrict__ betab, const double *__restrict__ Sigb, int d, int dstr,
-                                  double *__restrict__ coef, double *__restrict__ tstat, double *__restrict__ cov) {
+                                  double *__restrict__ coef, double *__restrict__ tstat, double *__restrict__ cov,
+                                  int flip) {
   const int rep = blockIdx.y;
   const double *beta = betab + (int64_t)rep * d, *Sig = Sigb + (int64_t)rep * d * d;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < d * d; e += gridDim.x * 256) {
@@ -255,7 +257,7 @@ __global__ void ols_finish_kernel(const double *__restrict__ betab, const double
     if (cov) cov[(int64_t)c * d + a] = Sig[e];
     if (a == c) {
       coef[(int64_t)rep * dstr + a] = beta[a];
-      tstat[(int64_t)rep * dstr + a] = beta[a] / sqrt(Sig[e]);
+      tstat[(int64_t)rep * dstr + a] = beta[a] / sqrt(flip ? fabs(Sig[e]) : Sig[e]);
     }
   }
   for (int a = d + blockIdx.x * 256 + threadIdx.x; a < dstr; a += gridDim.x * 256) {
@@ -269,9 +271,11 @@ int64_t ols_wide_work(int T, int d) { return 3 * (int64_t)T * d + 6 * (int64_t)d
 // src/DynamicFactorModel.jl:40-48 for nb fits of any width d = q + k: F of
 // replicate rep at F + rep * T * kF (first k of kF columns), optional sample
 // sizes Tn; coef / tstat rows of stride q + kF; work: nb * ols_wide_work(T, d).
+// hc0: White (1980) HC0 meat instead of HC2 and negative variances flipped
+// (targeted_predictors, src/targeted_predictors.jl:13-24).
 hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
                                    int k, const int *Tn, double *coef, double *tstat, double *cov_out,
-                                   double *resid_out, int *status, double *work, hipStream_t st) {
+                                   double *resid_out, int *status, double *work, hipStream_t st, int hc0) {
   const int d = q + k, dstr = q + kF;
   const int64_t Td = (int64_t)T * d, dd = (int64_t)d * d;
   double *D = work, *H1 = D + nb * Td, *Ds = H1 + nb * Td, *DtD = Ds + nb * Td;
@@ -284,20 +288,47 @@ hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int
   hipLaunchKernelGGL(chol_inv_kernel, dim3(nb), dim3(1024), 0, st, DtD, d, Lt, status);
   gemm_batched(nb, d, d, d, 1.0, Lt, d, 1, dd, Lt, 1, d, dd, 0.0, Inv, d, 1, dd, st);      // Linv' Linv
   gemm_batched(nb, d, 1, d, 1.0, Inv, d, 1, dd, Dty, 1, 0, d, 0.0, beta, 1, 0, d, st);     // beta
-  gemm_batched(nb, T, d, d, 1.0, D, d, 1, Td, Inv, d, 1, dd, 0.0, H1, d, 1, Td, st);       // D inv(D'D)
+  if (!hc0) gemm_batched(nb, T, d, d, 1.0, D, d, 1, Td, Inv, d, 1, dd, 0.0, H1, d, 1, Td, st);   // D inv(D'D)
   hipLaunchKernelGGL(hc2_rows_kernel, dim3((T + 3) / 4, nb), dim3(256), 0, st, D, H1, y, beta, T, d, Tn, Ds,
-                     resid_out);
+                     resid_out, hc0);
   gemm_batched(nb, d, d, T, 1.0, D, 1, d, Td, Ds, d, 1, Td, 0.0, Meat, d, 1, dd, st);     // sum sigma2_t d_t d_t'
   gemm_batched(nb, d, d, d, 1.0, Meat, d, 1, dd, Inv, d, 1, dd, 0.0, Tmp, d, 1, dd, st);
   gemm_batched(nb, d, d, d, 1.0, Inv, d, 1, dd, Tmp, d, 1, dd, 0.0, Sig, d, 1, dd, st);
   hipLaunchKernelGGL(ols_finish_kernel, dim3((unsigned)std::min<int64_t>(64, (dd + 255) / 256), nb), dim3(256), 0,
-                     st, beta, Sig, d, dstr, coef, tstat, nb == 1 ? cov_out : nullptr);
+                     st, beta, Sig, d, dstr, coef, tstat, nb == 1 ? cov_out : nullptr, hc0);
   return hipGetLastError();
 }
 hipError_t launch_ols_wide(const double *y, const double *w, int q, const double *F, int T, int k, double *coef,
                            double *tstat, double *cov_out, double *resid_out, int *status, double *work,
                            hipStream_t st) {
-  return launch_ols_wide_batched(1, y, w, q, F, T, k, k, nullptr, coef, tstat, cov_out, resid_out, status, work, st);
+  return launch_ols_wide_batched(1, y, w, q, F, T, k, k, nullptr, coef, tstat, cov_out, resid_out, status, work, st,
+                                 0);
+}
+
+__global__ void tp_mask_kernel(const double *__restrict__ t, int q, int N, double cv, double *__restrict__ tx,
+                               uint8_t *__restrict__ mask) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const double v = t[q + i];
+  tx[i] = v;
+  mask[i] = fabs(v) > cv ? 1 : 0;
+}
+// JOINT hard thresholding at any width (src/targeted_predictors.jl:9-30):
+// OLS of y on [w x] with HC0, |diag| flip, |t_x| > cv.  X: row-major T x ld.
+hipError_t launch_targeted_joint_wide(const double *y, const double *w, int q, const double *X, int64_t ld, int T,
+                                      int N, double cv, double *tx, uint8_t *mask, int *status, double *work,
+                                      hipStream_t st) {
+  const int d = q + N, dstr = q + (int)ld;
+  double *coef = work, *tst = coef + dstr, *wk = tst + dstr;
+  hipError_t e = launch_ols_wide_batched(1, y, w, q, X, T, (int)ld, N, nullptr, coef, tst, nullptr, nullptr, status,
+                                         wk, st, 1);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tp_mask_kernel, dim3((N + 255) / 256), dim3(256), 0, st, tst, q, N, cv, tx, mask);
+  (void)d;
+  return hipGetLastError();
+}
+int64_t targeted_joint_wide_work(int T, int q, int N, int64_t ld) {
+  return 2 * (q + ld) + ols_wide_work(T, q + N);
 }
 
 // ------------------------------------------------------------ wide Chow

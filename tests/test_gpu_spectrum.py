@@ -205,3 +205,22 @@ def test_bootstrap_chow_batched(dfm, oracle, r):
         assert rel(out[b, :8], [oracle.LR_test(d, bp, i) for i in range(8)]) < 1e-9
         assert rel(out[b, N], oracle.LM_test(d, bp, i0)) < 1e-9
         assert rel(out[b, N + 1], oracle.Wald_test(d, bp, i0)) < 1e-8
+
+
+# ---------------------------------------- JOINT hard thresholding, q + N > 64
+@pytest.mark.parametrize("T,N,q", [(400, 150, 3), (260, 200, 5)])
+def test_targeted_joint_wide(dfm, oracle, T, N, q):
+    rng = np.random.default_rng(8000 + N)
+    y, x, *_ = oracle.factor_model_DGP(T, N, 4, rng)
+    x = oracle.normalize(x)
+    w = np.hstack([np.ones((T, 1)), rng.standard_normal((T, q - 1))])
+    mask, t = dfm.targeted_predictors(y, w, x, return_tstats=True)
+    to, mo = oracle.targeted_predictors_hard(y, w, x, mode="joint")
+    assert rel(t, to) < 1e-8
+    # the mask may differ only where |t| sits within rounding of the critical value
+    cv = oracle.sps.t.ppf(0.975, T - q - N) if hasattr(oracle, "sps") else None
+    diff = np.flatnonzero(mask != mo)
+    if cv is not None:
+        assert np.all(np.abs(np.abs(to[diff]) - cv) < 1e-8 * cv)
+    else:
+        assert diff.size == 0
