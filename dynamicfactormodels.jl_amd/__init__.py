@@ -9,7 +9,8 @@ exported Julia API (``src/DynamicFactorModels.jl:16-20``).  Import it through
 the repo-root helper ``dfm_pkg.load()`` (the directory name contains a dot).
 """
 from .host import (normalize, factor_model_DGP, draw_wild, draw_wild_fast, draw_residual,
-                   t_quantile, glmnet_default_folds)
+                   t_quantile, glmnet_default_folds, lag_vector, lag_matrix, norm_vector, norm_matrix,
+                   possemidef, read_panel_csv, reference_test_design)
 from .api import (Context, DFMError, Stat, DynamicFactorModel, DynamicFactorModelResult,
                   calculate_factors, principal_components, gram_spectrum, calculate_criterion,
                   factor_residual_variance, criterion_value, wild_bootstrap, residual_bootstrap,

@@ -98,3 +98,85 @@ def t_quantile(p: float, df: float) -> float:
     """``quantile(TDist(df), p)`` (``src/targeted_predictors.jl:27``)."""
     from scipy import stats
     return float(stats.t.ppf(p, df))
+
+
+# --------------------------------------------------------------- data input
+def lag_vector(vec) -> np.ma.MaskedArray:
+    """``src/utils.jl:5-10``: the one-period lag [0, vec[1:end-1]] with the
+    first entry missing (a DataArray NA there; a masked entry here).  A masked
+    input keeps its mask shifted along."""
+    v = np.ma.asarray(vec, dtype=np.float64)
+    out = np.ma.empty(v.shape, dtype=np.float64)
+    out[0] = 0.0
+    out[1:] = v[:-1]
+    mask = np.zeros(v.shape, dtype=bool)
+    mask[0] = True
+    mask[1:] = np.ma.getmaskarray(v)[:-1]
+    out.mask = mask
+    return out
+
+
+def lag_matrix(matr) -> np.ma.MaskedArray:
+    """``src/utils.jl:11-16``: lag_vector applied to every column."""
+    m = np.ma.asarray(matr, dtype=np.float64)
+    return np.ma.column_stack([lag_vector(m[:, c]) for c in range(m.shape[1])])
+
+
+def norm_vector(vec) -> np.ndarray:
+    """``src/utils.jl:43``: vec ./ norm(vec)."""
+    v = np.asarray(vec, dtype=np.float64)
+    return v / np.linalg.norm(v)
+
+
+def norm_matrix(mat) -> np.ndarray:
+    """``src/utils.jl:44``: mapslices(norm_vector, mat, 2) — every ROW scaled to
+    unit norm (slices along dimension 2, as the code does; its comment says
+    columns)."""
+    m = np.asarray(mat, dtype=np.float64)
+    return m / np.linalg.norm(m, axis=1, keepdims=True)
+
+
+def possemidef(x) -> bool:
+    """``src/utils.jl:46-51``: whether the Cholesky factorisation succeeds."""
+    try:
+        np.linalg.cholesky(np.asarray(x, dtype=np.float64))
+        return True
+    except np.linalg.LinAlgError:
+        return False
+
+
+def read_panel_csv(path: str):
+    """The data load of ``test/DynamicFactorModel.jl:6-7``: ``readtable`` of a
+    CSV whose first column is the date / id and whose other columns are the
+    series; returns (series names, T x (columns-1) float64 matrix).  Missing
+    values raise, as ``convert(Array{Float64}, col)`` does on an NA."""
+    import csv
+    with open(path, newline="") as fh:
+        rows = list(csv.reader(fh))
+    header, body = rows[0], [r for r in rows[1:] if r]
+    names = [h.strip() for h in header[1:]]
+    data = np.empty((len(body), len(names)))
+    for t, row in enumerate(body):
+        if len(row) != len(header):
+            raise ValueError(f"row {t + 2}: {len(row)} fields, expected {len(header)}")
+        for c, cell in enumerate(row[1:]):
+            cell = cell.strip()
+            if cell in ("", "NA", "NaN", "nan"):
+                raise ValueError(f"missing value in column {names[c]!r}, row {t + 2}")
+            data[t, c] = float(cell)
+    return names, data
+
+
+def reference_test_design(data_matrix, nlags: int = 4):
+    """``test/DynamicFactorModel.jl:8-20``: y = the first series, x = the
+    others, w = [1, y_{t-1}, ..., y_{t-nlags}] built with lag_vector, and the
+    first nlags rows (whose lags are missing) dropped.  Returns (y, w, x)."""
+    d = np.asarray(data_matrix, dtype=np.float64)
+    T = d.shape[0] - nlags
+    y_full, x_full = d[:, 0], d[:, 1:]
+    lags, cur = [], y_full
+    for _ in range(nlags):
+        cur = lag_vector(cur)
+        lags.append(cur)
+    w = np.column_stack([np.ones(T)] + [np.ma.getdata(l)[nlags:] for l in lags])
+    return y_full[nlags:].copy(), w, x_full[nlags:].copy()

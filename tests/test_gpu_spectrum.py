@@ -224,3 +224,25 @@ def test_targeted_joint_wide(dfm, oracle, T, N, q):
         assert np.all(np.abs(np.abs(to[diff]) - cv) < 1e-8 * cv)
     else:
         assert diff.size == 0
+
+
+def test_reference_test_workflow_from_csv(dfm, oracle, tmp_path):
+    """test/DynamicFactorModel.jl end to end: readtable of a panel CSV, y = the
+    first series, 4 lags of y in w, the 3-argument constructor (r = ceil(m/2)),
+    sum(model.factor_residuals.^2)."""
+    rng = np.random.default_rng(88)
+    _, x0, *_ = oracle.factor_model_DGP(160, 61, 3, rng)
+    data = oracle.normalize(x0)
+    p = tmp_path / "1959-2014_normalized.csv"
+    with open(p, "w") as fh:
+        fh.write("date," + ",".join(f"V{i}" for i in range(61)) + "\n")
+        for t in range(160):
+            fh.write(f"d{t}," + ",".join(repr(float(v)) for v in data[t]) + "\n")
+    _, d = dfm.read_panel_csv(str(p))
+    y, w, x = dfm.reference_test_design(d, 4)
+    g = dfm.DynamicFactorModel(y, w, x)
+    o = oracle.DynamicFactorModel(y, w, x)
+    assert g.number_of_factors == o.number_of_factors == 30
+    ssr_g, ssr_o = np.sum(g.factor_residuals ** 2), np.sum(o.factor_residuals ** 2)
+    assert abs(ssr_g - ssr_o) <= 1e-10 * ssr_o
+    assert rel(g.t_stats[:5], o.t_stats[:5]) < 1e-8       # intercept and lags: sign-invariant
