@@ -174,12 +174,13 @@ def main():
     gemm_ms, gemm_n = timing.get("gemm", (0.0, 0))
     roof = None
     if gemm_n:
-        # factored path: every eigen-iteration of a batch is one GEMM
+        # factored path: every product of the eigen-iteration (two per
+        # Rayleigh-Ritz step with the degree-2 Chebyshev filter) is one GEMM
         # H (T x T) . Z (T x nb*P).  Algorithmic flop = 2 T^2 P per replicate
         # still unconverged when the GEMM runs (converged replicates' column
         # blocks are skipped), summed by the library over the timed region.
         P = 16
-        flop_total = 2.0 * T * T * P * eig["replicate_iterations"]
+        flop_total = 2.0 * T * T * P * eig["gemm_products"]
         per_launch_ms = gemm_ms / gemm_n
         achieved = flop_total / (gemm_ms * 1e-3) / 1e12
         roof = {"kernel": "gemmh_kernel (batched eigen-iteration H.Z: LDS-DMA 4-deep ring, v_mfma_f64_4x4x4_4b)",
@@ -188,7 +189,7 @@ def main():
                 "traffic": pmc_traffic("gemmh_kernel_t<4, 2, false>"),
                 "avg_launch_ms": round(per_launch_ms, 4),
                 "flop_per_launch": round(flop_total / gemm_n), "launches": gemm_n,
-                "flop_per_replicate_iteration": 2 * T * T * P}
+                "flop_per_replicate_product": 2 * T * T * P}
     elif gram_n:
         per_launch_ms = gram_ms / gram_n
         reps_per_launch = Bn * args.steps / gram_n
@@ -216,6 +217,8 @@ def main():
         "stopping_rule": "eigenvector residual (strict)" if args.strict else
                          "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
         "eig_iterations": eig,
+        "eig_filter": ("subspace iteration" if os.environ.get("DFM_CHEB") == "1" else
+                       "degree-2 Chebyshev filter on [0, theta_p] between Rayleigh-Ritz steps"),
         "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -37,6 +37,7 @@ SIGNATURES = [
     ("dfm_ctx_reset_timing", C.c_int, [C.c_void_p]),
     ("dfm_ctx_eig_stats", C.c_int, [C.c_void_p, c_int64_p, c_int64_p, c_int64_p]),
     ("dfm_ctx_rep_iters", C.c_int, [C.c_void_p, c_int64_p]),
+    ("dfm_ctx_gemm_products", C.c_int, [C.c_void_p, c_int64_p]),
     ("dfm_ctx_set_value_tol", C.c_int, [C.c_void_p, C.c_double]),
     ("dfm_kernel_class_name", C.c_char_p, [C.c_int]),
     ("dfm_pca", C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,

@@ -90,10 +90,11 @@ class Context:
     def eig_stats(self):
         b, t, m = C.c_int64(), C.c_int64(), C.c_int64()
         self.check(self.lib.dfm_ctx_eig_stats(self.h, C.byref(b), C.byref(t), C.byref(m)))
-        ri = C.c_int64()
+        ri, gp = C.c_int64(), C.c_int64()
         self.check(self.lib.dfm_ctx_rep_iters(self.h, C.byref(ri)))
+        self.check(self.lib.dfm_ctx_gemm_products(self.h, C.byref(gp)))
         return {"batches": b.value, "iterations": t.value, "max_iterations": m.value,
-                "replicate_iterations": ri.value}
+                "replicate_iterations": ri.value, "gemm_products": gp.value}
 
     def close(self):
         if getattr(self, "h", None) and not _lib.shutting_down():

@@ -23,6 +23,7 @@ size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
 extern int g_last_iters;
 extern int64_t g_last_rep_iters;
+extern int64_t g_last_gemm_products;
 int spectrum_max();
 int spectrum_any_max();
 int64_t spectrum_work(int m, int nb);
@@ -127,7 +128,7 @@ struct dfm_ctx {
   hipEvent_t cur_a[DFM_KC_COUNT] = {};
   double ms[DFM_KC_COUNT] = {};
   int64_t launches[DFM_KC_COUNT] = {};
-  int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0, rep_iters = 0;
+  int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0, rep_iters = 0, gemm_products = 0;
 };
 
 struct dfm_model {
@@ -301,7 +302,7 @@ int dfm_ctx_reset_timing(dfm_ctx *ctx) {
   if (!ctx) return -1;
   harvest(ctx);
   for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
-  ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = ctx->rep_iters = 0;
+  ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = ctx->rep_iters = ctx->gemm_products = 0;
   return 0;
 }
 int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max) {
@@ -316,6 +317,12 @@ static void note_iters(dfm_ctx *ctx) {
   ctx->eig_iters += g_last_iters;
   ctx->eig_iters_max = std::max<int64_t>(ctx->eig_iters_max, g_last_iters);
   ctx->rep_iters += g_last_rep_iters;
+  ctx->gemm_products += g_last_gemm_products;
+}
+int dfm_ctx_gemm_products(dfm_ctx *ctx, int64_t *products) {
+  if (!ctx || !products) return -1;
+  *products = ctx->gemm_products;
+  return 0;
 }
 int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters) {
   if (!ctx || !rep_iters) return -1;

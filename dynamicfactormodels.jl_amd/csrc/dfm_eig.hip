@@ -629,6 +629,16 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 // from the (nearly) rotated basis, so the inner sweeps accumulate across outer
 // iterations, and the residual test of check_converged includes any leftover
 // off-diagonal coupling.  DFM_JACOBI_SWEEPS overrides (development).
+// Filter degree of the factored bootstrap iteration: 1 = subspace (power)
+// iteration, 2 = degree-2 Chebyshev filter (boot_cheb_kernel).  DFM_CHEB
+// overrides (development A/B).
+static int cheb_degree() {
+  static const int d = [] {
+    const char *e = getenv("DFM_CHEB");
+    return e ? atoi(e) : 2;
+  }();
+  return d;
+}
 static int jacobi_sweeps() {
   static const int n = [] { const char *e = getenv("DFM_JACOBI_SWEEPS"); return e ? atoi(e) : 2; }();
   return n;
@@ -638,6 +648,7 @@ int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored
 // the H.Z GEMM in the factored solver) that still had an unconverged
 // replicate: the algorithmic work the roofline figure is priced on.
 int64_t g_last_rep_iters = 0;
+int64_t g_last_gemm_products = 0;   // replicate-products H . Z of the last factored run (both Chebyshev GEMMs)
 
 // Sum of the unconverged-replicate counts seen by the products of iterations
 // 0..last (shift = 1: the product of iteration it runs before that
@@ -699,6 +710,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   (void)finished;
   g_last_iters = it;
   g_last_rep_iters = count_rep_iters(w.active, std::min(it, maxit - 1), 0, nb, st);
+  g_last_gemm_products = g_last_rep_iters;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -993,6 +1005,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     g_last_iters = it;
   }
   g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
+  g_last_gemm_products = g_last_rep_iters;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -1251,161 +1264,16 @@ DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init,
   }
 }
 
-// ap2: one workgroup per replicate.  init = 1: Qn := Q (the warm start), no
-// Ritz step.  Qn goes to global memory (over the Y rows this wave just read)
-// and is gathered back through the CSR after the barrier: same-CU L1, so the
-// workgroup-scope fence of __syncthreads makes it visible.  Dynamic LDS:
-// eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
+// Shared tail of ap2 and the Chebyshev step: Z = P' D Qn by CSR gather
+// (bucket s lists t ascending), cc = EL' Z, and the fixed-order wave sums of
+// a = F' Qn (aacc, accumulated by the caller) and cc into ab[rep].
 template <int P>
-// 4 workgroups per CU (see boot_y2_kernel)
-__global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
-                                                       int it, int init, int last,
-                                                       const double *__restrict__ eta,
-                                                       const int *__restrict__ off, const int *__restrict__ lst,
-                                                       const double *__restrict__ Qc, double *__restrict__ Yq,
-                                                       double *__restrict__ Zc, int64_t ldz,
-                                                       double *__restrict__ ab, uint64_t seed) {
-  constexpr int NT = P / 16, KP = P / 4;
-  const int rep = blockIdx.x;
-  if (!init && w.done[rep]) return;
-  extern __shared__ double sdyn[];
-  double *set = sdyn;                          // eta_t
-  int *so = (int *)(sdyn + T), *sl = so + T + 1;
-  __shared__ double sred[NT * 256];
-  __shared__ double sres[4][P];
-  __shared__ int s_conv;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
+                           const double *set, const int *so, const int *sl, const double *Qn,
+                           double *__restrict__ Zc, int64_t ldz, int rep, double *__restrict__ ab,
+                           const dv4 *aacc, double *sred) {
+  constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
-  {
-    const double *et = eta ? eta + (int64_t)rep * T : nullptr;
-    const int *o = off + (int64_t)rep * (T + 1);
-    const int *L = lst + (int64_t)rep * T;
-    for (int e = tid; e < T; e += 256) { set[e] = et ? et[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
-    if (tid == 0) so[T] = o[T];
-  }
-  double *small = w.small + (int64_t)rep * small_stride<P>();
-  double bAm[KP][NT], bBm[KP][NT], th[NT];
-  bool dd[NT];
-#pragma unroll
-  for (int ct = 0; ct < NT; ++ct) {
-    const int c = 16 * ct + li;
-    th[ct] = init ? 0.0 : small[2 * P * P + c];
-    dd[ct] = init ? false : (small[2 * P * P + P + c] != 0.0);
-#pragma unroll
-    for (int kk = 0; kk < KP; ++kk) {
-      bAm[kk][ct] = init ? 0.0 : small[(4 * kk + lk) * P + c];
-      bBm[kk][ct] = init ? 0.0 : small[P * P + (4 * kk + lk) * P + c];
-    }
-  }
-  const double *Qr = Qc + (int64_t)rep * T * P;
-  double *Yr = Yq + (int64_t)rep * T * P;
-  double res2[NT];
-  dv4 aacc[NT];
-#pragma unroll
-  for (int ct = 0; ct < NT; ++ct) { res2[ct] = 0.0; aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; }
-  const int ntile = (T + 15) >> 4;
-  // each tile's operands load at the top of its iteration (occupancy hides the latency)
-  Ap2Tile<P> cur;
-  for (int tile = wave; tile < ntile; tile += 4) {
-    ap2_load<P>(cur, tile, T, r, lane, init, Qr, Yr, fb);
-    const int t0 = tile * 16;
-    double qv[NT][4];
-    if (init) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) qv[ct][g] = (t0 + 4 * g + lk < T) ? cur.q[ct][g] : 0.0;
-    } else {
-      dv4 u[NT], ya[NT], qn[NT];
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) { u[ct] = dv4{0.0, 0.0, 0.0, 0.0}; ya[ct] = u[ct]; qn[ct] = u[ct]; }
-#pragma unroll
-      for (int kk = 0; kk < KP; ++kk)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          u[ct] = mfma16(cur.qa[kk], bAm[kk][ct], u[ct]);
-          ya[ct] = mfma16(cur.yo[kk], bAm[kk][ct], ya[ct]);
-          qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
-        }
-      // every wave reads only its own tiles' Y rows, loaded (above) before
-      // these stores: Qn may overwrite this tile's Y rows
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int t = t0 + 4 * g + lk;
-        const bool v = t < T;
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          const int c = 16 * ct + li;
-          const double wr = ya[ct][g] - th[ct] * u[ct][g];
-          if (v && c < k) res2[ct] = fma(wr, wr, res2[ct]);
-          double q = qn[ct][g];
-          if (c < p && dd[ct]) q = hash_unit(seed, t, 1000003ull * (it + 1) + c);
-          if (c >= p || !v) q = 0.0;
-          qv[ct][g] = q;
-          if (v) Yr[(int64_t)t * P + c] = q;
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(cur.fa[g], qv[ct][g], aacc[ct]);
-  }
-  // residuals: sum over the 4 row-lanes of a column, then over waves (fixed order)
-  if (!init) {
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      double v = res2[ct];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lk == 0) sres[wave][16 * ct + li] = v;
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    int conv = 0;
-    if (!init) {
-      if (lane < P) sres[0][lane] = ((sres[0][lane] + sres[1][lane]) + sres[2][lane]) + sres[3][lane];
-      __builtin_amdgcn_wave_barrier();
-      const int itc = it + 1;
-      const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
-      double *next = small + 2 * P * P + 2 * P + (itc & 1) * P;
-      conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc) ? 1 : 0;
-    }
-    if (lane == 0) {
-      s_conv = conv;
-      if (conv) { w.done[rep] = 1; w.iters[rep] = it + 1; }
-      else if (!init) atomicAdd(&w.active[it], 1);
-    }
-  }
-  __syncthreads();
-  if (!init && (s_conv || last)) {
-    // Ritz vectors U = Q A for the final output (eig_final_kernel)
-    double *Ur = w.U + (int64_t)rep * T * P;
-    for (int tile = wave; tile < ntile; tile += 4) {
-      const int t0 = tile * 16, ta = t0 + li;
-      dv4 u[NT];
-#pragma unroll
-      for (int ct = 0; ct < NT; ++ct) u[ct] = dv4{0.0, 0.0, 0.0, 0.0};
-      double qa[KP];
-#pragma unroll
-      for (int kk = 0; kk < KP; ++kk) qa[kk] = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
-#pragma unroll
-      for (int kk = 0; kk < KP; ++kk)
-#pragma unroll
-        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa[kk], bAm[kk][ct], u[ct]);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int t = t0 + 4 * g + lk;
-        if (t < T)
-#pragma unroll
-          for (int ct = 0; ct < NT; ++ct) Ur[(int64_t)t * P + 16 * ct + li] = u[ct][g];
-      }
-    }
-    return;
-  }
-  // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
-  const double *Qn = init ? Qr : Yr;
   dv4 cacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) cacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
@@ -1485,6 +1353,291 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   }
 }
 
+// ap2: one workgroup per replicate.  init = 1: Qn := Q (the warm start), no
+// Ritz step.  Qn goes to global memory (over the Y rows this wave just read)
+// and is gathered back through the CSR after the barrier: same-CU L1, so the
+// workgroup-scope fence of __syncthreads makes it visible.  Dynamic LDS:
+// eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
+template <int P>
+// 4 workgroups per CU (see boot_y2_kernel)
+__global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
+                                                       int it, int init, int last, int cheb,
+                                                       const double *__restrict__ eta,
+                                                       const int *__restrict__ off, const int *__restrict__ lst,
+                                                       const double *__restrict__ Qc, double *__restrict__ Yq,
+                                                       double *__restrict__ Zc, int64_t ldz,
+                                                       double *__restrict__ ab, uint64_t seed) {
+  constexpr int NT = P / 16, KP = P / 4;
+  const int rep = blockIdx.x;
+  if (!init && w.done[rep]) return;
+  extern __shared__ double sdyn[];
+  double *set = sdyn;                          // eta_t
+  int *so = (int *)(sdyn + T), *sl = so + T + 1;
+  __shared__ double sred[NT * 256];
+  __shared__ double sres[4][P];
+  __shared__ int s_conv;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  {
+    const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+    const int *o = off + (int64_t)rep * (T + 1);
+    const int *L = lst + (int64_t)rep * T;
+    for (int e = tid; e < T; e += 256) { set[e] = et ? et[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
+    if (tid == 0) so[T] = o[T];
+  }
+  double *small = w.small + (int64_t)rep * small_stride<P>();
+  double bAm[KP][NT], bBm[KP][NT], th[NT];
+  bool dd[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) {
+    const int c = 16 * ct + li;
+    th[ct] = init ? 0.0 : small[2 * P * P + c];
+    dd[ct] = init ? false : (small[2 * P * P + P + c] != 0.0);
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) {
+      bAm[kk][ct] = init ? 0.0 : small[(4 * kk + lk) * P + c];
+      bBm[kk][ct] = init ? 0.0 : small[P * P + (4 * kk + lk) * P + c];
+    }
+  }
+  const double *Qr = Qc + (int64_t)rep * T * P;
+  double *Yr = Yq + (int64_t)rep * T * P;
+  double res2[NT];
+  dv4 aacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) { res2[ct] = 0.0; aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; }
+  const int ntile = (T + 15) >> 4;
+  // each tile's operands load at the top of its iteration (occupancy hides the latency)
+  Ap2Tile<P> cur;
+  for (int tile = wave; tile < ntile; tile += 4) {
+    ap2_load<P>(cur, tile, T, r, lane, init, Qr, Yr, fb);
+    const int t0 = tile * 16;
+    double qv[NT][4];
+    if (init) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) qv[ct][g] = (t0 + 4 * g + lk < T) ? cur.q[ct][g] : 0.0;
+    } else {
+      dv4 u[NT], ya[NT], qn[NT], qb[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) { u[ct] = dv4{0.0, 0.0, 0.0, 0.0}; ya[ct] = u[ct]; qn[ct] = u[ct]; qb[ct] = u[ct]; }
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          u[ct] = mfma16(cur.qa[kk], bAm[kk][ct], u[ct]);
+          ya[ct] = mfma16(cur.yo[kk], bAm[kk][ct], ya[ct]);
+          qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
+          if (cheb) qb[ct] = mfma16(cur.qa[kk], bBm[kk][ct], qb[ct]);
+        }
+      if (cheb) {   // Q Bm: the third term of the Chebyshev step (boot_cheb_kernel), kept in w.U
+        double *QBr = w.U + (int64_t)rep * T * P;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int t = t0 + 4 * g + lk;
+          if (t < T)
+#pragma unroll
+            for (int ct = 0; ct < NT; ++ct) QBr[(int64_t)t * P + 16 * ct + li] = qb[ct][g];
+        }
+      }
+      // every wave reads only its own tiles' Y rows, loaded (above) before
+      // these stores: Qn may overwrite this tile's Y rows
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+        const bool v = t < T;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const int c = 16 * ct + li;
+          const double wr = ya[ct][g] - th[ct] * u[ct][g];
+          if (v && c < k) res2[ct] = fma(wr, wr, res2[ct]);
+          double q = qn[ct][g];
+          if (c < p && dd[ct]) q = hash_unit(seed, t, 1000003ull * (it + 1) + c);
+          if (c >= p || !v) q = 0.0;
+          qv[ct][g] = q;
+          if (v) Yr[(int64_t)t * P + c] = q;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(cur.fa[g], qv[ct][g], aacc[ct]);
+  }
+  // residuals: sum over the 4 row-lanes of a column, then over waves (fixed order)
+  if (!init) {
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      double v = res2[ct];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lk == 0) sres[wave][16 * ct + li] = v;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int conv = 0;
+    if (!init) {
+      if (lane < P) sres[0][lane] = ((sres[0][lane] + sres[1][lane]) + sres[2][lane]) + sres[3][lane];
+      __builtin_amdgcn_wave_barrier();
+      const int itc = it + 1;
+      const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
+      double *next = small + 2 * P * P + 2 * P + (itc & 1) * P;
+      conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc) ? 1 : 0;
+    }
+    if (lane == 0) {
+      s_conv = conv;
+      if (conv) { w.done[rep] = 1; w.iters[rep] = it + 1; }
+      else if (!init) atomicAdd(&w.active[it], 1);
+    }
+  }
+  __syncthreads();
+  if (!init && (s_conv || last)) {
+    // Ritz vectors U = Q A for the final output (eig_final_kernel)
+    double *Ur = w.U + (int64_t)rep * T * P;
+    for (int tile = wave; tile < ntile; tile += 4) {
+      const int t0 = tile * 16, ta = t0 + li;
+      dv4 u[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) u[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+      double qa[KP];
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk) qa[kk] = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa[kk], bAm[kk][ct], u[ct]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+        if (t < T)
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct) Ur[(int64_t)t * P + 16 * ct + li] = u[ct][g];
+      }
+    }
+    return;
+  }
+  // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
+  const double *Qn = init ? Qr : Yr;
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, rep, ab, aacc, sred);
+}
+
+// Chebyshev step (degree 2) of the factored solver.  After ap2 has produced
+// V = Y Bm (= G* Q Bm, orthonormal), QB = Q Bm (in w.U) and Z(V), and the GEMM
+// H . Z(V), this forms W = G* V exactly as y2 forms Y and replaces the power
+// step by the degree-2 Chebyshev filter on [0, b], b = theta_p (the block's
+// smallest Ritz value, above every unwanted eigenvalue):
+//   T2(2G/b - 1) (Q Bm) = (8/b^2) W - (8/b) V + QB
+// which damps the unwanted spectrum ~T2(2 lambda_k/b - 1) times faster than
+// two power steps relative to the wanted one.  The new basis is orthonormalised
+// by the next Rayleigh-Ritz step (CholQR folded into eig_small), and its
+// Z = P'D Qn, a = F'Qn, cc = EL'Z are produced here for the next GEMM.
+template <int P>
+__global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork w, int T, int p,
+                                                        const int32_t *__restrict__ idx,
+                                                        const double *__restrict__ eta,
+                                                        const int *__restrict__ off, const int *__restrict__ lst,
+                                                        const double *__restrict__ HZ, int64_t ldz,
+                                                        double *__restrict__ ab, const double *__restrict__ Vc,
+                                                        double *__restrict__ Qo, double *__restrict__ Zc) {
+  constexpr int NT = P / 16;
+  const int rep = blockIdx.x;
+  if (w.done[rep]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  __shared__ double sa[16 * P], sb[16 * P];
+  __shared__ double sred[NT * 256];
+  extern __shared__ double sdyn[];
+  double *set = sdyn;                          // eta_t
+  int *six = (int *)(sdyn + T);                // idx_t
+  int *so = six + T, *sl = so + T + 1;         // CSR of idx
+  {
+    const int32_t *ixg = idx + (int64_t)rep * T;
+    const double *etg = eta ? eta + (int64_t)rep * T : nullptr;
+    const int *o = off + (int64_t)rep * (T + 1);
+    const int *L = lst + (int64_t)rep * T;
+    for (int e = tid; e < T; e += 256) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
+    if (tid == 0) so[T] = o[T];
+  }
+  double *abr = ab + (int64_t)rep * 32 * P;
+  for (int e = tid; e < 16 * P; e += 256) sa[e] = abr[e];
+  __syncthreads();
+  for (int e = tid; e < 16 * P; e += 256) {
+    const int j = e / P, c = e % P;
+    double v = abr[16 * P + e];
+    if (j < r)
+      for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], sa[i * P + c], v);
+    sb[e] = v;
+  }
+  __syncthreads();
+  const double *small = w.small + (int64_t)rep * small_stride<P>();
+  const double b = small[2 * P * P + p - 1];
+  const bool ok = b > 0.0;
+  const double c2 = ok ? 8.0 / (b * b) : 0.0, c1 = ok ? -8.0 / b : 1.0, c0 = ok ? 1.0 : 0.0;
+  bool dd[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) dd[ct] = small[2 * P * P + P + 16 * ct + li] != 0.0;
+  const int KR = (r + 3) >> 2;
+  double bA[4][NT], bB[4][NT];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
+      bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
+    }
+  const double *Vr = Vc + (int64_t)rep * T * P;
+  const double *QBr = w.U + (int64_t)rep * T * P;
+  double *Qr = Qo + (int64_t)rep * T * P;
+  dv4 aacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+  const int ntile = (T + 15) >> 4;
+  Y2Tile<P> cur;
+  for (int tile = wave; tile < ntile; tile += 4) {
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Vr);   // cur.q = V rows
+    const int t0 = tile * 16;
+    dv4 yF[NT], yE[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) { yF[ct] = dv4{0.0, 0.0, 0.0, 0.0}; yE[ct] = yF[ct]; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < KR) {
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          yF[ct] = mfma16(cur.fA[kk], bB[kk][ct], yF[ct]);
+          yE[ct] = mfma16(cur.eA[kk], bA[kk][ct], yE[ct]);
+        }
+      }
+    }
+    double qv[NT][4], fa[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int t = t0 + 4 * g + lk;
+      const bool v = t < T;
+      const int tc = min(t, T - 1);
+      fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
+      const double e = v ? set[t] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const int c = 16 * ct + li;
+        const double wv = fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]);
+        const double vv = cur.q[ct][g];
+        double q = dd[ct] ? vv : fma(c2, wv, fma(c1, vv, c0 * QBr[(int64_t)tc * P + c]));
+        if (c >= p || !v) q = 0.0;
+        qv[ct][g] = q;
+        if (v) Qr[(int64_t)t * P + c] = q;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
+  }
+  __syncthreads();   // every wave's Qn rows visible to the CSR gather
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, rep, ab, aacc, sred);
+}
+
 template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
@@ -1501,6 +1654,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
   double *cur = w.Q, *alt = w.Y;
+  const int cheb = cheb_degree() == 2 ? 1 : 0;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   {
     const int64_t n = (int64_t)m * P;
@@ -1508,11 +1662,11 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, (int64_t)0);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace);
-    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, -1, 1, 0, eta,
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, eta,
                        off, lst, cur, alt, Zc, ldz, ab, seed);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  int it = 0, last_gemm = -1;
+  int it = 0, last_gemm = -1, last_cheb = -1;
   for (; it < maxit; ++it) {
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
     hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
@@ -1528,9 +1682,23 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
-                       it == maxit - 1 ? 1 : 0, eta, off, lst, cur, alt, Zc, ldz, ab, seed);
+                       it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, cur, alt, Zc, ldz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
-    std::swap(cur, alt);
+    if (cheb && it < maxit - 1) {
+      // second product G* V and the degree-2 Chebyshev combination: the new
+      // basis goes back into cur (Q), Y/V stay in alt
+      if (tf) tf(tctx, DFM_KC_GEMM, 1);
+      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+      if (tf) tf(tctx, DFM_KC_GEMM, 0);
+      if (e != hipSuccess) return 1000 + (int)e;
+      last_cheb = it;
+      if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
+      hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(256), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st, fb,
+                         w, m, p, idx, eta, off, lst, HZ, ldz, ab, alt, cur, Zc);
+      if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+    } else {
+      std::swap(cur, alt);
+    }
     if ((it + 1) % poll == 0) {
       int a = -1;
       hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
@@ -1541,6 +1709,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   }
   g_last_iters = it;
   g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
+  // the Chebyshev GEMM of iteration it runs after that iteration's check
+  g_last_gemm_products = g_last_rep_iters + count_rep_iters(w.active, last_cheb, 0, nb, st);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);

@@ -91,6 +91,10 @@ int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int6
    the factored bootstrap, G.Q otherwise) summed over the calls since the last
    dfm_ctx_reset_timing: each counts one unconverged replicate in one
    iteration (2 m^2 P flop).  Instrumentation for the roofline figure. */
+/* Replicate-products H . Z run by the factored bootstrap's GEMMs since the
+ * last reset (two per Rayleigh-Ritz iteration with the Chebyshev filter):
+ * the GEMM's algorithmic work is 2 T^2 p per product. */
+int dfm_ctx_gemm_products(dfm_ctx *ctx, int64_t *products);
 int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters);
 const char *dfm_kernel_class_name(int cls);
 
