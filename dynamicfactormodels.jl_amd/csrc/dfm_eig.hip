@@ -239,6 +239,79 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
 }
 
+// Chebyshev step of the direct path (the factored path's boot_cheb_kernel on
+// an explicit Gram): with V = Y Bm in w.Y and Q Bm in w.Q (eig_apply, cheb),
+// Qn = (8/b^2) G V - (8/b) V + Q Bm = T2(2G/b - 1) Q Bm, b = theta_p; dead
+// (re-randomised) columns keep V.  Rows of one 64-row block per workgroup.
+template <int P>
+__global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict__ G, int64_t ldg,
+                                                       int64_t strideG, EigWork w, int m, int p) {
+  constexpr int SQ = P + 4;
+  __shared__ __attribute__((aligned(16))) double sV[EROWS * SQ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rep = blockIdx.y, rb = blockIdx.x;
+  if (w.done[rep]) return;
+  const double *small = w.small + (int64_t)rep * small_stride<P>();
+  const double b = small[2 * P * P + p - 1];
+  const bool ok = b > 0.0;
+  const double c2 = ok ? 8.0 / (b * b) : 0.0, c1 = ok ? -8.0 / b : 1.0, c0 = ok ? 1.0 : 0.0;
+  const double *Gr = G + (int64_t)rep * strideG;
+  const double *Vr = w.Y + (int64_t)rep * m * P;
+  double *Qr = w.Q + (int64_t)rep * m * P;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int row0 = rb * EROWS + wave * 16;
+  double acc[4][P / 4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int bb = 0; bb < P / 4; ++bb) acc[a][bb] = 0.0;
+  for (int kc0 = 0; kc0 < m; kc0 += EROWS) {
+    for (int e = tid; e < EROWS * P; e += 256) {
+      const int r = e / P, c = e % P;
+      sV[r * SQ + c] = (kc0 + r < m) ? Vr[(int64_t)(kc0 + r) * P + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < EROWS / 16; ++ks) {
+      const int kg = kc0 + ks * 16 + fkc;
+      double af[4], bf[P / 4];
+#pragma unroll
+      for (int fa = 0; fa < 4; ++fa) {
+        const int row = row0 + 4 * fa + fi;
+        af[fa] = (row < m && kg < m) ? Gr[(int64_t)row * ldg + kg] : 0.0;
+      }
+#pragma unroll
+      for (int fb = 0; fb < P / 4; ++fb) bf[fb] = sV[(ks * 16 + fkc) * SQ + 4 * fb + fi];
+#pragma unroll
+      for (int fa = 0; fa < 4; ++fa)
+#pragma unroll
+        for (int fb = 0; fb < P / 4; ++fb) acc[fa][fb] = mfma4(af[fa], bf[fb], acc[fa][fb]);
+    }
+    __syncthreads();
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+#pragma unroll
+  for (int fa = 0; fa < 4; ++fa)
+#pragma unroll
+    for (int q = 0; q < P / 16; ++q) {
+      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2],
+                   a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double gv = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int lr = wave * 16 + 4 * fa + oi, col = 16 * q + 4 * blk + oj;
+      const int row = rb * EROWS + lr;
+      if (row < m) {
+        const double v = Vr[(int64_t)row * P + col];
+        const bool dead = small[2 * P * P + P + col] != 0.0;
+        double qn = dead ? v : fma(c2, gv, fma(c1, v, c0 * Qr[(int64_t)row * P + col]));
+        if (col >= p) qn = 0.0;
+        Qr[(int64_t)row * P + col] = qn;
+      }
+    }
+}
+
 // ---------------------------------------------------------------- small
 // One wave per replicate, all p x p algebra in LDS, written for latency:
 // Cholesky with the pivot broadcast by a lane shuffle, explicit triangular
@@ -492,8 +565,10 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
 
 // ---------------------------------------------------------------- apply
 template <int P>
+// cheb = 1: the next basis is formed by eig_cheb_kernel; here V = Y Bm goes
+// to w.Y and Q Bm to w.Q (both over this block's own rows, already staged).
 __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p, int k, int it,
-                                                        uint64_t seed, int64_t rep0) {
+                                                        uint64_t seed, int64_t rep0, int cheb) {
   constexpr int SQ = P + 1;
   __shared__ double sQ[EROWS * SQ], sY[EROWS * SQ], sW[EROWS * P];
   __shared__ double sA[P * P], sB[P * P], sT[2 * P];
@@ -501,7 +576,7 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
   if (w.done[rep]) return;
   const double *small = w.small + (int64_t)rep * small_stride<P>();
   double *Qr = w.Q + (int64_t)rep * m * P;
-  const double *Yr = w.Y + (int64_t)rep * m * P;
+  double *Yr = w.Y + (int64_t)rep * m * P;
   double *Ur = w.U + (int64_t)rep * m * P;
   for (int e = tid; e < EROWS * P; e += 256) {
     const int r = e / P, c = e % P, row = rb * EROWS + r;
@@ -513,16 +588,21 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
   __syncthreads();
   for (int e = tid; e < EROWS * P; e += 256) {
     const int r = e / P, c = e % P, row = rb * EROWS + r;
-    double u = 0.0, ya = 0.0, qn = 0.0;
+    double u = 0.0, ya = 0.0, qn = 0.0, qb = 0.0;
     for (int a = 0; a < p; ++a) {
       u = fma(sQ[r * SQ + a], sA[a * P + c], u);
       ya = fma(sY[r * SQ + a], sA[a * P + c], ya);
       qn = fma(sY[r * SQ + a], sB[a * P + c], qn);
+      if (cheb) qb = fma(sQ[r * SQ + a], sB[a * P + c], qb);
     }
     if (c < p && sT[P + c] != 0.0) qn = hash_unit(seed, row, 1000003ull * (it + 1) + c);
-    if (c >= p) qn = 0.0;
+    if (c >= p) { qn = 0.0; qb = 0.0; }
     if (c < k) { const double wv = ya - sT[c] * u; sW[r * P + c] = row < m ? wv * wv : 0.0; }
-    if (row < m) { Ur[(int64_t)row * P + c] = u; Qr[(int64_t)row * P + c] = qn; }
+    if (row < m) {
+      Ur[(int64_t)row * P + c] = u;
+      if (cheb) { Yr[(int64_t)row * P + c] = qn; Qr[(int64_t)row * P + c] = qb; }
+      else Qr[(int64_t)row * P + c] = qn;
+    }
   }
   __syncthreads();
   if (tid < k) {
@@ -686,6 +766,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   int it = 0;
   bool finished = false;
   std::vector<int> act;
+  const int cheb = cheb_degree() == 2 ? 1 : 0;
   for (; it <= maxit; ++it) {
     const int check_only = (it == maxit);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
@@ -697,7 +778,8 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, jacobi_sweeps());
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0);
+    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0, cheb);
+    if (cheb) hipLaunchKernelGGL(eig_cheb_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, p);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it > 0 && (it % poll) == 0) {
       int a = -1;
@@ -976,7 +1058,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
     }
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0);
+    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     static const bool trace_on = getenv("DFM_EIG_TRACE") != nullptr;
     if (trace_on) {   // debug: residual trajectory of replicate 0, active count
