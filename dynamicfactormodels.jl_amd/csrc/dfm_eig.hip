@@ -253,8 +253,7 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
   if (w.done[rep]) return;
   const double *small = w.small + (int64_t)rep * small_stride<P>();
   const double b = small[2 * P * P + p - 1];
-  const bool ok = b > 0.0;
-  const double c2 = ok ? 8.0 / (b * b) : 0.0, c1 = ok ? -8.0 / b : 1.0, c0 = ok ? 1.0 : 0.0;
+  const double c2 = b > 0.0 ? 8.0 / (b * b) : 0.0;
   const double *Gr = G + (int64_t)rep * strideG;
   const double *Vr = w.Y + (int64_t)rep * m * P;
   double *Qr = w.Q + (int64_t)rep * m * P;
@@ -303,9 +302,9 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
       const int lr = wave * 16 + 4 * fa + oi, col = 16 * q + 4 * blk + oj;
       const int row = rb * EROWS + lr;
       if (row < m) {
-        const double v = Vr[(int64_t)row * P + col];
         const bool dead = small[2 * P * P + P + col] != 0.0;
-        double qn = dead ? v : fma(c2, gv, fma(c1, v, c0 * Qr[(int64_t)row * P + col]));
+        const double x = Qr[(int64_t)row * P + col];   // c1 V + c0 Q Bm (eig_apply)
+        double qn = dead ? x : fma(c2, gv, x);
         if (col >= p) qn = 0.0;
         Qr[(int64_t)row * P + col] = qn;
       }
@@ -600,8 +599,14 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
     if (c < k) { const double wv = ya - sT[c] * u; sW[r * P + c] = row < m ? wv * wv : 0.0; }
     if (row < m) {
       Ur[(int64_t)row * P + c] = u;
-      if (cheb) { Yr[(int64_t)row * P + c] = qn; Qr[(int64_t)row * P + c] = qb; }
-      else Qr[(int64_t)row * P + c] = qn;
+      if (cheb) {   // V, and X = c1 V + c0 Q Bm (dead columns: V) for eig_cheb_kernel
+        const double bch = sT[p - 1];
+        const double x = (c < p && sT[P + c] != 0.0) ? qn : (bch > 0.0 ? fma(-8.0 / bch, qn, qb) : qn);
+        Yr[(int64_t)row * P + c] = qn;
+        Qr[(int64_t)row * P + c] = c >= p ? 0.0 : x;
+      } else {
+        Qr[(int64_t)row * P + c] = qn;
+      }
     }
   }
   __syncthreads();
@@ -1483,6 +1488,9 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   }
   const double *Qr = Qc + (int64_t)rep * T * P;
   double *Yr = Yq + (int64_t)rep * T * P;
+  // Chebyshev coefficients from b = theta_p (boot_cheb_kernel): X = cf1 V + cf0 Q Bm
+  const double bch = init ? 0.0 : small[2 * P * P + p - 1];
+  const double cf1 = bch > 0.0 ? -8.0 / bch : 1.0, cf0 = bch > 0.0 ? 1.0 : 0.0;
   double res2[NT];
   dv4 aacc[NT];
 #pragma unroll
@@ -1512,14 +1520,20 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
           qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
           if (cheb) qb[ct] = mfma16(cur.qa[kk], bBm[kk][ct], qb[ct]);
         }
-      if (cheb) {   // Q Bm: the third term of the Chebyshev step (boot_cheb_kernel), kept in w.U
-        double *QBr = w.U + (int64_t)rep * T * P;
+      if (cheb) {   // X = c1 V + c0 Q Bm, the filter's low-order terms (boot_cheb_kernel), kept in w.U
+        double *Xr = w.U + (int64_t)rep * T * P;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int t = t0 + 4 * g + lk;
           if (t < T)
 #pragma unroll
-            for (int ct = 0; ct < NT; ++ct) QBr[(int64_t)t * P + 16 * ct + li] = qb[ct][g];
+            for (int ct = 0; ct < NT; ++ct) {
+              const int c = 16 * ct + li;
+              double x = fma(cf1, qn[ct][g], cf0 * qb[ct][g]);
+              if (c < p && dd[ct]) x = hash_unit(seed, t, 1000003ull * (it + 1) + c);   // = V
+              if (c >= p) x = 0.0;
+              Xr[(int64_t)t * P + c] = x;
+            }
         }
       }
       // every wave reads only its own tiles' Y rows, loaded (above) before
@@ -1605,7 +1619,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
 }
 
 // Chebyshev step (degree 2) of the factored solver.  After ap2 has produced
-// V = Y Bm (= G* Q Bm, orthonormal), QB = Q Bm (in w.U) and Z(V), and the GEMM
+// V = Y Bm (= G* Q Bm, orthonormal), X = -(8/b) V + Q Bm (in w.U) and Z(V), and the GEMM
 // H . Z(V), this forms W = G* V exactly as y2 forms Y and replaces the power
 // step by the degree-2 Chebyshev filter on [0, b], b = theta_p (the block's
 // smallest Ritz value, above every unwanted eigenvalue):
@@ -1654,8 +1668,7 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
   __syncthreads();
   const double *small = w.small + (int64_t)rep * small_stride<P>();
   const double b = small[2 * P * P + p - 1];
-  const bool ok = b > 0.0;
-  const double c2 = ok ? 8.0 / (b * b) : 0.0, c1 = ok ? -8.0 / b : 1.0, c0 = ok ? 1.0 : 0.0;
+  const double c2 = b > 0.0 ? 8.0 / (b * b) : 0.0;
   bool dd[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) dd[ct] = small[2 * P * P + P + 16 * ct + li] != 0.0;
@@ -1668,16 +1681,16 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
       bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
       bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
     }
-  const double *Vr = Vc + (int64_t)rep * T * P;
-  const double *QBr = w.U + (int64_t)rep * T * P;
+  const double *Xr = w.U + (int64_t)rep * T * P;   // X = c1 V + c0 Q Bm (ap2)
   double *Qr = Qo + (int64_t)rep * T * P;
+  (void)Vc;
   dv4 aacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += 4) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Vr);   // cur.q = V rows
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Xr);   // cur.q = X rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1704,8 +1717,7 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         const double wv = fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]);
-        const double vv = cur.q[ct][g];
-        double q = dd[ct] ? vv : fma(c2, wv, fma(c1, vv, c0 * QBr[(int64_t)tc * P + c]));
+        double q = dd[ct] ? cur.q[ct][g] : fma(c2, wv, cur.q[ct][g]);
         if (c >= p || !v) q = 0.0;
         qv[ct][g] = q;
         if (v) Qr[(int64_t)t * P + c] = q;
