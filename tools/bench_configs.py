@@ -154,8 +154,10 @@ def c5(D, ctx, args):
     rng = np.random.default_rng(20261015 + 5)
     T, N, P = 2000, 20000, 200
     y, x, *_ = D.factor_model_DGP(T, N, 8, rng=rng)
-    x = D.normalize(x)
-    w = np.ones((T, 1))
+    # column-major host panel, as a Julia caller hands it over (no harness
+    # transpose inside the timed region; the PCIe upload stays in)
+    x = np.asfortranarray(D.normalize(x))
+    w = np.asfortranarray(np.ones((T, 1)))
     out = {}
     s = timed(lambda: out.update(D.pseudo_out_of_sample_refits(y, w, x, "ICp2", num_predictions=P, kmax=8,
                                                                 ctx=ctx)), max(1, args.reps // 2), ctx.synchronize)
