@@ -87,6 +87,9 @@ def main():
     ap.add_argument("--eig-tol", type=float, default=-1.0, help="eigensolver gap tolerance (default 1e-12)")
     ap.add_argument("--strict", action="store_true",
                     help="eigenvector-residual stopping rule even for eigenvalue-only stats")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
+                    help="c3 (default, the metric's config) or c5: 200 expanding windows x ICp2 sweep at "
+                         "T=2000 N=20000, windows sharded over the ranks (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -105,6 +108,8 @@ def main():
     import dfm_pkg
     D = dfm_pkg.load()
     ctx = D.Context(local)
+    if args.workload == "c5":
+        return bench_windows(args, D, ctx, torch, dist, world, rank, dev)
     if args.eig_tol > 0:
         ctx.set_eig_params(tol=args.eig_tol)
     if args.strict:
@@ -223,6 +228,89 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+C5_T, C5_N, C5_P, C5_KMAX = 2000, 20000, 200, 8
+
+
+def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
+    """BASELINE.json configs[4]: the refits of pseudo_out_of_sample_forecasts
+    (src/utils.jl:54-72), P = 200 expanding windows x ICp2 sweep k <= 8 on a
+    T=2000 N=20000 panel.  The panel is resident in HBM (column-major, as Julia
+    holds it); a step = all 200 windows, sharded over the ranks as contiguous
+    window blocks (parallel.window_shard: a rank reads only the leading rows its
+    windows reach) + one all-gather of the per-window rows.  Strong scaling."""
+    from dfm_amd.parallel import window_shard, _pack_windows, gather_rows
+    from dfm_amd.api import _window_kmax
+    T5, N5, P5, km = C5_T, C5_N, C5_P, C5_KMAX
+    rng = np.random.default_rng(20261015 + 5)
+    y, x, *_ = D.factor_model_DGP(T5, N5, 8, rng=rng)
+    x = D.normalize(x)
+    yd = torch.from_numpy(np.ascontiguousarray(y)).to(dev)
+    wd = torch.ones((T5, 1), dtype=torch.float64, device=dev)
+    xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major T x N in HBM
+    del x
+    w0, w1, rows = window_shard(T5, P5, world, rank)
+    K = _window_kmax(T5, N5, km)
+    holder = {}
+
+    def step():
+        res = D.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=w1 - w0, kmax=km,
+                                                rows=rows, ctx=ctx) if w1 > w0 else {}
+        loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, 1)).to(dev)
+        holder["all"] = gather_rows(loc, P5) if world > 1 else loc
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.enable_timing(False)
+    timing = ctx.read_timing()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    allrows = holder["all"].cpu().numpy()
+    gram_ms, gram_n = timing.get("gram", (0.0, 0))
+    roof = None
+    if gram_n:   # rank-local prefix Gram of the rows its windows reach: rows (rows+1) N flop (SYRK count)
+        per = gram_ms / gram_n
+        ach = rows * (rows + 1) * N5 / (per * 1e-3) / 1e12
+        roof = {"kernel": "gram_kernel<ROWS> (prefix Gram X X' of the leading rows, v_mfma_f64_4x4x4_4b)",
+                "bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(per, 4),
+                "flop_per_launch": rows * (rows + 1) * N5}
+    rec = {
+        "metric": "expanding-window refits/sec (node), T=2000 N=20000, 200 windows x ICp2 sweep kmax 8",
+        "value": round(P5 * args.steps / el, 2), "unit": "windows/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "C5: pseudo_out_of_sample_forecasts refits, Bai-Ng DGP T=2000 N=20000 r=8, "
+                               "P=200 windows per step (all ranks together), panel resident in HBM",
+                   "T": T5, "N": N5, "P": P5, "kmax": km, "parallelism": f"window-sharded x{world}"},
+        "roofline": roof,
+        "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
+        "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
+        "outputs_finite": bool(np.all(np.isfinite(allrows[:, :3]))),
+        "r_selected": sorted(set(int(v) for v in allrows[:, 0])),
+    }
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

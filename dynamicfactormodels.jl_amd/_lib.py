@@ -71,6 +71,9 @@ SIGNATURES = [
     ("dfm_windows", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
                               C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
                               c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("dfm_windows_dev", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                                  C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
+                                  c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
     ("dfm_windows_forecast", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
                                        C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
                                        c_double_p, c_double_p]),
@@ -116,6 +119,13 @@ def load():
             raise LibraryMissing(
                 f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
                 "g.build()'` (hipcc, gfx950). There is no CPU fallback.")
+        # torch (device memory for the *_dev entry points, torch.distributed)
+        # must bring up the HIP runtime before libdfm does: loaded the other
+        # way round, torch's later device init reports no HIP GPUs
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(lib, name)

@@ -597,6 +597,52 @@ def pseudo_out_of_sample_refits(y, w, x, criterion: str = "ICp2", num_prediction
             "criterion_value": cv, "eigenvalues": ev, "coefficients": coef, "t_stats": ts}
 
 
+def _is_device_tensor(a) -> bool:
+    return type(a).__module__.startswith("torch") and getattr(a, "is_cuda", False)
+
+
+def pseudo_out_of_sample_refits_dev(y, w, x, criterion: str = "ICp2", num_predictions: int = 200,
+                                    kmax: Optional[int] = None, *, rows: Optional[int] = None,
+                                    ctx: Optional[Context] = None):
+    """``pseudo_out_of_sample_refits`` with the panel already resident in HBM
+    (``dfm_windows_dev``): ``y`` (T,), ``w`` (T, q) and ``x`` (T, N) are float64
+    torch tensors on the context's device, ``w`` and ``x`` COLUMN-major (the
+    Julia layout: ``x.stride() == (1, ldx)``, e.g. ``xt.t()`` of a contiguous
+    (N, T) tensor).  ``rows`` (default T) restricts the job to the leading
+    ``rows`` rows without a copy: the windows are then those of the
+    (rows, num_predictions) problem — the multi-GPU window shard
+    (``parallel.windows_sharded``)."""
+    ctx = ctx or default_context()
+    for a, nm in ((y, "y"), (w, "w"), (x, "x")):
+        if not _is_device_tensor(a) or a.dtype.itemsize != 8 or not a.dtype.is_floating_point:
+            raise TypeError(f"{nm} must be a float64 torch tensor on the GPU")
+    if x.dim() != 2 or x.stride(0) != 1 or x.stride(1) < x.shape[0]:
+        raise ValueError("x must be column-major (stride (1, ldx >= T))")
+    if w.dim() == 1:
+        w = w.reshape(-1, 1)
+    if w.shape[1] > 1 and (w.stride(0) != 1 or w.stride(1) < w.shape[0]):
+        raise ValueError("w must be column-major (stride (1, ldw >= T))")
+    if y.dim() != 1 or y.stride(0) != 1:
+        raise ValueError("y must be a contiguous vector")
+    Tfull, N = int(x.shape[0]), int(x.shape[1])
+    T = Tfull if rows is None else int(rows)
+    if not (0 < T <= Tfull) or y.shape[0] < T or w.shape[0] < T:
+        raise ValueError("rows out of range")
+    q, P = int(w.shape[1]), int(num_predictions)
+    ldw = int(w.stride(1)) if q > 1 else max(int(w.shape[0]), 1)
+    km = _window_kmax(T, N, kmax)
+    r = np.zeros(P, dtype=np.int64)
+    V, cv = np.zeros(P), np.zeros(P)
+    ev = np.zeros((P, km))
+    coef, ts = np.zeros((P, q + km)), np.zeros((P, q + km))
+    ctx.check(ctx.lib.dfm_windows_dev(ctx.h, y.data_ptr(), w.data_ptr(), q, ldw, x.data_ptr(), T, N,
+                                      int(x.stride(1)), P, _CRIT_CODE[criterion], int(kmax) if kmax else 0,
+                                      r.ctypes.data_as(_lib.c_int64_p), _lib.ptr(V), _lib.ptr(cv), _lib.ptr(ev),
+                                      _lib.ptr(coef), _lib.ptr(ts)))
+    return {"window_rows": np.arange(T - P, T), "number_of_factors": r, "V": V,
+            "criterion_value": cv, "eigenvalues": ev, "coefficients": coef, "t_stats": ts}
+
+
 def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions: int = 200,
                                    kmax: Optional[int] = None, ctx: Optional[Context] = None):
     """``src/utils.jl:54-72``: one-step-ahead pseudo out-of-sample forecasts.

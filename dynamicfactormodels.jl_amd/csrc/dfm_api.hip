@@ -238,6 +238,13 @@ int dfm_ctx_create(int device, dfm_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) { delete c; return -3; }
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return -4; }
   c->stream = c->own;
+  {   // stream-ordered scratch (split-K Gram partials) stays mapped between calls
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   *out = c;
   return 0;
 }
@@ -1190,20 +1197,33 @@ int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const d
 
 // --------------------------------------------------------- stand-alone entry points
 namespace {
-struct DevPanel {
+struct DevPanel {   // stream-ordered (pool) allocations: no device-wide sync in hipFree
   double *raw = nullptr, *P = nullptr;
   int64_t ld = 0;
-  ~DevPanel() { hipFree(raw); hipFree(P); }
+  hipStream_t st = nullptr;
+  ~DevPanel() {
+    if (raw) hipFreeAsync(raw, st);
+    if (P) hipFreeAsync(P, st);
+  }
 };
-int upload_panel(dfm_ctx *ctx, const double *X, int T, int N, int64_t ldx, DevPanel &dp) {
+// X column-major T x N (leading dimension ldx) in host memory, or already in
+// HBM when dev (then it is transposed in place of the copy, never duplicated)
+int upload_panel(dfm_ctx *ctx, const double *X, int T, int N, int64_t ldx, DevPanel &dp, bool dev = false) {
   hipStream_t st = ctx->stream;
   dp.ld = round_up(N, 16);
-  HIPCHK(ctx, dalloc(&dp.raw, (size_t)T * N));
-  HIPCHK(ctx, dalloc(&dp.P, (size_t)T * dp.ld));
-  HIPCHK(ctx, hipMemcpy2DAsync(dp.raw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N,
-                               hipMemcpyHostToDevice, st));
+  dp.st = st;
+  HIPCHK(ctx, hipMallocAsync((void **)&dp.P, (size_t)T * dp.ld * 8, st));
+  const double *src = X;
+  int64_t lds = ldx;
+  if (!dev) {
+    HIPCHK(ctx, hipMallocAsync((void **)&dp.raw, (size_t)T * N * 8, st));
+    HIPCHK(ctx, hipMemcpy2DAsync(dp.raw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N,
+                                 hipMemcpyHostToDevice, st));
+    src = dp.raw;
+    lds = T;
+  }
   hipLaunchKernelGGL(panel_from_colmajor_kernel, dim3((unsigned)((dp.ld + 31) / 32), (T + 31) / 32),
-                     dim3(256), 0, st, dp.raw, (int64_t)T, T, N, dp.P, dp.ld);
+                     dim3(256), 0, st, src, lds, T, N, dp.P, dp.ld);
   HIPCHK(ctx, hipGetLastError());
   return 0;
 }
@@ -1485,10 +1505,16 @@ __global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp
   }
 }
 
+__global__ void window_draws_kernel(int T, int n0, int32_t *__restrict__ idx, double *__restrict__ eta) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, wi = blockIdx.y;
+  if (t >= T) return;
+  idx[(int64_t)wi * T + t] = t;
+  eta[(int64_t)wi * T + t] = t < n0 + wi ? 1.0 : 0.0;
+}
 static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
                         int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
-                        double *pred_out, double *true_out);
+                        double *pred_out, double *true_out, bool dev);
 #define LCKW(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(ctx, 1000 + (int)e_, "%s", hipGetErrorString(e_)); } while (0)
 
 extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
@@ -1496,7 +1522,15 @@ extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q
                            int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                            double *coef_out, double *tstat_out) {
   return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, V_out, crit_out, eig_out,
-                      coef_out, tstat_out, nullptr, nullptr);
+                      coef_out, tstat_out, nullptr, nullptr, false);
+}
+
+extern "C" int dfm_windows_dev(dfm_ctx *ctx, const double *y_dev, const double *w_dev, int q, int64_t ldw,
+                               const double *X_dev, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
+                               int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
+                               double *coef_out, double *tstat_out) {
+  return windows_impl(ctx, y_dev, w_dev, q, ldw, X_dev, T64, N64, ldx, P, crit, kmax, r_out, V_out, crit_out,
+                      eig_out, coef_out, tstat_out, nullptr, nullptr, true);
 }
 
 extern "C" int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
@@ -1504,13 +1538,13 @@ extern "C" int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double 
                                     int kmax, int64_t *r_out, double *pred_out, double *true_out) {
   if (!pred_out || !true_out) return fail(ctx, -2, "dfm_windows_forecast: output pointers required");
   return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, nullptr, nullptr, nullptr,
-                      nullptr, nullptr, pred_out, true_out);
+                      nullptr, nullptr, pred_out, true_out, false);
 }
 
 static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
                         int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
-                        double *pred_out, double *true_out) {
+                        double *pred_out, double *true_out, bool dev) {
   if (!ctx) return -1;
   const int T = (int)T64, N = (int)N64;
   if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
@@ -1543,29 +1577,26 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
                           "min(T,N) <= %d", std::min(spectrum_any_max(), dense_eig_max()));
   const int Pb = (p <= 16 || wide) ? 16 : 32;
   DevPanel dp;
-  int rc = upload_panel(ctx, X, T, N, ldx, dp);
+  int rc = upload_panel(ctx, X, T, N, ldx, dp, dev);
   if (rc) return rc;
-  // host draws: identity + masks
-  std::vector<int32_t> hidx((size_t)P * T);
-  std::vector<double> heta((size_t)P * T);
   std::vector<int> hTn(P), hkr(P);
-  for (int wi = 0; wi < P; ++wi)
-    for (int t = 0; t < T; ++t) { hidx[(size_t)wi * T + t] = t; heta[(size_t)wi * T + t] = t < n0 + wi ? 1.0 : 0.0; }
+  // scratch: stream-ordered pool allocations (no device-wide sync on free)
   std::vector<void *> frees;
-  auto dal = [&](size_t bytes) -> void * { void *ptr = nullptr; if (hipMalloc(&ptr, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr; frees.push_back(ptr); return ptr; };
-  struct Freer { std::vector<void *> &v; ~Freer() { for (void *x : v) hipFree(x); } } freer{frees};
-  int32_t *didx = (int32_t *)dal(hidx.size() * 4);
-  double *deta = (double *)dal(heta.size() * 8);
+  auto dal = [&](size_t bytes) -> void * { void *ptr = nullptr; if (hipMallocAsync(&ptr, std::max<size_t>(bytes, 8), st) != hipSuccess) return nullptr; frees.push_back(ptr); return ptr; };
+  struct Freer { std::vector<void *> &v; hipStream_t s; ~Freer() { for (void *x : v) hipFreeAsync(x, s); } } freer{frees, st};
+  // window w as a "replicate" of the panel: identity rows, row mask t < n0 + w
+  int32_t *didx = (int32_t *)dal((size_t)P * T * 4);
+  double *deta = (double *)dal((size_t)P * T * 8);
   double *dy = (double *)dal((size_t)T * 8), *dw = (double *)dal((size_t)T * std::max(q, 1) * 8);
   double *tr = (double *)dal((size_t)P * 8);
   int *stt = (int *)dal((size_t)P * 4), *ost = (int *)dal((size_t)P * 4);
   int *dTn = (int *)dal((size_t)P * 4), *dkr = (int *)dal((size_t)P * 4);
   if (!didx || !deta || !dy || !dw || !tr || !stt || !ost || !dTn || !dkr)
     return fail(ctx, 1002, "dfm_windows: out of device memory");
-  HIPCHK(ctx, hipMemcpyAsync(didx, hidx.data(), hidx.size() * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipMemcpyAsync(deta, heta.data(), heta.size() * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
-  if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(window_draws_kernel, dim3((unsigned)((T + 255) / 256), P), dim3(256), 0, st, T, n0, didx, deta);
+  const hipMemcpyKind yk = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, yk, st));
+  if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, yk, st));
   PanelSrc msrc{nullptr, dp.P, didx, deta, dp.ld, T};   // window w = rows < n0 + w of X
   // ---- the windows' Grams: N > T one prefix Gram H; T >= N per-window G
   double *H = nullptr, *G = nullptr;

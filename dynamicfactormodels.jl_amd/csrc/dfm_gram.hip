@@ -19,6 +19,8 @@
 //
 // Requirements: panels C/E have zero-filled padding columns N..ld-1 and
 // ld % 16 == 0.  Output G is the full symmetric m x m matrix (row-major, ldg).
+#include <algorithm>
+
 #include "dfm_common.h"
 
 namespace dfm {
@@ -37,7 +39,7 @@ DFM_DEV int lds_off(int a, int kc) {
 template <int ORIENT, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
 __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K, int T,
                                                       double *__restrict__ G, int64_t ldg,
-                                                      int64_t strideG) {
+                                                      int64_t strideG, int ksteps, int64_t strideZ) {
   __shared__ __attribute__((aligned(16))) double lds[2][2][GT * KS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -133,12 +135,15 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
 
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
-  const int nst = (K + KS - 1) / KS;
-  load_stage(0);
+  // split-K: this workgroup reduces k-steps [s0, s1) (blockIdx.z) into its
+  // own partial image (strideZ apart); launch_gram sums them in fixed order
+  const int s0 = blockIdx.z * ksteps;
+  const int nst = min((K + KS - 1) / KS, s0 + ksteps);
+  load_stage(s0 * KS);
   store_stage(0);
   __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
+  for (int s = s0; s < nst; ++s) {
+    const int buf = (s - s0) & 1;
     if (s + 1 < nst) load_stage((s + 1) * KS);
     const double *la = lds[buf][0];
     const double *lb = diag ? lds[buf][0] : lds[buf][1];
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
   // ---------------- epilogue: transpose-reduce over the 4 MFMA blocks, store
   const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
   const int oi = lane >> 4, oj = lane & 3;
-  double *Gr = G + (int64_t)rep * strideG;
+  double *Gr = G + (int64_t)rep * strideG + (int64_t)blockIdx.z * strideZ;
 #pragma unroll
   for (int fa = 0; fa < 8; ++fa)
 #pragma unroll
@@ -178,14 +183,58 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
     }
 }
 
+// Fixed-order sum of the split-K partial images: G[r] = sum_z W[r][z].
+__global__ void gram_splitk_sum_kernel(const double *__restrict__ W, int S, int m, int64_t ldg,
+                                       int64_t elems, double *__restrict__ G, int64_t strideG) {
+  const int r = blockIdx.y;
+  const double *w = W + (int64_t)r * S * elems;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < elems; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / ldg, j = e - i * ldg;
+    if (j >= m) continue;
+    double a = 0.0;
+    for (int z = 0; z < S; ++z) a += w[(int64_t)z * elems + e];
+    G[(int64_t)r * strideG + i * ldg + j] = a;
+  }
+}
+
+// K-split of one Gram: a function of (m, K) only — never of the batch — so a
+// replicate's Gram is bit-identical however the replicates are batched.  A
+// lone large Gram (C5's prefix Gram: m = 2000, 528 tiles of 64 x 64 over 20000
+// columns) otherwise runs 1.03 rounds of a 512-slot chip; split over the
+// reduction it fills ~13 rounds at 96 %.
+int gram_ksplit(int m, int K) {
+  const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2;
+  if (tiles < 64 || K < 4096) return 1;
+  return std::max(1, std::min(16, K / 1536));
+}
+
 // Dispatch.  Returns hipError of the launch.
 hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G,
                        int64_t ldg, int64_t strideG, int nrep, hipStream_t st) {
   const int nt = (m + GT - 1) / GT;
-  dim3 grid(nt * (nt + 1) / 2, nrep), block(256);
+  const int nsteps = (K + KS - 1) / KS;
+  const int S0 = gram_ksplit(m, K);
+  const int ksteps = (nsteps + S0 - 1) / S0, S = (nsteps + ksteps - 1) / ksteps;
+  double *Gk = G, *W = nullptr;
+  int64_t sG = strideG, sZ = 0;
+  const int64_t elems = (int64_t)m * ldg;
+  int nrc = nrep;   // replicates per launch (bounds the partial images to ~1 GB)
+  if (S > 1) {
+    nrc = (int)std::max<int64_t>(1, std::min<int64_t>(nrep, ((int64_t)1 << 27) / (elems * S)));
+    hipError_t e = hipMallocAsync((void **)&W, (size_t)nrc * S * elems * 8, st);
+    if (e != hipSuccess) return e;
+    Gk = W; sZ = elems; sG = elems * S;
+  }
   const bool c = src.C != nullptr, e = src.eta != nullptr, x = src.idx != nullptr;
+  for (int r0 = 0; r0 < nrep; r0 += nrc) {
+  const int nr = std::min(nrc, nrep - r0);
+  PanelSrc sub = src;
+  if (x) sub.idx = src.idx + (int64_t)r0 * src.rs;
+  if (e) sub.eta = src.eta + (int64_t)r0 * src.rs;
+  double *Gout = S > 1 ? Gk : G + (int64_t)r0 * strideG;
+  dim3 grid(nt * (nt + 1) / 2, nr, S), block(256);
 #define DFM_GRAM_L(O, C_, E_, X_) \
-  hipLaunchKernelGGL((gram_kernel<O, C_, E_, X_>), grid, block, 0, st, src, m, K, T, G, ldg, strideG)
+  hipLaunchKernelGGL((gram_kernel<O, C_, E_, X_>), grid, block, 0, st, sub, m, K, T, Gout, ldg, sG, ksteps, sZ)
   if (orient == ORIENT_ROWS) {
     if (c && e && x) DFM_GRAM_L(ORIENT_ROWS, true, true, true);
     else if (c && !e && x) DFM_GRAM_L(ORIENT_ROWS, true, false, true);
@@ -202,6 +251,12 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
     else return hipErrorInvalidValue;
   }
 #undef DFM_GRAM_L
+  if (S > 1) {
+    hipLaunchKernelGGL(gram_splitk_sum_kernel, dim3((unsigned)std::min<int64_t>((elems + 255) / 256, 4096), nr),
+                       dim3(256), 0, st, W, S, m, ldg, elems, G + (int64_t)r0 * strideG, strideG);
+  }
+  }
+  if (W) hipFreeAsync(W, st);
   return hipGetLastError();
 }
 

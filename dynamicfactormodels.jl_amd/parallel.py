@@ -71,3 +71,71 @@ def wild_bootstrap_sharded(dfm, B: int, stat, idx: np.ndarray, eta: np.ndarray, 
         return out if out.ndim == 2 else out[:, None]
 
     return sharded_bootstrap(run, B, group, device)
+
+
+# ---------------------------------------------------------------- windows
+# Expanding windows (pseudo_out_of_sample_forecasts, src/utils.jl:54-72) are
+# independent given the panel: window w refits on rows 0..T-P+w-1 only.  A
+# contiguous shard [w0, w1) of the P windows is therefore exactly the
+# (T - P + w1, w1 - w0) windows problem on the panel's leading T - P + w1 rows
+# (a zero-copy view: same pointer, same leading dimension).  With N > T every
+# window's Gram is a leading block of the one prefix Gram, so
+# a rank forms only the Gram of the rows its windows reach.
+
+WINDOW_FIELDS = ("number_of_factors", "V", "criterion_value", "eigenvalues", "coefficients", "t_stats")
+
+
+def window_shard(T: int, P: int, world: int, rank: int) -> Tuple[int, int, int]:
+    """(w0, w1, rows): this rank's windows [w0, w1) and the leading rows of the
+    panel they read (window w reads rows < T - P + w)."""
+    w0, w1 = shard_range(P, world, rank)
+    return w0, w1, T - P + w1
+
+
+def _pack_windows(res: dict, n: int, K: int, q: int) -> np.ndarray:
+    """One (n, 3 + K + 2 (q + K)) float64 row block per shard; columns past the
+    shard's own sweep bound are NaN."""
+    out = np.full((n, 3 + K + 2 * (q + K)), np.nan)
+    if n == 0:
+        return out
+    out[:, 0] = res["number_of_factors"]
+    out[:, 1] = res["V"]
+    out[:, 2] = res["criterion_value"]
+    ev = res["eigenvalues"]
+    out[:, 3:3 + ev.shape[1]] = ev
+    c0 = 3 + K
+    for f in ("coefficients", "t_stats"):
+        a = res[f]
+        out[:, c0:c0 + a.shape[1]] = a
+        c0 += q + K
+    return out
+
+
+def _unpack_windows(rows: np.ndarray, T: int, P: int, K: int, q: int) -> dict:
+    c0 = 3 + K
+    return {"window_rows": np.arange(T - P, T), "number_of_factors": rows[:, 0].astype(np.int64),
+            "V": rows[:, 1].copy(), "criterion_value": rows[:, 2].copy(),
+            "eigenvalues": rows[:, 3:3 + K].copy(), "coefficients": rows[:, c0:c0 + q + K].copy(),
+            "t_stats": rows[:, c0 + q + K:c0 + 2 * (q + K)].copy()}
+
+
+def windows_sharded(run_local: Callable[[int, int], dict], T: int, N: int, q: int, P: int,
+                    kmax: Optional[int] = None, group=None, device=None) -> dict:
+    """All P windows over all ranks: this rank runs its shard through
+    ``run_local(rows, n)`` (the windows problem on the leading ``rows`` rows with
+    ``n`` windows; returns ``pseudo_out_of_sample_refits``' dict), then one
+    all-gather of the packed per-window rows.  The eigenvalue / coefficient
+    columns keep the unsharded width K = min(kmax, ceil(min(T-1, N)/2)); with
+    kmax unset a shard whose widest window sweeps fewer than K factors fills
+    the rest with NaN (its windows' own sweep bounds are unchanged)."""
+    import torch
+    import torch.distributed as dist
+    from .api import _window_kmax
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    K = _window_kmax(T, N, kmax)
+    w0, w1, rows = window_shard(T, P, world, rank)
+    res = run_local(rows, w1 - w0) if w1 > w0 else {}
+    loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, q))
+    if device is not None:
+        loc = loc.to(device)
+    return _unpack_windows(gather_rows(loc, P, group).cpu().numpy(), T, P, K, q)

@@ -227,6 +227,16 @@ int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t l
 int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                          const double *X, int64_t T, int64_t N, int64_t ldx, int P, int crit,
                          int kmax, int64_t *r_out, double *pred_out, double *true_out);
+/* dfm_windows with the inputs already resident in HBM (y_dev: T, w_dev: ldw x q
+ * column-major, X_dev: column-major T x N with leading dimension ldx, all on the
+ * context's device); outputs as dfm_windows, in host memory (a few hundred
+ * bytes per window).  A multi-GPU caller shards the windows by truncating the
+ * panel: windows [w0, w1) of (T, P) are windows 0..w1-w0-1 of the leading
+ * T - P + w1 rows with P' = w1 - w0 (window w only reads rows < T - P + w). */
+int dfm_windows_dev(dfm_ctx *ctx, const double *y_dev, const double *w_dev, int q, int64_t ldw,
+                    const double *X_dev, int64_t T, int64_t N, int64_t ldx, int P, int crit,
+                    int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
+                    double *coef_out, double *tstat_out);
 
 /* --------------------------------------------------- targeted predictors
  * targeted_predictors(..., thresholding="hard") (src/targeted_predictors.jl:9-30).

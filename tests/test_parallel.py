@@ -70,3 +70,85 @@ def test_gloo_world2_gather_order(dfm, B):
     ref = np.stack([b, b * b + 0.5, np.sin(b)], axis=1)
     for r in (0, 1):
         assert np.array_equal(res[r], ref)
+
+
+def test_window_shard_ranges(dfm):
+    from dfm_amd.parallel import window_shard
+    for T, P in ((2000, 200), (30, 7), (50, 3)):
+        for world in (1, 2, 3, 8):
+            got = []
+            for r in range(world):
+                w0, w1, rows = window_shard(T, P, world, r)
+                assert rows == T - P + w1 and rows <= T
+                got.extend(range(w0, w1))
+            assert got == list(range(P))
+
+
+def _oracle_windows(O, y, w, x, P, kmax):
+    """pseudo_out_of_sample_refits' dict from the oracle's serial refit loop
+    (src/utils.jl:54-72) on the given rows."""
+    T, N = x.shape
+    from dfm_amd.api import _window_kmax
+    K = _window_kmax(T, N, kmax)
+    fits = O.expanding_window_refits(y, w, x, P, lambda yy, ww, xx: O.DynamicFactorModel_ic(
+        yy, ww, xx, "ICp2", kmax=kmax))
+    out = {"number_of_factors": np.array([o.number_of_factors for o in fits], dtype=np.int64),
+           "V": np.array([O.factor_residual_variance(o) for o in fits]),
+           "criterion_value": np.array([o.number_of_factors_criterion_value for o in fits]),
+           "eigenvalues": np.full((P, K), np.nan), "coefficients": np.full((P, 1 + K), np.nan),
+           "t_stats": np.full((P, 1 + K), np.nan)}
+    for j, o in enumerate(fits):
+        ev = o.eigenvalues[0][:K]
+        out["eigenvalues"][j, :ev.size] = ev
+        out["coefficients"][j, :o.coefficients.size] = o.coefficients
+        out["t_stats"][j, :o.t_stats.size] = o.t_stats
+    return out
+
+
+def _window_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch.distributed as dist
+    import dfm_pkg
+    import dfm_oracle as O
+    dfm_pkg.load()
+    from dfm_amd.parallel import windows_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T, N, P, kmax = 40, 90, 5, 4
+    rng = np.random.default_rng(5)
+    y, x, *_ = O.factor_model_DGP(T, N, 2, rng)
+    x, w = O.normalize(x), np.ones((T, 1))
+    # stand-in for the per-rank GPU call: the oracle on the shard's leading rows
+    got = windows_sharded(lambda rows, n: _oracle_windows(O, y[:rows], w[:rows], x[:rows], n, kmax),
+                          T, N, 1, P, kmax)
+    q.put((rank, got, _oracle_windows(O, y, w, x, P, kmax) if rank == 0 else None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_windows_sharded(dfm):
+    """Windows sharded over 2 ranks by leading-row truncation and gathered in
+    window order equal the unsharded serial refit loop exactly."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_window_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, got, ref = q.get(timeout=180)
+        res[r] = (got, ref)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = res[0][1]
+    for r in (0, 1):
+        got = res[r][0]
+        for f in ("number_of_factors", "V", "criterion_value", "eigenvalues", "coefficients", "t_stats"):
+            assert np.array_equal(got[f], ref[f], equal_nan=True), f
