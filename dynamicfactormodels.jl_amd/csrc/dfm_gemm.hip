@@ -405,6 +405,118 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// gram_dma_kernel: G = X X' of a plain row-major panel (m x K, ld % 16 == 0,
+// zero columns K..ld-1) — the N > T Gram of principal_components
+// (src/DynamicFactorModel.jl:87 `x*x'`) when no resample gather is fused: the
+// base fit's H = E E' and the expanding windows' one prefix Gram
+// (src/utils.jl:59-65 through the prefix identity).  Both
+// operands are row blocks of X in [a][k] images, staged by LDS-DMA through the
+// 4-deep ring of gemmh_kernel; only lower-triangular 64 x 64 tiles run, the
+// epilogue writes both halves.  Split-K over blockIdx-derived z (partial
+// images summed in fixed order by the caller).  XCD-aware order: the work
+// list (z-major, then column tile J, then row tile I >= J) is cut into 8
+// contiguous spans, XCD x taking span x, so the workgroups resident on one XCD
+// share one k-range and a few column blocks (operands re-read from its L2).
+DFM_DEV void gd_issue(double *stage, const double *__restrict__ X, const G2Src &src, int k0) {
+  double *la = stage, *lb = stage + GT * G2_KS;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c_off = (2 * (threadIdx.x >> 6) + h) * 128;
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(X + src.a[h] + k0), (lds_void_t *)(la + c_off), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)(X + src.b[h] + k0), (lds_void_t *)(lb + c_off), 16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gram_dma_kernel(const double *__restrict__ X, int64_t ld, int m, int K,
+                                                          int nt, int tiles, int items, int span, int ksteps,
+                                                          double *__restrict__ G, int64_t ldg, int64_t strideZ) {
+  constexpr int NBUF = 4;
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int item = (blockIdx.x & 7) * span + (blockIdx.x >> 3);
+  if (item >= items) return;
+  const int z = item / tiles;
+  int u = item - z * tiles, J = 0;
+  while (u >= nt - J) { u -= nt - J; ++J; }
+  const int I = J + u;
+  const int abase = I * GT, bbase = J * GT;
+  // per-lane DMA sources: A chunk rows of block I, B chunk rows of block J
+  G2Src src;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 2 * wave + h;
+    const int a = 8 * c + (lane >> 3);
+    const int ka = (2 * (lane & 7)) ^ (((a >> 1) & 1) << 3);
+    src.a[h] = (int64_t)min(abase + a, m - 1) * ld + ka;   // rows past m: finite, discarded outputs
+    src.b[h] = (int64_t)min(bbase + a, m - 1) * ld + ka;
+    src.kb[h] = 0;
+  }
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int s0 = z * ksteps;
+  const int nst = min((K + G2_KS - 1) / G2_KS, s0 + ksteps) - s0;   // the k tail reads ld's zero padding
+  const int kbase = s0 * G2_KS;
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) gd_issue(lds + (s % NBUF) * G2_STAGE, X, src, kbase + s * G2_KS);
+  for (int s = 0; s < nst; ++s) {
+    const int ahead = min(NBUF - 2, nst - 1 - s);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NBUF - 1 < nst)
+      gd_issue(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, X, src, kbase + (s + NBUF - 1) * G2_KS);
+    const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    double af[8], bf[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = la[g2_offA(wr * 32 + 4 * f + fi, fkc)];
+      bf[f] = lb[g2_offA(wc * 32 + 4 * f + fi, fkc)];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+  const bool diag = I == J;
+  double *Gz = G + (int64_t)z * strideZ;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2],
+                   a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int row = abase + wr * 32 + 4 * fa + oi;
+      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+      if (row < m && col < m) {
+        Gz[(int64_t)row * ldg + col] = v;
+        if (!diag) Gz[(int64_t)col * ldg + row] = v;
+      }
+    }
+}
+
+// One launch of gram_dma_kernel over split-K partial images: S images of
+// strideZ elements at G (S == 1: G is the output itself).
+hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int ksteps, double *G, int64_t ldg,
+                           int64_t strideZ, hipStream_t st) {
+  const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2, items = tiles * S;
+  const int span = (items + 7) / 8;
+  hipLaunchKernelGGL(gram_dma_kernel, dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span, ksteps,
+                     G, ldg, strideZ);
+  return hipGetLastError();
+}
+
 static int gemm_variant() {
   static const int v = [] { const char *e = getenv("DFM_GEMM"); return e ? atoi(e) : 2; }();
   return v;

@@ -20,6 +20,7 @@
 // Requirements: panels C/E have zero-filled padding columns N..ld-1 and
 // ld % 16 == 0.  Output G is the full symmetric m x m matrix (row-major, ldg).
 #include <algorithm>
+#include <cstdlib>
 
 #include "dfm_common.h"
 
@@ -208,12 +209,46 @@ int gram_ksplit(int m, int K) {
   return std::max(1, std::min(16, K / 1536));
 }
 
+hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int ksteps, double *G, int64_t ldg,
+                           int64_t strideZ, hipStream_t st);
+// DFM_GRAM_DMA=0 keeps the register-staged kernel for plain panels (A/B switch)
+static bool gram_dma_enabled() {
+  static const bool on = [] { const char *e = getenv("DFM_GRAM_DMA"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
+// K-split of ONE plain-panel Gram (no replicate batch, so no batch
+// invariance to keep): enough (tile, split) workgroups to fill the 512
+// two-per-CU slots several times over with a last round >= 90 % full, each
+// split >= 256 deep.  C5's prefix Gram (528 tiles, K = 20000): S = 7.
+int gram_ksplit_single(int m, int K) {
+  static const int force = [] { const char *e = getenv("DFM_GRAM_SPLIT"); return e ? atoi(e) : 0; }();
+  if (force > 0) return std::min(force, std::max(1, K / 16));   // tuning override
+  const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2, slots = 512;
+  const int smax = std::max(1, std::min(32, K / 256));
+  for (int S = 1; S <= smax; ++S) {
+    const int64_t items = (int64_t)tiles * S, rounds = (items + slots - 1) / slots;
+    if (items >= 4 * slots && items * 10 >= rounds * slots * 9) return S;
+  }
+  if ((int64_t)tiles * smax <= slots) return smax;   // small Gram: one partial round, deepest split
+  int best = 1;
+  double beff = 0.0;
+  for (int S = 1; S <= smax; ++S) {
+    const int64_t items = (int64_t)tiles * S, rounds = (items + slots - 1) / slots;
+    const double eff = (double)items / (double)(rounds * slots);
+    if (items >= slots && eff > beff + 1e-9) { beff = eff; best = S; }
+  }
+  return best;
+}
+
 // Dispatch.  Returns hipError of the launch.
 hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G,
                        int64_t ldg, int64_t strideG, int nrep, hipStream_t st) {
   const int nt = (m + GT - 1) / GT;
   const int nsteps = (K + KS - 1) / KS;
-  const int S0 = gram_ksplit(m, K);
+  const bool plain = orient == ORIENT_ROWS && !src.C && !src.eta && !src.idx && src.ld % 16 == 0 && nrep == 1 &&
+                     m >= GT && gram_dma_enabled();
+  const int S0 = plain ? gram_ksplit_single(m, K) : gram_ksplit(m, K);
   const int ksteps = (nsteps + S0 - 1) / S0, S = (nsteps + ksteps - 1) / ksteps;
   double *Gk = G, *W = nullptr;
   int64_t sG = strideG, sZ = 0;
@@ -226,6 +261,17 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
     Gk = W; sZ = elems; sG = elems * S;
   }
   const bool c = src.C != nullptr, e = src.eta != nullptr, x = src.idx != nullptr;
+  // a plain row-major panel (no fused gather): LDS-DMA SYRK (dfm_gemm.hip).
+  // The k-split counts 16-deep steps of both kernels alike, so the partial
+  // sums (and the result bits) do not depend on which kernel ran.
+  if (plain) {
+    hipError_t er = launch_gram_dma(src.E, src.ld, m, K, S, ksteps, Gk, ldg, sZ, st);
+    if (er == hipSuccess && S > 1)
+      hipLaunchKernelGGL(gram_splitk_sum_kernel, dim3((unsigned)std::min<int64_t>((elems + 255) / 256, 4096), 1),
+                         dim3(256), 0, st, W, S, m, ldg, elems, G, strideG);
+    if (W) hipFreeAsync(W, st);
+    return er != hipSuccess ? er : hipGetLastError();
+  }
   for (int r0 = 0; r0 < nrep; r0 += nrc) {
   const int nr = std::min(nrc, nrep - r0);
   PanelSrc sub = src;
