@@ -12,7 +12,10 @@ from test_gpu_parity import panel, STAT_RTOL, assert_fit_matches, max_sin_angle,
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("T,N", [(400, 300), (250, 900), (141, 500), (900, 141), (1100, 1300)])
+# (70, 5003), (700, 6001): the N > T plain-panel Gram on LDS-DMA (gram_dma_kernel)
+# with m % 64 != 0, K % 16 != 0 and deep split-K (S = 19, 15)
+@pytest.mark.parametrize("T,N", [(400, 300), (250, 900), (141, 500), (900, 141), (1100, 1300), (70, 5003),
+                                 (700, 6001)])
 def test_gram_spectrum_any_size(dfm, oracle, T, N):
     _, x, _ = panel(oracle, T, N, 4, 7000 + T)
     G = x.T @ x if T >= N else x @ x.T
