@@ -292,7 +292,7 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     if gram_n:   # rank-local prefix Gram of the rows its windows reach: rows (rows+1) N flop (SYRK count)
         per = gram_ms / gram_n
         ach = rows * (rows + 1) * N5 / (per * 1e-3) / 1e12
-        roof = {"kernel": "gram_kernel<ROWS> (prefix Gram X X' of the leading rows, v_mfma_f64_4x4x4_4b)",
+        roof = {"kernel": "gram_dma_kernel (prefix Gram X X' of the leading rows: LDS-DMA ring, v_mfma_f64_4x4x4_4b)",
                 "bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(per, 4),
                 "flop_per_launch": rows * (rows + 1) * N5}
