@@ -405,6 +405,16 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
   return hipGetLastError();
 }
 
+// Ring/occupancy choice of the LDS-DMA kernels by output height: rows >= 1024
+// run the 3-deep ring at 3 workgroups per CU (DFM_GEMM_RING3=0/1 forces).
+static bool gemm_ring3(int M) {
+  static const int f = [] { const char *e = getenv("DFM_GEMM_RING3"); return e ? atoi(e) : -1; }();
+  return f >= 0 ? f != 0 : M >= 1024;
+}
+
+// resident gram_dma_kernel workgroups on the chip for an m-row Gram
+int gram_dma_slots(int m) { return (gemm_ring3(m) ? 3 : 2) * 256; }
+
 // ---------------------------------------------------------------------------
 // gram_dma_kernel: G = X X' of a plain row-major panel (m x K, ld % 16 == 0,
 // zero columns K..ld-1) — the N > T Gram of principal_components
@@ -428,10 +438,10 @@ DFM_DEV void gd_issue(double *stage, const double *__restrict__ X, const G2Src &
   }
 }
 
-__global__ __launch_bounds__(256, 2) void gram_dma_kernel(const double *__restrict__ X, int64_t ld, int m, int K,
-                                                          int nt, int tiles, int items, int span, int ksteps,
-                                                          double *__restrict__ G, int64_t ldg, int64_t strideZ) {
-  constexpr int NBUF = 4;
+template <int NBUF, int MINB>
+__global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__restrict__ X, int64_t ld, int m, int K,
+                                                             int nt, int tiles, int items, int span, int ksteps,
+                                                             double *__restrict__ G, int64_t ldg, int64_t strideZ) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -512,8 +522,14 @@ hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int
                            int64_t strideZ, hipStream_t st) {
   const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2, items = tiles * S;
   const int span = (items + 7) / 8;
-  hipLaunchKernelGGL(gram_dma_kernel, dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span, ksteps,
-                     G, ldg, strideZ);
+  // 3-deep ring at 3 workgroups per CU for the large Grams (more resident
+  // waves beat a deeper ring there: tools/gemm_bench.hip, M = 2000)
+  if (gemm_ring3(m))
+    hipLaunchKernelGGL((gram_dma_kernel<3, 3>), dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span,
+                       ksteps, G, ldg, strideZ);
+  else
+    hipLaunchKernelGGL((gram_dma_kernel<4, 2>), dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span,
+                       ksteps, G, ldg, strideZ);
   return hipGetLastError();
 }
 
@@ -533,8 +549,14 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
   if (!a_trans && gemm_variant() == 2 && lda >= (K + G2_KS - 1) / G2_KS * G2_KS && Nc % 2 == 0 && Nc >= 2)
-    hipLaunchKernelGGL(gemmh_kernel, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb, col_done,
-                       col_group);
+  {
+    if (gemm_ring3(M))
+      hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
+                         col_done, col_group);
+    else
+      hipLaunchKernelGGL(gemmh_kernel, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb, col_done,
+                         col_group);
+  }
   else if (a_trans)
     hipLaunchKernelGGL(gemm_kernel<true>, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
                        col_done, col_group);
