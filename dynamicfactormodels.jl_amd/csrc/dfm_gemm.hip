@@ -28,6 +28,13 @@ DFM_DEV int off_rows(int a, int kc) { return a * KS + (kc ^ ((a & 3) << 3)); }  
 DFM_DEV int off_cols(int a, int kc) { return kc * GT + (a ^ ((kc & 7) << 2)); }  // [k][a]
 }  // namespace
 
+// Ring/occupancy choice of the LDS-DMA kernels by output height: rows >= 1024
+// run the 3-deep ring at 3 workgroups per CU (DFM_GEMM_RING3=0/1 forces).
+static bool gemm_ring3(int M) {
+  static const int f = [] { const char *e = getenv("DFM_GEMM_RING3"); return e ? atoi(e) : -1; }();
+  return f >= 0 ? f != 0 : M >= 1024;
+}
+
 // One stage of staging registers (4 A chunks + 4 B chunks of 16 B per
 // thread) kept as a plain struct of scalars: no lambdas capturing arrays by
 // reference and no conditional loads, both of which make the compiler route
@@ -332,11 +339,11 @@ DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda
   }
 }
 
-__global__ __launch_bounds__(256, 2) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
-                                                               const double *__restrict__ B, int64_t ldb, int M,
-                                                               int Nc, int K, int nrb, int ncb, int r, double invT,
-                                                               double *__restrict__ Lout) {
-  constexpr int NBUF = 4;
+template <int NBUF, int MINB>
+__global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
+                                                                  const double *__restrict__ B, int64_t ldb, int M,
+                                                                  int Nc, int K, int nrb, int ncb, int r, double invT,
+                                                                  double *__restrict__ Lout) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -400,16 +407,11 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
                                 int r, double invT, double *Lout, hipStream_t st) {
   const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int nrb8 = (nrb + 7) / 8;
-  hipLaunchKernelGGL(gemm_loadings_kernel, dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N, Nc, K, nrb,
-                     ncb, r, invT, Lout);
+  // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here: the
+  // skinny K = T + r reduction leaves too few stages to hide the ring's fill)
+  hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N, Nc,
+                     K, nrb, ncb, r, invT, Lout);
   return hipGetLastError();
-}
-
-// Ring/occupancy choice of the LDS-DMA kernels by output height: rows >= 1024
-// run the 3-deep ring at 3 workgroups per CU (DFM_GEMM_RING3=0/1 forces).
-static bool gemm_ring3(int M) {
-  static const int f = [] { const char *e = getenv("DFM_GEMM_RING3"); return e ? atoi(e) : -1; }();
-  return f >= 0 ? f != 0 : M >= 1024;
 }
 
 // resident gram_dma_kernel workgroups on the chip for an m-row Gram
