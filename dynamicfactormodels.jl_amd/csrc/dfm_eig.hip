@@ -1203,7 +1203,8 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
                                                       const double *__restrict__ eta,
                                                       const double *__restrict__ HZ, int64_t ldz,
                                                       const double *__restrict__ ab,
-                                                      const double *__restrict__ Qc, double *__restrict__ Yo) {
+                                                      const double *__restrict__ Qc, int64_t qs,
+                                                      double *__restrict__ Yo) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -1246,7 +1247,7 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
     for (int a = 0; a < NT; ++a)
 #pragma unroll
       for (int b = 0; b < NT; ++b) acc[m3][a][b] = dv4{0.0, 0.0, 0.0, 0.0};
-  const double *Qr = Qc + (int64_t)rep * T * P;
+  const double *Qr = Qc + (int64_t)rep * qs;   // qs = 0: the shared warm start (first step)
   double *Yr = Yo + (int64_t)rep * T * P;
   const int ntile = (T + 15) >> 4;
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
@@ -1451,8 +1452,8 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
                                                        int it, int init, int last, int cheb,
                                                        const double *__restrict__ eta,
                                                        const int *__restrict__ off, const int *__restrict__ lst,
-                                                       const double *__restrict__ Qc, double *__restrict__ Yq,
-                                                       double *__restrict__ Zc, int64_t ldz,
+                                                       const double *__restrict__ Qc, int64_t qs,
+                                                       double *__restrict__ Yq, double *__restrict__ Zc, int64_t ldz,
                                                        double *__restrict__ ab, uint64_t seed) {
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
@@ -1486,7 +1487,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
       bBm[kk][ct] = init ? 0.0 : small[P * P + (4 * kk + lk) * P + c];
     }
   }
-  const double *Qr = Qc + (int64_t)rep * T * P;
+  const double *Qr = Qc + (int64_t)rep * qs;   // qs = 0: the shared warm start (init / first step)
   double *Yr = Yq + (int64_t)rep * T * P;
   // Chebyshev coefficients from b = theta_p (boot_cheb_kernel): X = cf1 V + cf0 Q Bm
   const double bch = init ? 0.0 : small[2 * P * P + p - 1];
@@ -1749,18 +1750,27 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
   double *cur = w.Q, *alt = w.Y;
   const int cheb = cheb_degree() == 2 ? 1 : 0;
+  // the warm start is the same for every replicate: ONE m x P block (Q0),
+  // read with replicate stride 0 by the init pass and the first step's y2 /
+  // ap2 (L2-resident) instead of nb materialised copies
+  double *Q0 = nullptr;
+  if (hipMallocAsync((void **)&Q0, (size_t)m * P * 8, st) != hipSuccess) return 1002;
+  struct Q0Free { double *q; hipStream_t s; ~Q0Free() { hipFreeAsync(q, s); } } q0free{Q0, st};
+  const double *qin = Q0;
+  int64_t qs = 0;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   {
     const int64_t n = (int64_t)m * P;
-    dim3 grid((unsigned)((n + 255) / 256), nb);
-    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, (int64_t)0);
+    dim3 grid((unsigned)((n + 255) / 256), 1);
+    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0);
+    hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, eta,
-                       off, lst, cur, alt, Zc, ldz, ab, seed);
+                       off, lst, qin, qs, alt, Zc, ldz, ab, seed);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  int it = 0, last_gemm = -1, last_cheb = -1;
+  int it = 0, last_gemm = -1, last_cheb = -1, next_poll = poll - 1;
   for (; it < maxit; ++it) {
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
     hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
@@ -1769,14 +1779,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
     hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(256), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, ab,
-                       cur, alt);
+                       qin, qs, alt);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, jacobi_sweeps());
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
-                       it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, cur, alt, Zc, ldz, ab, seed);
+                       it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, qin, qs, alt, Zc, ldz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (cheb && it < maxit - 1) {
       // second product G* V and the degree-2 Chebyshev combination: the new
@@ -1793,12 +1803,17 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     } else {
       std::swap(cur, alt);
     }
-    if ((it + 1) % poll == 0) {
+    qin = cur;
+    qs = (int64_t)m * P;
+    if (it == next_poll) {
       int a = -1;
       hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
       e = hipStreamSynchronize(st);
       if (e != hipSuccess) return 1000 + (int)e;
       if (a == 0) { ++it; break; }
+      // a straggler tail (< 1/8 of the batch active): poll every step, so the
+      // empty iterations after its last replicate retires are not launched
+      next_poll = it + ((int64_t)a * 8 < nb ? 1 : poll);
     }
   }
   g_last_iters = it;
