@@ -853,23 +853,58 @@ struct FactBase {
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta, int *__restrict__ off,
                                                         int *__restrict__ lst, double *__restrict__ trace) {
-  extern __shared__ int sh[];   // cnt[T+1], cur[T]
+  extern __shared__ int sh[];   // cnt[T+1], six[T]
   __shared__ double red[256];
+  __shared__ int scan[256];
   const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
   const int32_t *ix = idx + (int64_t)rep * T;
   const double *et = eta ? eta + (int64_t)rep * T : nullptr;
-  int *cnt = sh, *cur = sh + T + 1;
+  int *cnt = sh, *six = sh + T + 1;
   for (int s = tid; s <= T; s += 256) cnt[s] = 0;
+  for (int t = tid; t < T; t += 256) six[t] = ix[t];
   __syncthreads();
-  for (int t = tid; t < T; t += 256) atomicAdd(&cnt[ix[t] + 1], 1);
+  for (int t = tid; t < T; t += 256) atomicAdd(&cnt[six[t] + 1], 1);
   __syncthreads();
-  if (tid == 0) {
-    for (int s = 1; s <= T; ++s) cnt[s] += cnt[s - 1];
-    for (int s = 0; s < T; ++s) cur[s] = cnt[s];
-    int *L = lst + (int64_t)rep * T;
-    for (int t = 0; t < T; ++t) L[cur[ix[t]]++] = t;   // stable: ascending t per bucket
+  // inclusive scan of cnt[0..T]: per-thread chunks, a 256-wide scan of the chunk sums
+  const int per = (T + 1 + 255) / 256, c0 = min(T + 1, tid * per), c1 = min(T + 1, c0 + per);
+  int run = 0;
+  for (int s = c0; s < c1; ++s) run += cnt[s];
+  scan[tid] = run;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int v = tid >= o ? scan[tid - o] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
   }
+  run = scan[tid] - run;
+  for (int s = c0; s < c1; ++s) { run += cnt[s]; cnt[s] = run; }   // cnt[s] = start of bucket s
   __syncthreads();
+  // stable placement: t goes to start(ix_t) + #{t' < t : ix_t' = ix_t}
+  // (ascending t per bucket — the serial counting sort's order); the t' loop
+  // is uniform across the workgroup, so six[t'] is a broadcast read
+  int *L = lst + (int64_t)rep * T;
+  constexpr int TPT = 2;   // t's per thread per pass
+  for (int base = 0; base < T; base += 256 * TPT) {
+    int mine[TPT], rank[TPT];
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+      const int t = base + q * 256 + tid;
+      mine[q] = t < T ? six[t] : -1;
+      rank[q] = 0;
+    }
+    const int tend = min(T, base + 256 * TPT);
+    for (int u = 0; u < tend; ++u) {
+      const int v = six[u];
+#pragma unroll
+      for (int q = 0; q < TPT; ++q) rank[q] += (v == mine[q] && u < base + q * 256 + tid) ? 1 : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < TPT; ++q) {
+      const int t = base + q * 256 + tid;
+      if (t < T) L[cnt[mine[q]] + rank[q]] = t;
+    }
+  }
   for (int s = tid; s <= T; s += 256) off[(int64_t)rep * (T + 1) + s] = cnt[s];
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
