@@ -76,6 +76,32 @@ def pmc_traffic(kernel):
     return None if rec is None else rec.get("hbm_bytes_per_launch")
 
 
+def hbm_rooflines(timing, eig, Bn, steps):
+    """Achieved HBM bandwidth of the per-replicate gather/residual passes of
+    the factored solver (HIP-event time of their kernel class over the timed
+    region; algorithmic bytes per replicate-pass, DESIGN.md section 3, P = 16):
+      y2  (class eig_gq):    Y = G*Q rows from the gathered HZ rows, Q'Y / Y'Y / Q'Q:
+                             reads Q and HZ[idx], writes Y = 3 T P 8 B per Rayleigh-Ritz step
+      ap2 + Chebyshev step (class eig_apply): 5 T P 8 B per pass (Q, Y in; X, Qn, Z out);
+                             passes = Rayleigh-Ritz steps + one init per replicate + Chebyshev steps
+    Replicate-passes come from the library's own counters (eig_iterations)."""
+    P = 16
+    out = []
+    rr = eig.get("replicate_iterations", 0)
+    cheb = eig.get("gemm_products", 0) - rr
+    for cls, name, per, units in (
+            ("eig_gq", "boot_y2_kernel", 3 * T * P * 8, rr),
+            ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel", 5 * T * P * 8, rr + Bn * steps + max(cheb, 0))):
+        ms, n = timing.get(cls, (0.0, 0))
+        if not n or not units:
+            continue
+        gbs = per * units / (ms * 1e-3) / 1e9
+        out.append({"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_replicate_pass": per,
+                    "replicate_passes": int(units)})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,6 +251,7 @@ def main():
         "eig_filter": ("subspace iteration" if os.environ.get("DFM_CHEB") == "1" else
                        "degree-2 Chebyshev filter on [0, theta_p] between Rayleigh-Ritz steps"),
         "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
+        "roofline_hbm": hbm_rooflines(timing, eig, Bn, args.steps),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
