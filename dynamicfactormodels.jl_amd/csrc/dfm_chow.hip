@@ -14,6 +14,8 @@
 //         Cov22 = sum_t u_t^2 z_t z_t',  z_t = Wa'f_t (t < bp), (Wa+Wb)'f_t
 //         (t >= bp) — one r x r accumulator per variable instead of the
 //         reference's T x T diagm sandwich (:25-33).
+#include <algorithm>
+
 #include "dfm_small.h"
 
 namespace dfm {
@@ -111,8 +113,9 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
   __shared__ double sF[TR * R], sZ[TR * R], sE[TR];
   __shared__ int sI[TR];
   __shared__ ChowPrep P;
-  const int tid = threadIdx.x, rep = blockIdx.y, i = blockIdx.x * 256 + tid;
-  for (int e = tid; e < (int)(sizeof(ChowPrep) / 8); e += 256)
+  // one thread per variable; the block is sized to the panel width (64 .. 256)
+  const int tid = threadIdx.x, nth = blockDim.x, rep = blockIdx.y, i = blockIdx.x * nth + tid;
+  for (int e = tid; e < (int)(sizeof(ChowPrep) / 8); e += nth)
     reinterpret_cast<double *>(&P)[e] = reinterpret_cast<const double *>(prep + rep)[e];
   const double *Fr = F + (int64_t)rep * T * r;
   const double *Zr = Z + (int64_t)rep * T * r;
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
   const double *eta = HAS_ETA ? src.eta + (int64_t)rep * src.rs : nullptr;
   const bool ok = i < N;
   auto stage = [&](int t0) {
-    for (int e = tid; e < TR * R; e += 256) {
+    for (int e = tid; e < TR * R; e += nth) {
       const int rr = e / R, j = e % R, t = t0 + rr;
       sF[e] = (t < T && j < r) ? Fr[(int64_t)t * r + j] : 0.0;
       sZ[e] = (t < T && j < r) ? Zr[(int64_t)t * r + j] : 0.0;
@@ -262,7 +265,9 @@ static void launch_chow_r(const PanelSrc &src, int T, int N, int r, int bp, int 
                           const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
                           double *LM, double *WD, hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
-  dim3 grid((N + 255) / 256, nb), block(256);
+  // narrow panels (C2: N = 130) get a 192-thread block, not a half-idle 256
+  const int nth = std::min(256, (N + 63) / 64 * 64);
+  dim3 grid((N + nth - 1) / nth, nb), block(nth);
 #define DFM_CH(C_, E_, X_)                                                                       \
   hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_>), grid, block, 0, st, src, T, N, r, bp, F, Z, \
                      prep, Lm, LR, LM, WD)
@@ -283,7 +288,10 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
   double *scr = (double *)(ws + ws_bytes) - (size_t)3 * nb * N;
   hipLaunchKernelGGL(chow_prep_kernel, dim3(nb), dim3(256), 0, st, F, T, r, bp, prep, Z);
   double *LR = scr, *LM = scr + (size_t)nb * N, *WD = scr + (size_t)2 * nb * N;
-  if (r <= 8) launch_chow_r<8>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  // R = padded factor count of the per-variable register blocks (zero
+  // padding: r <= 4 runs 4-wide, 10 HC0 accumulators instead of 36)
+  if (r <= 4) launch_chow_r<4>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  else if (r <= 8) launch_chow_r<8>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
   else launch_chow_r<16>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
   // scatter into the caller's strided output rows
   if (LRo) hipMemcpy2DAsync(LRo, (size_t)out_stride * 8, LR, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);
