@@ -51,6 +51,7 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
   extern __shared__ double sm[];
   double *vp = sm, *wp = sm + mst, *v = sm + 2 * mst, *p = sm + 3 * mst;
   __shared__ double red[TRI_WAVES];
+  __shared__ double pcol[TRI_WAVES * 128];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int rep = blockIdx.x;
   const double *g = G + (int64_t)rep * strideG;
@@ -98,44 +99,50 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
     if (tout && tid == 0) tout[(int64_t)rep * mst + k] = tau;
     __syncthreads();
     if (k + 1 >= m) break;
-    // 2. one pass over the trailing triangle: apply the pending rank-2 update,
-    //    store, and accumulate p = A v (row part by wave reduction, the
-    //    mirrored column part by LDS atomics)
+    // 2. one pass over the trailing triangle in 128-column panels: apply the
+    //    pending rank-2 update, store, and accumulate p = A v in a FIXED order
+    //    (bit-reproducible, no float atomics): a row's part by one wave
+    //    reduction per (row, panel), added by the row's owning wave in panel
+    //    order; the mirrored column part per lane over the wave's rows, summed
+    //    over the waves in wave order once the panel is done
     const bool refl = tau != 0.0;
-    for (int a = k + 1 + wv; a < m; a += TRI_WAVES) {
-      const double vpa = vp[a], wpa = wp[a], va = v[a];
-      double *Sa = S + (int64_t)a * m;
-      double acc = 0.0;
-      int b = a + lane;
-      for (; b + 192 < m; b += 256) {
-        double s0 = Sa[b], s1 = Sa[b + 64], s2 = Sa[b + 128], s3 = Sa[b + 192];
-        s0 -= vpa * wp[b] + wpa * vp[b];
-        s1 -= vpa * wp[b + 64] + wpa * vp[b + 64];
-        s2 -= vpa * wp[b + 128] + wpa * vp[b + 128];
-        s3 -= vpa * wp[b + 192] + wpa * vp[b + 192];
-        Sa[b] = s0; Sa[b + 64] = s1; Sa[b + 128] = s2; Sa[b + 192] = s3;
-        if (refl) {
-          acc += s0 * v[b] + s1 * v[b + 64] + s2 * v[b + 128] + s3 * v[b + 192];
-          if (b > a) atomicAdd(&p[b], s0 * va);
-          atomicAdd(&p[b + 64], s1 * va);
-          atomicAdd(&p[b + 128], s2 * va);
-          atomicAdd(&p[b + 192], s3 * va);
+    for (int b0 = (k + 1) & ~127; b0 < m; b0 += 128) {
+      const int bA = b0 + lane, bB = b0 + 64 + lane;
+      const int alast = min(m - 1, b0 + 127);
+      double cA = 0.0, cB = 0.0;
+      for (int a = k + 1 + wv; a <= alast; a += TRI_WAVES) {
+        const double vpa = vp[a], wpa = wp[a], va = v[a];
+        double *Sa = S + (int64_t)a * m;
+        double rp = 0.0;
+        if (bA >= a && bA < m) {
+          const double s = Sa[bA] - (vpa * wp[bA] + wpa * vp[bA]);
+          Sa[bA] = s;
+          rp = s * v[bA];
+          if (bA > a) cA = fma(s, va, cA);
         }
-      }
-      for (; b < m; b += 64) {
-        const double s = Sa[b] - (vpa * wp[b] + wpa * vp[b]);
-        Sa[b] = s;
+        if (bB >= a && bB < m) {
+          const double s = Sa[bB] - (vpa * wp[bB] + wpa * vp[bB]);
+          Sa[bB] = s;
+          rp = fma(s, v[bB], rp);
+          if (bB > a) cB = fma(s, va, cB);
+        }
         if (refl) {
-          acc += s * v[b];
-          if (b > a) atomicAdd(&p[b], s * va);
+          rp = wave_sum(rp);
+          if (lane == 0) p[a] += rp;
         }
       }
       if (refl) {
-        acc = wave_sum(acc);
-        if (lane == 0) atomicAdd(&p[a], acc);
+        pcol[wv * 128 + lane] = cA;
+        pcol[wv * 128 + 64 + lane] = cB;
       }
+      __syncthreads();
+      if (refl && tid < 128 && b0 + tid < m) {
+        double sum = 0.0;
+        for (int w2 = 0; w2 < TRI_WAVES; ++w2) sum += pcol[w2 * 128 + tid];
+        p[b0 + tid] += sum;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     // 3. w = tau p - (tau^2/2)(p'v) v becomes the pending update
     double pv = 0.0;
     for (int i = k + 1 + tid; i < m; i += TRI_THREADS) pv += p[i] * v[i];

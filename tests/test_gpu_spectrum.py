@@ -249,3 +249,17 @@ def test_reference_test_workflow_from_csv(dfm, oracle, tmp_path):
     ssr_g, ssr_o = np.sum(g.factor_residuals ** 2), np.sum(o.factor_residuals ** 2)
     assert abs(ssr_g - ssr_o) <= 1e-10 * ssr_o
     assert rel(g.t_stats[:5], o.t_stats[:5]) < 1e-8       # intercept and lags: sign-invariant
+
+
+def test_dense_spectrum_bit_reproducible(dfm, oracle):
+    """tridiag_kernel accumulates p = A v in a fixed order (no float atomics):
+    repeated calls return identical bits, and the many-factor loadings stay
+    within the parity bar of test_principal_components_many."""
+    import hashlib
+    T, N = 150, 500
+    _, x, _ = panel(oracle, T, N, 4, 7500 + T)
+    digests = set()
+    for _ in range(3):
+        ev, F, L, tr = dfm.principal_components(x, 60)
+        digests.add(hashlib.sha1(np.concatenate([ev, F.ravel(), L.ravel()]).tobytes()).hexdigest())
+    assert len(digests) == 1
