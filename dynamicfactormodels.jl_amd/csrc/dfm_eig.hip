@@ -1028,12 +1028,15 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
                                 int r, double invT, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
-                       const int *col_done = nullptr, int col_group = 1);
+                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false);
 
+// Z (the GEMM's B operand) has round_up(T, 16) rows, the pad rows zero, so
+// the H.Z GEMM streams it with running DMA pointers and no k-tail clamp
+static int64_t z_rows(int T) { return ((int64_t)T + 15) / 16 * 16; }
 size_t fact_workspace_bytes(int T, int nb, int P) {
   const int64_t ldz = (int64_t)nb * P;
   const int nrb = (T + EROWS - 1) / EROWS;
-  return 2 * (size_t)T * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096;
+  return (size_t)(z_rows(T) + T) * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096;
 }
 
 template <int P>
@@ -1045,8 +1048,9 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
   EigWork w = carve(ws, m, nb, P, maxit);
   const int64_t ldz = (int64_t)nb * P;
   double *Zc = (double *)fws;
-  double *HZ = Zc + (size_t)m * ldz;
+  double *HZ = Zc + (size_t)z_rows(m) * ldz;
   double *ab = HZ + (size_t)m * ldz;
+  if (z_rows(m) > m) hipMemsetAsync(Zc + (size_t)m * ldz, 0, (size_t)(z_rows(m) - m) * ldz * 8, st);
   int *off = off_out, *lst = lst_out;
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
@@ -1068,7 +1072,7 @@ static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *
       hipLaunchKernelGGL(boot_fz_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, fb, w, m, eta, off, lst, Zc, ldz, ab);
       if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
       if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
       last_gemm = it;
       if (tf) tf(tctx, DFM_KC_GEMM, 0);
       if (e != hipSuccess) return 1000 + (int)e;
@@ -1777,8 +1781,9 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   EigWork w = carve(ws, m, nb, P, maxit);
   const int64_t ldz = (int64_t)nb * P;
   double *Zc = (double *)fws;
-  double *HZ = Zc + (size_t)m * ldz;
+  double *HZ = Zc + (size_t)z_rows(m) * ldz;
   double *ab = HZ + (size_t)m * ldz;
+  if (z_rows(m) > m) hipMemsetAsync(Zc + (size_t)m * ldz, 0, (size_t)(z_rows(m) - m) * ldz * 8, st);
   const size_t lds = (size_t)m * 8 + (size_t)(2 * m + 1) * 4;
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
@@ -1808,7 +1813,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   int it = 0, last_gemm = -1, last_cheb = -1, next_poll = poll - 1;
   for (; it < maxit; ++it) {
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
-    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
     if (tf) tf(tctx, DFM_KC_GEMM, 0);
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
@@ -1827,7 +1832,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       // second product G* V and the degree-2 Chebyshev combination: the new
       // basis goes back into cur (Q), Y/V stay in alt
       if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P);
+      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
       if (tf) tf(tctx, DFM_KC_GEMM, 0);
       if (e != hipSuccess) return 1000 + (int)e;
       last_cheb = it;

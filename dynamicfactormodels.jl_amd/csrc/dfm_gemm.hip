@@ -235,7 +235,7 @@ DFM_DEV void g2_issue(double *stage, const double *__restrict__ A, const double 
   }
 }
 
-template <int NBUF, int MINB, bool PRIO>
+template <int NBUF, int MINB, bool PRIO, bool RUN = false>
 __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__restrict__ A, int64_t lda,
                                                        const double *__restrict__ B, int64_t ldb,
                                                        double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
@@ -263,7 +263,26 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int nst = (K + G2_KS - 1) / G2_KS;
   const G2Src src = g2_sources(lda, ldb, abase, bbase, M, Nc, wave, lane);
-  for (int s = 0; s < NBUF - 1 && s < nst; ++s) g2_issue(lds + (s % NBUF) * G2_STAGE, A, B, ldb, src, s * G2_KS, K);
+  // RUN: the DMA sources are running pointers advanced by one stage per
+  // issue (no per-stage 64-bit address arithmetic, no k-tail clamp: B holds
+  // zero rows up to round_up(K, 16), as A holds zero k-columns)
+  const double *pa0 = A + src.a[0], *pa1 = A + src.a[1], *pb0 = B + src.b[0], *pb1 = B + src.b[1];
+  const int64_t bstep = (int64_t)G2_KS * ldb;
+  auto issue = [&](int s) {
+    double *stage = lds + (s % NBUF) * G2_STAGE;
+    if (RUN) {
+      double *la = stage, *lb = stage + GT * G2_KS;
+      const int c0 = (2 * wave) * 128, c1 = c0 + 128;
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pa0, (lds_void_t *)(la + c0), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pb0, (lds_void_t *)(lb + c0), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pa1, (lds_void_t *)(la + c1), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pb1, (lds_void_t *)(lb + c1), 16, 0, 0);
+      pa0 += G2_KS; pa1 += G2_KS; pb0 += bstep; pb1 += bstep;
+    } else {
+      g2_issue(stage, A, B, ldb, src, s * G2_KS, K);
+    }
+  };
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
   for (int s = 0; s < nst; ++s) {
     const int ahead = min(AHEAD, nst - 1 - s);   // later stages already issued (4 DMAs each per wave)
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -271,8 +290,7 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + NBUF - 1 < nst)   // ring slot (s-1)%NBUF: its readers all passed this barrier
-      g2_issue(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, A, B, ldb, src, (s + NBUF - 1) * G2_KS, K);
+    if (s + NBUF - 1 < nst) issue(s + NBUF - 1);   // ring slot (s-1)%NBUF: its readers all passed this barrier
     const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
     double af[8], bf[8];
 #pragma unroll
@@ -546,13 +564,19 @@ static int gemm_variant() {
 // the register-staged kernel runs.
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
-                       const int *col_done = nullptr, int col_group = 1) {
+                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false) {
   const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
   if (!a_trans && gemm_variant() == 2 && lda >= (K + G2_KS - 1) / G2_KS * G2_KS && Nc % 2 == 0 && Nc >= 2)
   {
-    if (gemm_ring3(M))
+    // B zero-padded to round_up(K, 16) rows: running DMA pointers, 3-deep
+    // ring at 3 workgroups per CU (tools/gemm_bench.hip: 0.62 of peak at the
+    // C3 shape, 0.75 at M = K = 2000, vs 0.60 / 0.71 for the clamped kernels)
+    if (b_padded && gemm_variant() == 2)
+      hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false, true>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb,
+                         ncb, col_done, col_group);
+    else if (gemm_ring3(M))
       hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
                          col_done, col_group);
     else
