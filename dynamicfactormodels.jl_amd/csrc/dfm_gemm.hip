@@ -357,7 +357,7 @@ DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda
   }
 }
 
-template <int NBUF, int MINB>
+template <int NBUF, int MINB, bool RUN>
 __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
                                                                   const double *__restrict__ B, int64_t ldb, int M,
                                                                   int Nc, int K, int nrb, int ncb, int r, double invT,
@@ -377,8 +377,34 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
     for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int nst = (K + G2_KS - 1) / G2_KS;
-  for (int s = 0; s < NBUF - 1 && s < nst; ++s)
-    g2_issue_t(lds + (s % NBUF) * G2_STAGE, A, lda, B, ldb, s * G2_KS, abase, bbase, M, Nc, K, wave, lane);
+  // RUN: running DMA pointers (both operands hold zero k-rows up to
+  // round_up(K, 16), so the last stage needs no clamp)
+  const double *pa[2], *pb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kc = 2 * (2 * wave + h) + (lane >> 5);
+    const int sw = (2 * (lane & 31)) ^ ((kc & 7) << 2);
+    pa[h] = A + (int64_t)kc * lda + min(abase + sw, (int)lda - 2);
+    pb[h] = B + (int64_t)kc * ldb + min(bbase + sw, Nc - 2);
+  }
+  const int64_t astep = (int64_t)G2_KS * lda, bstep = (int64_t)G2_KS * ldb;
+  auto issue = [&](int s) {
+    double *stage = lds + (s % NBUF) * G2_STAGE;
+    if (RUN) {
+      double *la = stage, *lb = stage + GT * G2_KS;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = 2 * wave + h;
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)pa[h], (lds_void_t *)(la + c * 128), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)pb[h], (lds_void_t *)(lb + c * 128), 16, 0, 0);
+        pa[h] += astep;
+        pb[h] += bstep;
+      }
+    } else {
+      g2_issue_t(stage, A, lda, B, ldb, s * G2_KS, abase, bbase, M, Nc, K, wave, lane);
+    }
+  };
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
   for (int s = 0; s < nst; ++s) {
     const int ahead = min(NBUF - 2, nst - 1 - s);
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -386,9 +412,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + NBUF - 1 < nst)
-      g2_issue_t(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, A, lda, B, ldb, (s + NBUF - 1) * G2_KS, abase, bbase, M,
-                 Nc, K, wave, lane);
+    if (s + NBUF - 1 < nst) issue(s + NBUF - 1);
     const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
     double af[8], bf[8];
 #pragma unroll
@@ -425,10 +449,16 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
                                 int r, double invT, double *Lout, hipStream_t st) {
   const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int nrb8 = (nrb + 7) / 8;
-  // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here: the
-  // skinny K = T + r reduction leaves too few stages to hide the ring's fill)
-  hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N, Nc,
-                     K, nrb, ncb, r, invT, Lout);
+  // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here, with
+  // running pointers still 23 % slower: 4-deep at 2 per CU stays)
+  // running DMA pointers (DFM_LOAD_CFG=0: the clamped per-stage addressing, A/B switch)
+  static const int cfg = [] { const char *e = getenv("DFM_LOAD_CFG"); return e ? atoi(e) : 1; }();
+  if (cfg == 0)
+    hipLaunchKernelGGL((gemm_loadings_kernel<4, 2, false>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb,
+                       N, Nc, K, nrb, ncb, r, invT, Lout);
+  else
+    hipLaunchKernelGGL((gemm_loadings_kernel<4, 2, true>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N,
+                       Nc, K, nrb, ncb, r, invT, Lout);
   return hipGetLastError();
 }
 
