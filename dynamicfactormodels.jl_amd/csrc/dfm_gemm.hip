@@ -478,15 +478,6 @@ int gram_dma_slots(int m) { return (gemm_ring3(m) ? 3 : 2) * 256; }
 // list (z-major, then column tile J, then row tile I >= J) is cut into 8
 // contiguous spans, XCD x taking span x, so the workgroups resident on one XCD
 // share one k-range and a few column blocks (operands re-read from its L2).
-DFM_DEV void gd_issue(double *stage, const double *__restrict__ X, const G2Src &src, int k0) {
-  double *la = stage, *lb = stage + GT * G2_KS;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c_off = (2 * (threadIdx.x >> 6) + h) * 128;
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)(X + src.a[h] + k0), (lds_void_t *)(la + c_off), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)(X + src.b[h] + k0), (lds_void_t *)(lb + c_off), 16, 0, 0);
-  }
-}
 
 template <int NBUF, int MINB>
 __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__restrict__ X, int64_t ld, int m, int K,
@@ -522,7 +513,19 @@ __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__res
   const int s0 = z * ksteps;
   const int nst = min((K + G2_KS - 1) / G2_KS, s0 + ksteps) - s0;   // the k tail reads ld's zero padding
   const int kbase = s0 * G2_KS;
-  for (int s = 0; s < NBUF - 1 && s < nst; ++s) gd_issue(lds + (s % NBUF) * G2_STAGE, X, src, kbase + s * G2_KS);
+  // running DMA pointers: one 64-bit add per operand and stage
+  const double *pa0 = X + src.a[0] + kbase, *pa1 = X + src.a[1] + kbase;
+  const double *pb0 = X + src.b[0] + kbase, *pb1 = X + src.b[1] + kbase;
+  const int c0 = (2 * wave) * 128, c1 = c0 + 128;
+  auto issue = [&](int s) {
+    double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa0, (lds_void_t *)(la + c0), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb0, (lds_void_t *)(lb + c0), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa1, (lds_void_t *)(la + c1), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb1, (lds_void_t *)(lb + c1), 16, 0, 0);
+    pa0 += G2_KS; pa1 += G2_KS; pb0 += G2_KS; pb1 += G2_KS;
+  };
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
   for (int s = 0; s < nst; ++s) {
     const int ahead = min(NBUF - 2, nst - 1 - s);
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -531,7 +534,7 @@ __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__res
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (s + NBUF - 1 < nst)
-      gd_issue(lds + ((s + NBUF - 1) % NBUF) * G2_STAGE, X, src, kbase + (s + NBUF - 1) * G2_KS);
+      issue(s + NBUF - 1);
     const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
     double af[8], bf[8];
 #pragma unroll
