@@ -214,10 +214,11 @@ def main():
         flop_total = 2.0 * T * T * P * eig["gemm_products"]
         per_launch_ms = gemm_ms / gemm_n
         achieved = flop_total / (gemm_ms * 1e-3) / 1e12
-        roof = {"kernel": "gemmh_kernel (batched eigen-iteration H.Z: LDS-DMA 4-deep ring, v_mfma_f64_4x4x4_4b)",
+        roof = {"kernel": "gemmh_kernel_t<3,3,RUN> (batched eigen-iteration H.Z: LDS-DMA 3-deep ring, running "
+                          "source pointers over the zero-padded Z, 3 workgroups/CU, v_mfma_f64_4x4x4_4b)",
                 "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4),
-                "traffic": pmc_traffic("gemmh_kernel_t<4, 2, false>"),
+                "traffic": pmc_traffic("gemmh_kernel_t<3, 3, false, true>"),
                 "avg_launch_ms": round(per_launch_ms, 4),
                 "flop_per_launch": round(flop_total / gemm_n), "launches": gemm_n,
                 "flop_per_replicate_product": 2 * T * T * P}
