@@ -1391,6 +1391,55 @@ DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init,
   }
 }
 
+// ap2_load through a wave-private LDS transpose: the tile's Q and Y rows
+// (16 x P each) are read with coalesced 16-B loads (4 lanes per 128-B row)
+// and re-read from LDS in the MFMA A-operand layout (row lane & 15, column
+// 4 kk + (lane >> 4)), instead of 2 P/4 loads that each touch 16 rows.
+// Row stride P + 1: conflict-free A-layout reads.  F rows and the init
+// layout as ap2_load.
+template <int P>
+DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init, const double *__restrict__ Qr,
+                          const double *Yr, const FactBase &fb, double *tq, double *ty) {
+  constexpr int NT = P / 16, KP = P / 4, PER = P / 4;   // doubles per lane per matrix
+  const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
+  if (!init) {
+    const int rr = lane >> 2, c0 = (lane & 3) * PER, t = t0 + rr;
+    const bool ok = t < T;
+    const int tc = ok ? t : T - 1;
+    double2 qv[PER / 2], yv[PER / 2];
+#pragma unroll
+    for (int j = 0; j < PER / 2; ++j) {
+      qv[j] = *reinterpret_cast<const double2 *>(Qr + (int64_t)tc * P + c0 + 2 * j);
+      yv[j] = *reinterpret_cast<const double2 *>(Yr + (int64_t)tc * P + c0 + 2 * j);
+    }
+#pragma unroll
+    for (int j = 0; j < PER / 2; ++j) {
+      tq[rr * (P + 1) + c0 + 2 * j] = ok ? qv[j].x : 0.0;
+      tq[rr * (P + 1) + c0 + 2 * j + 1] = ok ? qv[j].y : 0.0;
+      ty[rr * (P + 1) + c0 + 2 * j] = ok ? yv[j].x : 0.0;
+      ty[rr * (P + 1) + c0 + 2 * j + 1] = ok ? yv[j].y : 0.0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's writes land before its reads
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) {
+      L.qa[kk] = tq[li * (P + 1) + 4 * kk + lk];
+      L.yo[kk] = ty[li * (P + 1) + 4 * kk + lk];
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) { L.qa[kk] = 0.0; L.yo[kk] = 0.0; }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int t = t0 + 4 * g + lk;
+    const int tc = min(t, T - 1);
+    const double f = fb.F[(int64_t)tc * r + min(li, r - 1)];
+    L.fa[g] = (t < T && li < r) ? f : 0.0;
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = init ? Qr[(int64_t)tc * P + 16 * ct + li] : 0.0;
+  }
+}
+
 // Shared tail of ap2 and the Chebyshev step: Z = P' D Qn by CSR gather
 // (bucket s lists t ascending), cc = EL' Z, and the fixed-order wave sums of
 // a = F' Qn (aacc, accumulated by the caller) and cc into ab[rep].
@@ -1502,6 +1551,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   int *so = (int *)(sdyn + T), *sl = so + T + 1;
   __shared__ double sred[NT * 256];
   __shared__ double sres[4][P];
+  __shared__ double stile[4][2][16 * (P + 1)];   // per-wave Q / Y tile transposes (ap2_load_lds)
   __shared__ int s_conv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
   const int li = lane & 15, lk = lane >> 4;
@@ -1539,7 +1589,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Ap2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += 4) {
-    ap2_load<P>(cur, tile, T, r, lane, init, Qr, Yr, fb);
+    ap2_load_lds<P>(cur, tile, T, r, lane, init, Qr, Yr, fb, stile[wave][0], stile[wave][1]);
     const int t0 = tile * 16;
     double qv[NT][4];
     if (init) {
