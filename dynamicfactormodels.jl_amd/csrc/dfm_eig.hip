@@ -1358,7 +1358,7 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
   }
 }
 
-// One 16-row tile's operands for ap2: Q and Y rows in A-operand layout
+// One 16-row tile's operands for ap2 (ap2_load_lds): Q and Y rows in A-operand layout
 // (row t0 + (lane & 15), column 4kk + (lane >> 4)), F rows for a = F'Qn in
 // A-operand layout per row group g (row t0 + 4g + (lane >> 4), factor lane & 15),
 // and (init) Q in the accumulator layout.  Rows >= T read row T-1 (masked later).
@@ -1366,30 +1366,6 @@ template <int P>
 struct Ap2Tile {
   double qa[P / 4], yo[P / 4], fa[4], q[P / 16][4];
 };
-template <int P>
-DFM_DEV void ap2_load(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init, const double *__restrict__ Qr,
-                      const double *Yr, const FactBase &fb) {
-  constexpr int NT = P / 16, KP = P / 4;
-  const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
-  const int ta = min(t0 + li, T - 1);
-#pragma unroll
-  for (int kk = 0; kk < KP; ++kk) {
-    L.qa[kk] = init ? 0.0 : Qr[(int64_t)ta * P + 4 * kk + lk];
-    L.yo[kk] = init ? 0.0 : Yr[(int64_t)ta * P + 4 * kk + lk];
-  }
-  const bool rowok = t0 + li < T;
-#pragma unroll
-  for (int kk = 0; kk < KP; ++kk) { L.qa[kk] = rowok ? L.qa[kk] : 0.0; L.yo[kk] = rowok ? L.yo[kk] : 0.0; }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int t = t0 + 4 * g + lk;
-    const int tc = min(t, T - 1);
-    const double f = fb.F[(int64_t)tc * r + min(li, r - 1)];
-    L.fa[g] = (t < T && li < r) ? f : 0.0;
-#pragma unroll
-    for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = init ? Qr[(int64_t)tc * P + 16 * ct + li] : 0.0;
-  }
-}
 
 // ap2_load through a wave-private LDS transpose: the tile's Q and Y rows
 // (16 x P each) are read with coalesced 16-B loads (4 lanes per 128-B row)
