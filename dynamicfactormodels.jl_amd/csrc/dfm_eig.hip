@@ -1028,7 +1028,8 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
                                 int r, double invT, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
-                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false);
+                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false,
+                       const int *clist = nullptr, const int *ccount = nullptr);
 
 // Z (the GEMM's B operand) has round_up(T, 16) rows, the pad rows zero, so
 // the H.Z GEMM streams it with running DMA pointers and no k-tail clamp
@@ -1798,6 +1799,34 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
   zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, rep, ab, aacc, sred);
 }
 
+static bool gemm_compact_enabled() {   // DFM_GEMM_COMPACT=0: A/B switch
+  static const bool on = [] { const char *e = getenv("DFM_GEMM_COMPACT"); return !(e && e[0] == '0'); }();
+  return on;
+}
+// Ascending list of the still-active replicates (done == 0) and their count,
+// one 1024-thread workgroup: per-thread chunk counts, an LDS scan, in-order
+// writes.  Feeds the compacted H.Z GEMM of the straggler phase.
+__global__ __launch_bounds__(1024) void active_list_kernel(const int *__restrict__ done, int nb,
+                                                           int *__restrict__ list, int *__restrict__ count) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x, per = (nb + 1023) / 1024;
+  const int b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+  int c = 0;
+  for (int i = b0; i < b1; ++i) c += done[i] ? 0 : 1;
+  part[tid] = c;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int pos = part[tid] - c;
+  for (int i = b0; i < b1; ++i)
+    if (!done[i]) list[pos++] = i;
+  if (tid == 1023) *count = part[1023];
+}
+
 template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
@@ -1820,7 +1849,12 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // read with replicate stride 0 by the init pass and the first step's y2 /
   // ap2 (L2-resident) instead of nb materialised copies
   double *Q0 = nullptr;
-  if (hipMallocAsync((void **)&Q0, (size_t)m * P * 8, st) != hipSuccess) return 1002;
+  if (hipMallocAsync((void **)&Q0, (size_t)m * P * 8 + (size_t)(nb + 4) * 4, st) != hipSuccess) return 1002;
+  // straggler phase (< 1/8 of the batch active at a poll): the GEMMs tile only
+  // the listed replicates' column groups (list built once, a superset of the
+  // later active sets; replicates retired since are computed and ignored)
+  int *alist = (int *)(Q0 + (size_t)m * P), *acount = alist + nb;
+  bool cl_on = false;
   struct Q0Free { double *q; hipStream_t s; ~Q0Free() { hipFreeAsync(q, s); } } q0free{Q0, st};
   const double *qin = Q0;
   int64_t qs = 0;
@@ -1839,7 +1873,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   int it = 0, last_gemm = -1, last_cheb = -1, next_poll = poll - 1;
   for (; it < maxit; ++it) {
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
-    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
+    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
+                               cl_on ? alist : nullptr, cl_on ? acount : nullptr);
     if (tf) tf(tctx, DFM_KC_GEMM, 0);
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
@@ -1854,11 +1889,28 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
                        it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, qin, qs, alt, Zc, ldz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+    if (it == next_poll) {   // convergence poll, right after the step that retires replicates
+      int a = -1;
+      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return 1000 + (int)e;
+      if (a == 0) { ++it; break; }
+      // a straggler tail (< 1/8 of the batch active): poll every step, so the
+      // empty iterations after its last replicate retires are not launched,
+      // and compact the GEMMs to the stragglers' columns
+      const bool tail = (int64_t)a * 8 < nb;
+      next_poll = it + (tail ? 1 : poll);
+      if (tail && !cl_on && gemm_compact_enabled()) {
+        hipLaunchKernelGGL(active_list_kernel, dim3(1), dim3(1024), 0, st, w.done, nb, alist, acount);
+        cl_on = true;
+      }
+    }
     if (cheb && it < maxit - 1) {
       // second product G* V and the degree-2 Chebyshev combination: the new
       // basis goes back into cur (Q), Y/V stay in alt
       if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
+      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
+                      cl_on ? alist : nullptr, cl_on ? acount : nullptr);
       if (tf) tf(tctx, DFM_KC_GEMM, 0);
       if (e != hipSuccess) return 1000 + (int)e;
       last_cheb = it;
@@ -1871,16 +1923,6 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     }
     qin = cur;
     qs = (int64_t)m * P;
-    if (it == next_poll) {
-      int a = -1;
-      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
-      e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return 1000 + (int)e;
-      if (a == 0) { ++it; break; }
-      // a straggler tail (< 1/8 of the batch active): poll every step, so the
-      // empty iterations after its last replicate retires are not launched
-      next_poll = it + ((int64_t)a * 8 < nb ? 1 : poll);
-    }
   }
   g_last_iters = it;
   g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);

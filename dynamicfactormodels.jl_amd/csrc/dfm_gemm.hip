@@ -207,7 +207,15 @@ struct G2Src {
   int64_t a[2], b[2];   // element offsets at k0 = 0
   int kb[2];            // B k-row within the stage
 };
-DFM_DEV G2Src g2_sources(int64_t lda, int64_t ldb, int abase, int bbase, int M, int Nc, int wave, int lane) {
+// clist (optional): column compaction by indirection — compact column x of
+// B / C is physical column clist[x / cg] * cg + x % cg (x / cg < ccount);
+// pairs (x, x+1) never straddle a group (x even, cg even).
+DFM_DEV int64_t g2_phys_col(int x, const int *__restrict__ clist, int ccount, int cg) {
+  const int slot = min(x / cg, ccount - 1);   // past the list: finite data, discarded outputs
+  return (int64_t)clist[slot] * cg + (x - (x / cg) * cg);
+}
+DFM_DEV G2Src g2_sources(int64_t lda, int64_t ldb, int abase, int bbase, int M, int Nc, int wave, int lane,
+                         const int *__restrict__ clist = nullptr, int ccount = 0, int cg = 1) {
   G2Src s;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -217,7 +225,8 @@ DFM_DEV G2Src g2_sources(int64_t lda, int64_t ldb, int abase, int bbase, int M, 
     s.a[h] = (int64_t)min(abase + a, M - 1) * lda + ka;
     const int kc = 2 * c + (lane >> 5);
     s.kb[h] = kc;
-    s.b[h] = (int64_t)kc * ldb + min(bbase + ((2 * (lane & 31)) ^ ((kc & 7) << 2)), Nc - 2);
+    const int x = bbase + ((2 * (lane & 31)) ^ ((kc & 7) << 2));
+    s.b[h] = (int64_t)kc * ldb + (clist ? g2_phys_col(x, clist, ccount, cg) : (int64_t)min(x, Nc - 2));
   }
   return s;
 }
@@ -240,7 +249,8 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
                                                        const double *__restrict__ B, int64_t ldb,
                                                        double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
                                                        int nrb, int ncb, const int *__restrict__ col_done,
-                                                       int col_group) {
+                                                       int col_group, const int *__restrict__ clist = nullptr,
+                                                       const int *__restrict__ ccount_p = nullptr) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   constexpr int AHEAD = NBUF - 2;   // stages in flight across a barrier
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -249,7 +259,11 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
   const int rb = j % nrb, cb = (j / nrb) * 8 + xcd;
   if (cb >= ncb) return;
   const int abase = rb * GT, bbase = cb * GT;
-  if (col_done) {
+  // compacted launch (straggler phase): column block cb of the listed
+  // replicates' column groups only
+  const int ccount = clist ? *ccount_p : 0;
+  if (clist && bbase >= ccount * col_group) return;
+  if (col_done && !clist) {
     bool all = true;
     const int r0 = bbase / col_group, r1 = min(Nc - 1, bbase + GT - 1) / col_group;
     for (int q = r0; q <= r1; ++q) all = all && col_done[q];
@@ -262,7 +276,7 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
     for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int nst = (K + G2_KS - 1) / G2_KS;
-  const G2Src src = g2_sources(lda, ldb, abase, bbase, M, Nc, wave, lane);
+  const G2Src src = g2_sources(lda, ldb, abase, bbase, M, Nc, wave, lane, clist, ccount, col_group);
   // RUN: the DMA sources are running pointers advanced by one stage per
   // issue (no per-stage 64-bit address arithmetic, no k-tail clamp: B holds
   // zero rows up to round_up(K, 16), as A holds zero k-columns)
@@ -318,7 +332,11 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
       const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
       const int row = abase + wr * 32 + 4 * fa + oi;
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
-      if (row < M && col < Nc) C[(int64_t)row * ldc + col] = v;
+      if (clist) {
+        if (row < M && col < ccount * col_group) C[(int64_t)row * ldc + g2_phys_col(col, clist, ccount, col_group)] = v;
+      } else if (row < M && col < Nc) {
+        C[(int64_t)row * ldc + col] = v;
+      }
     }
 }
 
@@ -597,7 +615,8 @@ static int gemm_variant() {
 // the register-staged kernel runs.
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
-                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false) {
+                       const int *col_done = nullptr, int col_group = 1, bool b_padded = false,
+                       const int *clist = nullptr, const int *ccount = nullptr) {
   const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
@@ -608,7 +627,7 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
     // C3 shape, 0.75 at M = K = 2000, vs 0.60 / 0.71 for the clamped kernels)
     if (b_padded && gemm_variant() == 2)
       hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false, true>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb,
-                         ncb, col_done, col_group);
+                         ncb, col_done, col_group, clist, ccount);
     else if (gemm_ring3(M))
       hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
                          col_done, col_group);
