@@ -20,76 +20,6 @@ __global__ void maxdiff(const double *a, const double *b, size_t n, unsigned lon
   }
 }
 
-// experiment: running DMA source pointers (no per-stage 64-bit address math,
-// no k-tail clamp: B must hold zero rows up to round_up(K, 16))
-template <int NBUF, int MINB>
-__global__ __launch_bounds__(256, MINB) void gemmh_run_kernel(const double *__restrict__ A, int64_t lda,
-                                                       const double *__restrict__ B, int64_t ldb,
-                                                       double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
-                                                       int nrb, int ncb) {
-  __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
-  constexpr int AHEAD = NBUF - 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
-  const int rb = j % nrb, cb = (j / nrb) * 8 + xcd;
-  if (cb >= ncb) return;
-  const int abase = rb * GT, bbase = cb * GT;
-  double acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
-  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
-  const int nst = (K + G2_KS - 1) / G2_KS;
-  const G2Src src = g2_sources(lda, ldb, abase, bbase, M, Nc, wave, lane);
-  const double *pa0 = A + src.a[0], *pa1 = A + src.a[1], *pb0 = B + src.b[0], *pb1 = B + src.b[1];
-  const int64_t bstep = (int64_t)G2_KS * ldb;
-  const int c_off0 = (2 * wave) * 128, c_off1 = (2 * wave + 1) * 128;
-  auto issue = [&](int slot) {
-    double *la = lds + slot * G2_STAGE, *lb = la + GT * G2_KS;
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa0, (lds_void_t *)(la + c_off0), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb0, (lds_void_t *)(lb + c_off0), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa1, (lds_void_t *)(la + c_off1), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb1, (lds_void_t *)(lb + c_off1), 16, 0, 0);
-    pa0 += G2_KS; pa1 += G2_KS; pb0 += bstep; pb1 += bstep;
-  };
-  for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s % NBUF);
-  for (int s = 0; s < nst; ++s) {
-    const int ahead = min(AHEAD, nst - 1 - s);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + NBUF - 1 < nst) issue((s + NBUF - 1) % NBUF);
-    const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
-    double af[8], bf[8];
-#pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      af[f] = la[g2_offA(wr * 32 + 4 * f + fi, fkc)];
-      bf[f] = lb[g2_offB(fkc, wc * 32 + 4 * f + fi)];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
-  }
-  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
-  const int oi = lane >> 4, oj = lane & 3;
-#pragma unroll
-  for (int fa = 0; fa < 8; ++fa)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2], a3 = acc[fa][4 * q + 3];
-      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
-      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
-      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
-      const int row = abase + wr * 32 + 4 * fa + oi;
-      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
-      if (row < M && col < Nc) C[(int64_t)row * ldc + col] = v;
-    }
-}
 int main() {
   struct Cfg { bool at; int M, K, Nc; };
   std::vector<Cfg> cfgs = {{false, 500, 500, 160000}, {false, 512, 512, 160000}, {false, 500, 500, 40000},
@@ -116,8 +46,8 @@ int main() {
         else if (v == 3) hipLaunchKernelGGL((gemmh_kernel_t<3, 2, false>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
         else if (v == 4) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
         else if (v == 5) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 6) hipLaunchKernelGGL((gemmh_run_kernel<4, 2>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb);
-        else hipLaunchKernelGGL((gemmh_run_kernel<3, 3>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb);
+        else if (v == 6) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1, nullptr, nullptr);
+        else hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1, nullptr, nullptr);
       };
       double *Cout = v == 0 ? C : C2;
       if (v > 0) hipMemset(C2, 0, (size_t)c.M * ldc * 8);
@@ -128,7 +58,7 @@ int main() {
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       const double t = ms / reps * 1e-3, fl = 2.0 * c.M * (double)c.Nc * c.K;
-      static const char *names[] = {"reg     ", "glds4/2 ", "glds4/2p", "glds3/2 ", "glds3/3 ", "glds3/3p", "run4/2  ", "run3/3  "};
+      static const char *names[] = {"reg     ", "glds4/2 ", "glds4/2p", "glds3/2 ", "glds3/3 ", "glds3/3p", "run3/3  ", "run3/3p "};
       printf("%s A%s M=%5d K=%5d Nc=%6d : %8.3f ms  %6.2f TF/s (%.1f%% of 78.6)\n", names[v],
              c.at ? "^T" : "  ", c.M, c.K, c.Nc, t * 1e3, fl / t / 1e12, fl / t / 1e12 / 78.6 * 100);
       if (v > 0) {
