@@ -880,32 +880,23 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   run = scan[tid] - run;
   for (int s = c0; s < c1; ++s) { run += cnt[s]; cnt[s] = run; }   // cnt[s] = start of bucket s
   __syncthreads();
-  // stable placement: t goes to start(ix_t) + #{t' < t : ix_t' = ix_t}
-  // (ascending t per bucket — the serial counting sort's order); the t' loop
-  // is uniform across the workgroup, so six[t'] is a broadcast read
+  for (int s = tid; s <= T; s += 256) off[(int64_t)rep * (T + 1) + s] = cnt[s];
+  __syncthreads();
+  // placement: LDS atomics hand out slots inside each bucket (any order),
+  // then each bucket is insertion-sorted by t — ascending t per bucket, the
+  // serial counting sort's order, in O(T) work (buckets are short)
   int *L = lst + (int64_t)rep * T;
-  constexpr int TPT = 2;   // t's per thread per pass
-  for (int base = 0; base < T; base += 256 * TPT) {
-    int mine[TPT], rank[TPT];
-#pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      const int t = base + q * 256 + tid;
-      mine[q] = t < T ? six[t] : -1;
-      rank[q] = 0;
-    }
-    const int tend = min(T, base + 256 * TPT);
-    for (int u = 0; u < tend; ++u) {
-      const int v = six[u];
-#pragma unroll
-      for (int q = 0; q < TPT; ++q) rank[q] += (v == mine[q] && u < base + q * 256 + tid) ? 1 : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      const int t = base + q * 256 + tid;
-      if (t < T) L[cnt[mine[q]] + rank[q]] = t;
+  for (int t = tid; t < T; t += 256) L[atomicAdd(&cnt[six[t]], 1)] = t;
+  __syncthreads();   // cnt[s] is now the END of bucket s; L visible workgroup-wide
+  for (int s = tid; s < T; s += 256) {
+    const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
+    for (int i = b0 + 1; i < b1; ++i) {
+      const int v = L[i];
+      int j = i - 1;
+      while (j >= b0 && L[j] > v) { L[j + 1] = L[j]; --j; }
+      L[j + 1] = v;
     }
   }
-  for (int s = tid; s <= T; s += 256) off[(int64_t)rep * (T + 1) + s] = cnt[s];
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
     const int i = ix[t];
