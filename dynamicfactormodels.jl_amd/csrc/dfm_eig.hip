@@ -1207,7 +1207,7 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
   const int ia = six[ta];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
-    const int j = min(4 * kk + lk, r - 1);
+    const int j = max(0, min(4 * kk + lk, r - 1));   // never index -1 (r = 0: expanding windows)
     L.fA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.F[(int64_t)ta * r + j] : 0.0;
     L.eA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.EL[(int64_t)ia * r + j] : 0.0;
   }
@@ -1401,7 +1401,9 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
   for (int g = 0; g < 4; ++g) {
     const int t = t0 + 4 * g + lk;
     const int tc = min(t, T - 1);
-    const double f = fb.F[(int64_t)tc * r + min(li, r - 1)];
+    // r = 0 (expanding windows: no base factors): no load at all — the
+    // clamped column would be F[-1], one element before the buffer
+    const double f = r > 0 ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
     L.fa[g] = (t < T && li < r) ? f : 0.0;
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = init ? Qr[(int64_t)tc * P + 16 * ct + li] : 0.0;
@@ -1769,7 +1771,7 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
       const int t = t0 + 4 * g + lk;
       const bool v = t < T;
       const int tc = min(t, T - 1);
-      fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
+      fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, max(r - 1, 0))] : 0.0;   // never F[-1] (r = 0)
       const double e = v ? set[t] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
