@@ -33,6 +33,11 @@ __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, do
 
 constexpr int LS_AMAX = 1024;   // active-set capacity (glmnet's pmax analogue)
 constexpr int LS_GC = 112;      // G_AA cached in LDS while the active set is this small (98 KB)
+// development timing of lasso_path_kernel phases (DFM_SOFT_PROF=1): problem
+// 0's thread 0 accumulates s_memrealtime ticks (100 MHz) per phase
+__device__ unsigned long long g_soft_prof[8];
+#define SPROF_START() unsigned long long sp_t0 = wall_clock64()
+#define SPROF(i) do { if (f == 0 && tid == 0) { const unsigned long long sp_t1 = wall_clock64(); g_soft_prof[i] += sp_t1 - sp_t0; sp_t0 = sp_t1; } } while (0)
 
 // y mean / population sd over each problem's training rows (fold != f; f = 0: all).
 __global__ void soft_ystats_kernel(const double *__restrict__ y, const int32_t *__restrict__ fold, int n,
@@ -102,9 +107,9 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 
 // One workgroup per problem: the lasso path over lambdas alm[0..nlam-1]
 // (standardised units), warm-started, by coordinate descent on the active
-// set.  Per pass thread 0 walks the active list in entry order (the serial
-// dependency of coordinate descent), every coordinate change is broadcast
-// and applied to g_A by all threads; after a converged pass the non-active
+// set.  Per pass the active list is walked in entry order (the serial
+// dependency of coordinate descent) and every coordinate change applied to
+// g_A (wave 0 alone while G_AA sits in LDS, else all threads); after a converged pass the non-active
 // gradients are refreshed with the pass's accumulated changes (rows of G for
 // the active variables, coalesced along j) and the KKT scan appends every
 // violator |g_j| > lambda in index order.  status[f]: 0 ok, 1 no convergence,
@@ -115,7 +120,8 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 __global__ __launch_bounds__(256) void lasso_path_kernel(
     const double *__restrict__ Gall, int64_t strideG, int p, const double *__restrict__ call,
     const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early,
-    double thr, int maxit, double *__restrict__ gws, int *__restrict__ actws, double *__restrict__ bpath,
+    double thr, int maxit, double *__restrict__ gws, int *__restrict__ actws, double *__restrict__ gaaws,
+    double *__restrict__ bpath,
     double *__restrict__ rsq_out, int *__restrict__ nlam_out, int *__restrict__ status) {
   const int f = prob0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double *G = Gall + (int64_t)f * strideG;
@@ -124,11 +130,15 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
   const double *alm = almall + (int64_t)f * nlam;
   double *g = gws + (int64_t)f * p;
   int *act = actws + (int64_t)f * p;
+  // G_AA compacted in entry order (row stride LS_AMAX) for active sets past
+  // LS_GC: one coalesced 8 na-byte row per coordinate step instead of a
+  // gather that touches nearly every cache line of a p-wide G row
+  double *GAA = gaaws + (int64_t)f * LS_AMAX * LS_AMAX;
   double *bp = bpath + (int64_t)f * nlam * p;
-  __shared__ int ia[LS_AMAX];
+  __shared__ int ia[LS_AMAX], rows[LS_AMAX];
   __shared__ double bA[LS_AMAX], gA[LS_AMAX], dA[LS_AMAX];
   __shared__ double GC[LS_GC * LS_GC];
-  __shared__ double s_d, s_red[4];
+  __shared__ double s_red[4];
   __shared__ int s_flag, s_cnt[4];
   for (int j = tid; j < p; j += 256) { g[j] = c[j]; act[j] = 0; }
   __syncthreads();
@@ -137,63 +147,135 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
   for (int m = 0; m < nlam && !st; ++m) {
     const double lam = alm[m];
     for (;;) {
+      SPROF_START();
       // ---- passes over the active set until max delta^2 < thr
+      // Small active sets (G_AA cached in LDS): wave 0 alone runs the passes —
+      // every lane reads gA[k], bA[k] (an LDS broadcast) and computes the same
+      // d, so no cross-wave barrier per coordinate; the wave's LDS accesses
+      // complete in program order and the wavefront fences keep the compiler
+      // from reordering them across steps.  Larger sets (G_AA rows gathered
+      // from HBM) keep all four waves on the update, thread 0 broadcasting d.
+      // Same arithmetic in the same order either way.
       int it = 0;
-      for (; it < maxit; ++it) {
-        double dlx = 0.0;
-        for (int k = 0; k < na; ++k) {
-          if (tid == 0) {
-            const double u = gA[k] + bA[k], v = fabs(u) - lam;
-            const double nb = v > 0.0 ? copysign(v, u) : 0.0;
-            const double d = nb - bA[k];
-            if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
-            s_d = d;
-          }
-          __syncthreads();
-          const double d = s_d;
-          if (d != 0.0) {
-            if (na <= LS_GC) {
-              for (int t = tid; t < na; t += 256) gA[t] -= GC[k * LS_GC + t] * d;
-            } else {
-              const double *Gk = G + (int64_t)ia[k] * p;
-              for (int t = tid; t < na; t += 256) gA[t] -= Gk[ia[t]] * d;
+      if (na <= LS_GC) {
+        if (wave == 0) {
+          for (; it < maxit; ++it) {
+            double dlx = 0.0;
+            for (int k = 0; k < na; ++k) {
+              const double bk = bA[k];
+              const double u = gA[k] + bk, v = fabs(u) - lam;
+              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
+              const double d = nb - bk;
+              if (d != 0.0) {   // uniform over the wave
+                dlx = fmax(dlx, d * d);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) { bA[k] = nb; dA[k] += d; }
+                for (int t = lane; t < na; t += 64) gA[t] -= GC[k * LS_GC + t] * d;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+              }
             }
+            if (dlx < thr) break;
           }
-          __syncthreads();
+          if (lane == 0) s_flag = it;
         }
-        if (tid == 0) s_flag = dlx < thr;
         __syncthreads();
-        const bool done = s_flag;
+        it = s_flag;
         __syncthreads();
-        if (done) break;
+      } else {
+        for (; it < maxit; ++it) {
+          double dlx = 0.0;
+          for (int k = 0; k < na; ++k) {
+            if (tid == 0) {
+              const double u = gA[k] + bA[k], v = fabs(u) - lam;
+              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
+              const double d = nb - bA[k];
+              if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
+              s_red[0] = d;
+            }
+            __syncthreads();
+            const double d = s_red[0];
+            if (d != 0.0) {
+              // (L1-bypassing loads: the rows were written by this workgroup)
+              const double *Gk = GAA + (int64_t)k * LS_AMAX;
+              for (int t = tid; t < na; t += 256)
+                gA[t] -= __hip_atomic_load(Gk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * d;
+            }
+            __syncthreads();
+          }
+          if (tid == 0) s_flag = dlx < thr;
+          __syncthreads();
+          const bool done = s_flag;
+          __syncthreads();
+          if (done) break;
+        }
       }
+      SPROF(0);
       if (it == maxit) { st = 1; fail_m = m; break; }
       // ---- refresh the non-active gradients with this round's changes:
-      // row-outer, so each thread keeps SEG loads in flight (one per owned j)
-      // instead of one dependent load per FMA; rows with no change skipped
-      // (adding 0 * G leaves the sum unchanged), t ascending as before
-      constexpr int SEG = 8;
-      for (int j0 = 0; j0 < p; j0 += 256 * SEG) {
-        double acc[SEG];
+      // row-outer, so each thread keeps SEG loads in flight per row (one per
+      // owned j), RU rows at a time (RU x SEG independent loads before their
+      // FMAs: the pass is latency-bound on one CU otherwise); rows with no
+      // change are compacted out first (adding 0 * G leaves the sum
+      // unchanged), t ascending as before, so the sums are bit-identical
+      {
+        int nr = 0;
+        for (int t0 = 0; t0 < na; t0 += 256) {
+          const int t = t0 + tid;
+          const bool v = t < na && dA[t] != 0.0;
+          const unsigned long long bal = __ballot(v);
+          if (lane == 0) s_cnt[wave] = __popcll(bal);
+          __syncthreads();
+          int off = nr;
+          for (int w2 = 0; w2 < wave; ++w2) off += s_cnt[w2];
+          if (v) rows[off + __popcll(bal & ((1ull << lane) - 1ull))] = t;
+          nr += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+          __syncthreads();
+        }
+        constexpr int SEG = 8, RU = 4;
+        for (int j0 = 0; j0 < p; j0 += 256 * SEG) {
+          double acc[SEG];
 #pragma unroll
-        for (int u = 0; u < SEG; ++u) acc[u] = 0.0;
-        for (int t = 0; t < na; ++t) {
-          const double dt = dA[t];
-          if (dt == 0.0) continue;
-          const double *Gt = G + (int64_t)ia[t] * p;
+          for (int u = 0; u < SEG; ++u) acc[u] = 0.0;
+          int q = 0;
+          for (; q + RU <= nr; q += RU) {
+            double gv[RU][SEG], dt[RU];
+#pragma unroll
+            for (int h = 0; h < RU; ++h) {
+              const int t = rows[q + h];
+              dt[h] = dA[t];
+              const double *Gt = G + (int64_t)ia[t] * p;
+#pragma unroll
+              for (int u = 0; u < SEG; ++u) {
+                const int j = j0 + tid + 256 * u;
+                gv[h][u] = j < p ? Gt[j] : 0.0;
+              }
+            }
+#pragma unroll
+            for (int h = 0; h < RU; ++h)
+#pragma unroll
+              for (int u = 0; u < SEG; ++u) acc[u] = fma(gv[h][u], dt[h], acc[u]);
+          }
+          for (; q < nr; ++q) {
+            const int t = rows[q];
+            const double dt = dA[t];
+            const double *Gt = G + (int64_t)ia[t] * p;
+#pragma unroll
+            for (int u = 0; u < SEG; ++u) {
+              const int j = j0 + tid + 256 * u;
+              if (j < p) acc[u] = fma(Gt[j], dt, acc[u]);
+            }
+          }
 #pragma unroll
           for (int u = 0; u < SEG; ++u) {
             const int j = j0 + tid + 256 * u;
-            if (j < p) acc[u] = fma(Gt[j], dt, acc[u]);
+            if (j < p && !act[j]) g[j] -= acc[u];
           }
-        }
-#pragma unroll
-        for (int u = 0; u < SEG; ++u) {
-          const int j = j0 + tid + 256 * u;
-          if (j < p && !act[j]) g[j] -= acc[u];
         }
       }
       __syncthreads();
+      SPROF(1);
       for (int t = tid; t < na; t += 256) dA[t] = 0.0;
       // ---- KKT scan: append violators in index order
       const int na0 = na;
@@ -214,17 +296,25 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
         base += tot;
         __syncthreads();
       }
+      SPROF(2);
       if (base > LS_AMAX) { st = 2; fail_m = m; break; }
       na = base;
       if (na == na0) break;
-      if (na <= LS_GC)   // G_AA entries of the new variables (G symmetric)
-        for (int e = tid; e < (na - na0) * na; e += 256) {
-          const int k = na0 + e / na, t = e % na;
-          const double v = G[(int64_t)ia[k] * p + ia[t]];
+      // G_AA entries of the new variables (G symmetric): LDS while small,
+      // and always the compacted global copy (read once the set outgrows LDS)
+      for (int e = tid; e < (na - na0) * na; e += 256) {
+        const int k = na0 + e / na, t = e % na;
+        const double v = G[(int64_t)ia[k] * p + ia[t]];
+        if (na <= LS_GC) {
           GC[k * LS_GC + t] = v;
           GC[t * LS_GC + k] = v;
         }
+        __hip_atomic_store(GAA + (int64_t)k * LS_AMAX + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(GAA + (int64_t)t * LS_AMAX + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __threadfence();
       __syncthreads();
+      SPROF(3);
     }
     if (st) break;
     // ---- record: dense beta_m, R^2 = beta'(c + g)
@@ -350,6 +440,7 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   double *alm = (double *)alloc((size_t)nprob * nlambda * 8);
   double *gws = (double *)alloc((size_t)nprob * p * 8);
   int *actws = (int *)alloc((size_t)nprob * p * 4);
+  double *gaaws = (double *)alloc((size_t)nprob * LS_AMAX * LS_AMAX * 8);
   double *bpath = (double *)alloc((size_t)nprob * nlambda * p * 8);
   double *rsq = (double *)alloc((size_t)nprob * nlambda * 8);
   int *nl = (int *)alloc((size_t)nprob * 4), *sts = (int *)alloc((size_t)nprob * 8);
@@ -414,14 +505,25 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
   e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: memset failed"); }
+  static const bool sprof = getenv("DFM_SOFT_PROF") != nullptr;
+  if (sprof) {
+    unsigned long long z[8] = {};
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_soft_prof), z, sizeof z, 0, hipMemcpyHostToDevice, st);
+  }
   hipLaunchKernelGGL(lasso_path_kernel, dim3(nprob), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1,
-                     thr, maxit, gws, actws, bpath, rsq, nl, sts);
+                     thr, maxit, gws, actws, gaaws, bpath, rsq, nl, sts);
   std::vector<int> hnl(nprob), hst(2 * nprob);
   e = hipMemcpyAsync(hnl.data(), nl, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), sts, (size_t)nprob * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: path kernel failed"); }
   const int L = hnl[0];
+  if (sprof) {
+    unsigned long long z[8];
+    hipMemcpyFromSymbol(z, HIP_SYMBOL(g_soft_prof), sizeof z, 0, hipMemcpyDeviceToHost);
+    fprintf(stderr, "[soft prof] ms: passes %.2f refresh %.2f kkt %.2f fill %.2f\n", z[0] * 1e-5, z[1] * 1e-5,
+            z[2] * 1e-5, z[3] * 1e-5);
+  }
   for (int f = 0; f < nprob; ++f)   // a fold's failure past L concerns lambdas the CV never reads
     if (hst[f] && (f == 0 || hst[nprob + f] < L))
       { cleanup(); return fail(2, hst[f] == 1 ? "lasso coordinate descent did not converge"
