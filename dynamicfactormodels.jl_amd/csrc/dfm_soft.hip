@@ -119,7 +119,7 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 // other problems stop when they reach it.
 __global__ __launch_bounds__(256) void lasso_path_kernel(
     const double *__restrict__ Gall, int64_t strideG, int p, const double *__restrict__ call,
-    const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early,
+    const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early, int cdmode,
     double thr, int maxit, double *__restrict__ gws, int *__restrict__ actws, double *__restrict__ gaaws,
     double *__restrict__ bpath,
     double *__restrict__ rsq_out, int *__restrict__ nlam_out, int *__restrict__ status) {
@@ -183,6 +183,80 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
         __syncthreads();
         it = s_flag;
         __syncthreads();
+      } else if (cdmode == 1) {
+        if (wave == 0) {
+          for (; it < maxit; ++it) {
+            double dlx = 0.0;
+            for (int k = 0; k < na; ++k) {
+              const double bk = bA[k];
+              const double u = gA[k] + bk, v = fabs(u) - lam;
+              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
+              const double d = nb - bk;
+              if (d != 0.0) {   // uniform over the wave
+                dlx = fmax(dlx, d * d);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) { bA[k] = nb; dA[k] += d; }
+                const double *Gk = GAA + (int64_t)k * LS_AMAX;
+                for (int t = lane; t < na; t += 64)
+                  gA[t] -= __hip_atomic_load(Gk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * d;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+              }
+            }
+            if (dlx < thr) break;
+          }
+          if (lane == 0) s_flag = it;
+        }
+        __syncthreads();
+        it = s_flag;
+        __syncthreads();
+      } else if (cdmode == 0) {
+        // all four waves; row k + 1 of G_AA prefetched into registers (4 per
+        // thread: na <= LS_AMAX = 1024) while step k runs — it does not
+        // depend on d — so a step waits on no global-memory latency
+        constexpr int RV = LS_AMAX / 256;
+        for (; it < maxit; ++it) {
+          double dlx = 0.0;
+          double cur[RV], nxt[RV];
+#pragma unroll
+          for (int i = 0; i < RV; ++i) {
+            const int t = tid + 256 * i;
+            cur[i] = t < na ? __hip_atomic_load(GAA + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+          }
+          for (int k = 0; k < na; ++k) {
+            const double *Gn = GAA + (int64_t)min(k + 1, na - 1) * LS_AMAX;
+#pragma unroll
+            for (int i = 0; i < RV; ++i) {
+              const int t = tid + 256 * i;
+              nxt[i] = t < na ? __hip_atomic_load(Gn + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            }
+            if (tid == 0) {
+              const double u = gA[k] + bA[k], v = fabs(u) - lam;
+              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
+              const double d = nb - bA[k];
+              if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
+              s_red[0] = d;
+            }
+            __syncthreads();
+            const double d = s_red[0];
+            if (d != 0.0) {
+#pragma unroll
+              for (int i = 0; i < RV; ++i) {
+                const int t = tid + 256 * i;
+                if (t < na) gA[t] -= cur[i] * d;
+              }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < RV; ++i) cur[i] = nxt[i];
+          }
+          if (tid == 0) s_flag = dlx < thr;
+          __syncthreads();
+          const bool done = s_flag;
+          __syncthreads();
+          if (done) break;
+        }
       } else {
         for (; it < maxit; ++it) {
           double dlx = 0.0;
@@ -211,7 +285,7 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
           if (done) break;
         }
       }
-      SPROF(0);
+      SPROF(na <= LS_GC ? 0 : 4);
       if (it == maxit) { st = 1; fail_m = m; break; }
       // ---- refresh the non-active gradients with this round's changes:
       // row-outer, so each thread keeps SEG loads in flight per row (one per
@@ -506,11 +580,12 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: memset failed"); }
   static const bool sprof = getenv("DFM_SOFT_PROF") != nullptr;
+  static const int cdmode = [] { const char *e_ = getenv("DFM_SOFT_CD"); return e_ ? atoi(e_) : 0; }();
   if (sprof) {
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_soft_prof), z, sizeof z, 0, hipMemcpyHostToDevice, st);
   }
-  hipLaunchKernelGGL(lasso_path_kernel, dim3(nprob), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1,
+  hipLaunchKernelGGL(lasso_path_kernel, dim3(nprob), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1, cdmode,
                      thr, maxit, gws, actws, gaaws, bpath, rsq, nl, sts);
   std::vector<int> hnl(nprob), hst(2 * nprob);
   e = hipMemcpyAsync(hnl.data(), nl, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
@@ -521,8 +596,8 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   if (sprof) {
     unsigned long long z[8];
     hipMemcpyFromSymbol(z, HIP_SYMBOL(g_soft_prof), sizeof z, 0, hipMemcpyDeviceToHost);
-    fprintf(stderr, "[soft prof] ms: passes %.2f refresh %.2f kkt %.2f fill %.2f\n", z[0] * 1e-5, z[1] * 1e-5,
-            z[2] * 1e-5, z[3] * 1e-5);
+    fprintf(stderr, "[soft prof] ms: passes (LDS G_AA) %.2f passes (global G_AA) %.2f refresh %.2f kkt %.2f fill %.2f\n",
+            z[0] * 1e-5, z[4] * 1e-5, z[1] * 1e-5, z[2] * 1e-5, z[3] * 1e-5);
   }
   for (int f = 0; f < nprob; ++f)   // a fold's failure past L concerns lambdas the CV never reads
     if (hst[f] && (f == 0 || hst[nprob + f] < L))
