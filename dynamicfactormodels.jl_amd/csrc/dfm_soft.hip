@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void lasso_path_kernel(
           nr += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
           __syncthreads();
         }
-        constexpr int SEG = 8, RU = 4;
+        constexpr int SEG = 8, RU = 8;
         for (int j0 = 0; j0 < p; j0 += 256 * SEG) {
           double acc[SEG];
 #pragma unroll
