@@ -32,7 +32,7 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
 
 constexpr int LS_AMAX = 1024;   // active-set capacity (glmnet's pmax analogue)
-constexpr int LS_GC = 112;      // G_AA cached in LDS while the active set is this small (98 KB)
+constexpr int LS_GC = 126;      // G_AA cached in LDS while the active set is this small (124 KB of the 160)
 // development timing of lasso_path_kernel phases (DFM_SOFT_PROF=1): problem
 // 0's thread 0 accumulates s_memrealtime ticks (100 MHz) per phase
 __device__ unsigned long long g_soft_prof[8];
