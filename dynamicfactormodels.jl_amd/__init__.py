@@ -8,7 +8,7 @@ The compute lives in ``libdfm.so`` (HIP, gfx950) behind the C ABI of
 exported Julia API (``src/DynamicFactorModels.jl:16-20``).  Import it through
 the repo-root helper ``dfm_pkg.load()`` (the directory name contains a dot).
 """
-from .host import (normalize, factor_model_DGP, draw_wild, draw_wild_fast, draw_residual,
+from .host import (factor_model_DGP, draw_wild, draw_wild_fast, draw_residual,
                    t_quantile, glmnet_default_folds, lag_vector, lag_matrix, norm_vector, norm_matrix,
                    possemidef, read_panel_csv, reference_test_design)
 from .api import (Context, DFMError, Stat, DynamicFactorModel, DynamicFactorModelResult,
@@ -16,7 +16,7 @@ from .api import (Context, DFMError, Stat, DynamicFactorModel, DynamicFactorMode
                   factor_residual_variance, criterion_value, wild_bootstrap, residual_bootstrap,
                   chow_all, LR_test, LM_test, Wald_test, targeted_predictors, default_context,
                   CRITERIA, pseudo_out_of_sample_refits, pseudo_out_of_sample_refits_dev,
-                  pseudo_out_of_sample_forecasts, MSE)
+                  pseudo_out_of_sample_forecasts, MSE, normalize, normalize_dev, clone_model)
 from .api import (criterion_PCp1, criterion_PCp2, criterion_PCp3, criterion_ICp1,  # noqa: F401
                   criterion_ICp2, criterion_ICp3, criterion_BIC)
 from . import _lib
@@ -29,5 +29,5 @@ __all__ = [
     "factor_residual_variance", "criterion_value", "wild_bootstrap", "residual_bootstrap",
     "chow_all", "LR_test", "LM_test", "Wald_test", "targeted_predictors", "default_context",
     "CRITERIA", "pseudo_out_of_sample_refits", "pseudo_out_of_sample_refits_dev",
-    "pseudo_out_of_sample_forecasts", "MSE",
+    "pseudo_out_of_sample_forecasts", "MSE", "normalize_dev", "clone_model",
 ]

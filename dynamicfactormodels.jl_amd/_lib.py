@@ -64,6 +64,13 @@ SIGNATURES = [
                                 C.POINTER(dfm_stat), C.c_int, c_double_p]),
     ("dfm_bootstrap_dev", C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.POINTER(dfm_stat), C.c_int, C.c_void_p]),
+    ("dfm_bootstrap_multi", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int64, c_int32_p,
+                                      c_double_p, C.POINTER(dfm_stat), C.c_int, c_double_p]),
+    ("dfm_model_clone", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("dfm_normalize", C.c_int, [C.c_void_p, c_double_p, C.c_int64, C.c_int64, C.c_int64, c_double_p,
+                                C.c_int64]),
+    ("dfm_normalize_dev", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
+                                    C.c_int64]),
     ("dfm_stats_width", C.c_int64, [C.c_void_p, C.POINTER(dfm_stat), C.c_int]),
     ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
     ("dfm_model_set_mode", C.c_int, [C.c_void_p, C.c_int]),

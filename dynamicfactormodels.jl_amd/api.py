@@ -29,6 +29,7 @@ import numpy as np
 
 from . import _lib
 from .host import draw_residual, draw_wild, glmnet_default_folds, t_quantile
+from .host import normalize as host_normalize
 
 CRITERIA = ("PCp1", "PCp2", "PCp3", "ICp1", "ICp2", "ICp3", "BIC")
 _CRIT_CODE = {n: i for i, n in enumerate(CRITERIA)}
@@ -147,15 +148,15 @@ class Stat:
 
     @staticmethod
     def eigenvalue(j: int):       # 1-based, descending
-        return Stat(2, j - 1)
+        return Stat(2, _one_based(j))
 
     @staticmethod
     def coefficient(j: int):      # 1-based into [w F_r]
-        return Stat(3, j - 1)
+        return Stat(3, _one_based(j))
 
     @staticmethod
     def t_stat(j: int):
-        return Stat(4, j - 1)
+        return Stat(4, _one_based(j))
 
     @staticmethod
     def trace():
@@ -184,6 +185,16 @@ class Stat:
     @staticmethod
     def Wald_all(break_period: int):
         return Stat(11, break_period)
+
+    @staticmethod
+    def iterations():             # diagnostic: the replicate's eigensolver steps
+        return Stat(12)
+
+
+def _one_based(j: int) -> int:
+    if int(j) < 1:
+        raise ValueError(f"index {j}: the reference's indices are 1-based")
+    return int(j) - 1
 
 
 def _stat_array(stats: Sequence[Stat]):
@@ -388,7 +399,9 @@ def principal_components(x, k: int, *, ctx: Optional[Context] = None):
 
 
 def gram_spectrum(x, *, ctx: Optional[Context] = None):
-    """All eigenvalues (descending) of the smaller Gram, min(T,N) <= 140."""
+    """All eigenvalues (descending) of the smaller Gram, min(T,N) <=
+    ``dfm_full_spectrum_max()`` (4096): Jacobi in LDS up to 140, Householder
+    tridiagonalisation + bisection beyond."""
     ctx = ctx or default_context()
     x = _f64(x, 2)
     T, N = x.shape
@@ -398,6 +411,40 @@ def gram_spectrum(x, *, ctx: Optional[Context] = None):
     ctx.check(ctx.lib.dfm_gram_spectrum(ctx.h, xc.ctypes.data_as(_lib.c_double_p), T, N, T,
                                         _lib.ptr(ev), C.byref(tr)))
     return ev, float(tr.value)
+
+
+def normalize(A, by=None, *, ctx: Optional[Context] = None) -> np.ndarray:
+    """``src/utils.jl:33``: (A .- mean(A, 1)) ./ std(A, 1), sample std, on the
+    device (``dfm_normalize``).  ``normalize_dev`` keeps the panel in HBM.
+    ``by = (mean, std)`` is the second method (``:34``), a plain elementwise
+    rescaling by the caller's moments (host arithmetic, ``host.normalize``)."""
+    if by is not None:
+        return host_normalize(A, by)
+    ctx = ctx or default_context()
+    A = _f64(A, 2)
+    T, N = A.shape
+    ac = _colmajor(A)
+    out = np.zeros((T, N), order="F")
+    ctx.check(ctx.lib.dfm_normalize(ctx.h, ac.ctypes.data_as(_lib.c_double_p), T, N, T,
+                                    out.ctypes.data_as(_lib.c_double_p), T))
+    return np.ascontiguousarray(out)
+
+
+def normalize_dev(x, out=None, *, ctx: Optional[Context] = None):
+    """``normalize`` of a column-major float64 torch tensor on the GPU
+    (stride (1, ldx)); in place when ``out`` is ``x``.  Asynchronous on the
+    context stream."""
+    ctx = ctx or default_context()
+    if not _is_device_tensor(x) or x.dtype.itemsize != 8 or x.dim() != 2 or x.stride(0) != 1:
+        raise ValueError("x must be a column-major float64 GPU tensor (stride (1, ldx))")
+    if out is None:
+        import torch
+        out = torch.empty_strided(tuple(x.shape), (1, int(x.shape[0])), dtype=x.dtype, device=x.device)
+    if tuple(out.shape) != tuple(x.shape) or out.stride(0) != 1:
+        raise ValueError("out must be column-major with x's shape")
+    ctx.check(ctx.lib.dfm_normalize_dev(ctx.h, x.data_ptr(), int(x.shape[0]), int(x.shape[1]), int(x.stride(1)),
+                                        out.data_ptr(), int(out.stride(1))))
+    return out
 
 
 def factor_residual_variance(dfm: DynamicFactorModelResult) -> float:
@@ -454,20 +501,67 @@ def _run_bootstrap(dfm, kind, B, stat, idx, eta):
     return out
 
 
-def wild_bootstrap(dfm: DynamicFactorModelResult, B: int, stat, *, idx=None, eta=None,
-                   rng: Optional[np.random.Generator] = None):
+def _run_bootstrap_multi(models, kind, B, stat, idx, eta):
+    """The replicate loop sharded over several models (``dfm_bootstrap_multi``):
+    replicate b on model floor(b n / B), one host thread per context."""
+    m0 = models[0]
+    ctx = m0._ctx
+    stats = list(stat) if isinstance(stat, (list, tuple)) else [stat]
+    arr = _stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(m0.handle, arr, len(stats)))
+    T = m0.x.shape[0]
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    if idx.shape != (B, T):
+        raise ValueError(f"idx must be (B, T) = ({B}, {T})")
+    etap = None
+    if eta is not None:
+        eta = np.ascontiguousarray(eta, dtype=np.float64)
+        if eta.shape != (B, T):
+            raise ValueError("eta must be (B, T)")
+        etap = _lib.ptr(eta)
+    out = np.zeros((B, max(width, 1)))
+    hs = (C.c_void_p * len(models))(*[m.handle for m in models])
+    ctx.check(ctx.lib.dfm_bootstrap_multi(hs, len(models), kind, B, idx.ctypes.data_as(_lib.c_int32_p), etap,
+                                          arr, len(stats), _lib.ptr(out)))
+    if len(stats) == 1 and width == 1:
+        return out[:, 0]
+    return out
+
+
+def clone_model(dfm: DynamicFactorModelResult, ctx: Context) -> DynamicFactorModelResult:
+    """A copy of a fitted model on another context (another GPU), for the
+    sharded bootstrap (``dfm_model_clone``)."""
+    h = C.c_void_p()
+    ctx.check(ctx.lib.dfm_model_clone(dfm.handle, ctx.h, C.byref(h)))
+    res = DynamicFactorModelResult(ctx, h, dfm.y, dfm.w, dfm.x, dfm.number_of_factors_criterion,
+                                   dfm.break_indices)
+    res.targeted_predictors = getattr(dfm, "targeted_predictors", None)
+    return res
+
+
+def wild_bootstrap(dfm, B: int, stat, *, idx=None, eta=None, rng: Optional[np.random.Generator] = None):
     """``src/bootstrap.jl:41-51``.  ``idx`` (B×T, 0-based) and ``eta`` (B×T)
-    are the host draws of ``:44-45``; drawn from ``rng`` when omitted."""
+    are the host draws of ``:44-45``; drawn from ``rng`` when omitted.  ``dfm``
+    may be a list of copies of one fit on several contexts (``clone_model``):
+    the replicate loop is then sharded over them (``dfm_bootstrap_multi``)."""
+    models = list(dfm) if isinstance(dfm, (list, tuple)) else None
+    first = models[0] if models else dfm
     if idx is None or eta is None:
-        idx, eta = draw_wild(rng or np.random.default_rng(), B, dfm.x.shape[0])
+        idx, eta = draw_wild(rng or np.random.default_rng(), B, first.x.shape[0])
+    if models:
+        return _run_bootstrap_multi(models, 0, B, stat, idx, eta)
     return _run_bootstrap(dfm, 0, B, stat, idx, eta)
 
 
-def residual_bootstrap(dfm: DynamicFactorModelResult, B: int, stat, *, idx=None,
-                       rng: Optional[np.random.Generator] = None):
-    """``src/bootstrap.jl:21-39``."""
+def residual_bootstrap(dfm, B: int, stat, *, idx=None, rng: Optional[np.random.Generator] = None):
+    """``src/bootstrap.jl:21-39`` (``dfm``: one fit or a list of its copies,
+    as ``wild_bootstrap``)."""
+    models = list(dfm) if isinstance(dfm, (list, tuple)) else None
+    first = models[0] if models else dfm
     if idx is None:
-        idx = draw_residual(rng or np.random.default_rng(), B, dfm.x.shape[0], dfm.break_indices)
+        idx = draw_residual(rng or np.random.default_rng(), B, first.x.shape[0], first.break_indices)
+    if models:
+        return _run_bootstrap_multi(models, 1, B, stat, idx, None)
     return _run_bootstrap(dfm, 1, B, stat, idx, None)
 
 
@@ -619,8 +713,10 @@ def pseudo_out_of_sample_refits_dev(y, w, x, criterion: str = "ICp2", num_predic
     if x.dim() != 2 or x.stride(0) != 1 or x.stride(1) < x.shape[0]:
         raise ValueError("x must be column-major (stride (1, ldx >= T))")
     if w.dim() == 1:
+        if w.stride(0) != 1:
+            raise ValueError("w must be a contiguous vector or column-major (stride (1, ldw >= T))")
         w = w.reshape(-1, 1)
-    if w.shape[1] > 1 and (w.stride(0) != 1 or w.stride(1) < w.shape[0]):
+    if w.stride(0) != 1 or (w.shape[1] > 1 and w.stride(1) < w.shape[0]):
         raise ValueError("w must be column-major (stride (1, ldw >= T))")
     if y.dim() != 1 or y.stride(0) != 1:
         raise ValueError("y must be a contiguous vector")

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace dfm {
@@ -20,6 +21,7 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
             timer_fn tf, void *tctx, int64_t rep0);
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
+const int *eig_iters_ptr(char *ws, int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
 extern int g_last_iters;
 extern int64_t g_last_rep_iters;
@@ -35,7 +37,8 @@ hipError_t launch_materialize(const PanelSrc &src, int T, int N, int64_t ld, int
 int64_t chow_wide_work(int T, int N, int r);
 hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, const double *E, int T, int N, int r,
                             int bp, const double *F, int64_t sF, const double *L, int64_t sL, double *LR, double *LM,
-                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st);
+                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st, int nblk = 1,
+                            const int *brow = nullptr, int64_t lbs = 0);
 hipError_t launch_ols_wide_batched(int nb, const double *y, const double *w, int q, const double *F, int T, int kF,
                                    int k, const int *Tn, double *coef, double *tstat, double *cov_out,
                                    double *resid_out, int *status, double *work, hipStream_t st, int hc0 = 0);
@@ -75,12 +78,13 @@ hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, 
                       double *resid_out, int *status);
 struct StatDesc { int kind, arg0, arg1, off; };
 __global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *, const double *,
-                             const double *, const double *, const StatDesc *, int, double *, int64_t);
+                             const double *, const double *, const int *, const StatDesc *, int, double *, int64_t);
 __global__ void tail_sigma2_kernel(const double *, int, int, int, double, double *);
 // dfm_chow.hip
 hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
                        const double *F, const double *Lm, double *LR, double *LM, double *Wald,
-                       int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st);
+                       int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st, int nblk = 1,
+                       const int *brow = nullptr, int64_t lbs = 0);
 size_t chow_workspace_bytes(int T, int N, int r, int nb);
 struct FactBase {
   int T, r;
@@ -92,6 +96,7 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
                      timer_fn tf, void *tctx, int *off, int *lst);
 size_t fact_workspace_bytes(int T, int nb, int P);
+int fact_t_max();
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
                   const double *Uk, const double *eta, const int *off, const int *lst, int nb,
                   double *Fout, double *Lout, char *ws, hipStream_t st);
@@ -156,7 +161,8 @@ struct dfm_model {
   // are aliased by Ub and L
   int nblk = 1;
   std::vector<int> ba, bt, bm;
-  std::vector<double *> Ubs, Ls;
+  std::vector<double *> Ubs, Ls;   // Ls[j] = Lall + j N r (contiguous: the Chow kernels index blocks)
+  double *Lall = nullptr;
   std::vector<std::vector<double>> blam;
 };
 
@@ -221,6 +227,8 @@ int ctx_device(dfm_ctx *ctx) { return ctx->device; }
 }  // namespace dfm
 
 static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+static bool chow_stat(int k) { return k >= DFM_STAT_LR && k <= DFM_STAT_WALD_ALL; }
+static bool all_var_stat(int k) { return k >= DFM_STAT_LR_ALL && k <= DFM_STAT_WALD_ALL; }
 static int ceil_half(int m) { return (m + 1) / 2; }
 
 template <class T>
@@ -414,11 +422,10 @@ int dfm_model_destroy(dfm_model *m) {
   if (!m) return -1;
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
-  for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->L, m->Ub, m->colssr, m->H, m->EL, m->S,
+  for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->Lall, m->Ub, m->colssr, m->H, m->EL, m->S,
                     m->cF, m->hd})
     hipFree(p);
   for (size_t j = 1; j < m->Ubs.size(); ++j) hipFree(m->Ubs[j]);
-  for (size_t j = 1; j < m->Ls.size(); ++j) hipFree(m->Ls[j]);
   hipFree(m->ws);
   hipFree(m->sd_dev);
   hipFree(m->flag_dev);
@@ -647,10 +654,11 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   CK(dalloc(&M->colssr, N));
   M->Ubs.assign(nblk, nullptr);
   M->Ls.assign(nblk, nullptr);
+  CK(dalloc(&M->Lall, (size_t)nblk * N * r));
   for (int j = 0; j < nblk; ++j) {
     const int mj = M->bm[j];
     CK(dalloc(&M->Ubs[j], (size_t)mj * r));
-    CK(dalloc(&M->Ls[j], (size_t)N * r));
+    M->Ls[j] = M->Lall + (size_t)j * N * r;
     if (j == 0) { M->Ub = M->Ubs[0]; M->L = M->Ls[0]; }
     CK(hipMemcpy2DAsync(M->Ubs[j], (size_t)r * 8, Ukd[j], (size_t)kk[j] * 8, (size_t)r * 8, mj,
                         hipMemcpyDeviceToDevice, st));
@@ -837,7 +845,7 @@ int dfm_model_set_batch(dfm_model *m, int64_t batch) {
 int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
   if (!m || (!stats && nstats)) return -1;
   int64_t w = 0;
-  for (int i = 0; i < nstats; ++i) w += (stats[i].kind >= DFM_STAT_LR_ALL) ? m->N : 1;
+  for (int i = 0; i < nstats; ++i) w += all_var_stat(stats[i].kind) ? m->N : 1;
   return w;
 }
 
@@ -859,7 +867,7 @@ static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool c
   w.Uk = (double *)take((size_t)nb * m * r * 8);
   w.trace = (double *)take((size_t)nb * 8);
   w.F = (double *)take((size_t)nb * T * r * 8);
-  w.L = (double *)take((size_t)nb * N * r * 8);
+  w.L = (double *)take((size_t)M->nblk * nb * N * r * 8);   // block j at w.L + j nb N r
   w.colssr = (double *)take((size_t)nb * N * 8);
   w.coef = (double *)take((size_t)nb * d * 8);
   w.tstat = (double *)take((size_t)nb * d * 8);
@@ -912,22 +920,25 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   int chow_bp = -1;
   for (int i = 0; i < ns; ++i) {
     const dfm_stat s = stats[i];
-    if (s.kind < 0 || s.kind > DFM_STAT_WALD_ALL) return fail(ctx, -6, "unknown stat kind %d", s.kind);
+    if (s.kind < 0 || s.kind > DFM_STAT_ITERS) return fail(ctx, -6, "unknown stat kind %d", s.kind);
     if (s.kind == DFM_STAT_CRIT) {
       const int c = s.arg0 >= 0 ? s.arg0 : M->crit;
       if (c < 0 || c > 6) return fail(ctx, -6, "criterion stat without a criterion");
       if (c <= 2) pcp = true;
     }
-    if (s.kind >= DFM_STAT_LR) {
+    if (s.kind == DFM_STAT_EIGVAL && (s.arg0 < 0 || s.arg0 >= r))
+      return fail(ctx, -6, "eigenvalue index %d outside 0..%d", s.arg0, r - 1);
+    if ((s.kind == DFM_STAT_COEF || s.kind == DFM_STAT_TSTAT) && (s.arg0 < 0 || s.arg0 >= q + r))
+      return fail(ctx, -6, "coefficient index %d outside 0..%d", s.arg0, q + r - 1);
+    if (chow_stat(s.kind)) {
       if (s.arg0 < r || s.arg0 > T - r) return fail(ctx, -7, "break period %d out of range", s.arg0);
       if (chow && s.arg0 != chow_bp) return fail(ctx, -7, "one break period per call");
-      if (M->nblk > 1) return fail(ctx, -7, "Chow statistics of a model fitted with break_indices are not "
-                                           "supported (the tests read one loadings matrix: defect D1)");
+      if (M->nblk > 64) return fail(ctx, -7, "Chow statistics support at most 64 break blocks");
       chow = true; chow_bp = s.arg0;
       if (s.kind <= DFM_STAT_WALD && (s.arg1 < 0 || s.arg1 >= N)) return fail(ctx, -7, "variable index");
     }
     sd[i] = {s.kind, s.arg0, s.arg1, (int)width};
-    width += (s.kind >= DFM_STAT_LR_ALL) ? N : 1;
+    width += all_var_stat(s.kind) ? N : 1;
   }
   // Statistics that read only the eigenvalues and the trace let the
   // eigensolver stop on the (quadratic) eigenvalue bound instead of the
@@ -935,7 +946,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   bool values_only = ns > 0;
   for (int i = 0; i < ns; ++i)
     values_only = values_only && (stats[i].kind == DFM_STAT_V || stats[i].kind == DFM_STAT_CRIT ||
-                                  stats[i].kind == DFM_STAT_EIGVAL || stats[i].kind == DFM_STAT_TRACE);
+                                  stats[i].kind == DFM_STAT_EIGVAL || stats[i].kind == DFM_STAT_TRACE ||
+                                  stats[i].kind == DFM_STAT_ITERS);
   const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
   const int p = eig_block_p(m, r, ctx->block);
   // r beyond the subspace eigensolver's block: dense batched eigenpairs,
@@ -946,7 +958,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     return fail(ctx, -20, "bootstrap at r=%d > 24 needs min(T,N) <= %d", r, dense_eig_max());
   const bool chow_wide = chow && r > 16;   // GEMM-built Chow tests on materialised replicates
   // PCp reads each replicate's full spectrum, so its Gram is formed: direct path
-  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 32 && M->nblk == 1 && !pcp && !wide;
+  const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 16 && T <= fact_t_max() && M->nblk == 1 && !pcp &&
+                    !wide;
   if (pcp && m > spectrum_any_max())
     return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
                           "supported for min(T,N) <= %d", spectrum_any_max());
@@ -1034,14 +1047,14 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     return e == hipSuccess ? 0 : fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));
   };
   // factors of n replicate panels (rows T_rows of src) into F (+ row offset)
-  auto factors_any = [&](const PanelSrc &ps, int Trows, int n, double *Fo, const double *Uk) -> int {
+  auto factors_any = [&](const PanelSrc &ps, int Trows, int n, double *Fo, const double *Uk, double *Lo) -> int {
     Scope sc(ctx, DFM_KC_FACTORS);
     if (r <= 32) {
-      launch_factors(M->orient, ps, Trows, N, r, n, Uk, Fo, w.L, nullptr, st, (double)T, (int64_t)T * r);
+      launch_factors(M->orient, ps, Trows, N, r, n, Uk, Fo, Lo, nullptr, st, (double)T, (int64_t)T * r);
       return 0;
     }
     HIPCHK(ctx, launch_materialize(ps, Trows, N, M->ld, n, wX.p, st));
-    if (launch_factors_wide(M->orient, wX.p, M->ld, Trows, N, r, Uk, Fo, w.L, nullptr, st, (double)T, n,
+    if (launch_factors_wide(M->orient, wX.p, M->ld, Trows, N, r, Uk, Fo, Lo, nullptr, st, (double)T, n,
                             (int64_t)Trows * M->ld, (int64_t)T * r))
       return fail(ctx, 1001, "factor kernels failed");
     return 0;
@@ -1079,7 +1092,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
         int rc = eig_any(w.G, mj, n, M->Ubs[j], w.blam, w.Uk, w.btr, b0);
         if (rc) return rc;
         hipLaunchKernelGGL(or_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, n, M->flag_dev, 1);
-        if ((rc = factors_any(sj, tj, n, w.F + (size_t)a * r, w.Uk))) return rc;
+        if ((rc = factors_any(sj, tj, n, w.F + (size_t)a * r, w.Uk, w.L + (size_t)j * nb * N * r))) return rc;
         hipLaunchKernelGGL(block_accum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.blam, w.btr, n, r,
                            w.lam, w.trace, j == 0 ? 1 : 0);
       }
@@ -1090,7 +1103,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       }
       int rc = eig_any(w.G, m, n, M->Ub, w.lam, w.Uk, w.trace, b0);
       if (rc) return rc;
-      if ((rc = factors_any(src, T, n, w.F, w.Uk))) return rc;
+      if ((rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
     }
     if (q + r <= 32) {
       Scope sc(ctx, DFM_KC_OLS);
@@ -1116,9 +1129,14 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     {
       Scope sc(ctx, DFM_KC_STATS);
       if (ns)
+      {
+        // the eigensolver's per-replicate step counts (DFM_STAT_ITERS): the
+        // workspace of this batch's (last block's) subspace solve
+        const int *iters = wide ? nullptr : eig_iters_ptr(w.eig, M->nblk > 1 ? M->bm.back() : m, n, P, ctx->maxit);
         hipLaunchKernelGGL(stats_kernel, dim3((n + 127) / 128), dim3(128), 0, st, n, T, N, r, q,
-                           M->crit, M->sigma2, pcp ? pSig.p : nullptr, w.lam, w.trace, w.coef, w.tstat,
+                           M->crit, M->sigma2, pcp ? pSig.p : nullptr, w.lam, w.trace, w.coef, w.tstat, iters,
                            M->sd_dev, ns, out + b0 * width, width);
+      }
       hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
                          n, M->flag_dev);
     }
@@ -1141,13 +1159,15 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       const double *scr;
       if (!chow_wide) {
         HIPCHK(ctx, launch_chow(M->orient, src, T, N, r, chow_bp, n, w.F, w.L, LR, LM, WD, ostride,
-                                w.chow, w.chow_bytes, st));
+                                w.chow, w.chow_bytes, st, M->nblk, M->ba.data(), (int64_t)nb * N * r));
         // scratch rows live at the end of the chow workspace: [3][nb][N]
         scr = (const double *)(w.chow + w.chow_bytes) - (size_t)3 * n * N;   // launch_chow's [3][n][N]
       } else {
-        if (r <= 32) HIPCHK(ctx, launch_materialize(src, T, N, M->ld, n, wX.p, st));   // (r > 32: factors_any did)
+        // the whole replicate panel (r > 32 without breaks: factors_any already did)
+        if (r <= 32 || M->nblk > 1) HIPCHK(ctx, launch_materialize(src, T, N, M->ld, n, wX.p, st));
         HIPCHK(ctx, launch_chow_wide(n, wX.p, M->ld, (int64_t)T * M->ld, nullptr, T, N, r, chow_bp, w.F,
-                                     (int64_t)T * r, w.L, (int64_t)N * r, LR, LM, WD, ostride, wSc.p, wCh.p, st));
+                                     (int64_t)T * r, w.L, (int64_t)N * r, LR, LM, WD, ostride, wSc.p, wCh.p, st,
+                                     M->nblk, M->ba.data(), (int64_t)nb * N * r));
         scr = wSc.p;
       }
       for (int i = 0; i < ns; ++i) {
@@ -1326,6 +1346,7 @@ int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald)
   if (!M) return -1;
   dfm_ctx *ctx = M->ctx;
   if (bp < M->r || bp > M->T - M->r) return fail(ctx, -7, "break period %lld out of range", (long long)bp);
+  if (M->nblk > 64) return fail(ctx, -7, "Chow statistics support at most 64 break blocks");
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   if (M->r > 16) {   // any r: the GEMM-built tests (dfm_wide.hip)
@@ -1350,7 +1371,7 @@ int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald)
   {
     Scope sc(ctx, DFM_KC_CHOW);
     HIPCHK(ctx, launch_chow(M->orient, src, M->T, M->N, M->r, (int)bp, 1, M->F, M->L, nullptr, nullptr,
-                            nullptr, M->N, ws, bytes, st));
+                            nullptr, M->N, ws, bytes, st, M->nblk, M->ba.data(), (int64_t)M->N * M->r));
   }
   const double *scr = (const double *)(ws + bytes) - (size_t)3 * M->N;
   double *outs[3] = {LR, LM, Wald};
@@ -1576,6 +1597,8 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     return fail(ctx, -31, "dfm_windows: PCp / kmax > 24 need each window's full spectrum: supported for "
                           "min(T,N) <= %d", std::min(spectrum_any_max(), dense_eig_max()));
   const int Pb = (p <= 16 || wide) ? 16 : 32;
+  if (orient == 0 && !wide && T > fact_t_max())
+    return fail(ctx, -20, "dfm_windows: N > T windows need T <= %d (got %d)", fact_t_max(), T);
   DevPanel dp;
   int rc = upload_panel(ctx, X, T, N, ldx, dp, dev);
   if (rc) return rc;
@@ -1798,5 +1821,154 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     HIPCHK(ctx, hipMemcpyAsync(true_out, dt_, (size_t)P * 8, hipMemcpyDeviceToHost, st));
   }
   HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
+// ------------------------------------------------------------------ normalize
+// normalize (src/utils.jl:33): (A .- mean(A, 1)) ./ std(A, 1) — column z-score
+// with the sample std (n - 1 denominator), two passes over the column (mean,
+// then the centred sum of squares), then the scaled write.  One wave per
+// column of the column-major panel (contiguous in Julia's layout: coalesced);
+// Y may alias X.
+__global__ __launch_bounds__(256) void normalize_cols_kernel(const double *X, int64_t ldx, int T, int N, double *Y,
+                                                             int64_t ldy) {
+  const int lane = threadIdx.x & 63, c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= N) return;
+  const double *x = X + (int64_t)c * ldx;
+  double s = 0.0;
+  for (int t = lane; t < T; t += 64) s += x[t];
+  const double mu = wave_sum(s) / T;
+  double v = 0.0;
+  for (int t = lane; t < T; t += 64) { const double d = x[t] - mu; v = fma(d, d, v); }
+  const double sd = sqrt(wave_sum(v) / (T - 1));
+  double *y = Y + (int64_t)c * ldy;
+  for (int t = lane; t < T; t += 64) y[t] = (x[t] - mu) / sd;
+}
+
+extern "C" int dfm_normalize_dev(dfm_ctx *ctx, const double *X, int64_t T, int64_t N, int64_t ldx, double *out,
+                                 int64_t ldo) {
+  if (!ctx) return -1;
+  if (!X || !out || T < 2 || N < 1 || ldx < T || ldo < T || T > INT32_MAX || N > INT32_MAX)
+    return fail(ctx, -2, "dfm_normalize: bad arguments");
+  hipSetDevice(ctx->device);
+  Scope sc(ctx, DFM_KC_MISC);
+  hipLaunchKernelGGL(normalize_cols_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, ctx->stream, X, ldx, (int)T,
+                     (int)N, out, ldo);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+extern "C" int dfm_normalize(dfm_ctx *ctx, const double *X, int64_t T, int64_t N, int64_t ldx, double *out,
+                             int64_t ldo) {
+  if (!ctx) return -1;
+  if (!X || !out || T < 2 || N < 1 || ldx < T || ldo < T) return fail(ctx, -2, "dfm_normalize: bad arguments");
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  DevBuf d;
+  HIPCHK(ctx, dalloc(&d.p, (size_t)T * N));
+  HIPCHK(ctx, hipMemcpy2DAsync(d.p, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N, hipMemcpyHostToDevice, st));
+  int rc = dfm_normalize_dev(ctx, d.p, T, N, T, d.p, T);
+  if (rc) return rc;
+  HIPCHK(ctx, hipMemcpy2DAsync(out, (size_t)ldo * 8, d.p, (size_t)T * 8, (size_t)T * 8, N, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
+// ------------------------------------------------------------ multi-device
+// A fitted model copied onto another context (another GPU, or a second
+// context of the same GPU): every device buffer and host field, so the copy's
+// bootstrap replicates are bit-identical to the original's.
+extern "C" int dfm_model_clone(const dfm_model *S, dfm_ctx *ctx, dfm_model **out) {
+  if (!S || !ctx || !out) return -1;
+  *out = nullptr;
+  dfm_ctx *sc = S->ctx;
+  hipSetDevice(sc->device);
+  HIPCHK(ctx, hipStreamSynchronize(sc->stream));
+  dfm_model *M = new dfm_model();
+  ++ctx->refs;
+  M->ctx = ctx;
+  M->T = S->T; M->N = S->N; M->q = S->q; M->r = S->r; M->crit = S->crit; M->kmax = S->kmax; M->m = S->m;
+  M->orient = S->orient; M->k_eig = S->k_eig; M->swept = S->swept; M->ld = S->ld;
+  M->lam = S->lam; M->coef = S->coef; M->tstat = S->tstat; M->cov = S->cov; M->resid = S->resid; M->ic = S->ic;
+  M->trace = S->trace; M->V = S->V; M->critval = S->critval; M->sigma2 = S->sigma2;
+  M->batch = S->batch; M->mode = S->mode;
+  M->nblk = S->nblk; M->ba = S->ba; M->bt = S->bt; M->bm = S->bm; M->blam = S->blam;
+  std::vector<double> stage;
+  auto dup = [&](const double *src, size_t n, double **dst) -> int {
+    stage.resize(std::max<size_t>(n, 1));
+    hipSetDevice(sc->device);
+    if (hipMemcpy(stage.data(), src, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    hipSetDevice(ctx->device);
+    if (dalloc(dst, n) != hipSuccess) return 1;
+    return hipMemcpy(*dst, stage.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : 1;
+  };
+  const size_t T = S->T, N = S->N, r = S->r, panel = T * S->ld;
+  int bad = 0;
+  bad |= dup(S->Xp, panel, &M->Xp);
+  bad |= dup(S->Cp, panel, &M->Cp);
+  bad |= dup(S->Ep, panel, &M->Ep);
+  bad |= dup(S->y, T, &M->y);
+  bad |= dup(S->w, T * std::max(S->q, 1), &M->w);
+  bad |= dup(S->F, T * r, &M->F);
+  bad |= dup(S->colssr, N, &M->colssr);
+  bad |= dup(S->Lall, (size_t)S->nblk * N * r, &M->Lall);
+  M->Ubs.assign(S->nblk, nullptr);
+  M->Ls.assign(S->nblk, nullptr);
+  for (int j = 0; j < S->nblk && !bad; ++j) {
+    bad |= dup(S->Ubs[j], (size_t)S->bm[j] * r, &M->Ubs[j]);
+    M->Ls[j] = M->Lall + (size_t)j * N * r;
+  }
+  M->Ub = M->Ubs.empty() ? nullptr : M->Ubs[0];
+  M->L = M->Lall;
+  hipSetDevice(ctx->device);
+  if (!bad) bad = dalloc(&M->flag_dev, 4) != hipSuccess;
+  if (bad) {
+    dfm_model_destroy(M);
+    return fail(ctx, 1002, "dfm_model_clone: device copy failed");
+  }
+  *out = M;
+  return 0;
+}
+
+// wild_bootstrap / residual_bootstrap (src/bootstrap.jl:21-51) with the
+// replicate loop (:43) sharded over n models (one per context, typically one
+// per GPU, each a dfm_model_clone of the same fit): replicate b runs on model
+// floor(b n / B), i.e. contiguous shards, each driven by its own host thread
+// on its own stream; rows land in order in the caller's out (B x width).
+// No collective: the shards are independent and the host buffer is the
+// gather.  Contexts must be distinct (one host thread per context).
+extern "C" int dfm_bootstrap_multi(dfm_model *const *models, int n, int kind, int64_t B, const int32_t *idx,
+                                   const double *eta, const dfm_stat *stats, int ns, double *out) {
+  if (!models || n < 1 || !models[0]) return -1;
+  dfm_ctx *c0 = models[0]->ctx;
+  for (int g = 0; g < n; ++g) {
+    if (!models[g]) return fail(c0, -2, "dfm_bootstrap_multi: model %d is NULL", g);
+    const dfm_model *a = models[g], *b = models[0];
+    if (a->T != b->T || a->N != b->N || a->r != b->r || a->q != b->q || a->nblk != b->nblk || a->crit != b->crit)
+      return fail(c0, -2, "dfm_bootstrap_multi: model %d is not a copy of model 0", g);
+    for (int h = 0; h < g; ++h)
+      if (models[h]->ctx == a->ctx) return fail(c0, -2, "dfm_bootstrap_multi: models %d and %d share a context", h, g);
+  }
+  if (B < 0 || !idx || (kind == DFM_BOOT_WILD && !eta)) return fail(c0, -2, "dfm_bootstrap_multi: bad arguments");
+  if (B == 0) return 0;
+  const int64_t width = dfm_stats_width(models[0], stats, ns);
+  if (width < 0) return fail(c0, -2, "dfm_bootstrap_multi: bad stat list");
+  const int64_t T = models[0]->T;
+  std::vector<int> rcs(n, 0);
+  std::vector<std::thread> th;
+  for (int g = 0; g < n; ++g) {
+    const int64_t b0 = ((int64_t)g * B + n - 1) / n, b1 = ((int64_t)(g + 1) * B + n - 1) / n;
+    if (b1 <= b0) continue;
+    th.emplace_back([=, &rcs]() {
+      rcs[g] = dfm_bootstrap(models[g], kind, b1 - b0, idx + b0 * T, eta ? eta + b0 * T : nullptr, stats, ns,
+                             out ? out + b0 * width : nullptr);
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int g = 0; g < n; ++g)
+    if (rcs[g]) {
+      const std::string msg = models[g]->ctx->err;
+      return fail(c0, rcs[g], "shard %d: %s", g, msg.c_str());
+    }
   return 0;
 }

@@ -10,6 +10,10 @@
 //   LM  = T c' [M^-1]_22 c / ||E_i||^2 with D'E_i = [0; c], c = g2 - A2 l_i
 //         (F'E_i = 0 for PCA loadings): the uncentred R^2 of :35-42
 //   ||E_i||^2 and the subperiod SSRs are summed explicitly (no cancellation)
+//   A model fitted with break_indices (src/DynamicFactorModel.jl:73, :98)
+//   has one loadings matrix per break block: E_i = x_i - F_t l_i^(block(t)),
+//   and F = vcat(F_j) (defect D1).  F_j'E_ij = 0 still holds block by block,
+//   so D'E_i = [0; c] with c = sum_{t >= bp} f_t e_ti, summed explicitly.
 //   Wald: beta = M^-1 [g1+g2; g2]; HC0 meat; with W = M^-1[:, r:] = [Wa; Wb]
 //         Cov22 = sum_t u_t^2 z_t z_t',  z_t = Wa'f_t (t < bp), (Wa+Wb)'f_t
 //         (t >= bp) — one r x r accumulator per variable instead of the
@@ -21,6 +25,15 @@
 namespace dfm {
 
 constexpr int CH_RMAX = 16;
+constexpr int CH_BMAX = 64;   // break blocks of a Chow call
+
+// Row ranges of the model's break blocks: block j is rows a[j] .. a[j+1]-1,
+// its loadings at Lm + j * lbs (+ replicate stride N r).
+struct ChowBlocks {
+  int n;
+  int a[CH_BMAX + 1];
+  int64_t lbs;
+};
 
 struct ChowPrep {   // per replicate, written by chow_prep_kernel
   // Mi: 2r x 2r, A1i, A2i, ApS = A1 + A2: r x r (row stride CH_RMAX*2)
@@ -99,8 +112,8 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
   }
 }
 
-template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
-__global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int N, int r, int bp,
+template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK>
+__global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
                                                        const double *__restrict__ F,
                                                        const double *__restrict__ Z,
                                                        const ChowPrep *__restrict__ prep,
@@ -141,13 +154,18 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
     return x;
   };
   // loadings of variable i (src/chowtest.jl uses dfm.factor_residuals = x - F L')
+  // (break models: block b's loadings for rows a[b] .. a[b+1]-1)
   double l[R];
+  auto load_l = [&](int b) {
 #pragma unroll
-  for (int j = 0; j < R; ++j) l[j] = (ok && j < r) ? Lm[((int64_t)rep * N + i) * r + j] : 0.0;
-  // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2
-  double g1[R], g2[R], e2 = 0.0;
+    for (int j = 0; j < R; ++j) l[j] = (ok && j < r) ? Lm[b * blk.lbs + ((int64_t)rep * N + i) * r + j] : 0.0;
+  };
+  load_l(0);
+  int cb = 0, next = BRK ? blk.a[1] : T;
+  // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2 (BRK: cx = sum_{t>=bp} f_t e_t)
+  double g1[R], g2[R], cx[R], e2 = 0.0;
 #pragma unroll
-  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; }
+  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; cx[j] = 0.0; }
   for (int t0 = 0; t0 < T; t0 += TR) {
     __syncthreads();
     stage(t0);
@@ -156,11 +174,16 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
     const int tn = min(TR, T - t0);
     for (int rr = 0; rr < tn; ++rr) {
       const int t = t0 + rr;
+      if (BRK && t == next) { ++cb; next = blk.a[cb + 1]; load_l(cb); }
       const double x = xval(rr, t);
       double ev = x;
 #pragma unroll
       for (int j = 0; j < R; ++j) ev -= sF[rr * R + j] * l[j];
       e2 = fma(ev, ev, e2);
+      if (BRK && t >= bp) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[rr * R + j], cx[j]);
+      }
       if (t < bp) {
 #pragma unroll
         for (int j = 0; j < R; ++j) g1[j] = fma(x, sF[rr * R + j], g1[j]);
@@ -182,9 +205,9 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
       u2 = fma(P.A2i[a * RR + c2], g2[c2], u2);
       v1 = fma(P.Va[c2 * RR + a], g1[c2], fma(P.Vc[c2 * RR + a], g2[c2], v1));
       v2 = fma(P.Wa[c2 * RR + a], g1[c2], fma(P.Wc[c2 * RR + a], g2[c2], v2));
-      c -= P.A2[a * RR + c2] * l[c2];
+      if (!BRK) c -= P.A2[a * RR + c2] * l[c2];
     }
-    ga1[a] = u1; ga2[a] = u2; b1[a] = v1; b2[a] = v2; cv[a] = c;
+    ga1[a] = u1; ga2[a] = u2; b1[a] = v1; b2[a] = v2; cv[a] = BRK ? cx[a] : c;
   }
   double lmq = 0.0;
 #pragma unroll
@@ -261,28 +284,42 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, int T, int 
 }
 
 template <int R>
-static void launch_chow_r(const PanelSrc &src, int T, int N, int r, int bp, int nb, const double *F,
-                          const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
+static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int N, int r, int bp, int nb,
+                          const double *F, const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
                           double *LM, double *WD, hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
   // narrow panels (C2: N = 130) get a 192-thread block, not a half-idle 256
   const int nth = std::min(256, (N + 63) / 64 * 64);
   dim3 grid((N + nth - 1) / nth, nb), block(nth);
-#define DFM_CH(C_, E_, X_)                                                                       \
-  hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_>), grid, block, 0, st, src, T, N, r, bp, F, Z, \
+#define DFM_CH(C_, E_, X_, B_)                                                                          \
+  hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_>), grid, block, 0, st, src, blk, T, N, r, bp, F, Z, \
                      prep, Lm, LR, LM, WD)
-  if (c && e && x) DFM_CH(true, true, true);
-  else if (c && !e && x) DFM_CH(true, false, true);
-  else DFM_CH(false, false, false);
+  if (blk.n > 1) {
+    if (c && e && x) DFM_CH(true, true, true, true);
+    else if (c && !e && x) DFM_CH(true, false, true, true);
+    else DFM_CH(false, false, false, true);
+  } else {
+    if (c && e && x) DFM_CH(true, true, true, false);
+    else if (c && !e && x) DFM_CH(true, false, true, false);
+    else DFM_CH(false, false, false, false);
+  }
 #undef DFM_CH
 }
 
 // scratch layout in ws: [ChowPrep x nb][Z: nb x T x r] ... [3][nb][N] at the END.
+// Break models: nblk > 1 blocks with first rows brow[0..nblk-1] (brow[0] = 0),
+// loadings of block j at Lm + j * lbs.
 hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
                        const double *F, const double *Lm, double *LRo, double *LMo, double *WDo,
-                       int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st) {
+                       int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st, int nblk,
+                       const int *brow, int64_t lbs) {
   (void)orient;
-  if (r < 1 || r > CH_RMAX) return hipErrorInvalidValue;
+  if (r < 1 || r > CH_RMAX || nblk < 1 || nblk > CH_BMAX) return hipErrorInvalidValue;
+  ChowBlocks blk{};
+  blk.n = nblk;
+  blk.lbs = lbs;
+  for (int j = 0; j < nblk; ++j) blk.a[j] = nblk > 1 ? brow[j] : 0;
+  blk.a[nblk] = T;
   ChowPrep *prep = (ChowPrep *)ws;
   double *Z = (double *)(ws + (size_t)nb * sizeof(ChowPrep));
   double *scr = (double *)(ws + ws_bytes) - (size_t)3 * nb * N;
@@ -290,9 +327,9 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
   double *LR = scr, *LM = scr + (size_t)nb * N, *WD = scr + (size_t)2 * nb * N;
   // R = padded factor count of the per-variable register blocks (zero
   // padding: r <= 4 runs 4-wide, 10 HC0 accumulators instead of 36)
-  if (r <= 4) launch_chow_r<4>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
-  else if (r <= 8) launch_chow_r<8>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
-  else launch_chow_r<16>(src, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  if (r <= 4) launch_chow_r<4>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  else if (r <= 8) launch_chow_r<8>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  else launch_chow_r<16>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
   // scatter into the caller's strided output rows
   if (LRo) hipMemcpy2DAsync(LRo, (size_t)out_stride * 8, LR, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);
   if (LMo) hipMemcpy2DAsync(LMo, (size_t)out_stride * 8, LM, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);

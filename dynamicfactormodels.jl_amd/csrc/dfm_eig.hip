@@ -704,6 +704,9 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   return w;
 }
 
+// per-replicate Rayleigh-Ritz steps of the last solve carved from ws (diagnostic stat)
+const int *eig_iters_ptr(char *ws, int m, int nb, int P, int maxit) { return carve(ws, m, nb, P, maxit).iters; }
+
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit) {
   return eig_workspace_bytes(m, nb, P, maxit) + 16 * 256;
 }
@@ -713,21 +716,8 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 // diagonalised exactly at every outer iteration: the next iteration starts
 // from the (nearly) rotated basis, so the inner sweeps accumulate across outer
 // iterations, and the residual test of check_converged includes any leftover
-// off-diagonal coupling.  DFM_JACOBI_SWEEPS overrides (development).
-// Filter degree of the factored bootstrap iteration: 1 = subspace (power)
-// iteration, 2 = degree-2 Chebyshev filter (boot_cheb_kernel).  DFM_CHEB
-// overrides (development A/B).
-static int cheb_degree() {
-  static const int d = [] {
-    const char *e = getenv("DFM_CHEB");
-    return e ? atoi(e) : 2;
-  }();
-  return d;
-}
-static int jacobi_sweeps() {
-  static const int n = [] { const char *e = getenv("DFM_JACOBI_SWEEPS"); return e ? atoi(e) : 2; }();
-  return n;
-}
+// off-diagonal coupling.
+constexpr int kJacobiSweeps = 2;
 int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
 // replicate-iterations of the last run's dominant product (G.Q in eig_gq, or
 // the H.Z GEMM in the factored solver) that still had an unconverged
@@ -771,7 +761,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   int it = 0;
   bool finished = false;
   std::vector<int> act;
-  const int cheb = cheb_degree() == 2 ? 1 : 0;
+  const int cheb = 1;   // degree-2 Chebyshev filter between Rayleigh-Ritz steps
   for (; it <= maxit; ++it) {
     const int check_only = (it == maxit);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
@@ -780,7 +770,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (check_only) break;
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, jacobi_sweeps());
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, kJacobiSweeps);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0, cheb);
@@ -911,110 +901,6 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   if (tid == 0) trace[rep] = red[0];
 }
 
-// Z = P' D Q into the GEMM operand Zc[s][rep*P + c] for the 64 rows s of this
-// block, plus the block's partial a = F'Q (rows t of the block) and
-// cc = EL'Z (rows s of the block) into abp[rep][rb][2][r][P].
-template <int P>
-__global__ __launch_bounds__(256) void boot_fz_kernel(FactBase fb, EigWork w, int m, const double *__restrict__ eta,
-                                                      const int *__restrict__ off, const int *__restrict__ lst,
-                                                      double *__restrict__ Zc, int64_t ldz,
-                                                      double *__restrict__ abp) {
-  constexpr int RM = 32;
-  __shared__ double sZ[EROWS * P], sQ[EROWS * P];
-  const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, T = fb.T, r = fb.r;
-  if (w.done[rep]) return;
-  const double *Q = w.Q + (int64_t)rep * m * P;
-  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
-  const int *o = off + (int64_t)rep * (T + 1);
-  const int *L = lst + (int64_t)rep * T;
-  const int s0 = rb * EROWS;
-  for (int e = tid; e < EROWS * P; e += 256) {
-    const int ls = e / P, c = e % P, sI = s0 + ls;
-    double z = 0.0, qv = 0.0;
-    if (sI < T) {
-      for (int q = o[sI]; q < o[sI + 1]; ++q) {
-        const int t = L[q];
-        z = fma(et ? et[t] : 1.0, Q[(int64_t)t * P + c], z);
-      }
-      Zc[(int64_t)sI * ldz + (int64_t)rep * P + c] = z;
-      qv = Q[(int64_t)sI * P + c];
-    }
-    sZ[e] = z;
-    sQ[e] = qv;
-  }
-  __syncthreads();
-  double *pp = abp + ((int64_t)rep * nrb + rb) * 2 * RM * P;
-  const int rows = min(EROWS, T - s0);
-  for (int e = tid; e < 2 * r * P; e += 256) {
-    const int which = e / (r * P), j = (e / P) % r, c = e % P;
-    const double *X = which ? sZ : sQ;
-    const double *B = which ? fb.EL : fb.F;
-    double acc = 0.0;
-    for (int ls = 0; ls < rows; ++ls) acc = fma(B[(int64_t)(s0 + ls) * r + j], X[ls * P + c], acc);
-    pp[e] = acc;
-  }
-}
-
-// Y[t] = F_t (S a + cc) + eta_t ((EL)_idx_t a + (H Z)_idx_t), then the same
-// partial products as eig_gq (the convergence preamble first).
-template <int P>
-__global__ __launch_bounds__(256) void boot_gq_kernel(FactBase fb, EigWork w, int m, int k, int p, double tol,
-                                                      int it, int check_only, const int32_t *__restrict__ idx,
-                                                      const double *__restrict__ eta,
-                                                      const double *__restrict__ HZ, int64_t ldz,
-                                                      const double *__restrict__ ab) {
-  constexpr int SQ = P + 4;
-  constexpr int RM = 32;
-  __shared__ __attribute__((aligned(16))) double sQ[EROWS * SQ];
-  __shared__ __attribute__((aligned(16))) double sY[EROWS * SQ];
-  __shared__ double sA[RM * P], sB[RM * P], sC[RM * P];
-  __shared__ int s_skip;
-  const int tid = threadIdx.x, rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x, r = fb.r;
-  double *small = w.small + (int64_t)rep * small_stride<P>();
-  if (tid < 64) { const int d = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only); if (tid == 0) s_skip = d; }
-  __syncthreads();
-  if (s_skip) return;
-  // a and cc: fixed-order sums of the row-block partials of boot_fz; sB = S a + cc
-  const double *abp = ab + (int64_t)rep * nrb * 2 * RM * P;
-  for (int e = tid; e < 2 * r * P; e += 256) {
-    double acc = 0.0;
-    for (int q = 0; q < nrb; ++q) acc += abp[(int64_t)q * 2 * RM * P + e];
-    (e < r * P ? sA[e] : sC[e - r * P]) = acc;
-  }
-  __syncthreads();
-  for (int e = tid; e < r * P; e += 256) {
-    const int j = e / P, c = e % P;
-    double v = sC[e];
-    for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], sA[i * P + c], v);
-    sB[e] = v;
-  }
-  __syncthreads();
-  const double *Qr = w.Q + (int64_t)rep * m * P;
-  double *Yr = w.Y + (int64_t)rep * m * P;
-  const int32_t *ix = idx + (int64_t)rep * fb.T;
-  const double *et = eta ? eta + (int64_t)rep * fb.T : nullptr;
-  for (int e = tid; e < EROWS * P; e += 256) {
-    const int lr = e / P, c = e % P, t = rb * EROWS + lr;
-    double y = 0.0, q = 0.0;
-    if (t < m) {
-      const int i = ix[t];
-      double u = HZ[(int64_t)i * ldz + (int64_t)rep * P + c];
-      double v = 0.0;
-      for (int j = 0; j < r; ++j) {
-        u = fma(fb.EL[(int64_t)i * r + j], sA[j * P + c], u);
-        v = fma(fb.F[(int64_t)t * r + j], sB[j * P + c], v);
-      }
-      y = fma(et ? et[t] : 1.0, u, v);
-      q = Qr[(int64_t)t * P + c];
-      Yr[(int64_t)t * P + c] = y;
-    }
-    sY[lr * SQ + c] = y;
-    sQ[lr * SQ + c] = q;
-  }
-  __syncthreads();
-  emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
-}
-
 hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
                                 int r, double invT, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
@@ -1029,108 +915,6 @@ size_t fact_workspace_bytes(int T, int nb, int P) {
   const int64_t ldz = (int64_t)nb * P;
   const int nrb = (T + EROWS - 1) / EROWS;
   return (size_t)(z_rows(T) + T) * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096;
-}
-
-template <int P>
-static int eig_run_fact_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
-                          const double *warm, int kw, double tol, int maxit, int poll, char *ws,
-                          char *fws, double *lam, double *Uk, double *trace_out, int *status,
-                          hipStream_t st, timer_fn tf, void *tctx, int *off_out, int *lst_out) {
-  const int m = fb.T, nrb = (m + EROWS - 1) / EROWS;
-  EigWork w = carve(ws, m, nb, P, maxit);
-  const int64_t ldz = (int64_t)nb * P;
-  double *Zc = (double *)fws;
-  double *HZ = Zc + (size_t)z_rows(m) * ldz;
-  double *ab = HZ + (size_t)m * ldz;
-  if (z_rows(m) > m) hipMemsetAsync(Zc + (size_t)m * ldz, 0, (size_t)(z_rows(m) - m) * ldz * 8, st);
-  int *off = off_out, *lst = lst_out;
-  hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
-  hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
-  const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
-  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
-  {
-    const int64_t n = (int64_t)m * P;
-    dim3 grid((unsigned)((n + 255) / 256), nb);
-    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, w.Q, m, p, warm, kw, w.done, seed, (int64_t)0);
-    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
-                       off, lst, w.trace);
-  }
-  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  int last_gemm = -1;
-  for (int it = 0; it <= maxit; ++it) {
-    const int check_only = (it == maxit);
-    if (!check_only) {
-      if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-      hipLaunchKernelGGL(boot_fz_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, fb, w, m, eta, off, lst, Zc, ldz, ab);
-      if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
-      if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true);
-      last_gemm = it;
-      if (tf) tf(tctx, DFM_KC_GEMM, 0);
-      if (e != hipSuccess) return 1000 + (int)e;
-    }
-    if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-    hipLaunchKernelGGL(boot_gq_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, fb, w, m, k, p, tol, it, check_only,
-                       idx, eta, HZ, ldz, ab);
-    if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
-    if (check_only) break;
-    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-    static const bool stamps_on = getenv("DFM_SMALL_STAMPS") != nullptr;
-    static long long *dbg_dev = nullptr;
-    if (stamps_on) {
-      if (!dbg_dev) hipMalloc(&dbg_dev, 64 * 8);
-      hipMemsetAsync(dbg_dev, 0, 64 * 8, st);
-      w.dbg = dbg_dev;
-    }
-    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, jacobi_sweeps());
-    if (stamps_on) {
-      long long h[64];
-      hipMemcpyAsync(h, dbg_dev, 64 * 8, hipMemcpyDeviceToHost, st);
-      hipStreamSynchronize(st);
-      fprintf(stderr, "small it %d sweeps %lld:", it, h[15]);
-      for (int i = 1; i <= 10; ++i) fprintf(stderr, " %lld", h[i] ? h[i] - h[i - 1] : -1);
-      fprintf(stderr, "\n");
-      w.dbg = nullptr;
-    }
-    if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
-    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, (int64_t)0, 0);
-    if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
-    static const bool trace_on = getenv("DFM_EIG_TRACE") != nullptr;
-    if (trace_on) {   // debug: residual trajectory of replicate 0, active count
-      std::vector<double> rp((size_t)nrb * P), th(P);
-      int act = -1;
-      hipMemcpyAsync(&act, w.active + it, 4, hipMemcpyDeviceToHost, st);
-      hipMemcpyAsync(rp.data(), w.rpart, rp.size() * 8, hipMemcpyDeviceToHost, st);
-      hipMemcpyAsync(th.data(), w.small + 2 * P * P, P * 8, hipMemcpyDeviceToHost, st);
-      hipStreamSynchronize(st);
-      fprintf(stderr, "it %2d act %4d:", it, act);
-      for (int j = 0; j < k; ++j) {
-        double sacc = 0; for (int r = 0; r < nrb; ++r) sacc += rp[(size_t)r * P + j];
-        fprintf(stderr, " %.1e", sqrt(sacc) / fabs(th[0]));
-      }
-      fprintf(stderr, "  th:");
-      for (int j = 0; j < p && j < 12; ++j) fprintf(stderr, " %.6g", th[j]);
-      fprintf(stderr, "\n");
-    }
-    if (it > 0 && (it % poll) == 0) {
-      int a = -1;
-      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
-      hipError_t e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return 1000 + (int)e;
-      if (a == 0) { g_last_iters = it; break; }
-    }
-    g_last_iters = it;
-  }
-  g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
-  g_last_gemm_products = g_last_rep_iters;
-  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
-  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
-  if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
-  if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return 1000 + (int)e;
-  return 0;
 }
 
 // ================================================= fused factored iteration
@@ -1837,7 +1621,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
   double *cur = w.Q, *alt = w.Y;
-  const int cheb = cheb_degree() == 2 ? 1 : 0;
+  const int cheb = 1;   // degree-2 Chebyshev filter between Rayleigh-Ritz steps
   // the warm start is the same for every replicate: ONE m x P block (Q0),
   // read with replicate stride 0 by the init pass and the first step's y2 /
   // ap2 (L2-resident) instead of nb materialised copies
@@ -1876,7 +1660,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
                        qin, qs, alt);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
-    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, jacobi_sweeps());
+    hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, kJacobiSweeps);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
@@ -1935,22 +1719,14 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
                      timer_fn tf, void *tctx, int *off, int *lst) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
-  static const bool legacy = getenv("DFM_FACT_LEGACY") != nullptr;   // development A/B switch
-  const int Pb = p <= 16 ? 16 : 32;
-  if (!legacy && fb.r <= 16 && fb.T <= F2_T_MAX) {
-    if (Pb == 16)
-      return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                                 trace_out, status, st, tf, tctx, off, lst);
-    return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                               trace_out, status, st, tf, tctx, off, lst);
-  }
+  if (fb.r > 16 || fb.T > F2_T_MAX) return -1;   // callers take the direct path
   if (p <= 16)
-    return eig_run_fact_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                              trace_out, status, st, tf, tctx, off, lst);
-  return eig_run_fact_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                            trace_out, status, st, tf, tctx, off, lst);
+    return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                               trace_out, status, st, tf, tctx, off, lst);
+  return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
+                             trace_out, status, st, tf, tctx, off, lst);
 }
-
+int fact_t_max() { return F2_T_MAX; }
 
 // ---- factored loadings pass: L* = X*' F* / T = (L (F'F*) + E' P' D F*) / T
 // boot_zf: ZF[s][rep*r + j] = sum_{t in bucket s} eta_t F*[t][j]  and

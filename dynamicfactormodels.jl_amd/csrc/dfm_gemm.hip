@@ -29,11 +29,9 @@ DFM_DEV int off_cols(int a, int kc) { return kc * GT + (a ^ ((kc & 7) << 2)); } 
 }  // namespace
 
 // Ring/occupancy choice of the LDS-DMA kernels by output height: rows >= 1024
-// run the 3-deep ring at 3 workgroups per CU (DFM_GEMM_RING3=0/1 forces).
-static bool gemm_ring3(int M) {
-  static const int f = [] { const char *e = getenv("DFM_GEMM_RING3"); return e ? atoi(e) : -1; }();
-  return f >= 0 ? f != 0 : M >= 1024;
-}
+// run the 3-deep ring at 3 workgroups per CU (more resident waves beat a
+// deeper ring there: tools/gemm_bench.hip, M = 2000).
+static bool gemm_ring3(int M) { return M >= 1024; }
 
 // One stage of staging registers (4 A chunks + 4 B chunks of 16 B per
 // thread) kept as a plain struct of scalars: no lambdas capturing arrays by
@@ -244,7 +242,7 @@ DFM_DEV void g2_issue(double *stage, const double *__restrict__ A, const double 
   }
 }
 
-template <int NBUF, int MINB, bool PRIO, bool RUN = false>
+template <int NBUF, int MINB, bool RUN = false>
 __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__restrict__ A, int64_t lda,
                                                        const double *__restrict__ B, int64_t ldb,
                                                        double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
@@ -312,12 +310,10 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
       af[f] = la[g2_offA(wr * 32 + 4 * f + fi, fkc)];
       bf[f] = lb[g2_offB(fkc, wc * 32 + 4 * f + fi)];
     }
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
   const int oi = lane >> 4, oj = lane & 3;
@@ -341,7 +337,7 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 }
 
 // the production configuration
-#define gemmh_kernel gemmh_kernel_t<4, 2, false>
+#define gemmh_kernel gemmh_kernel_t<4, 2>
 
 // ---------------------------------------------------------------------------
 // Loadings GEMM of the factored bootstrap:
@@ -357,25 +353,7 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 // (64 x T x 8 B each) stay in its L2 — and every XCD walks the column blocks
 // in the same order, so a ZF tile is fetched from HBM once and served to the
 // other XCDs from the Infinity Cache.
-DFM_DEV void g2_issue_t(double *stage, const double *__restrict__ A, int64_t lda, const double *__restrict__ B,
-                        int64_t ldb, int k0, int abase, int bbase, int M, int Nc, int K, int wave, int lane) {
-  double *la = stage, *lb = stage + GT * G2_KS;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = 2 * wave + h;
-    const int kc = 2 * c + (lane >> 5);
-    const int sw = (2 * (lane & 31)) ^ ((kc & 7) << 2);
-    const int ra = min(k0 + kc, K - 1);             // rows past K: finite, times B's zero rows
-    const int ca = min(abase + sw, (int)lda - 2);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)(A + (int64_t)ra * lda + ca), (lds_void_t *)(la + c * 128), 16,
-                                     0, 0);
-    const int cb = min(bbase + sw, Nc - 2);
-    __builtin_amdgcn_global_load_lds((gbl_void_t *)(B + (int64_t)(k0 + kc) * ldb + cb), (lds_void_t *)(lb + c * 128),
-                                     16, 0, 0);
-  }
-}
-
-template <int NBUF, int MINB, bool RUN>
+template <int NBUF, int MINB>
 __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
                                                                   const double *__restrict__ B, int64_t ldb, int M,
                                                                   int Nc, int K, int nrb, int ncb, int r, double invT,
@@ -395,7 +373,7 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
     for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int nst = (K + G2_KS - 1) / G2_KS;
-  // RUN: running DMA pointers (both operands hold zero k-rows up to
+  // running DMA pointers (both operands hold zero k-rows up to
   // round_up(K, 16), so the last stage needs no clamp)
   const double *pa[2], *pb[2];
 #pragma unroll
@@ -407,19 +385,14 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
   }
   const int64_t astep = (int64_t)G2_KS * lda, bstep = (int64_t)G2_KS * ldb;
   auto issue = [&](int s) {
-    double *stage = lds + (s % NBUF) * G2_STAGE;
-    if (RUN) {
-      double *la = stage, *lb = stage + GT * G2_KS;
+    double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = 2 * wave + h;
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)pa[h], (lds_void_t *)(la + c * 128), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)pb[h], (lds_void_t *)(lb + c * 128), 16, 0, 0);
-        pa[h] += astep;
-        pb[h] += bstep;
-      }
-    } else {
-      g2_issue_t(stage, A, lda, B, ldb, s * G2_KS, abase, bbase, M, Nc, K, wave, lane);
+    for (int h = 0; h < 2; ++h) {
+      const int c = 2 * wave + h;
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pa[h], (lds_void_t *)(la + c * 128), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)pb[h], (lds_void_t *)(lb + c * 128), 16, 0, 0);
+      pa[h] += astep;
+      pb[h] += bstep;
     }
   };
   for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
@@ -469,14 +442,9 @@ hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *Z
   const int nrb8 = (nrb + 7) / 8;
   // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here, with
   // running pointers still 23 % slower: 4-deep at 2 per CU stays)
-  // running DMA pointers (DFM_LOAD_CFG=0: the clamped per-stage addressing, A/B switch)
-  static const int cfg = [] { const char *e = getenv("DFM_LOAD_CFG"); return e ? atoi(e) : 1; }();
-  if (cfg == 0)
-    hipLaunchKernelGGL((gemm_loadings_kernel<4, 2, false>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb,
-                       N, Nc, K, nrb, ncb, r, invT, Lout);
-  else
-    hipLaunchKernelGGL((gemm_loadings_kernel<4, 2, true>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N,
-                       Nc, K, nrb, ncb, r, invT, Lout);
+  // running DMA pointers over the zero k-padding of both operands
+  hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N,
+                     Nc, K, nrb, ncb, r, invT, Lout);
   return hipGetLastError();
 }
 
@@ -604,11 +572,6 @@ hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int
   return hipGetLastError();
 }
 
-static int gemm_variant() {
-  static const int v = [] { const char *e = getenv("DFM_GEMM"); return e ? atoi(e) : 2; }();
-  return v;
-}
-
 // Requirements: lda, ldb even (16-B aligned pairs); B/A padding beyond the
 // logical size is never read (masked).  The LDS-DMA kernel additionally
 // needs Nc even and A's zero k-padding (lda >= round_up(K, 16)); otherwise
@@ -620,16 +583,16 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
   const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int ncb8 = (ncb + 7) / 8 * 8;
   dim3 grid(nrb * ncb8), block(256);
-  if (!a_trans && gemm_variant() == 2 && lda >= (K + G2_KS - 1) / G2_KS * G2_KS && Nc % 2 == 0 && Nc >= 2)
+  if (!a_trans && lda >= (K + G2_KS - 1) / G2_KS * G2_KS && Nc % 2 == 0 && Nc >= 2)
   {
     // B zero-padded to round_up(K, 16) rows: running DMA pointers, 3-deep
     // ring at 3 workgroups per CU (tools/gemm_bench.hip: 0.62 of peak at the
     // C3 shape, 0.75 at M = K = 2000, vs 0.60 / 0.71 for the clamped kernels)
-    if (b_padded && gemm_variant() == 2)
-      hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false, true>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb,
+    if (b_padded)
+      hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb,
                          ncb, col_done, col_group, clist, ccount);
     else if (gemm_ring3(M))
-      hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
+      hipLaunchKernelGGL((gemmh_kernel_t<3, 3>), grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb,
                          col_done, col_group);
     else
       hipLaunchKernelGGL(gemmh_kernel, grid, block, 0, st, A, lda, B, ldb, C, ldc, M, Nc, K, nrb, ncb, col_done,

@@ -212,19 +212,11 @@ int gram_ksplit(int m, int K) {
 hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int ksteps, double *G, int64_t ldg,
                            int64_t strideZ, hipStream_t st);
 int gram_dma_slots(int m);
-// DFM_GRAM_DMA=0 keeps the register-staged kernel for plain panels (A/B switch)
-static bool gram_dma_enabled() {
-  static const bool on = [] { const char *e = getenv("DFM_GRAM_DMA"); return !(e && e[0] == '0'); }();
-  return on;
-}
-
 // K-split of ONE plain-panel Gram (no replicate batch, so no batch
 // invariance to keep): enough (tile, split) workgroups to fill the chip's
 // resident slots (gram_dma_slots) several times over with a last round >= 90 % full, each
 // split >= 256 deep.  C5's prefix Gram (528 tiles, K = 20000): S = 7.
 int gram_ksplit_single(int m, int K) {
-  static const int force = [] { const char *e = getenv("DFM_GRAM_SPLIT"); return e ? atoi(e) : 0; }();
-  if (force > 0) return std::min(force, std::max(1, K / 16));   // tuning override
   const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2, slots = gram_dma_slots(m);
   const int smax = std::max(1, std::min(32, K / 256));
   for (int S = 1; S <= smax; ++S) {
@@ -248,7 +240,7 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
   const int nt = (m + GT - 1) / GT;
   const int nsteps = (K + KS - 1) / KS;
   const bool plain = orient == ORIENT_ROWS && !src.C && !src.eta && !src.idx && src.ld % 16 == 0 && nrep == 1 &&
-                     m >= GT && gram_dma_enabled();
+                     m >= GT;
   const int S0 = plain ? gram_ksplit_single(m, K) : gram_ksplit(m, K);
   const int ksteps = (nsteps + S0 - 1) / S0, S = (nsteps + ksteps - 1) / ksteps;
   double *Gk = G, *W = nullptr;

@@ -417,8 +417,8 @@ __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, doubl
                              const double *__restrict__ sig2v,
                              const double *__restrict__ lam, const double *__restrict__ trace,
                              const double *__restrict__ coef, const double *__restrict__ tstat,
-                             const StatDesc *__restrict__ sd, int ns, double *__restrict__ out,
-                             int64_t width) {
+                             const int *__restrict__ iters, const StatDesc *__restrict__ sd, int ns,
+                             double *__restrict__ out, int64_t width) {
   const int rep = blockIdx.x * blockDim.x + threadIdx.x;
   if (rep >= nb) return;
   double s = trace[rep];
@@ -435,6 +435,7 @@ __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, doubl
       case 3: v = st.arg0 < d ? coef[(int64_t)rep * d + st.arg0] : NAN; break;
       case 4: v = st.arg0 < d ? tstat[(int64_t)rep * d + st.arg0] : NAN; break;
       case 5: v = trace[rep]; break;
+      case 12: v = iters ? (double)iters[rep] : NAN; break;   // DFM_STAT_ITERS (diagnostic)
       default: continue;   // per-variable stats are written by the Chow kernel
     }
     out[(int64_t)rep * width + st.off] = v;

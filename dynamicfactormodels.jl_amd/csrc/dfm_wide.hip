@@ -418,9 +418,12 @@ int64_t chow_wide_work(int T, int N, int r) {   // doubles per panel
 // L + rep sL (N x r); E (the factor residuals, same layout as X) or nullptr
 // (then E = X - F L').  Outputs: rows rep * ostr of LR / LM / WD (any may be
 // null) and, if scr != nullptr, [3][nb][N] scratch rows.
+// Break models (nblk > 1, E == nullptr): E = X - F_j L_j' per block j, rows
+// brow[j] .. brow[j+1]-1, block j's loadings at L + j * lbs.
 hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, const double *E, int T, int N, int r,
                             int bp, const double *F, int64_t sF, const double *L, int64_t sL, double *LR, double *LM,
-                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st) {
+                            double *WD, int64_t ostr, double *scr, double *work, hipStream_t st, int nblk,
+                            const int *brow, int64_t lbs) {
   const int64_t TN = (int64_t)T * N, rN = (int64_t)r * N, rr = (int64_t)r * r, r2 = 2 * (int64_t)r;
   double *Eb = work, *R = Eb + nb * TN, *eE = R + nb * TN, *ssr = eE + (int64_t)nb * N, *vv = ssr + (int64_t)nb * N;
   double *A1 = vv + (int64_t)nb * N, *A2 = A1 + nb * rr, *Lt1 = A2 + nb * rr, *Lt2 = Lt1 + nb * rr;
@@ -434,7 +437,13 @@ hipError_t launch_chow_wide(int nb, const double *X, int64_t ld, int64_t sX, con
 #define GB(...) if ((e = gemm_batched(__VA_ARGS__)) != hipSuccess) return e
   // ||E_i||^2
   hipLaunchKernelGGL(copy_panel_kernel, g1, dim3(256), 0, st, E ? E : X, ld, sX, T, N, Eb);
-  if (!E) GB(nb, T, N, r, -1.0, F, r, 1, sF, L, 1, r, sL, 1.0, Eb, N, 1, TN, st);
+  if (!E) {
+    for (int j = 0; j < nblk; ++j) {
+      const int a = nblk > 1 ? brow[j] : 0, b = (nblk > 1 && j + 1 < nblk) ? brow[j + 1] : T;
+      GB(nb, b - a, N, r, -1.0, F + (int64_t)a * r, r, 1, sF, L + j * lbs, 1, r, sL, 1.0, Eb + (int64_t)a * N, N, 1,
+         TN, st);
+    }
+  }
   hipLaunchKernelGGL(col_ssq_batched_kernel, dim3((N + 255) / 256, nb), dim3(256), 0, st, Eb, T, N, eE);
   // LR: x_i on F within each subperiod, residuals explicit
   hipLaunchKernelGGL(copy_panel_kernel, g1, dim3(256), 0, st, X, ld, sX, T, N, R);

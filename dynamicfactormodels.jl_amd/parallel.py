@@ -21,7 +21,21 @@ def shard_range(B: int, world: int, rank: int) -> Tuple[int, int]:
     blocks whose sizes differ by at most one."""
     if world < 1 or not (0 <= rank < world):
         raise ValueError("bad world/rank")
-    return (rank * B) // world, ((rank + 1) * B) // world
+    return (rank * B + world - 1) // world, ((rank + 1) * B + world - 1) // world
+
+
+def _comm_device(group, device):
+    """Where the exchanged rows must live: RCCL ("nccl") moves device tensors
+    only, so with that backend and no explicit device the rows go to this
+    rank's GPU (LOCAL_RANK); gloo takes host tensors."""
+    import os
+    import torch
+    import torch.distributed as dist
+    if device is not None:
+        return device
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    return None
 
 
 def gather_rows(local, B: int, group=None, device=None):
@@ -55,6 +69,7 @@ def sharded_bootstrap(run_local: Callable[[int, int], np.ndarray], B: int, group
     if loc.ndim == 1:
         loc = loc[:, None]
     t = torch.from_numpy(np.ascontiguousarray(loc))
+    device = _comm_device(group, device)
     if device is not None:
         t = t.to(device)
     return gather_rows(t, B, group).cpu().numpy()
@@ -136,6 +151,7 @@ def windows_sharded(run_local: Callable[[int, int], dict], T: int, N: int, q: in
     w0, w1, rows = window_shard(T, P, world, rank)
     res = run_local(rows, w1 - w0) if w1 > w0 else {}
     loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, q))
+    device = _comm_device(group, device)
     if device is not None:
         loc = loc.to(device)
     return _unpack_windows(gather_rows(loc, P, group).cpu().numpy(), T, P, K, q)

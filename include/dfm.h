@@ -56,7 +56,9 @@ enum dfm_stat_kind {
   DFM_STAT_WALD = 8,       /* Wald_test, src/chowtest.jl:25                     */
   DFM_STAT_LR_ALL = 9,     /* LR for every variable i (N values), bp = arg0     */
   DFM_STAT_LM_ALL = 10,
-  DFM_STAT_WALD_ALL = 11
+  DFM_STAT_WALD_ALL = 11,
+  DFM_STAT_ITERS = 12      /* diagnostic: Rayleigh-Ritz steps of the replicate's eigensolve
+                              (NaN on the dense path); an eigenvalue-only stat */
 };
 typedef struct dfm_stat { int32_t kind, arg0, arg1, pad; } dfm_stat;
 
@@ -115,6 +117,14 @@ int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T, int64_t N, int64_t ldx,
 int dfm_full_spectrum_max(void);
 int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T, int64_t N,
                       int64_t ldx, double *eigvals_m, double *trace_G);
+
+/* normalize (src/utils.jl:33): out = (X .- mean(X, 1)) ./ std(X, 1), the
+ * column z-score with the sample (n - 1) std.  X and out column-major T x N
+ * (ldx, ldo >= T); out may alias X.  dfm_normalize_dev: both on the device,
+ * asynchronous on the context stream. */
+int dfm_normalize(dfm_ctx *ctx, const double *X, int64_t T, int64_t N, int64_t ldx, double *out, int64_t ldo);
+int dfm_normalize_dev(dfm_ctx *ctx, const double *X_dev, int64_t T, int64_t N, int64_t ldx, double *out_dev,
+                      int64_t ldo);
 
 /* ----------------------------------------------------- IC sweep (host math)
  * Criteria for k = 1..kmax from the eigenvalues (identity ||E_k||_F^2 =
@@ -176,8 +186,8 @@ int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *ts
  * RESIDUAL), refit at the model's r and criterion, emit the stats.  A model
  * fitted with breaks refits per break block (:36, :48 pass break_indices);
  * the common component is the blockwise vcat(F_j L_j'); the residual
- * bootstrap's block-wise draws (:23-28) are the caller's idx.  Chow stats
- * are refused for such models (-7).
+ * bootstrap's block-wise draws (:23-28) are the caller's idx.  Chow stats of
+ * such models read F = vcat(F_j) and the blockwise factor residuals (D1).
  * idx: B x T int32 (row-major, 0-based), eta: B x T.  out: B rows of
  * sum(width(stat)) doubles (row-major). */
 int dfm_bootstrap(dfm_model *m, int kind, int64_t B, const int32_t *idx,
@@ -186,6 +196,17 @@ int dfm_bootstrap(dfm_model *m, int kind, int64_t B, const int32_t *idx,
 int dfm_bootstrap_dev(dfm_model *m, int kind, int64_t B, const int32_t *idx_dev,
                       const double *eta_dev, const dfm_stat *stats, int nstats,
                       double *out_dev);
+/* The replicate loop (src/bootstrap.jl:43) sharded over n models, one per
+ * context (typically one per GPU; contexts must be distinct), each a
+ * dfm_model_clone of the same fit: replicate b runs on model floor(b n / B)
+ * (contiguous shards), every shard on its own host thread and stream, rows
+ * written in order into the caller's out (B x width, host).  Same arguments and
+ * results as dfm_bootstrap: rows are bit-identical to a one-model call. */
+int dfm_bootstrap_multi(dfm_model *const *models, int n, int kind, int64_t B, const int32_t *idx,
+                        const double *eta, const dfm_stat *stats, int nstats, double *out);
+/* Copy of a fitted model on another context (device buffers and host fields),
+ * for dfm_bootstrap_multi.  Destroy it with dfm_model_destroy. */
+int dfm_model_clone(const dfm_model *m, dfm_ctx *ctx, dfm_model **out);
 /* Width of one replicate's output row for a stat list. */
 int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats);
 /* Replicates per device batch (0 = auto). */

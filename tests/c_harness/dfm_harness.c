@@ -1,0 +1,199 @@
+/*
+ * dfm_harness.c — a plain-C (C99) caller of include/dfm.h that makes the same
+ * calls as the Julia ccall shim of INTEGRATION.md, independently of the
+ * Python ctypes table (_lib.py), so header / ABI drift is caught here.
+ *
+ *   dfm_harness IN OUT
+ *
+ * IN  (raw, little endian): int64 T, N, B; double y[T]; double X[T*N]
+ *     (column-major, Julia's layout); int32 idx[B*T] (0-based); double eta[B*T].
+ * OUT (text): one line per result, "name v0 v1 ..." with %.17g values.
+ * Exit: 0 ok, 3 no usable GPU (dfm_ctx_create failed cleanly), 1 any error.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dfm.h"
+
+static FILE *out;
+
+static void put(const char *name, const double *v, int64_t n) {
+  int64_t i;
+  fprintf(out, "%s", name);
+  for (i = 0; i < n; ++i) fprintf(out, " %.17g", v[i]);
+  fprintf(out, "\n");
+}
+
+static void puti(const char *name, const int64_t *v, int64_t n) {
+  int64_t i;
+  fprintf(out, "%s", name);
+  for (i = 0; i < n; ++i) fprintf(out, " %lld", (long long)v[i]);
+  fprintf(out, "\n");
+}
+
+#define CHECK(ctx, call)                                                                 \
+  do {                                                                                   \
+    int rc_ = (call);                                                                    \
+    if (rc_ != 0) {                                                                      \
+      fprintf(stderr, "%s:%d %s -> %d: %s\n", __FILE__, __LINE__, #call, rc_, dfm_last_error(ctx)); \
+      return 1;                                                                          \
+    }                                                                                    \
+  } while (0)
+
+static void *xmalloc(size_t n) {
+  void *p = calloc(n ? n : 1, 1);
+  if (!p) {
+    fprintf(stderr, "out of memory\n");
+    exit(1);
+  }
+  return p;
+}
+
+int main(int argc, char **argv) {
+  FILE *in;
+  int64_t T, N, B, t, width, r = 0, kmax = 0, n_eig = 0;
+  double *y, *X, *eta, *w, *ev, *coef, *tst, *bo, *bm, *LR, *LM, *WD, *ic, *Xn, *F, *L, *tstat, tr;
+  double V, cv, trace, pred[4], truev[4];
+  int32_t *idx;
+  uint8_t *mask;
+  int64_t rw[4], brk[1];
+  dfm_ctx *ctx = NULL, *ctx2 = NULL;
+  dfm_model *m = NULL, *m2 = NULL, *mb = NULL;
+  dfm_model *pair[2];
+  dfm_stat st[3];
+  size_t got = 0;
+  if (argc != 3) {
+    fprintf(stderr, "usage: %s IN OUT\n", argv[0]);
+    return 1;
+  }
+  in = fopen(argv[1], "rb");
+  if (!in) return 1;
+  got += fread(&T, 8, 1, in);
+  got += fread(&N, 8, 1, in);
+  got += fread(&B, 8, 1, in);
+  if (got != 3 || T < 8 || N < 2 || B < 2) return 1;
+  y = xmalloc(8 * T);
+  X = xmalloc(8 * T * N);
+  idx = xmalloc(4 * B * T);
+  eta = xmalloc(8 * B * T);
+  got = fread(y, 8, T, in) + fread(X, 8, T * N, in) + fread(idx, 4, B * T, in) + fread(eta, 8, B * T, in);
+  fclose(in);
+  if ((int64_t)got != T + T * N + 2 * B * T) return 1;
+  out = fopen(argv[2], "w");
+  if (!out) return 1;
+
+  if (dfm_ctx_create(0, &ctx) != 0) {
+    fprintf(out, "NO_GPU\n");
+    fclose(out);
+    return 3;
+  }
+  w = xmalloc(8 * T);
+  for (t = 0; t < T; ++t) w[t] = 1.0;
+
+  /* DynamicFactorModel(y, w, x, "ICp2") with kmax 8: src/DynamicFactorModel.jl:53 */
+  CHECK(ctx, dfm_model_fit(ctx, y, w, 1, T, X, T, N, T, 0, DFM_CRIT_ICP2, 8, &m));
+  CHECK(ctx, dfm_model_dims(m, &r, &kmax, &n_eig));
+  CHECK(ctx, dfm_model_scalars(m, &r, &V, &cv, &trace));
+  ev = xmalloc(8 * n_eig);
+  coef = xmalloc(8 * (1 + r));
+  tst = xmalloc(8 * (1 + r));
+  ic = xmalloc(8 * 7 * kmax);
+  CHECK(ctx, dfm_model_read(m, ev, coef, tst, NULL, NULL, NULL, NULL, NULL, ic));
+  {
+    double s[4];
+    s[0] = (double)r; s[1] = V; s[2] = cv; s[3] = trace;
+    put("fit_scalars", s, 4);
+  }
+  put("fit_eigvals", ev, n_eig);
+  put("fit_coef", coef, 1 + r);
+  put("fit_tstat", tst, 1 + r);
+  put("fit_ic", ic, 7 * kmax);
+
+  /* criterion_* for k = 1..kmax from the eigenvalues (src/criteria.jl:17-53) */
+  {
+    double *crit = xmalloc(8 * 7 * kmax);
+    CHECK(ctx, dfm_ic_sweep(ev, (int)n_eig, (int)kmax, trace, T, N, 1.0 /* PCp sigma^2 given */, crit));
+    put("ic_sweep_sigma1", crit, 7 * kmax);
+    free(crit);
+  }
+
+  /* wild_bootstrap(dfm, B, stat) (src/bootstrap.jl:41-51) */
+  st[0].kind = DFM_STAT_V; st[0].arg0 = 0; st[0].arg1 = 0; st[0].pad = 0;
+  st[1].kind = DFM_STAT_CRIT; st[1].arg0 = -1; st[1].arg1 = 0; st[1].pad = 0;
+  st[2].kind = DFM_STAT_LR_ALL; st[2].arg0 = (int32_t)(T / 2); st[2].arg1 = 0; st[2].pad = 0;
+  width = dfm_stats_width(m, st, 3);
+  bo = xmalloc(8 * B * width);
+  bm = xmalloc(8 * B * width);
+  CHECK(ctx, dfm_bootstrap(m, DFM_BOOT_WILD, B, idx, eta, st, 3, bo));
+  put("wild", bo, B * width);
+  /* residual_bootstrap (src/bootstrap.jl:21-39) */
+  CHECK(ctx, dfm_bootstrap(m, DFM_BOOT_RESIDUAL, B, idx, NULL, st, 1, bm));
+  put("residual_V", bm, B);
+
+  /* the replicate loop sharded over two contexts (dfm_model_clone + multi) */
+  CHECK(ctx, dfm_ctx_create(0, &ctx2));
+  CHECK(ctx2, dfm_model_clone(m, ctx2, &m2));
+  pair[0] = m;
+  pair[1] = m2;
+  memset(bm, 0, 8 * B * width);
+  CHECK(ctx, dfm_bootstrap_multi(pair, 2, DFM_BOOT_WILD, B, idx, eta, st, 3, bm));
+  put("wild_multi", bm, B * width);
+
+  /* LR_test / LM_test / Wald_test for every variable (src/chowtest.jl) */
+  LR = xmalloc(8 * N);
+  LM = xmalloc(8 * N);
+  WD = xmalloc(8 * N);
+  CHECK(ctx, dfm_chow_all(m, T / 2, LR, LM, WD));
+  put("chow_LR", LR, N);
+  put("chow_LM", LM, N);
+  put("chow_Wald", WD, N);
+
+  /* the same with break_indices = [T/2 + 1] (1-based): rows split at T/2 */
+  brk[0] = T / 2;
+  CHECK(ctx, dfm_model_fit_breaks(ctx, y, w, 1, T, X, T, N, T, 2, DFM_CRIT_BIC, 0, brk, 1, &mb));
+  CHECK(ctx, dfm_chow_all(mb, T / 2 + 1, LR, NULL, WD));
+  put("break_chow_LR", LR, N);
+  put("break_chow_Wald", WD, N);
+
+  /* calculate_factors / principal_components (src/DynamicFactorModel.jl:71-121) */
+  F = xmalloc(8 * T * 3);
+  L = xmalloc(8 * N * 3);
+  CHECK(ctx, dfm_pca(ctx, X, T, N, T, 3, ev, F, L, &tr));
+  put("pca_eigvals", ev, 3);
+  put("pca_F", F, T * 3);
+
+  /* targeted_predictors(..., "hard"), per-candidate (D8 extension) */
+  tstat = xmalloc(8 * N);
+  mask = xmalloc(N);
+  CHECK(ctx, dfm_targeted_hard(ctx, y, w, 1, T, X, T, N, T, DFM_TP_PER_CANDIDATE, 1.96, tstat, mask));
+  put("tp_hard_t", tstat, N);
+
+  /* normalize (src/utils.jl:33) */
+  Xn = xmalloc(8 * T * N);
+  CHECK(ctx, dfm_normalize(ctx, X, T, N, T, Xn, T));
+  put("normalize_col0", Xn, T);
+
+  /* pseudo_out_of_sample_forecasts (src/utils.jl:54-72), 4 windows */
+  CHECK(ctx, dfm_windows_forecast(ctx, y, w, 1, T, X, T, N, T, 4, DFM_CRIT_ICP2, 4, rw, pred, truev));
+  puti("windows_r", rw, 4);
+  put("windows_pred", pred, 4);
+
+  /* error behaviour: a status code and a message, nothing thrown */
+  {
+    int rc = dfm_chow_all(m, 0, LR, LM, WD);
+    double e[1];
+    e[0] = (double)rc;
+    put("error_rc", e, 1);
+    fprintf(out, "error_msg_nonempty %d\n", (int)(strlen(dfm_last_error(ctx)) > 0));
+  }
+
+  dfm_model_destroy(mb);
+  dfm_model_destroy(m2);
+  dfm_model_destroy(m);
+  dfm_ctx_destroy(ctx2);
+  dfm_ctx_destroy(ctx);
+  fclose(out);
+  return 0;
+}

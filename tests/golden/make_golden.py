@@ -115,9 +115,49 @@ def soft():
         c4_beta=res4["betas"][res4["best"]])
 
 
+def c5():
+    """C5 (BASELINE.json configs[4]) at full size: Bai-Ng DGP T=2000 N=20000
+    r=8, normalised, w = 1; the refits of pseudo_out_of_sample_forecasts
+    (src/utils.jl:54-72, P = 200) for windows 0, 100, 199 — each the IC-sweep
+    constructor DynamicFactorModel_ic(kmax=8) on rows 1..T-P+w — by the
+    reference-faithful oracle.  The panel (320 MB) is not stored: its seed
+    and a digest are."""
+    rng = np.random.default_rng(20261015 + 5)
+    T, N, P = 2000, 20000, 200
+    y, x, *_ = O.factor_model_DGP(T, N, 8, rng)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    wins = [0, 100, 199]
+    rows = {"r": [], "V": [], "crit": [], "eigvals": [], "coef": [], "tstat": []}
+    for wi in wins:
+        n = T - P + wi
+        d = O.DynamicFactorModel_ic(y[:n], w[:n], x[:n], "ICp2", kmax=8)
+        r = d.number_of_factors
+        rows["r"].append(r)
+        rows["V"].append(O.factor_residual_variance(d))
+        rows["crit"].append(d.number_of_factors_criterion_value)
+        rows["eigvals"].append(d.eigenvalues[0][:8])
+        c = np.full(9, np.nan)
+        t = np.full(9, np.nan)
+        c[:1 + r] = d.coefficients
+        t[:1 + r] = d.t_stats
+        rows["coef"].append(c)
+        rows["tstat"].append(t)
+        print("c5 window", wi, "r", r, flush=True)
+    np.savez_compressed(os.path.join(HERE, "c5_windows.npz"), windows=np.array(wins),
+                        digest=np.array([x.sum(), np.abs(x).sum(), y.sum()]),
+                        **{k: np.array(v) for k, v in rows.items()})
+
+
 if __name__ == "__main__":
+    import sys as _s
+    if len(_s.argv) > 1:          # regenerate selected fixtures, e.g. `make_golden.py c5`
+        for name in _s.argv[1:]:
+            globals()[name]()
+        raise SystemExit(0)
     c1()
     c2()
     tp()
     soft()
+    c5()
     print("golden fixtures written to", HERE)

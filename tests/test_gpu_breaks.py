@@ -124,6 +124,60 @@ def test_break_errors(dfm, oracle):
     with pytest.raises(dfm.DFMError):           # outside 2..T
         dfm.DynamicFactorModel(y, w, x, 2, break_indices=[101])
     g = dfm.DynamicFactorModel(y, w, x, 2, break_indices=[50])
-    idx, eta = oracle.draw_wild(np.random.default_rng(1), 2, 100)
-    with pytest.raises(dfm.DFMError):           # Chow stats read one loadings matrix (D1)
-        dfm.wild_bootstrap(g, 2, dfm.Stat.LR(50, 1), idx=idx, eta=eta)
+    with pytest.raises(dfm.DFMError):           # break period leaves < r rows
+        dfm.chow_all(g, 1)
+
+
+# ---------------------------------------------- Chow tests of break-fitted models
+# src/chowtest.jl reads dfm.factors (F = vcat(F_j), D1), dfm.x and
+# dfm.factor_residuals (E = X - vcat(F_j L_j')) — never one loadings matrix —
+# so a model fitted with break_indices has well-defined LR / LM / Wald tests.
+@pytest.mark.parametrize("T,N,r,breaks", [
+    (120, 60, 2, [61]),                # T >= N: two blocks
+    (96, 150, 3, [31, 70]),            # N > T: three blocks, bp inside block 2
+    (200, 40, 2, [50, 101, 160]),      # four blocks
+    (120, 160, 17, [61]),              # r > 16: the GEMM-built (explicit-residual) Chow
+])
+def test_break_chow_all_matches_oracle(dfm, oracle, T, N, r, breaks):
+    y, x, w = panel(oracle, T, N, 2, 71 + T, model="Breitung_Eickmeier_2011", b=0.6)
+    g = dfm.DynamicFactorModel(y, w, x, r, break_indices=breaks)
+    o = oracle.DynamicFactorModel(y, w, x, r, "", breaks)
+    # break periods off the blocks' boundaries (at a boundary the subperiod
+    # SSRs equal ||E_i||^2 exactly — each block's loadings are its OLS
+    # coefficients — and LR, LM vanish to rounding)
+    for bp in (T // 2 + 7, breaks[0] + 3):
+        LR, LM, W = dfm.chow_all(g, bp)
+        nv = min(N, 30)
+        ref = np.array([[oracle.LR_test(o, bp, i), oracle.LM_test(o, bp, i), oracle.Wald_test(o, bp, i)]
+                        for i in range(nv)])
+        assert rel(LR[:nv], ref[:, 0]) < 1e-9, bp
+        assert rel(LM[:nv], ref[:, 1]) < 1e-9, bp
+        assert rel(W[:nv], ref[:, 2]) < 1e-9, bp
+        assert abs(dfm.LM_test(g, bp, 3) - ref[2, 1]) < 1e-9 * abs(ref[2, 1])
+
+
+@pytest.mark.parametrize("T,N,r,breaks", [(120, 60, 2, [61]), (96, 150, 3, [31, 70]), (120, 160, 17, [61])])
+def test_break_bootstrap_chow_matches_oracle(dfm, oracle, T, N, r, breaks):
+    y, x, w = panel(oracle, T, N, 2, 83 + T, model="Breitung_Eickmeier_2011", b=0.6)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2", break_indices=breaks)
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2", breaks)
+    B, bp = 3, T // 2 + 7
+    idx, eta = oracle.draw_wild(np.random.default_rng(12), B, T)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, B, [S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp), S.LR(bp, 2)], idx=idx, eta=eta)
+    nv = min(N, 20)
+    for b in range(B):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]],
+                                      r, "ICp2", breaks)
+        ref = np.array([[oracle.LR_test(d, bp, i), oracle.LM_test(d, bp, i), oracle.Wald_test(d, bp, i)]
+                        for i in range(nv)])
+        assert rel(out[b, :nv], ref[:, 0]) < 1e-9
+        assert rel(out[b, N:N + nv], ref[:, 1]) < 1e-9
+        assert rel(out[b, 2 * N:2 * N + nv], ref[:, 2]) < 1e-9
+        assert out[b, 3 * N] == out[b, 1]      # single-variable LR(bp, 2) = row entry 2
+    idx_r = oracle.draw_residual(np.random.default_rng(13), 2, T, breaks)
+    outr = dfm.residual_bootstrap(g, 2, [S.LM_all(bp)], idx=idx_r)
+    for b in range(2):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + o.factor_residuals[idx_r[b]], r, "ICp2", breaks)
+        ref = np.array([oracle.LM_test(d, bp, i) for i in range(nv)])
+        assert rel(outr[b, :nv], ref) < 1e-9

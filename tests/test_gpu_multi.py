@@ -1,0 +1,159 @@
+"""Multi-device paths through the C ABI, on one MI355X: several contexts on
+device 0 stand in for several GPUs ("on a one-GPU box, emulate with
+several contexts on one device").
+
+* dfm_model_clone + dfm_bootstrap_multi: the replicate loop of
+  src/bootstrap.jl:43 sharded over contexts (replicate b on context
+  floor(b n / B)) must give rows bit-identical to one context.
+* the torch.distributed path (parallel.wild_bootstrap_sharded): two processes,
+  each with its own context on the GPU and the real engine, rows exchanged by
+  a gloo all-gather, bit-identical to one process.
+* normalize (src/utils.jl:33) on the device vs the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import panel, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def contexts(dfm, n):
+    return [dfm.Context(0) for _ in range(n)]
+
+
+@pytest.mark.parametrize("T,N,r,mode", [(200, 400, 4, "factored"), (150, 60, 3, "auto"), (120, 300, 3, "direct")])
+@pytest.mark.parametrize("n", [2, 3])
+def test_bootstrap_multi_is_bit_identical(dfm, oracle, T, N, r, mode, n):
+    y, x, w = panel(oracle, T, N, r, 400 + T + n)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    g.set_bootstrap_mode(mode)
+    copies = [g] + [dfm.clone_model(g, c) for c in contexts(dfm, n - 1)]
+    for c in copies[1:]:
+        c.set_bootstrap_mode(mode)
+        assert c.V == g.V and np.array_equal(c.coefficients, g.coefficients)
+    B = 23
+    idx, eta = dfm.draw_wild_fast(31, B, T)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.eigenvalue(r), S.t_stat(1), S.LR_all(T // 2)]
+    one = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    many = dfm.wild_bootstrap(copies, B, stats, idx=idx, eta=eta)
+    assert np.array_equal(one, many)
+    ridx = oracle.draw_residual(np.random.default_rng(2), B, T)
+    assert np.array_equal(dfm.residual_bootstrap(g, B, S.V(), idx=ridx),
+                          dfm.residual_bootstrap(copies, B, S.V(), idx=ridx))
+
+
+def test_bootstrap_multi_break_model(dfm, oracle):
+    y, x, w = panel(oracle, 120, 200, 2, 91, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, 2, "ICp2", break_indices=[61])
+    c = dfm.clone_model(g, dfm.Context(0))
+    assert len(c.factors) == 2 and np.array_equal(c.loadings[1], g.loadings[1])
+    idx, eta = dfm.draw_wild_fast(5, 9, 120)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.LM_all(60)]
+    assert np.array_equal(dfm.wild_bootstrap(g, 9, stats, idx=idx, eta=eta),
+                          dfm.wild_bootstrap([g, c], 9, stats, idx=idx, eta=eta))
+
+
+def test_bootstrap_multi_errors(dfm, oracle):
+    y, x, w = panel(oracle, 80, 120, 2, 7)
+    g = dfm.DynamicFactorModel(y, w, x, 2, "ICp2")
+    idx, eta = dfm.draw_wild_fast(1, 4, 80)
+    with pytest.raises(dfm.DFMError):     # the same context twice: one host thread per context
+        dfm.wild_bootstrap([g, g], 4, dfm.Stat.V(), idx=idx, eta=eta)
+    h = dfm.DynamicFactorModel(y, w, x, 3, "ICp2", ctx=dfm.Context(0))
+    with pytest.raises(dfm.DFMError):     # not a copy of the same fit
+        dfm.wild_bootstrap([g, h], 4, dfm.Stat.V(), idx=idx, eta=eta)
+    bad = idx.copy()
+    bad[3, 5] = 80
+    c = dfm.clone_model(g, dfm.Context(0))
+    with pytest.raises(dfm.DFMError):     # out-of-range index inside the second shard
+        dfm.wild_bootstrap([g, c], 4, dfm.Stat.V(), idx=bad, eta=eta)
+
+
+def test_stat_indices_are_one_based(dfm, oracle):
+    with pytest.raises(ValueError):
+        dfm.Stat.eigenvalue(0)
+    with pytest.raises(ValueError):
+        dfm.Stat.t_stat(0)
+    y, x, w = panel(oracle, 80, 120, 2, 8)
+    g = dfm.DynamicFactorModel(y, w, x, 2, "ICp2")
+    idx, eta = dfm.draw_wild_fast(1, 2, 80)
+    import dfm_amd.api as A
+    for bad in (A.Stat(2, -1), A.Stat(3, -1), A.Stat(4, 3), A.Stat(2, 2)):   # raw 0-based: out of range
+        with pytest.raises(dfm.DFMError):
+            dfm.wild_bootstrap(g, 2, bad, idx=idx, eta=eta)
+
+
+@pytest.mark.parametrize("T,N", [(200, 100), (37, 1001), (500, 2000)])
+def test_normalize_matches_oracle(dfm, oracle, T, N):
+    x = np.random.default_rng(T).standard_normal((T, N)) * np.linspace(0.5, 4.0, N) + np.linspace(-3, 3, N)
+    got = dfm.normalize(x)
+    ref = oracle.normalize(x)
+    assert np.max(np.abs(got - ref)) < 1e-13 * np.max(np.abs(ref))
+
+
+def test_normalize_dev_in_place(dfm, oracle):
+    import torch
+    x = np.random.default_rng(3).standard_normal((300, 700)) * 3.0 + 1.0
+    xd = torch.from_numpy(np.ascontiguousarray(x.T)).cuda().t()       # column-major in HBM
+    dfm.normalize_dev(xd, xd)
+    torch.cuda.synchronize()
+    dfm.default_context().synchronize()
+    assert np.max(np.abs(xd.cpu().numpy() - oracle.normalize(x))) < 1e-13 * 10
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _engine_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch.distributed as dist
+    import dfm_pkg
+    import dfm_oracle as O
+    D = dfm_pkg.load()
+    from dfm_amd.parallel import wild_bootstrap_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    y, x, *_ = O.factor_model_DGP(150, 300, 3, np.random.default_rng(44))
+    x, w = O.normalize(x), np.ones((150, 1))
+    g = D.DynamicFactorModel(y, w, x, 3, "ICp2", ctx=D.Context(0))
+    idx, eta = D.draw_wild_fast(12, 17, 150)
+    stats = [D.Stat.V(), D.Stat.criterion(), D.Stat.Wald_all(75)]
+    got = wild_bootstrap_sharded(g, 17, stats, idx, eta)
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_real_engine(dfm, oracle):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    y, x, *_ = oracle.factor_model_DGP(150, 300, 3, np.random.default_rng(44))
+    x, w = oracle.normalize(x), np.ones((150, 1))
+    g = dfm.DynamicFactorModel(y, w, x, 3, "ICp2")
+    idx, eta = dfm.draw_wild_fast(12, 17, 150)
+    ref = dfm.wild_bootstrap(g, 17, [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.Wald_all(75)], idx=idx, eta=eta)
+    for r in (0, 1):
+        assert np.array_equal(res[r], ref)

@@ -1,0 +1,111 @@
+"""Production-size parity: the exact batch paths the benchmarks time, checked
+against the reference-faithful oracle (not only against themselves).
+
+* C3 (BASELINE.json configs[2]): B = 9999 replicates of T=500 N=2000 r=8 in ONE
+  device batch through dfm_bootstrap_dev — the 16 GB factored workspace, the
+  straggler phase with column compaction, the eigenvalue (Kato-Temple)
+  stopping rule of the bench's V + ICp2 stats — with sampled replicates
+  (first, last, the slowest stragglers by eigensolver steps, two random)
+  refit by the oracle (src/bootstrap.jl:41-51) at 1e-10.
+* C5 (configs[4]): T=2000 N=20000, P=200 expanding windows through
+  dfm_windows_dev (the bench's path), windows 0 / 100 / 199 against the
+  oracle's DynamicFactorModel_ic(kmax=8) refits (src/utils.jl:54-72), frozen
+  in tests/golden/c5_windows.npz by make_golden.py (an oracle window costs
+  ~40 s of CPU there); the panel is regenerated from its seed and its digest
+  checked first.
+* C4 (configs[3]): hard PER_CANDIDATE thresholding on the full T=400
+  N=5000 panel against the oracle (src/targeted_predictors.jl:9-30, D8)."""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import STAT_RTOL, rel
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_c3_full_batch_sampled_replicates_match_oracle(dfm, oracle):
+    import torch
+    T, N, r, B = 500, 2000, 8, 9999
+    rng = np.random.default_rng(20261015 + 3)
+    y, x, *_ = oracle.factor_model_DGP(T, N, r, rng)
+    x = oracle.normalize(x)
+    w = np.ones((T, 1))
+    ctx = dfm.Context(0)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2", ctx=ctx)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.trace(), S.iterations()] + [S.eigenvalue(j) for j in range(1, r + 1)]
+    arr = dfm.api._stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(g.handle, arr, len(stats)))
+    idx, eta = dfm.draw_wild_fast(1_000_003, B, T)          # the bench's first step draws
+    dev = torch.device("cuda", 0)
+    idx_d, eta_d = torch.from_numpy(idx).to(dev), torch.from_numpy(eta).to(dev)
+    out = torch.empty((B, width), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    ctx.check(ctx.lib.dfm_bootstrap_dev(g.handle, 0, B, idx_d.data_ptr(), eta_d.data_ptr(), arr, len(stats),
+                                        out.data_ptr()))
+    ctx.synchronize()
+    es = ctx.eig_stats()
+    assert es["batches"] == 1                                # the whole job in one device batch
+    res = out.cpu().numpy()
+    assert np.all(np.isfinite(res))
+    its = res[:, 3]
+    assert np.all(its >= 1)
+    order = np.argsort(-its, kind="stable")
+    sample = sorted(set([0, B - 1] + list(order[:6]) + list(np.random.default_rng(1).integers(1, B - 1, 2))))
+    assert its[order[0]] > np.median(its)                    # the stragglers are in the sample
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    common, E = o.common_component, o.factor_residuals
+    for b in sample:
+        xs = common + eta[b][:, None] * E[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, r, "ICp2")
+        ref = [oracle.factor_residual_variance(d), d.number_of_factors_criterion_value, np.sum(xs * xs)]
+        ref += list(d.eigenvalues[0][:r])
+        got = [res[b, 0], res[b, 1], res[b, 2]] + list(res[b, 4:])
+        assert rel(got, ref) < STAT_RTOL, (b, its[b])
+
+
+def c5_panel(oracle):
+    rng = np.random.default_rng(20261015 + 5)
+    y, x, *_ = oracle.factor_model_DGP(2000, 20000, 8, rng)
+    return y, oracle.normalize(x)
+
+
+def test_c5_full_panel_windows_match_frozen_oracle(dfm, oracle):
+    import torch
+    g = np.load(os.path.join(GOLD, "c5_windows.npz"))
+    y, x = c5_panel(oracle)
+    # same panel as the fixture's (the column means are ~0, so the plain sum
+    # is compared absolutely: NumPy's SIMD summation order differs by host)
+    assert abs(x.sum() - g["digest"][0]) < 1e-6
+    assert rel([np.abs(x).sum(), y.sum()], g["digest"][1:]) < 1e-12
+    dev = torch.device("cuda", 0)
+    yd = torch.from_numpy(np.ascontiguousarray(y)).to(dev)
+    wd = torch.ones((2000, 1), dtype=torch.float64, device=dev)
+    xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major, as the bench
+    del x
+    out = dfm.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=200, kmax=8)
+    for k, wi in enumerate(g["windows"]):
+        r = int(g["r"][k])
+        assert out["number_of_factors"][wi] == r, wi
+        assert abs(out["V"][wi] - g["V"][k]) <= STAT_RTOL * g["V"][k]
+        assert abs(out["criterion_value"][wi] - g["crit"][k]) <= STAT_RTOL * abs(g["crit"][k])
+        assert rel(out["eigenvalues"][wi][:8], g["eigvals"][k]) < STAT_RTOL
+        assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < 1e-9            # intercept: sign-free
+        assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < 1e-9
+
+
+def test_c4_full_panel_per_candidate_matches_oracle(dfm, oracle):
+    rng = np.random.default_rng(20261015 + 4)
+    T, N = 400, 5000
+    y, x, *_ = oracle.factor_model_DGP(T, N, 5, rng)
+    x = oracle.normalize(x)
+    w = np.ones((T, 1))
+    mask, t = dfm.targeted_predictors(y, w, x, "hard", mode="per_candidate", return_tstats=True)
+    to, mo = oracle.targeted_predictors_hard(y, w, x, "per_candidate")
+    assert rel(t, to) < 1e-9
+    assert np.array_equal(mask, mo)
+    assert 0 < mask.sum() < N

@@ -36,18 +36,15 @@ int main() {
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     const int nrb = (c.M + GT - 1) / GT, ncb = (c.Nc + GT - 1) / GT, ncb8 = (ncb + 7) / 8 * 8;
     const dim3 grid(nrb * ncb8);
-    const int variants = c.at ? 1 : 8;
+    const int variants = c.at ? 1 : 5;
     for (int v = 0; v < variants; ++v) {
       auto run = [&](double *Cout) {
         if (c.at) hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
         else if (v == 0) hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 1) hipLaunchKernelGGL((gemmh_kernel_t<4, 2, false>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 2) hipLaunchKernelGGL((gemmh_kernel_t<4, 2, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 3) hipLaunchKernelGGL((gemmh_kernel_t<3, 2, false>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 4) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 5) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
-        else if (v == 6) hipLaunchKernelGGL((gemmh_kernel_t<3, 3, false, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1, nullptr, nullptr);
-        else hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1, nullptr, nullptr);
+        else if (v == 1) hipLaunchKernelGGL((gemmh_kernel_t<4, 2>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
+        else if (v == 2) hipLaunchKernelGGL((gemmh_kernel_t<3, 2>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
+        else if (v == 3) hipLaunchKernelGGL((gemmh_kernel_t<3, 3>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1);
+        else hipLaunchKernelGGL((gemmh_kernel_t<3, 3, true>), grid, dim3(256), 0, 0, A, lda, B, ldb, Cout, ldc, c.M, c.Nc, c.K, nrb, ncb, nullptr, 1, nullptr, nullptr);
       };
       double *Cout = v == 0 ? C : C2;
       if (v > 0) hipMemset(C2, 0, (size_t)c.M * ldc * 8);
