@@ -24,7 +24,8 @@ def contexts(dfm, n):
     return [dfm.Context(0) for _ in range(n)]
 
 
-@pytest.mark.parametrize("T,N,r,mode", [(200, 400, 4, "factored"), (150, 60, 3, "auto"), (120, 300, 3, "direct")])
+@pytest.mark.parametrize("T,N,r,mode", [(200, 400, 4, "factored"), (96, 150, 3, "factored"), (150, 60, 3, "auto"),
+                                        (120, 300, 3, "direct")])
 @pytest.mark.parametrize("n", [2, 3])
 def test_bootstrap_multi_is_bit_identical(dfm, oracle, T, N, r, mode, n):
     y, x, w = panel(oracle, T, N, r, 400 + T + n)

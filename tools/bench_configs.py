@@ -90,10 +90,34 @@ def c2(D, ctx, args):
     def run():
         ctx.check(ctx.lib.dfm_bootstrap_dev(model.handle, 0, B, di.data_ptr(), de.data_ptr(), arr, len(stats),
                                             out.data_ptr()))
+    run()
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.enable_timing(True)
     s = timed(run, args.reps, ctx.synchronize)
+    ctx.enable_timing(False)
+    tm = ctx.read_timing()
     rec = {"config": "c2", "workload": f"wild bootstrap B={B}, T={T} N={N} r={model.number_of_factors}, "
                                        f"LR/LM/Wald all variables at bp={bp} + V + ICp2 (inputs resident)",
-           "value": round(B / s, 1), "unit": "replicates/s", "ms_per_job": round(s * 1e3, 3)}
+           "value": round(B / s, 1), "unit": "replicates/s", "ms_per_job": round(s * 1e3, 3),
+           "kernels_ms_per_job": {k: round(v[0] / (args.reps + 1), 4) for k, v in tm.items() if v[1]}}
+    # K1 roofline: the fused-gather Gram X*'X* (130 x 130 over T = 600) per
+    # replicate, SYRK count N (N + 1) T, over its HIP-event time
+    gms, gn = tm.get("gram", (0.0, 0))
+    if gn:
+        flop = B * (args.reps + 1) * N * (N + 1) * T
+        rec["roofline_gram"] = {"kernel": "gram_kernel<COLS> (fused resample gather, v_mfma_f64_4x4x4_4b)",
+                                "bound": "mfma", "achieved": round(flop / (gms * 1e-3) / 1e12, 3), "peak": 78.6,
+                                "unit": "TFLOP/s", "frac": round(flop / (gms * 1e-3) / 1e12 / 78.6, 4),
+                                "avg_launch_ms": round(gms / gn, 4), "flop_per_replicate": N * (N + 1) * T}
+    # Chow pass: two reads of X* (gathered rows of C + eta E) per replicate
+    cms, cn = tm.get("chow", (0.0, 0))
+    if cn:
+        by = B * (args.reps + 1) * 2 * T * N * 8
+        rec["roofline_chow"] = {"kernel": "chow_prep + chow_all_kernel", "bound": "hbm",
+                                "achieved": round(by / (cms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                                "frac": round(by / (cms * 1e-3) / 1e9 / 8000.0, 4),
+                                "bytes_per_replicate": 2 * T * N * 8}
     if args.cpu:
         O = oracle()
         o = O.DynamicFactorModel_ic(y, w, x, "ICp2", kmax=8)

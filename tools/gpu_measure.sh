@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round measurement session: -m gpu suite, the headline bench, rocprofv3
+# kernel stats of the bench (C3 factored) and of the direct-Gram mode and C2,
+# then the PMC HBM-traffic passes.  Every GPU step has its own time limit; a
+# fault / abort / timeout stops the session.
+OUT=${1:-gpurun_out/measure}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {   # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "[$name] rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -20 "$OUT/$name.err"; exit $rc; fi
+  return 0
+}
+if [ -z "$SKIP_TESTS" ]; then
+  step pytest 900 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 180 --timeout-method thread -p no:cacheprovider
+  tail -8 "$OUT/pytest.out"
+fi
+step bench 300 python -u bench.py --steps 20 --warmup 5
+cat "$OUT/bench.out"
+step trace 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+step bench_direct 300 python -u bench.py --steps 3 --warmup 1 --mode direct --no-cpu-baseline
+step trace_direct 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_direct" -o run -- python3 bench.py --steps 2 --warmup 1 --mode direct --no-cpu-baseline
+step configs 600 python -u tools/bench_configs.py --configs c1,c2,c4,c5 --reps 3
+cat "$OUT/configs.out"
+step trace_c2 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 2
+step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
+step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
+step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffic.json"
+echo ALLDONE
