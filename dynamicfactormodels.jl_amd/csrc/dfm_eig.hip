@@ -902,7 +902,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
 }
 
 hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, double invT, double *Lout, hipStream_t st);
+                                int r, double invT, double *Lout, hipStream_t st, int Ncv);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1, bool b_padded = false,
@@ -1776,19 +1776,6 @@ __global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double 
   }
 }
 
-// L*[rep][n][j] = (sum_i L[n][i] M1[rep][i][j] + GL[n][rep*r + j]) / T
-__global__ void boot_lfinish_kernel(const double *__restrict__ Lb, int N, int r, int T,
-                                    const double *__restrict__ M1, const double *__restrict__ GL,
-                                    int64_t ldgl, double *__restrict__ Lout) {
-  const int rep = blockIdx.y;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)N * r) return;
-  const int n = (int)(e / r), j = (int)(e % r);
-  double v = GL[(int64_t)n * ldgl + (int64_t)rep * r + j];
-  for (int i = 0; i < r; ++i) v = fma(Lb[(int64_t)n * r + i], M1[(int64_t)rep * r * r + i * r + j], v);
-  Lout[(int64_t)rep * N * r + e] = v / T;
-}
-
 // rows T.. of [E; L'; 0]: row T+i = column i of L (i < r), then zero rows
 __global__ void eaug_tail_kernel(const double *__restrict__ Lb, int N, int r, int64_t ld, double *__restrict__ tail) {
   const int i = blockIdx.y;
@@ -1806,32 +1793,27 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
   // T..T+r-1 (written by boot_zf), zero rows up to Kp (the GEMM's k padding)
   const int Kp = (T + r + 15) / 16 * 16;
   double *ZF = (double *)ws;
-  double *GL = ZF + (size_t)Kp * ldzf;
-  double *M1 = GL + (size_t)N * ldzf;
+  double *M1 = ZF + (size_t)Kp * ldzf;
   double *Eaug = M1 + (size_t)nb * r * r;   // [E; L'; 0]: Kp x ld
   hipMemsetAsync(ZF + (size_t)T * ldzf, 0, (size_t)(Kp - T) * ldzf * 8, st);
+  // the pad column of an odd nb r is streamed by the GEMM (its products are
+  // discarded): keep it finite
+  if (ldzf != (int64_t)nb * r) hipMemset2DAsync(ZF + ldzf - 1, (size_t)ldzf * 8, 0, 8, T, st);
   hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, ldzf, M1);
-  hipError_t e;
-  if (ldzf == (int64_t)nb * r && ld % 2 == 0) {
-    // one GEMM of depth T + r does the whole finish (see gemm_loadings_kernel)
-    hipMemcpy2DAsync(Eaug, (size_t)ld * 8, Ep, (size_t)ld * 8, (size_t)ld * 8, T, hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(eaug_tail_kernel, dim3((unsigned)((ld + 255) / 256), Kp - T), dim3(256), 0, st, Lb, N, r, ld,
-                       Eaug + (size_t)T * ld);
-    e = launch_gemm_loadings(Eaug, ld, ZF, ldzf, N, nb * r, T + r, r, 1.0 / T, Lout, st);
-    return e == hipSuccess ? 0 : 1000 + (int)e;
-  }
-  e = launch_gemm(true, Ep, ld, ZF, ldzf, GL, ldzf, N, (int)ldzf, T, st);
-  if (e != hipSuccess) return 1000 + (int)e;
-  hipLaunchKernelGGL(boot_lfinish_kernel, dim3((unsigned)(((int64_t)N * r + 255) / 256), nb), dim3(256), 0, st,
-                     Lb, N, r, T, M1, GL, ldzf, Lout);
-  e = hipGetLastError();
+  // one GEMM of depth T + r does the whole finish (see gemm_loadings_kernel),
+  // for every batch size: the same arithmetic for every replicate whatever
+  // the batch composition (batch- and shard-invariant loadings)
+  hipMemcpy2DAsync(Eaug, (size_t)ld * 8, Ep, (size_t)ld * 8, (size_t)ld * 8, T, hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(eaug_tail_kernel, dim3((unsigned)((ld + 255) / 256), Kp - T), dim3(256), 0, st, Lb, N, r, ld,
+                     Eaug + (size_t)T * ld);
+  const hipError_t e = launch_gemm_loadings(Eaug, ld, ZF, ldzf, N, (int)ldzf, T + r, r, 1.0 / T, Lout, st, nb * r);
   return e == hipSuccess ? 0 : 1000 + (int)e;
 }
 size_t fact_loadings_bytes(int T, int N, int r, int nb) {
   const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
   const int Kp = (T + r + 15) / 16 * 16;
   const int64_t ld = ((int64_t)N + 15) / 16 * 16;
-  return ((size_t)Kp * ldzf + (size_t)N * ldzf + (size_t)nb * r * r + (size_t)Kp * ld) * 8 + 1024;
+  return ((size_t)Kp * ldzf + (size_t)nb * r * r + (size_t)Kp * ld) * 8 + 1024;
 }
 
 // ---- model-level precompute: EL = E L (T x r), S = L'L, cF, hd

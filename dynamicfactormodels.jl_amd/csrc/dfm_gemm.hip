@@ -357,7 +357,7 @@ template <int NBUF, int MINB>
 __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
                                                                   const double *__restrict__ B, int64_t ldb, int M,
                                                                   int Nc, int K, int nrb, int ncb, int r, double invT,
-                                                                  double *__restrict__ Lout) {
+                                                                  double *__restrict__ Lout, int Ncv) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -429,22 +429,24 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
       const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
       const int n = abase + wr * 32 + 4 * fa + oi;
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
-      if (n < M && col < Nc) {
+      if (n < M && col < Ncv) {
         const int rep = col / r, jj = col - rep * r;
         Lout[((int64_t)rep * M + n) * r + jj] = v * invT;
       }
     }
 }
 
+// Nc: columns of ZF streamed (even: the 16-B DMA pairs never straddle the
+// valid range), Ncv <= Nc: columns stored (nb r).
 hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, double invT, double *Lout, hipStream_t st) {
+                                int r, double invT, double *Lout, hipStream_t st, int Ncv) {
   const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int nrb8 = (nrb + 7) / 8;
   // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here, with
   // running pointers still 23 % slower: 4-deep at 2 per CU stays)
   // running DMA pointers over the zero k-padding of both operands
   hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N,
-                     Nc, K, nrb, ncb, r, invT, Lout);
+                     Nc, K, nrb, ncb, r, invT, Lout, Ncv);
   return hipGetLastError();
 }
 
