@@ -16,7 +16,8 @@ from .api import (Context, DFMError, Stat, DynamicFactorModel, DynamicFactorMode
                   factor_residual_variance, criterion_value, wild_bootstrap, residual_bootstrap,
                   chow_all, LR_test, LM_test, Wald_test, targeted_predictors, default_context,
                   CRITERIA, pseudo_out_of_sample_refits, pseudo_out_of_sample_refits_dev,
-                  pseudo_out_of_sample_forecasts, MSE, normalize, normalize_dev, clone_model)
+                  pseudo_out_of_sample_forecasts, MSE, normalize, normalize_dev, clone_model,
+                  lasso_path)
 from .api import (criterion_PCp1, criterion_PCp2, criterion_PCp3, criterion_ICp1,  # noqa: F401
                   criterion_ICp2, criterion_ICp3, criterion_BIC)
 from . import _lib
@@ -29,5 +30,5 @@ __all__ = [
     "factor_residual_variance", "criterion_value", "wild_bootstrap", "residual_bootstrap",
     "chow_all", "LR_test", "LM_test", "Wald_test", "targeted_predictors", "default_context",
     "CRITERIA", "pseudo_out_of_sample_refits", "pseudo_out_of_sample_refits_dev",
-    "pseudo_out_of_sample_forecasts", "MSE", "normalize_dev", "clone_model",
+    "pseudo_out_of_sample_forecasts", "MSE", "normalize_dev", "clone_model", "lasso_path",
 ]

@@ -87,6 +87,8 @@ SIGNATURES = [
     ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                     C.c_double, c_double_p, c_uint8_p]),
+    ("dfm_lasso_path", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_uint8_p, C.c_int, c_double_p, C.c_int,
+                                 C.c_int, C.c_double, c_double_p, c_double_p, C.POINTER(C.c_int)]),
     ("dfm_targeted_soft", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, c_int32_p,
                                     C.c_int, C.c_double, C.POINTER(C.c_int), C.POINTER(C.c_int),

@@ -655,6 +655,28 @@ def _targeted_soft(y, w, x, folds, rng, nlambda, lambda_min_ratio, return_path, 
                  "a0": a0.value, "folds": folds}
 
 
+def lasso_path(G, c, ju, lambdas, *, early: bool = False, thresh: float = 1e-7, ctx: Optional[Context] = None):
+    """glmnet's elnet1 path on a standardised covariance (``dfm_lasso_path``,
+    the core of the soft threshold, src/targeted_predictors.jl:33): G (p, p)
+    with unit diagonal over the non-constant columns ``ju``, c = Zs'ys/n,
+    decreasing standardised lambdas.  Returns (betas (L, p), rsq (L,))."""
+    ctx = ctx or default_context()
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    c = np.ascontiguousarray(c, dtype=np.float64).ravel()
+    p = len(c)
+    if G.shape != (p, p):
+        raise ValueError("G must be p x p")
+    juv = np.ascontiguousarray(np.asarray(ju, dtype=bool).astype(np.uint8))
+    lam = np.ascontiguousarray(lambdas, dtype=np.float64)
+    betas = np.zeros((len(lam), p))
+    rsq = np.zeros(len(lam))
+    L = C.c_int()
+    ctx.check(ctx.lib.dfm_lasso_path(ctx.h, _lib.ptr(G), _lib.ptr(c), juv.ctypes.data_as(_lib.c_uint8_p), p,
+                                     _lib.ptr(lam), len(lam), int(early), float(thresh), _lib.ptr(betas),
+                                     _lib.ptr(rsq), C.byref(L)))
+    return betas[:L.value], rsq[:L.value]
+
+
 # ---------------------------------------------------------- expanding windows
 def _window_kmax(T: int, N: int, kmax) -> int:
     """Row width of the windows' eigenvalue / coefficient outputs: the last

@@ -4,9 +4,10 @@
 // Z = [w x], keep the x columns whose coefficient at the CV-optimal lambda is
 // nonzero).  GLMNet is never imported by the reference (defect D5); the
 // algorithm is glmnet's gaussian lasso (Friedman, Hastie & Tibshirani 2010),
-// the same restatement the parity tests' CPU checker holds: standardised coordinate descent with covariance
-// updates on the active set, KKT scan appending violators in index order,
-// warm starts along the lambda grid, early path exit on the full fit.
+// the same restatement the parity tests' CPU checker holds: elnet1's
+// covariance-updating coordinate descent in its loop order (full cyclic
+// passes with in-pass entry, active-set passes, gradient refresh), warm
+// starts along the lambda grid, early path exit on the full fit.
 //
 // Device work per call, K folds + the full fit = K + 1 "problems":
 //   soft_stats_kernel   per (problem, column): training-row mean / population
@@ -16,9 +17,11 @@
 //   gram_kernel (K1)    G_f = Zs_f' Zs_f over each problem's training rows,
 //                       gathered by row index (zero row pads ragged folds):
 //                       (K+1) p^2 n MACs on MFMA              (MFMA-bound)
-//   lasso_path_kernel   one workgroup per problem: the whole lambda path in
-//                       one launch; g_A updates against an LDS-cached G_AA
-//                       (latency-bound: sequential coordinate updates)
+//   lasso_coop_kernel   one cooperative launch, 1 leader + H helper
+//                       workgroups per problem: glmnet's elnet1 path (the
+//                       serial coordinate descent over the active set on the
+//                       leader, the O(p |A|) full-pass replays and gradient
+//                       refreshes spread over the helpers)
 //   soft_loss_kernel    hold-out SSE per (fold, lambda)        (HBM-bound)
 #include "dfm_common.h"
 #include "../../include/dfm.h"
@@ -30,14 +33,6 @@ namespace dfm {
 hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
                        int64_t strideG, int nrep, hipStream_t st);
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
-
-constexpr int LS_AMAX = 1024;   // active-set capacity (glmnet's pmax analogue)
-constexpr int LS_GC = 126;      // G_AA cached in LDS while the active set is this small (124 KB of the 160)
-// development timing of lasso_path_kernel phases (DFM_SOFT_PROF=1): problem
-// 0's thread 0 accumulates s_memrealtime ticks (100 MHz) per phase
-__device__ unsigned long long g_soft_prof[8];
-#define SPROF_START() unsigned long long sp_t0 = wall_clock64()
-#define SPROF(i) do { if (f == 0 && tid == 0) { const unsigned long long sp_t1 = wall_clock64(); g_soft_prof[i] += sp_t1 - sp_t0; sp_t0 = sp_t1; } } while (0)
 
 // y mean / population sd over each problem's training rows (fold != f; f = 0: all).
 __global__ void soft_ystats_kernel(const double *__restrict__ y, const int32_t *__restrict__ fold, int n,
@@ -105,322 +100,578 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
     Gf[e] *= inv;
 }
 
-// One workgroup per problem: the lasso path over lambdas alm[0..nlam-1]
-// (standardised units), warm-started, by coordinate descent on the active
-// set.  Per pass the active list is walked in entry order (the serial
-// dependency of coordinate descent) and every coordinate change applied to
-// g_A (wave 0 alone while G_AA sits in LDS, else all threads); after a converged pass the non-active
-// gradients are refreshed with the pass's accumulated changes (rows of G for
-// the active variables, coalesced along j) and the KKT scan appends every
-// violator |g_j| > lambda in index order.  status[f]: 0 ok, 1 no convergence,
-// 2 active set over LS_AMAX; status[nprob + f]: the lambda index of the failure.
-// early = 1: problem 0 (the full fit) applies glmnet's early path exit and
-// publishes its path length in nlam_out[0] (zeroed before the launch); the
-// other problems stop when they reach it.
-__global__ __launch_bounds__(256) void lasso_path_kernel(
-    const double *__restrict__ Gall, int64_t strideG, int p, const double *__restrict__ call,
-    const uint8_t *__restrict__ juall, const double *__restrict__ almall, int nlam, int prob0, int early, int cdmode,
-    double thr, int maxit, double *__restrict__ gws, int *__restrict__ actws, double *__restrict__ gaaws,
-    double *__restrict__ bpath,
-    double *__restrict__ rsq_out, int *__restrict__ nlam_out, int *__restrict__ status) {
-  const int f = prob0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double *G = Gall + (int64_t)f * strideG;
-  const double *c = call + (int64_t)f * p;
-  const uint8_t *ju = juall + (int64_t)f * p;
-  const double *alm = almall + (int64_t)f * nlam;
-  double *g = gws + (int64_t)f * p;
-  int *act = actws + (int64_t)f * p;
-  // G_AA compacted in entry order (row stride LS_AMAX) for active sets past
-  // LS_GC: one coalesced 8 na-byte row per coordinate step instead of a
-  // gather that touches nearly every cache line of a p-wide G row
-  double *GAA = gaaws + (int64_t)f * LS_AMAX * LS_AMAX;
-  double *bp = bpath + (int64_t)f * nlam * p;
-  __shared__ int ia[LS_AMAX], rows[LS_AMAX];
-  __shared__ double bA[LS_AMAX], gA[LS_AMAX], dA[LS_AMAX];
-  __shared__ double GC[LS_GC * LS_GC];
-  __shared__ double s_red[4];
-  __shared__ int s_flag, s_cnt[4];
-  for (int j = tid; j < p; j += 256) { g[j] = c[j]; act[j] = 0; }
-  __syncthreads();
-  int na = 0, L = nlam, st = 0, fail_m = nlam;
-  double rsq_prev = 0.0;
+// ------------------------------------------------------------- lasso path
+// glmnet's elnet1 (covariance updating) for K + 1 problems in ONE cooperative
+// launch.  The loop order is elnet1's (oracle/dfm_oracle.py lasso_path_cd):
+// per lambda a full cyclic pass over every variable in index order with
+// in-pass entry and eager gradient updates g_j -= c_jk d, then passes over
+// the active set in entry order until max d^2 < thr, the non-active
+// gradients refreshed by dot(da, c_j,A), and back to the full pass; from the
+// second lambda on a lambda starts with the active-set passes.  Every
+// product and difference is rounded separately (this file is compiled with
+// -ffp-contract=off): given the same G and c the path is bit-identical to
+// the restatement (tests/test_gpu_soft.py).
+//
+// Parallel form.  Problem f owns 1 + H workgroups:
+//   leader  (role 0): the serial coordinate descent over the ACTIVE set, on
+//           wave 0 in blocks of 64 coordinates (lane t = one coordinate, its
+//           column of the 64 x 64 block of G_AA in registers, deltas
+//           broadcast by readlane: no barrier per coordinate); each block's
+//           changes are applied to every other active gradient by all four
+//           waves, in the same order as elnet1's eager updates;
+//   helpers (roles 1..H): the O(p |A|) work over the NON-active variables,
+//           each on a contiguous slice of the p columns:
+//           FULL:    a full pass is run speculatively — the leader visits the
+//                    active coordinates in index order assuming no entry; the
+//                    helpers replay its change list against every non-active
+//                    gradient (the value at the variable's own visit, and the
+//                    final one), and report the first variable that enters.
+//                    The leader then adds it and re-runs the pass from the
+//                    pass-start state (identical up to the entry), until a
+//                    replay finds no entry: exactly elnet1's pass;
+//           REFRESH: g_j -= dot(da, c_j,A) after the active-set passes.
+// Leader and helpers meet through per-problem 8-byte granules in global
+// memory, each on a line of its own (cdna_hip_programming.md §6 Guideline
+// 16): the producer drains its stores (s_waitcnt vmcnt(0) in every storing
+// wave, barrier), ONE lane issues an agent release fence and stores the
+// granule {tag = task number, value}; the consumer polls the granule relaxed
+// with s_sleep, then ONE agent acquire before the barrier.  Task granule value:
+// type | gcur | nc; a helper's done granule carries its first entering
+// variable.  Every spin is bounded by a wall-clock timeout, so every wave
+// reaches the exit.
+constexpr int LP_LMAX = 4096;   // active-set capacity (leader LDS state; glmnet's pmax)
+constexpr int LP_B = 64;        // coordinate block = one wave
+constexpr int LP_NT = 512;      // threads per workgroup
+constexpr int LP_PF = (LP_B * LP_B + LP_NT - 64 - 1) / (LP_NT - 64);   // next-block loads per thread of waves 1..7
+enum { LP_FULL = 1, LP_REFRESH = 2, LP_EXIT = 3 };
+
+struct alignas(256) LpLine {   // one granule per 256-B line
+  unsigned long long v;
+  unsigned long long pad[31];
+};
+struct LassoCtl {   // per problem, zeroed before the launch
+  LpLine task;      // {tag = task number, value = type | gcur << 2 | nc << 3}
+  LpLine lam;       // the task's lambda (payload)
+  LpLine done[64];  // helper h: {tag = task number, value = first entering variable (or INT_MAX)}
+};
+
+struct LassoArgs {
+  const double *G;
+  int64_t strideG;
+  int p, nlam, early, maxit, H, ldaa;
+  double thr;
+  const double *c, *alm;
+  const uint8_t *ju;
+  LassoCtl *ctl;
+  double *g2;       // [nprob][2][p]  gradients: the current buffer and the FULL replay's output
+  int *isact;       // [nprob][p]
+  int *klist;       // [nprob][LP_LMAX] task payload: coordinates
+  double *dlist;    // [nprob][LP_LMAX]              deltas
+  double *save;     // [nprob][2][LP_LMAX] pass-start a, g (by entry position)
+  double *GAA;      // [nprob][ldaa][ldaa] G over the active set, entry order
+  double *bpath, *rsq_out;
+  int *nlam_out, *status;
+  long long tmo;    // spin timeout, wall-clock ticks (100 MHz)
+  long long *prof;  // diagnostics (nullable): [nprob][8] leader wall-clock ticks per phase + counts
+};
+
+DFM_DEV double lp_ld(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DFM_DEV unsigned long long lp_ldu(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DFM_DEV void lp_stu(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DFM_DEV unsigned long long lp_gran(int tag, unsigned int val) { return ((unsigned long long)(unsigned)tag << 32) | val; }
+// drain this wave's stores (the producer side of the hand-off; every storing wave)
+DFM_DEV void lp_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// ONE lane: agent release, then its own wait (ROCm 7.2 can drop the fence's, Guideline 16)
+DFM_DEV void lp_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+DFM_DEV void lp_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+DFM_DEV int lp_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DFM_DEV void lp_st(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DFM_DEV void lp_sti(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DFM_DEV double lp_rdlane(double x, int l) {   // l: a compile-time constant inside unrolled loops
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The helpers' share of a task over columns [j0, j1) of problem f (the
+// leader runs it itself when H == 0).  hk / hd: the task's change list.
+DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam, int gcur, int j0, int j1,
+                         const int *hk, const double *hd) {
+  const int p = A.p;
+  const double *G = A.G + (int64_t)f * A.strideG;
+  const uint8_t *ju = A.ju + (int64_t)f * p;
+  const int *isact = A.isact + (int64_t)f * p;
+  double *gin = A.g2 + ((int64_t)f * 2 + gcur) * p;
+  double *gout = A.g2 + ((int64_t)f * 2 + (gcur ^ 1)) * p;
+  constexpr int U = 32;
+  int first = INT_MAX;   // this thread's first entering variable
+  for (int j = j0 + (int)threadIdx.x; j < j1; j += blockDim.x) {
+    if (!ju[j] || lp_ldi(isact + j)) continue;
+    if (type == LP_FULL) {
+      // elnet1's eager updates in visit order; the entry test at the variable's own visit
+      double s = lp_ld(gin + j);
+      bool chk = false, in = false;
+      double ga[U], gb[U];   // two chunks of the change list in flight
+      auto ld = [&](double *gv, int i0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) gv[u] = (i0 + u < nc) ? G[(int64_t)hk[i0 + u] * p + j] : 0.0;
+      };
+      auto use = [&](const double *gv, int i0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (i0 + u < nc) {
+            if (!chk && hk[i0 + u] > j) { chk = true; in = fabs(s) - lam > 0.0; }
+            s = s - gv[u] * hd[i0 + u];
+          }
+        }
+      };
+      ld(ga, 0);
+      for (int i0 = 0; i0 < nc; i0 += 2 * U) {
+        if (i0 + U < nc) ld(gb, i0 + U);
+        use(ga, i0);
+        if (i0 + U >= nc) break;
+        if (i0 + 2 * U < nc) ld(ga, i0 + 2 * U);
+        use(gb, i0 + U);
+      }
+      if (!chk) in = fabs(s) - lam > 0.0;
+      if (in) first = min(first, j);
+      gout[j] = s;
+    } else {   // LP_REFRESH: g_j -= dot(da, c_j,A), the dot a sequential sum in entry order
+      double s = 0.0;
+      for (int i0 = 0; i0 < nc; i0 += U) {
+        double gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gv[u] = (i0 + u < nc) ? G[(int64_t)hk[i0 + u] * p + j] : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (i0 + u < nc) s = s + hd[i0 + u] * gv[u];
+      }
+      gin[j] = lp_ld(gin + j) - s;
+    }
+  }
+  return first;
+}
+
+DFM_DEV int lp_at(const int *ord, int x) { return ord ? ord[x] : x; }
+
+// s_gb := the 64 x 64 block of G_AA at sweep positions [b, b + 64) (zero outside n)
+DFM_DEV void lp_gblock_load(const int *ord, int b, int n, const double *GAA, int ldaa, double *s_gb) {
+  const int nb = min(LP_B, n - b);
+  for (int e = threadIdx.x; e < LP_B * LP_B; e += blockDim.x) {
+    const int s = e >> 6, t = e & 63;
+    s_gb[e] = (s < nb && t < nb) ? GAA[(int64_t)lp_at(ord, b + s) * ldaa + lp_at(ord, b + t)] : 0.0;
+  }
+}
+
+// One pass over n active positions, in entry order (ord == nullptr) or in
+// coordinate-index order (ord = s_srt).  rec: append every change
+// (coordinate, delta) to kl / dl in visit order.  All threads call it.
+//
+// Per block of 64 sweep positions: wave 0 runs the serial coordinate steps
+// (lane t = one coordinate, its column of the block's G_AA in registers from
+// the LDS copy s_gb, deltas broadcast by readlane); meanwhile waves 1..7 load
+// the NEXT block's G_AA block (-> s_gb after the barrier) and, for their
+// gradient q, this block's 64 G_AA rows, so that the block's changes reach
+// every other active gradient without a memory round trip after the
+// barrier.  G_AA is private to this workgroup: plain loads (its L1 lines are
+// invalidated after every update of G_AA, see the entry step).  s_gb holds the
+// first block of the sweep order `key` when gkey == key (the last block
+// prefetches the next sweep's first).
+DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int &gkey, const double *GAA, int ldaa,
+                      const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_d, double *s_gb,
+                      double *s_sc, int *s_nc, int *kl, double *dl, long long *tk) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), u = tid - 64;
+  if (n <= 0) return;
+  if (gkey != key) {
+    lp_gblock_load(ord, 0, n, GAA, ldaa, s_gb);
+    __syncthreads();
+    gkey = key;
+  }
+  for (int b0 = 0; b0 < n; b0 += LP_B) {
+    const int nb = min(LP_B, n - b0);
+    const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);
+    long long t0 = tk && tid == 0 ? wall_clock64() : 0;
+    // wave-uniform branches, each with its own barrier (every wave reaches one)
+    if (wave == 0) {
+      const bool on = lane < nb;
+      const int pt = on ? lp_at(ord, b0 + lane) : 0;
+      double g = on ? s_g[pt] : 0.0, a = on ? s_a[pt] : 0.0;
+      double Gr[LP_B];   // this lane's column of the block (rows: the block's coordinates)
+#pragma unroll
+      for (int s = 0; s < LP_B; ++s) Gr[s] = s_gb[s * LP_B + lane];
+      double rsq = s_sc[0], dlx = s_sc[1];
+#pragma unroll
+      for (int s = 0; s < LP_B; ++s) {
+        if (s < nb) {
+          const double gk = lp_rdlane(g, s), ak = lp_rdlane(a, s);
+          const double uu = gk + ak;
+          const double v = fabs(uu) - lam;
+          const double na = v > 0.0 ? copysign(v, uu) : 0.0;
+          double d = 0.0;
+          if (na != ak) {
+            d = na - ak;
+            if (lane == s) a = na;
+            rsq = rsq + d * (2.0 * gk - d);
+            dlx = fmax(dlx, d * d);
+            g = g - Gr[s] * d;
+          }
+          if (lane == 0) s_d[s] = d;
+        }
+      }
+      if (on) { s_g[pt] = g; s_a[pt] = a; }
+      const double dv = on ? s_d[lane] : 0.0;
+      const bool ch = on && dv != 0.0;
+      const unsigned long long bal = __ballot(ch);
+      if (lane == 0) { s_sc[0] = rsq; s_sc[1] = dlx; s_sc[2] = (double)__popcll(bal); }
+      if (rec) {   // changes in visit order
+        const int base = *s_nc;
+        if (ch) {
+          const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
+          kl[o] = s_ia[pt];
+          dl[o] = dv;
+        }
+        if (lane == 0) *s_nc = base + __popcll(bal);
+      }
+      __syncthreads();
+      if (tk && tid == 0) { const long long t1 = wall_clock64(); tk[0] += t1 - t0; t0 = t1; tk[2] += 1; }
+    } else {
+      double nx[LP_PF], pv[LP_B];
+      bool qon = false;
+#pragma unroll
+      for (int i = 0; i < LP_PF; ++i) {   // the next block's G_AA block
+        const int e = u + (LP_NT - 64) * i, s = e >> 6, t = e & 63;
+        nx[i] = (e < LP_B * LP_B && s < nb1 && t < nb1)
+                    ? GAA[(int64_t)lp_at(ord, b1 + s) * ldaa + lp_at(ord, b1 + t)] : 0.0;
+      }
+      const int q = u;   // gradient (entry position) q: this block's rows of G_AA at column q
+      if (q < n) {
+        const int rq = ord ? s_rank[q] : q;
+        qon = rq < b0 || rq >= b0 + nb;
+      }
+#pragma unroll
+      for (int s = 0; s < LP_B; ++s) {   // row base uniform (scalar), column offset per lane
+        const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at(ord, b0 + min(s, nb - 1))) * ldaa;
+        pv[s] = (qon && s < nb) ? row[q] : 0.0;
+      }
+      __syncthreads();
+      const int nch = (int)s_sc[2];
+#pragma unroll
+      for (int i = 0; i < LP_PF; ++i) {
+        const int e = u + (LP_NT - 64) * i;
+        if (e < LP_B * LP_B) s_gb[e] = nx[i];
+      }
+      if (qon && nch) {   // elnet1's eager updates, in visit order
+        double gq = s_g[u];
+#pragma unroll
+        for (int s = 0; s < LP_B; ++s) {
+          const double d = s_d[s];
+          if (s < nb && d != 0.0) gq = gq - pv[s] * d;
+        }
+        s_g[u] = gq;
+      }
+    }
+    const int nch = (int)s_sc[2];
+    if (nch && n > LP_NT - 64) {   // gradients past the prefetched ones: loads after the serial steps
+      for (int q = LP_NT - 64 + tid; q < n; q += blockDim.x) {
+        const int rq = ord ? s_rank[q] : q;
+        if (rq >= b0 && rq < b0 + nb) continue;
+        double gq = s_g[q];
+        for (int s0 = 0; s0 < nb; s0 += 32) {
+          double gv[32];
+#pragma unroll
+          for (int w = 0; w < 32; ++w) {
+            const int s = s0 + w;
+            const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at(ord, b0 + min(s, nb - 1))) * ldaa;
+            gv[w] = (s < nb && s_d[s] != 0.0) ? row[q] : 0.0;
+          }
+#pragma unroll
+          for (int w = 0; w < 32; ++w) {
+            const int s = s0 + w;
+            if (s < nb && s_d[s] != 0.0) gq = gq - gv[w] * s_d[s];
+          }
+        }
+        s_g[q] = gq;
+      }
+    }
+    __syncthreads();
+    if (tk && tid == 0) { tk[1] += wall_clock64() - t0; tk[3] += nch; }
+  }
+}
+
+__global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
+  __shared__ __attribute__((aligned(16))) char lds[3 * LP_LMAX * 4 + 2 * LP_LMAX * 8];
+  __shared__ double s_d[LP_B], s_sc[4], s_gb[LP_B * LP_B];
+  __shared__ int s_i[8], s_cnt[LP_NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
+  LassoCtl *ctl = A.ctl + f;
+  int *kl = A.klist + (int64_t)f * LP_LMAX;
+  double *dl = A.dlist + (int64_t)f * LP_LMAX;
+  if (role > 0) {   // ------------------------------------------------ helper
+    int *hk = (int *)lds;
+    double *hd = (double *)(lds + LP_LMAX * 4);
+    const int h = role - 1, j0 = (int)((int64_t)h * p / H), j1 = (int)((int64_t)(h + 1) * p / H);
+    for (int q = 1;; ++q) {
+      if (tid == 0) {   // ONE lane polls the task granule, then ONE acquire
+        const long long t0 = wall_clock64();
+        unsigned long long gv;
+        int ok = 1;
+        while ((int)((gv = lp_ldu(&ctl->task.v)) >> 32) < q) {
+          if (wall_clock64() - t0 > A.tmo) { ok = 0; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        lp_acquire();
+        s_i[0] = ok ? (int)(unsigned)gv : -1;
+        s_i[1] = INT_MAX;
+      }
+      __syncthreads();
+      const int tv = s_i[0];
+      if (tv < 0) break;
+      const int type = tv & 3, gcur = (tv >> 2) & 1, nc = tv >> 3;
+      if (type == LP_EXIT) break;
+      const double lam = __longlong_as_double((long long)lp_ldu(&ctl->lam.v));
+      for (int i = tid; i < nc; i += blockDim.x) { hk[i] = lp_ldi(kl + i); hd[i] = lp_ld(dl + i); }
+      __syncthreads();
+      const int first = lp_task_cols(A, f, type, nc, lam, gcur, j0, j1, hk, hd);
+      if (first != INT_MAX) atomicMin(&s_i[1], first);   // LDS
+      lp_drain();
+      __syncthreads();
+      if (tid == 0) {
+        lp_release();
+        lp_stu(&ctl->done[h].v, lp_gran(q, (unsigned)s_i[1]));
+      }
+    }
+    return;
+  }
+  // ----------------------------------------------------------------- leader
+  int *s_ia = (int *)lds, *s_srt = s_ia + LP_LMAX, *s_rank = s_srt + LP_LMAX;
+  double *s_g = (double *)(s_rank + LP_LMAX), *s_a = s_g + LP_LMAX;
+  const double *G = A.G + (int64_t)f * A.strideG;
+  const double *c = A.c + (int64_t)f * p;
+  const double *alm = A.alm + (int64_t)f * A.nlam;
+  const int ldaa = A.ldaa, cap = min(ldaa, LP_LMAX), nlam = A.nlam;
+  double *g2 = A.g2 + (int64_t)f * 2 * p;
+  int *isact = A.isact + (int64_t)f * p;
+  double *sv = A.save + (int64_t)f * 2 * LP_LMAX;
+  double *GAA = A.GAA + (int64_t)f * ldaa * ldaa;
+  double *bp = A.bpath + (int64_t)f * nlam * p;
+  for (int j = tid; j < p; j += blockDim.x) { lp_st(g2 + j, c[j]); lp_sti(isact + j, 0); }
+  if (tid == 0) { s_sc[0] = 0.0; s_sc[1] = 0.0; s_i[1] = 0; s_i[2] = 0; }
+  int seq = 0, gcur = 0, nlp = 0, iz = 0, L = nlam, st = 0, fail_m = nlam, nin = 0;
+  int ver = 0, gkey = -1;   // active-set version (entries); the sweep order s_gb's block belongs to
+  // publish a task to the helpers and wait for all of them (H == 0: run it here)
+  // publish a task to the helpers (payload: kl, dl, isact, g2, lam) and wait
+  // for every helper's done granule; s_i[3] = the first entering variable
+  auto run_task = [&](int type, int nc, double lam) -> bool {   // (H >= 1: the host guarantees it)
+    ++seq;
+    if (tid == 0) lp_stu(&ctl->lam.v, (unsigned long long)__double_as_longlong(lam));
+    lp_drain();
+    __syncthreads();
+    if (tid == 0) {
+      lp_release();
+      lp_stu(&ctl->task.v, lp_gran(seq, (unsigned)(type | gcur << 2 | nc << 3)));
+    }
+    if (type == LP_EXIT) return true;
+    if (wave == 0) {   // lane h polls helper h's granule
+      const long long t0 = wall_clock64();
+      int ok = 1;
+      unsigned int v = INT_MAX;
+      for (;;) {
+        bool mine = true;
+        if (lane < H) {
+          const unsigned long long gv = lp_ldu(&ctl->done[lane].v);
+          mine = (int)(gv >> 32) >= seq;
+          v = (unsigned)gv;
+        }
+        if (__all(mine)) break;
+        if (wall_clock64() - t0 > A.tmo) { ok = 0; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      lp_acquire();
+      int first = lane < H ? (int)v : INT_MAX;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) first = min(first, __shfl_xor(first, o));
+      if (lane == 0) { s_i[3] = first; s_i[4] = ok; }
+    }
+    __syncthreads();
+    return s_i[4] != 0;
+  };
+  long long pt = wall_clock64();
+  long long pacc[16] = {0};
+  long long *tk = A.prof ? pacc + 8 : nullptr;
+  auto ptick = [&](int i) {   // leader phase timing (A.prof): thread 0 only
+    if (A.prof && tid == 0) { const long long t = wall_clock64(); pacc[i] += t - pt; pt = t; }
+  };
   for (int m = 0; m < nlam && !st; ++m) {
     const double lam = alm[m];
+    __syncthreads();
+    const double rsq0 = s_sc[0];
+    int jz = 1;
     for (;;) {
-      SPROF_START();
-      // ---- passes over the active set until max delta^2 < thr
-      // Small active sets (G_AA cached in LDS): wave 0 alone runs the passes —
-      // every lane reads gA[k], bA[k] (an LDS broadcast) and computes the same
-      // d, so no cross-wave barrier per coordinate; the wave's LDS accesses
-      // complete in program order and the wavefront fences keep the compiler
-      // from reordering them across steps.  Larger sets (G_AA rows gathered
-      // from HBM) keep all four waves on the update, thread 0 broadcasting d.
-      // Same arithmetic in the same order either way.
-      int it = 0;
-      if (na <= LS_GC) {
-        if (wave == 0) {
-          for (; it < maxit; ++it) {
-            double dlx = 0.0;
-            for (int k = 0; k < na; ++k) {
-              const double bk = bA[k];
-              const double u = gA[k] + bk, v = fabs(u) - lam;
-              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
-              const double d = nb - bk;
-              if (d != 0.0) {   // uniform over the wave
-                dlx = fmax(dlx, d * d);
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) { bA[k] = nb; dA[k] += d; }
-                for (int t = lane; t < na; t += 64) gA[t] -= GC[k * LS_GC + t] * d;
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-              }
-            }
-            if (dlx < thr) break;
-          }
-          if (lane == 0) s_flag = it;
-        }
-        __syncthreads();
-        it = s_flag;
-        __syncthreads();
-      } else if (cdmode == 1) {
-        if (wave == 0) {
-          for (; it < maxit; ++it) {
-            double dlx = 0.0;
-            for (int k = 0; k < na; ++k) {
-              const double bk = bA[k];
-              const double u = gA[k] + bk, v = fabs(u) - lam;
-              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
-              const double d = nb - bk;
-              if (d != 0.0) {   // uniform over the wave
-                dlx = fmax(dlx, d * d);
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) { bA[k] = nb; dA[k] += d; }
-                const double *Gk = GAA + (int64_t)k * LS_AMAX;
-                for (int t = lane; t < na; t += 64)
-                  gA[t] -= __hip_atomic_load(Gk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * d;
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-              }
-            }
-            if (dlx < thr) break;
-          }
-          if (lane == 0) s_flag = it;
-        }
-        __syncthreads();
-        it = s_flag;
-        __syncthreads();
-      } else if (cdmode == 0) {
-        // all four waves; row k + 1 of G_AA prefetched into registers (4 per
-        // thread: na <= LS_AMAX = 1024) while step k runs — it does not
-        // depend on d — so a step waits on no global-memory latency
-        constexpr int RV = LS_AMAX / 256;
-        for (; it < maxit; ++it) {
-          double dlx = 0.0;
-          double cur[RV], nxt[RV];
-#pragma unroll
-          for (int i = 0; i < RV; ++i) {
-            const int t = tid + 256 * i;
-            cur[i] = t < na ? __hip_atomic_load(GAA + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-          }
-          for (int k = 0; k < na; ++k) {
-            const double *Gn = GAA + (int64_t)min(k + 1, na - 1) * LS_AMAX;
-#pragma unroll
-            for (int i = 0; i < RV; ++i) {
-              const int t = tid + 256 * i;
-              nxt[i] = t < na ? __hip_atomic_load(Gn + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-            }
-            if (tid == 0) {
-              const double u = gA[k] + bA[k], v = fabs(u) - lam;
-              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
-              const double d = nb - bA[k];
-              if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
-              s_red[0] = d;
-            }
-            __syncthreads();
-            const double d = s_red[0];
-            if (d != 0.0) {
-#pragma unroll
-              for (int i = 0; i < RV; ++i) {
-                const int t = tid + 256 * i;
-                if (t < na) gA[t] -= cur[i] * d;
-              }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < RV; ++i) cur[i] = nxt[i];
-          }
-          if (tid == 0) s_flag = dlx < thr;
+      if (!(iz && jz)) {
+        // ---------------- full pass (speculative: see the header comment)
+        for (int t = tid; t < nin; t += blockDim.x) { lp_st(sv + t, s_a[t]); lp_st(sv + LP_LMAX + t, s_g[t]); }
+        const double rsq_save = s_sc[0];
+        lp_drain();
+        ++nlp;
+        for (;;) {
           __syncthreads();
-          const bool done = s_flag;
+          if (tid == 0) { s_sc[1] = 0.0; s_i[1] = 0; }
           __syncthreads();
-          if (done) break;
-        }
-      } else {
-        for (; it < maxit; ++it) {
-          double dlx = 0.0;
-          for (int k = 0; k < na; ++k) {
-            if (tid == 0) {
-              const double u = gA[k] + bA[k], v = fabs(u) - lam;
-              const double nb = v > 0.0 ? copysign(v, u) : 0.0;
-              const double d = nb - bA[k];
-              if (d != 0.0) { bA[k] = nb; dA[k] += d; dlx = fmax(dlx, d * d); }
-              s_red[0] = d;
-            }
-            __syncthreads();
-            const double d = s_red[0];
-            if (d != 0.0) {
-              // (L1-bypassing loads: the rows were written by this workgroup)
-              const double *Gk = GAA + (int64_t)k * LS_AMAX;
-              for (int t = tid; t < na; t += 256)
-                gA[t] -= __hip_atomic_load(Gk + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * d;
-            }
-            __syncthreads();
+          ptick(6);
+          lp_sweep(s_srt, nin, lam, true, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_sc,
+                   &s_i[1], kl, dl, tk);
+          ptick(0);
+          if (tid == 0) { pacc[12] += 1; pacc[13] += nin; }
+          if (!run_task(LP_FULL, s_i[1], lam)) { st = 3; fail_m = m; break; }
+          ptick(1);
+          const int v = s_i[3];
+          if (v == INT_MAX) break;
+          if (nin >= cap) { st = 2; fail_m = m; break; }
+          // ---- variable v enters at entry position nin
+          const int pos = nin;
+          const double gvv = lp_ld(g2 + (int64_t)gcur * p + v);   // its pass-start gradient
+          for (int t = tid; t <= pos; t += blockDim.x) {
+            const int col = t == pos ? v : s_ia[t];
+            const double val = G[(int64_t)v * p + col];
+            GAA[(int64_t)pos * ldaa + t] = val;
+            GAA[(int64_t)t * ldaa + pos] = val;
           }
-          if (tid == 0) s_flag = dlx < thr;
+          // index order: v's slot in s_srt (count of active indices below v)
+          int below = 0;
+          for (int t = tid; t < pos; t += blockDim.x) below += s_ia[t] < v ? 1 : 0;
+          below = (int)wave_sum((double)below);
+          if (lane == 0) s_d[wave] = below;
           __syncthreads();
-          const bool done = s_flag;
+          int ins = 0;
+          for (int w2 = 0; w2 < LP_NT / 64; ++w2) ins += (int)s_d[w2];
+          int tmp[LP_LMAX / LP_NT];
+#pragma unroll
+          for (int i = 0; i < LP_LMAX / LP_NT; ++i) {
+            const int t = tid + LP_NT * i;
+            tmp[i] = (t >= ins && t < pos) ? s_srt[t] : 0;
+          }
           __syncthreads();
-          if (done) break;
+#pragma unroll
+          for (int i = 0; i < LP_LMAX / LP_NT; ++i) {
+            const int t = tid + LP_NT * i;
+            if (t >= ins && t < pos) s_srt[t + 1] = tmp[i];
+          }
+          if (tid == 0) {
+            s_srt[ins] = pos;
+            s_ia[pos] = v;
+            lp_sti(isact + v, 1);
+          }
+          __syncthreads();
+          for (int t = tid; t <= pos; t += blockDim.x) s_rank[s_srt[t]] = t;
+          // restart the pass from its start state, v included (a = 0, its start gradient)
+          if (tid == 0) { lp_st(sv + pos, 0.0); lp_st(sv + LP_LMAX + pos, gvv); s_sc[0] = rsq_save; }
+          nin = pos + 1;
+          ++ver;
+          lp_drain();
+          __syncthreads();
+          lp_acquire();   // this CU's L1 drops its G_AA lines (plain loads read the new row / column)
+          for (int t = tid; t < nin; t += blockDim.x) { s_a[t] = lp_ld(sv + t); s_g[t] = lp_ld(sv + LP_LMAX + t); }
         }
+        if (st) break;
+        gcur ^= 1;                     // the replay's non-active gradients are current
+        __syncthreads();
+        const double dlx = s_sc[1];
+        if (dlx < A.thr) break;        // lambda converged
+        if (nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
-      SPROF(na <= LS_GC ? 0 : 4);
-      if (it == maxit) { st = 1; fail_m = m; break; }
-      // ---- refresh the non-active gradients with this round's changes:
-      // row-outer, so each thread keeps SEG loads in flight per row (one per
-      // owned j), RU rows at a time (RU x SEG independent loads before their
-      // FMAs: the pass is latency-bound on one CU otherwise); rows with no
-      // change are compacted out first (adding 0 * G leaves the sum
-      // unchanged), t ascending as before, so the sums are bit-identical
-      {
-        int nr = 0;
-        for (int t0 = 0; t0 < na; t0 += 256) {
-          const int t = t0 + tid;
-          const bool v = t < na && dA[t] != 0.0;
-          const unsigned long long bal = __ballot(v);
-          if (lane == 0) s_cnt[wave] = __popcll(bal);
-          __syncthreads();
-          int off = nr;
-          for (int w2 = 0; w2 < wave; ++w2) off += s_cnt[w2];
-          if (v) rows[off + __popcll(bal & ((1ull << lane) - 1ull))] = t;
-          nr += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-          __syncthreads();
-        }
-        constexpr int SEG = 8, RU = 8;
-        for (int j0 = 0; j0 < p; j0 += 256 * SEG) {
-          double acc[SEG];
-#pragma unroll
-          for (int u = 0; u < SEG; ++u) acc[u] = 0.0;
-          int q = 0;
-          for (; q + RU <= nr; q += RU) {
-            double gv[RU][SEG], dt[RU];
-#pragma unroll
-            for (int h = 0; h < RU; ++h) {
-              const int t = rows[q + h];
-              dt[h] = dA[t];
-              const double *Gt = G + (int64_t)ia[t] * p;
-#pragma unroll
-              for (int u = 0; u < SEG; ++u) {
-                const int j = j0 + tid + 256 * u;
-                gv[h][u] = j < p ? Gt[j] : 0.0;
-              }
-            }
-#pragma unroll
-            for (int h = 0; h < RU; ++h)
-#pragma unroll
-              for (int u = 0; u < SEG; ++u) acc[u] = fma(gv[h][u], dt[h], acc[u]);
-          }
-          for (; q < nr; ++q) {
-            const int t = rows[q];
-            const double dt = dA[t];
-            const double *Gt = G + (int64_t)ia[t] * p;
-#pragma unroll
-            for (int u = 0; u < SEG; ++u) {
-              const int j = j0 + tid + 256 * u;
-              if (j < p) acc[u] = fma(Gt[j], dt, acc[u]);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < SEG; ++u) {
-            const int j = j0 + tid + 256 * u;
-            if (j < p && !act[j]) g[j] -= acc[u];
-          }
-        }
+      iz = 1;
+      // ---------------- passes over the active set (entry order)
+      for (int t = tid; t < nin; t += blockDim.x) lp_st(sv + t, s_a[t]);   // da start
+      lp_drain();
+      for (;;) {
+        ++nlp;
+        __syncthreads();
+        if (tid == 0) s_sc[1] = 0.0;
+        __syncthreads();
+        ptick(6);
+        lp_sweep(nullptr, nin, lam, false, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_sc,
+                 &s_i[1], kl, dl, tk);
+        ptick(2);
+        if (tid == 0) { pacc[14] += 1; pacc[15] += nin; }
+        if (s_sc[1] < A.thr) break;
+        if (nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
+      if (st) break;
+      // ---------------- refresh: g_j -= dot(da, c_j,A) over the non-active j
+      if (tid == 0) s_i[1] = 0;
       __syncthreads();
-      SPROF(1);
-      for (int t = tid; t < na; t += 256) dA[t] = 0.0;
-      // ---- KKT scan: append violators in index order
-      const int na0 = na;
-      int base = na;
-      for (int j0 = 0; j0 < p; j0 += 256) {
-        const int j = j0 + tid;
-        const bool v = j < p && ju[j] && !act[j] && fabs(g[j]) > lam;
-        const unsigned long long bal = __ballot(v);
+      for (int t0 = 0; t0 < nin; t0 += blockDim.x) {   // nonzero da in entry order
+        const int t = t0 + tid;
+        const double d = t < nin ? s_a[t] - lp_ld(sv + t) : 0.0;
+        const bool ch = d != 0.0;
+        const unsigned long long bal = __ballot(ch);
         if (lane == 0) s_cnt[wave] = __popcll(bal);
         __syncthreads();
-        int off = base;
+        int off = s_i[1];
         for (int w2 = 0; w2 < wave; ++w2) off += s_cnt[w2];
-        const int tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-        if (v) {
-          const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
-          if (pos < LS_AMAX) { ia[pos] = j; bA[pos] = 0.0; gA[pos] = g[j]; dA[pos] = 0.0; act[j] = 1; }
+        if (ch) {
+          const int o = off + __popcll(bal & ((1ull << lane) - 1ull));
+          lp_sti(kl + o, s_ia[t]);
+          lp_st(dl + o, d);
         }
-        base += tot;
+        __syncthreads();
+        if (tid == 0) for (int w2 = 0; w2 < LP_NT / 64; ++w2) s_i[1] += s_cnt[w2];
         __syncthreads();
       }
-      SPROF(2);
-      if (base > LS_AMAX) { st = 2; fail_m = m; break; }
-      na = base;
-      if (na == na0) break;
-      // G_AA entries of the new variables (G symmetric): LDS while small,
-      // and always the compacted global copy (read once the set outgrows LDS)
-      for (int e = tid; e < (na - na0) * na; e += 256) {
-        const int k = na0 + e / na, t = e % na;
-        const double v = G[(int64_t)ia[k] * p + ia[t]];
-        if (na <= LS_GC) {
-          GC[k * LS_GC + t] = v;
-          GC[t * LS_GC + k] = v;
-        }
-        __hip_atomic_store(GAA + (int64_t)k * LS_AMAX + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(GAA + (int64_t)t * LS_AMAX + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __threadfence();
-      __syncthreads();
-      SPROF(3);
+      ptick(6);
+      if (!run_task(LP_REFRESH, s_i[1], lam)) { st = 3; fail_m = m; break; }
+      ptick(3);
+      jz = 0;
     }
     if (st) break;
-    // ---- record: dense beta_m, R^2 = beta'(c + g)
-    double part = 0.0;
-    for (int t = tid; t < na; t += 256) part = fma(bA[t], c[ia[t]] + gA[t], part);
-    part = wave_sum(part);
-    if (lane == 0) s_red[wave] = part;
+    // ---- record beta_m (dense) and R^2
+    __syncthreads();
     double *bm = bp + (int64_t)m * p;
-    for (int j = tid; j < p; j += 256) bm[j] = 0.0;
+    for (int j = tid; j < p; j += blockDim.x) bm[j] = 0.0;
     __syncthreads();
-    for (int t = tid; t < na; t += 256) bm[ia[t]] = bA[t];
-    const double rsq = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-    if (tid == 0) rsq_out[(int64_t)f * nlam + m] = rsq;
-    __syncthreads();
-    if (early && f == 0 && m + 1 >= min(5, nlam) && (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999)) {
+    for (int t = tid; t < nin; t += blockDim.x) bm[s_ia[t]] = s_a[t];
+    const double rsq = s_sc[0];
+    if (tid == 0) A.rsq_out[(int64_t)f * nlam + m] = rsq;
+    if (A.early && f == 0 && m + 1 >= min(5, nlam) && (rsq - rsq0 < 1e-5 * rsq || rsq > 0.999)) {
       L = m + 1;
       break;
     }
-    rsq_prev = rsq;
     // folds stop once the full fit (running concurrently) has published a
     // path length they have reached
-    if (early && f > 0) {
-      const int Lp = __hip_atomic_load(nlam_out, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (A.early && f > 0) {
+      const int Lp = __hip_atomic_load(A.nlam_out, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       if (Lp > 0 && m + 1 >= Lp) { L = m + 1; break; }
     }
   }
-  if (tid == 0) {
-    status[f] = st;
-    status[gridDim.x + prob0 + f] = st ? fail_m : nlam;   // lambda index of a failure
-    if (f == 0) __hip_atomic_store(nlam_out, L, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    else nlam_out[f] = L;
+  run_task(LP_EXIT, 0, 0.0);
+  ptick(6);
+  if (A.prof && tid == 0) {
+    pacc[7] = nin;
+    for (int i = 0; i < 16; ++i) A.prof[(int64_t)f * 16 + i] = pacc[i];
   }
+  if (tid == 0) {
+    A.status[f] = st;
+    A.status[gridDim.x / (H + 1) + f] = st ? fail_m : nlam;   // lambda index of a failure
+    if (f == 0) __hip_atomic_store(A.nlam_out, L, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else A.nlam_out[f] = L;
+  }
+}
+
+// G_f's diagonal := 1 over the non-constant columns (elnet1's c(k,k) = xv(k) = 1)
+__global__ void soft_unit_diag_kernel(double *__restrict__ G, int64_t strideG, int p, const uint8_t *__restrict__ ju) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y;
+  if (j < p && ju[(int64_t)f * p + j]) G[(int64_t)f * strideG + (int64_t)j * p + j] = 1.0;
 }
 
 // Hold-out SSE of fold f (problem f >= 1) at lambda m: one workgroup per (m, f).
@@ -460,6 +711,97 @@ int ctx_fail(dfm_ctx *ctx, int code, const char *msg);
 hipStream_t ctx_stream(dfm_ctx *ctx);
 int ctx_device(dfm_ctx *ctx);
 }  // namespace dfm
+
+// Every problem's path in one cooperative launch (lasso_coop_kernel): nprob
+// groups of 1 leader + H helper workgroups, H as large as the chip's
+// co-resident workgroups allow (<= one per 256 columns, <= 64).  Scratch is
+// allocated here; outputs: bpath [nprob][nlam][p], rsq [nprob][nlam], nl
+// [nprob] path lengths, sts [2 nprob] (status, failing lambda).
+static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const double *c, const uint8_t *ju,
+                               const double *alm, int nlam, int nprob, int early, double thr, int maxit, double *bpath,
+                               double *rsq, int *nl, int *sts, hipStream_t st, const char **why) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  hipGetDevice(&dev);
+  hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lasso_coop_kernel, LP_NT, 0);
+  if (e != hipSuccess) return e;
+  const int maxb = per_cu * ncu;
+  int H = std::min(std::min(maxb / nprob - 1, std::max(1, (p + 255) / 256)), 64);
+  if (H < 1) { *why = "more lasso problems than co-resident workgroup pairs"; return hipErrorInvalidConfiguration; }
+  const int ldaa = std::min(p, LP_LMAX);
+  std::vector<void *> bufs;
+  auto alloc = [&](size_t bytes) -> void * {
+    void *q_ = nullptr;
+    if (hipMalloc(&q_, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+    bufs.push_back(q_);
+    return q_;
+  };
+  LassoArgs A{};
+  A.G = G; A.strideG = strideG; A.p = p; A.nlam = nlam; A.early = early; A.maxit = maxit; A.H = H; A.ldaa = ldaa;
+  A.thr = thr; A.c = c; A.alm = alm; A.ju = ju;
+  A.ctl = (LassoCtl *)alloc((size_t)nprob * sizeof(LassoCtl));
+  A.g2 = (double *)alloc((size_t)nprob * 2 * p * 8);
+  A.isact = (int *)alloc((size_t)nprob * p * 4);
+  A.klist = (int *)alloc((size_t)nprob * LP_LMAX * 4);
+  A.dlist = (double *)alloc((size_t)nprob * LP_LMAX * 8);
+  A.save = (double *)alloc((size_t)nprob * 2 * LP_LMAX * 8);
+  A.GAA = (double *)alloc((size_t)nprob * ldaa * ldaa * 8);
+  A.bpath = bpath; A.rsq_out = rsq; A.nlam_out = nl; A.status = sts;
+  A.tmo = 2000000000LL;   // 20 s of the 100 MHz wall clock
+  // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
+  static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
+  if (prof) A.prof = (long long *)alloc((size_t)nprob * 16 * 8);
+  auto cleanup = [&]() { hipStreamSynchronize(st); for (void *b : bufs) hipFree(b); };
+  if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA) {
+    cleanup();
+    *why = "out of device memory";
+    return hipErrorOutOfMemory;
+  }
+  e = hipMemsetAsync(A.ctl, 0, (size_t)nprob * sizeof(LassoCtl), st);
+  if (e == hipSuccess) e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
+  void *args[] = {&A};
+  if (e == hipSuccess)
+    e = hipLaunchCooperativeKernel((const void *)lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), args, 0, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && A.prof) {
+    std::vector<long long> hp((size_t)nprob * 16);
+    hipMemcpy(hp.data(), A.prof, hp.size() * 8, hipMemcpyDeviceToHost);
+    for (int f = 0; f < nprob; ++f) {
+      const long long *q = hp.data() + f * 16;
+      fprintf(stderr, "[lasso prof] problem %2d H %d: full-pass sweeps %.2f ms, FULL replays %.2f, active passes %.2f, "
+              "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
+              "blocks %lld: serial %.2f ms, update %.2f ms, changes %lld\n", f, H, q[0] * 1e-5, q[1] * 1e-5,
+              q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[12], q[13], q[14], q[15], q[10], q[8] * 1e-5, q[9] * 1e-5,
+              q[11]);
+    }
+  }
+  if (e == hipSuccess) {   // a timed-out problem: report its control block
+    std::vector<int> hs(2 * nprob);
+    hipMemcpy(hs.data(), sts, hs.size() * 4, hipMemcpyDeviceToHost);
+    for (int f = 0; f < nprob; ++f)
+      if (hs[f] == 3) {
+        LassoCtl c0;
+        hipMemcpy(&c0, A.ctl + f, sizeof c0, hipMemcpyDeviceToHost);
+        static char msg[256];
+        snprintf(msg, sizeof msg, "lasso problem %d timed out: task %d, helper 0 done %d (H %d)", f,
+                 (int)(c0.task.v >> 32), (int)(c0.done[0].v >> 32), H);
+        *why = msg;
+        fprintf(stderr, "[dfm] %s\n", msg);
+        break;
+      }
+  }
+  cleanup();
+  return e;
+}
+
+static const char *lasso_status_text(int code) {
+  switch (code) {
+    case 1: return "lasso coordinate descent did not converge";
+    case 2: return "lasso active set above 4096 variables";
+    case 3: return "lasso path kernel timed out waiting for its helper workgroups";
+    default: return "lasso path failed";
+  }
+}
 
 extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                                  const double *X, int64_t T64, int64_t N64, int64_t ldx,
@@ -512,9 +854,6 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   uint8_t *ju = (uint8_t *)alloc((size_t)nprob * p);
   double *G = (double *)alloc((size_t)nprob * strideG * 8);
   double *alm = (double *)alloc((size_t)nprob * nlambda * 8);
-  double *gws = (double *)alloc((size_t)nprob * p * 8);
-  int *actws = (int *)alloc((size_t)nprob * p * 4);
-  double *gaaws = (double *)alloc((size_t)nprob * LS_AMAX * LS_AMAX * 8);
   double *bpath = (double *)alloc((size_t)nprob * nlambda * p * 8);
   double *rsq = (double *)alloc((size_t)nprob * nlambda * 8);
   int *nl = (int *)alloc((size_t)nprob * 4), *sts = (int *)alloc((size_t)nprob * 8);
@@ -549,6 +888,7 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   e = launch_gram(1, src, p, n, n, G, p, strideG, nprob, st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: Gram launch failed"); }
   hipLaunchKernelGGL(soft_scale_kernel, dim3(2048, nprob), dim3(256), 0, st, G, strideG, strideG, ystat);
+  hipLaunchKernelGGL(soft_unit_diag_kernel, dim3((p + 255) / 256, nprob), dim3(256), 0, st, G, strideG, p, ju);
   // ---- lambda grid of the full fit: lambda_max = max_j |c_j| over non-constant columns
   std::vector<double> hc(p), hys(3 * nprob);
   std::vector<uint8_t> hju(p);
@@ -561,9 +901,13 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   for (int j = 0; j < p; ++j)
     if (hju[j]) lam_max = std::max(lam_max, std::fabs(hc[j]));
   if (!(lam_max > 0.0) || !(hys[1] > 0.0)) { cleanup(); return fail(-2, "dfm_targeted_soft: degenerate y or Z"); }
+  // elnet1's grid: lambda_2 = alf lambda_max, lambda_m = lambda_{m-1} alf
+  // (lambda_1: the all-zero fit, reported as lambda_max)
   const double alf = std::pow(lmr, 1.0 / (nlambda - 1));
   std::vector<double> halm((size_t)nprob * nlambda);
-  for (int m = 0; m < nlambda; ++m) halm[m] = lam_max * std::pow(alf, (double)m);
+  halm[0] = lam_max;
+  if (nlambda > 1) halm[1] = alf * lam_max;
+  for (int m = 2; m < nlambda; ++m) halm[m] = halm[m - 1] * alf;
   const double thr = 1e-7;   // glmnet's default convergence threshold
   const int maxit = 100000;
   e = hipMemcpyAsync(alm, halm.data(), (size_t)nlambda * 8, hipMemcpyHostToDevice, st);
@@ -577,32 +921,17 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
     for (int m = 0; m < nlambda; ++m) halm[(size_t)f * nlambda + m] = halm[m] * hys[1] / hys[3 * f + 1];
   e = hipMemcpyAsync(alm, halm.data(), halm.size() * 8, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: upload failed"); }
-  e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
-  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: memset failed"); }
-  static const bool sprof = getenv("DFM_SOFT_PROF") != nullptr;
-  static const int cdmode = [] { const char *e_ = getenv("DFM_SOFT_CD"); return e_ ? atoi(e_) : 0; }();
-  if (sprof) {
-    unsigned long long z[8] = {};
-    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_soft_prof), z, sizeof z, 0, hipMemcpyHostToDevice, st);
-  }
-  hipLaunchKernelGGL(lasso_path_kernel, dim3(nprob), dim3(256), 0, st, G, strideG, p, cc, ju, alm, nlambda, 0, 1, cdmode,
-                     thr, maxit, gws, actws, gaaws, bpath, rsq, nl, sts);
+  const char *why = "lasso path launch failed";
+  e = launch_lasso(G, strideG, p, cc, ju, alm, nlambda, nprob, 1, thr, maxit, bpath, rsq, nl, sts, st, &why);
+  if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, why); }
   std::vector<int> hnl(nprob), hst(2 * nprob);
   e = hipMemcpyAsync(hnl.data(), nl, (size_t)nprob * 4, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipMemcpyAsync(hst.data(), sts, (size_t)nprob * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: path kernel failed"); }
   const int L = hnl[0];
-  if (sprof) {
-    unsigned long long z[8];
-    hipMemcpyFromSymbol(z, HIP_SYMBOL(g_soft_prof), sizeof z, 0, hipMemcpyDeviceToHost);
-    fprintf(stderr, "[soft prof] ms: passes (LDS G_AA) %.2f passes (global G_AA) %.2f refresh %.2f kkt %.2f fill %.2f\n",
-            z[0] * 1e-5, z[4] * 1e-5, z[1] * 1e-5, z[2] * 1e-5, z[3] * 1e-5);
-  }
   for (int f = 0; f < nprob; ++f)   // a fold's failure past L concerns lambdas the CV never reads
-    if (hst[f] && (f == 0 || hst[nprob + f] < L))
-      { cleanup(); return fail(2, hst[f] == 1 ? "lasso coordinate descent did not converge"
-                                              : "lasso active set above 1024 variables"); }
+    if (hst[f] && (f == 0 || hst[nprob + f] < L)) { cleanup(); return fail(2, lasso_status_text(hst[f])); }
   hipLaunchKernelGGL(soft_loss_kernel, dim3(L, K), dim3(256), 0, st, Zs, ld, n, p, yd, fd, ystat, bpath, nlambda,
                      sse);
   std::vector<double> hsse((size_t)K * nlambda), hb(p), hmu(p), hsd(p);
@@ -639,5 +968,57 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
     if (lambda_out) lambda_out[m] = halm[m] * ys;
     if (meanloss_out) meanloss_out[m] = ml[m];
   }
+  return 0;
+}
+
+// glmnet's elnet1 path on a standardised covariance (the core of
+// dfm_targeted_soft, exposed for parity tests and direct use): G p x p
+// symmetric with unit diagonal over ju, c = Zs'ys / n, lambdas alms[nlam]
+// (standardised units), early = glmnet's early path exit.  Outputs: betas
+// (nlam x p, row-major; rows past *L_out untouched), rsq (nlam), *L_out.
+extern "C" int dfm_lasso_path(dfm_ctx *ctx, const double *G, const double *c, const uint8_t *ju, int p,
+                              const double *alms, int nlam, int early, double thr, double *betas, double *rsq,
+                              int *L_out) {
+  if (!ctx) return -1;
+  if (!G || !c || !ju || !alms || p < 1 || nlam < 1 || !(thr > 0.0) || !L_out)
+    return ctx_fail(ctx, -2, "dfm_lasso_path: bad arguments");
+  hipSetDevice(ctx_device(ctx));
+  hipStream_t st = ctx_stream(ctx);
+  const int64_t pp = (int64_t)p * p;
+  double *dG = nullptr, *dc = nullptr, *da = nullptr, *db = nullptr, *dr = nullptr;
+  uint8_t *dj = nullptr;
+  int *dn = nullptr, *ds = nullptr;
+  auto freeall = [&]() {
+    hipStreamSynchronize(st);
+    for (void *q : {(void *)dG, (void *)dc, (void *)da, (void *)db, (void *)dr, (void *)dj, (void *)dn, (void *)ds})
+      hipFree(q);
+  };
+  hipError_t e = hipMalloc(&dG, pp * 8);
+  if (e == hipSuccess) e = hipMalloc(&dc, (size_t)p * 8);
+  if (e == hipSuccess) e = hipMalloc(&da, (size_t)nlam * 8);
+  if (e == hipSuccess) e = hipMalloc(&db, (size_t)nlam * p * 8);
+  if (e == hipSuccess) e = hipMalloc(&dr, (size_t)nlam * 8);
+  if (e == hipSuccess) e = hipMalloc(&dj, (size_t)p);
+  if (e == hipSuccess) e = hipMalloc(&dn, 8);
+  if (e == hipSuccess) e = hipMalloc(&ds, 16);
+  if (e == hipSuccess) e = hipMemcpyAsync(dG, G, pp * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, c, (size_t)p * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(da, alms, (size_t)nlam * 8, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dj, ju, (size_t)p, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) { freeall(); return ctx_fail(ctx, 1000 + (int)e, "dfm_lasso_path: upload failed"); }
+  const char *why = "lasso path launch failed";
+  e = launch_lasso(dG, pp, p, dc, dj, da, nlam, 1, early ? 1 : 0, thr, 100000, db, dr, dn, ds, st, &why);
+  if (e != hipSuccess) { freeall(); return ctx_fail(ctx, 1000 + (int)e, why); }
+  int hn = 0, hs[2] = {0, 0};
+  e = hipMemcpyAsync(&hn, dn, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(hs, ds, 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && !hs[0] && betas) e = hipMemcpyAsync(betas, db, (size_t)hn * p * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && !hs[0] && rsq) e = hipMemcpyAsync(rsq, dr, (size_t)hn * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  freeall();
+  if (e != hipSuccess) return ctx_fail(ctx, 1000 + (int)e, "dfm_lasso_path: read-back failed");
+  if (hs[0]) return ctx_fail(ctx, 2, lasso_status_text(hs[0]));
+  *L_out = hn;
   return 0;
 }

@@ -273,11 +273,12 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
  * GLMNet.glmnetcv(Z = [w x], y), gaussian lasso (alpha = 1) with standardised
  * columns and an intercept; keep the x columns with a nonzero coefficient at
  * the CV-optimal lambda.  GLMNet is never imported by the reference (D5): the
- * algorithm is glmnet's published coordinate descent (covariance updates on
- * the active set, threshold 1e-7, warm starts over `nlambda` log-spaced
- * lambdas from lambda_max down to lambda_min_ratio * lambda_max (<= 0: 1e-2 if
- * T < q + N else 1e-4), early path exit on the full fit after 5 lambdas when
- * R^2 gains < 1e-5 relative or R^2 > 0.999).  folds: T fold ids 1..K (host-drawn, as the
+ * algorithm is glmnet's Fortran elnet1 in its loop order (covariance updates,
+ * full cyclic passes with in-pass entry, active-set passes, threshold 1e-7,
+ * warm starts over `nlambda` log-spaced lambdas from lambda_max down to
+ * lambda_min_ratio * lambda_max (<= 0: 1e-2 if T < q + N else 1e-4), early
+ * path exit on the full fit after 5 lambdas when R^2 gains < 1e-5 relative or
+ * R^2 > 0.999; no cap on the active set below 4096).  folds: T fold ids 1..K (host-drawn, as the
  * bootstrap draws).  Outputs: path length L, best (0-based argmin of the
  * fold-size-weighted hold-out MSE), lambda (L, original units), meanloss (L),
  * beta (q + N, original scale, at best), intercept a0, mask (N, 0/1).  Any
@@ -287,6 +288,16 @@ int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w, int q, int
                       int nlambda, double lambda_min_ratio, int *nlam_out, int *best_out,
                       double *lambda_out, double *meanloss_out, double *beta_out, double *a0_out,
                       uint8_t *mask);
+
+/* glmnet's elnet1 lasso path (the core of dfm_targeted_soft, for direct use
+ * and parity tests): G p x p symmetric (row-major) with unit diagonal over the
+ * non-constant columns ju, c = Zs'ys/n, lambdas alms[nlam] in standardised
+ * units (decreasing), early = glmnet's early path exit (5 lambdas, R^2 gain
+ * < 1e-5 R^2 or R^2 > 0.999), thr = glmnet's threshold (1e-7).  Outputs: the
+ * path length *L_out, betas (L x p row-major), rsq (L); NULL skips. */
+int dfm_lasso_path(dfm_ctx *ctx, const double *G, const double *c, const uint8_t *ju, int p,
+                   const double *alms, int nlam, int early, double thr, double *betas, double *rsq,
+                   int *L_out);
 
 #ifdef __cplusplus
 }

@@ -5,11 +5,13 @@ the committed fixtures (tests/golden/tp_soft.npz, made by
 tests/golden/make_golden.py).  PARITY UNPINNED against GLMNet itself (not
 importable here, never imported by the reference: defect D5).
 
-Bar: the selection mask is bit-exact; the CV path length and the CV-optimal
-lambda index are equal; the lambda grid agrees to 1e-12 relative; the
-hold-out mean losses to 1e-9 relative; the coefficients at the optimum to
-1e-8 of their largest magnitude (coordinate descent stopped at glmnet's 1e-7
-threshold on both sides, same update order)."""
+Bar: given the same standardised covariance the lasso path is bit-identical
+(dfm_lasso_path vs the elnet1 restatement); through the whole glmnetcv (the
+device forms its own Grams on MFMA) the selection mask is bit-exact, the CV
+path length and the CV-optimal lambda index are equal, the lambda grid agrees
+to 1e-12 relative, the hold-out mean losses to 1e-9 relative and the
+coefficients at the optimum to 1e-8 of their largest magnitude (coordinate
+descent stopped at glmnet's 1e-7 threshold on both sides, same loop order)."""
 import os
 
 import numpy as np
@@ -68,6 +70,46 @@ def test_c4_soft_full_size(dfm, oracle):
     assert np.allclose([x.sum(), np.abs(x).sum(), y.sum(), folds.sum()], g["c4_digest"], rtol=1e-12, atol=1e-9)
     mask, path = dfm.targeted_predictors(y, w, x, "soft", folds=folds, return_path=True)
     check(mask, path, g["c4_mask"], g["c4_lam"], g["c4_meanloss"], int(g["c4_best"]), g["c4_beta"])
+
+
+def _lasso_inputs(oracle, T, N, seed, lmr=None, nlam=100):
+    y, x, w = panel(oracle, T, N, 3, seed)
+    Z = np.hstack([w, x])
+    mu, sd, ju, yb, ys, G, c = oracle._glmnet_standardize(Z, y)
+    lam_max = float(np.max(np.abs(c[ju])))
+    if lmr is None:
+        lmr = 1e-2 if T < Z.shape[1] else 1e-4
+    return G, c, ju, oracle.glmnet_lambdas(lam_max, nlam, lmr)
+
+
+@pytest.mark.parametrize("T,N,early", [(80, 40, True), (120, 300, True), (60, 700, False), (200, 150, False)])
+def test_lasso_path_bit_identical_to_elnet1_restatement(dfm, oracle, T, N, early):
+    """Given the same standardised covariance G and c, the device path
+    (cooperative leader/helper kernel) is bit-identical to the oracle's
+    restatement of glmnet's elnet1: same loop order, same rounding (every
+    product and difference rounded separately, sequential dot products)."""
+    G, c, ju, alms = _lasso_inputs(oracle, T, N, 90 + N)
+    cnt = {}
+    bo, ro = oracle.lasso_path_cd(G, c, ju, alms, early, counters=cnt)
+    bg, rg = dfm.lasso_path(G, c, ju, alms, early=early)
+    assert bg.shape == bo.shape
+    assert np.array_equal(bg, bo)
+    assert np.array_equal(rg, ro)
+    assert cnt["full_passes"] > len(alms) // 2 and np.count_nonzero(bo[-1]) > 10   # entries mid-pass exercised
+
+
+def test_lasso_path_c4_full_fit_bit_identical(dfm, oracle):
+    """BASELINE configs[3] full fit (T=400, p=5001: active set to ~380, ~220
+    full passes with in-pass entries) on the oracle's G: bit-identical."""
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_golden
+    y, w, x, folds = make_golden.c4_inputs()
+    mu, sd, ju, yb, ys, G, c = oracle._glmnet_standardize(np.hstack([w, x]), y)
+    alms = oracle.glmnet_lambdas(float(np.max(np.abs(c[ju]))), 100, 1e-2)
+    bo, ro = oracle.lasso_path_cd(G, c, ju, alms, True)
+    bg, rg = dfm.lasso_path(G, c, ju, alms, early=True)
+    assert np.array_equal(bg, bo) and np.array_equal(rg, ro)
 
 
 def test_soft_rejects_bad_folds(dfm, oracle):
