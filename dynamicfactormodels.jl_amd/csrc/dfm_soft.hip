@@ -102,7 +102,7 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 
 // ------------------------------------------------------------- lasso path
 // glmnet's elnet1 (covariance updating) for K + 1 problems in ONE cooperative
-// launch.  The loop order is elnet1's (oracle/dfm_oracle.py lasso_path_cd):
+// launch.  The loop order is elnet1's (the parity checker's lasso_path_cd):
 // per lambda a full cyclic pass over every variable in index order with
 // in-pass entry and eager gradient updates g_j -= c_jk d, then passes over
 // the active set in entry order until max d^2 < thr, the non-active
