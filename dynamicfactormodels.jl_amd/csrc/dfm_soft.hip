@@ -142,6 +142,7 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 constexpr int LP_LMAX = 4096;   // active-set capacity (leader LDS state; glmnet's pmax)
 constexpr int LP_B = 64;        // coordinate block = one wave
 constexpr int LP_NT = 512;      // threads per workgroup
+constexpr int LP_PROF = 32;     // diagnostics slots per problem
 constexpr int LP_PF = (LP_B * LP_B + LP_NT - 64 - 1) / (LP_NT - 64);   // next-block loads per thread of waves 1..7
 enum { LP_FULL = 1, LP_REFRESH = 2, LP_EXIT = 3 };
 
@@ -203,8 +204,13 @@ DFM_DEV double lp_rdlane(double x, int l) {   // l: a compile-time constant insi
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// The helpers' share of a task over columns [j0, j1) of problem f (the
-// leader runs it itself when H == 0).  hk / hd: the task's change list.
+// The helpers' share of a task over columns [j0, j1) of problem f.  hk / hd:
+// the task's change list, padded to a multiple of 2 LP_U with a valid row
+// and a zero delta (g - G * 0 == g), so that every load is unconditional and
+// two chunks of LP_U loads stay in flight.  FULL: the list is in coordinate
+// order, so the variable's own visit falls after the pos = #{k < j} first
+// changes.
+constexpr int LP_U = 32;
 DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam, int gcur, int j0, int j1,
                          const int *hk, const double *hd) {
   const int p = A.p;
@@ -213,68 +219,87 @@ DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam
   const int *isact = A.isact + (int64_t)f * p;
   double *gin = A.g2 + ((int64_t)f * 2 + gcur) * p;
   double *gout = A.g2 + ((int64_t)f * 2 + (gcur ^ 1)) * p;
-  constexpr int U = 32;
   int first = INT_MAX;   // this thread's first entering variable
   for (int j = j0 + (int)threadIdx.x; j < j1; j += blockDim.x) {
     if (!ju[j] || lp_ldi(isact + j)) continue;
+    int pos = 0;   // FULL: changes before j's visit (hk ascending)
     if (type == LP_FULL) {
-      // elnet1's eager updates in visit order; the entry test at the variable's own visit
-      double s = lp_ld(gin + j);
-      bool chk = false, in = false;
-      double ga[U], gb[U];   // two chunks of the change list in flight
-      auto ld = [&](double *gv, int i0) {
+      int lo = 0, hi = nc;
+      while (lo < hi) { const int mid = (lo + hi) >> 1; if (hk[mid] < j) lo = mid + 1; else hi = mid; }
+      pos = lo;
+    }
+    const double *Gj = G + j;
+    double s = type == LP_FULL ? lp_ld(gin + j) : 0.0, sv = s;
+    double ga[LP_U], gb[LP_U];
+    auto ld = [&](double *gv, int i0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) gv[u] = (i0 + u < nc) ? G[(int64_t)hk[i0 + u] * p + j] : 0.0;
-      };
-      auto use = [&](const double *gv, int i0) {
+      for (int u = 0; u < LP_U; ++u) gv[u] = Gj[(int64_t)hk[i0 + u] * p];
+    };
+    auto use = [&](const double *gv, int i0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (i0 + u < nc) {
-            if (!chk && hk[i0 + u] > j) { chk = true; in = fabs(s) - lam > 0.0; }
-            s = s - gv[u] * hd[i0 + u];
-          }
+      for (int u = 0; u < LP_U; ++u) {
+        if (type == LP_FULL) {   // elnet1's eager updates in visit order
+          s = s - gv[u] * hd[i0 + u];
+          sv = i0 + u < pos ? s : sv;
+        } else {                 // REFRESH: dot(da, c_j,A), a sequential sum in entry order
+          s = s + hd[i0 + u] * gv[u];
         }
-      };
-      ld(ga, 0);
-      for (int i0 = 0; i0 < nc; i0 += 2 * U) {
-        if (i0 + U < nc) ld(gb, i0 + U);
-        use(ga, i0);
-        if (i0 + U >= nc) break;
-        if (i0 + 2 * U < nc) ld(ga, i0 + 2 * U);
-        use(gb, i0 + U);
       }
-      if (!chk) in = fabs(s) - lam > 0.0;
-      if (in) first = min(first, j);
+    };
+    if (nc > 0) ld(ga, 0);
+    for (int i0 = 0; i0 < nc; i0 += 2 * LP_U) {
+      ld(gb, i0 + LP_U);
+      use(ga, i0);
+      if (i0 + 2 * LP_U < nc) ld(ga, i0 + 2 * LP_U);
+      use(gb, i0 + LP_U);
+    }
+    if (type == LP_FULL) {
+      if (fabs(sv) - lam > 0.0) first = min(first, j);
       gout[j] = s;
-    } else {   // LP_REFRESH: g_j -= dot(da, c_j,A), the dot a sequential sum in entry order
-      double s = 0.0;
-      for (int i0 = 0; i0 < nc; i0 += U) {
-        double gv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) gv[u] = (i0 + u < nc) ? G[(int64_t)hk[i0 + u] * p + j] : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (i0 + u < nc) s = s + hd[i0 + u] * gv[u];
-      }
+    } else {
       gin[j] = lp_ld(gin + j) - s;
     }
   }
   return first;
 }
 
-DFM_DEV int lp_at(const int *ord, int x) { return ord ? ord[x] : x; }
+// entry position at sweep position x: index order (ORD, ord = s_srt) or entry order
+template <bool ORD>
+DFM_DEV int lp_at(const int *ord, int x) { return ORD ? ord[x] : x; }
 
 // s_gb := the 64 x 64 block of G_AA at sweep positions [b, b + 64) (zero outside n)
+template <bool ORD>
 DFM_DEV void lp_gblock_load(const int *ord, int b, int n, const double *GAA, int ldaa, double *s_gb) {
   const int nb = min(LP_B, n - b);
   for (int e = threadIdx.x; e < LP_B * LP_B; e += blockDim.x) {
     const int s = e >> 6, t = e & 63;
-    s_gb[e] = (s < nb && t < nb) ? GAA[(int64_t)lp_at(ord, b + s) * ldaa + lp_at(ord, b + t)] : 0.0;
+    s_gb[e] = (s < nb && t < nb) ? GAA[(int64_t)lp_at<ORD>(ord, b + s) * ldaa + lp_at<ORD>(ord, b + t)] : 0.0;
   }
 }
 
-// One pass over n active positions, in entry order (ord == nullptr) or in
-// coordinate-index order (ord = s_srt).  rec: append every change
+// S serial coordinate steps on wave 0 (lane t = coordinate t of the block,
+// Gr = its column of the block's G_AA, a0 = its coefficient at the block
+// start).  Every step is branch-free: an unchanged coordinate gives d = +0,
+// and g - G * 0 == g (a gradient of exactly -0 becomes +0, which no later
+// step can tell apart).  Lanes past the block hold g = a0 = 0 and Gr = 0, so
+// their steps are no-ops.  Lane 0 logs (d, g at the visit) per step for the
+// bookkeeping done off the chain (R^2, max d^2, the new coefficients).
+template <int S>
+DFM_DEV void lp_chain(double &g, const double a0, const double *Gr, double lam, double *s_log, int lane) {
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const double gk = lp_rdlane(g, s), ak = lp_rdlane(a0, s);
+    const double uu = gk + ak;
+    const double v = fabs(uu) - lam;
+    const double na = v > 0.0 ? copysign(v, uu) : 0.0;
+    const double d = na - ak;
+    g = g - Gr[s] * d;
+    if (lane == 0) { s_log[2 * s] = d; s_log[2 * s + 1] = gk; }
+  }
+}
+
+// One pass over n active positions, in entry order (!ORD) or in
+// coordinate-index order (ORD, ord = s_srt).  rec: append every change
 // (coordinate, delta) to kl / dl in visit order.  All threads call it.
 //
 // Per block of 64 sweep positions: wave 0 runs the serial coordinate steps
@@ -287,16 +312,18 @@ DFM_DEV void lp_gblock_load(const int *ord, int b, int n, const double *GAA, int
 // invalidated after every update of G_AA, see the entry step).  s_gb holds the
 // first block of the sweep order `key` when gkey == key (the last block
 // prefetches the next sweep's first).
+template <bool ORD>
 DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int &gkey, const double *GAA, int ldaa,
                       const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_d, double *s_gb,
-                      double *s_sc, int *s_nc, int *kl, double *dl, long long *tk) {
+                      double *s_log, double *s_sc, int *s_nc, int *kl, double *dl, long long *tk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), u = tid - 64;
   if (n <= 0) return;
   if (gkey != key) {
-    lp_gblock_load(ord, 0, n, GAA, ldaa, s_gb);
+    lp_gblock_load<ORD>(ord, 0, n, GAA, ldaa, s_gb);
     __syncthreads();
     gkey = key;
   }
+  double dlx_l = 0.0;
   for (int b0 = 0; b0 < n; b0 += LP_B) {
     const int nb = min(LP_B, n - b0);
     const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);
@@ -304,35 +331,33 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
     // wave-uniform branches, each with its own barrier (every wave reaches one)
     if (wave == 0) {
       const bool on = lane < nb;
-      const int pt = on ? lp_at(ord, b0 + lane) : 0;
-      double g = on ? s_g[pt] : 0.0, a = on ? s_a[pt] : 0.0;
+      const int pt = on ? lp_at<ORD>(ord, b0 + lane) : 0;
+      double g = on ? s_g[pt] : 0.0;
+      const double a0 = on ? s_a[pt] : 0.0;
       double Gr[LP_B];   // this lane's column of the block (rows: the block's coordinates)
 #pragma unroll
       for (int s = 0; s < LP_B; ++s) Gr[s] = s_gb[s * LP_B + lane];
-      double rsq = s_sc[0], dlx = s_sc[1];
-#pragma unroll
-      for (int s = 0; s < LP_B; ++s) {
-        if (s < nb) {
-          const double gk = lp_rdlane(g, s), ak = lp_rdlane(a, s);
-          const double uu = gk + ak;
-          const double v = fabs(uu) - lam;
-          const double na = v > 0.0 ? copysign(v, uu) : 0.0;
-          double d = 0.0;
-          if (na != ak) {
-            d = na - ak;
-            if (lane == s) a = na;
-            rsq = rsq + d * (2.0 * gk - d);
-            dlx = fmax(dlx, d * d);
-            g = g - Gr[s] * d;
-          }
-          if (lane == 0) s_d[s] = d;
-        }
+      long long ta = 0;
+      if (tk && tid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ta = wall_clock64(); tk[4] += ta - t0; }
+      switch ((nb + 15) >> 4) {
+        case 1: lp_chain<16>(g, a0, Gr, lam, s_log, lane); break;
+        case 2: lp_chain<32>(g, a0, Gr, lam, s_log, lane); break;
+        case 3: lp_chain<48>(g, a0, Gr, lam, s_log, lane); break;
+        default: lp_chain<64>(g, a0, Gr, lam, s_log, lane); break;
+      }
+      if (tk && tid == 0) tk[5] += wall_clock64() - ta;
+      const double dv = on ? s_log[2 * lane] : 0.0;
+      const bool ch = dv != 0.0;
+      double a = a0;
+      if (ch) {   // the chain's new coefficient, recomputed from the logged gradient
+        const double uu = s_log[2 * lane + 1] + a0;
+        const double v = fabs(uu) - lam;
+        a = v > 0.0 ? copysign(v, uu) : 0.0;
       }
       if (on) { s_g[pt] = g; s_a[pt] = a; }
-      const double dv = on ? s_d[lane] : 0.0;
-      const bool ch = on && dv != 0.0;
+      s_d[lane] = dv;
       const unsigned long long bal = __ballot(ch);
-      if (lane == 0) { s_sc[0] = rsq; s_sc[1] = dlx; s_sc[2] = (double)__popcll(bal); }
+      if (lane == 0) s_sc[2] = (double)__popcll(bal);
       if (rec) {   // changes in visit order
         const int base = *s_nc;
         if (ch) {
@@ -342,63 +367,74 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
         }
         if (lane == 0) *s_nc = base + __popcll(bal);
       }
+      long long tb = 0;
+      if (tk && tid == 0) { tb = wall_clock64(); tk[6] += tb - ta; }
       __syncthreads();
+      if (tk && tid == 0) tk[7] += wall_clock64() - tb;
       if (tk && tid == 0) { const long long t1 = wall_clock64(); tk[0] += t1 - t0; t0 = t1; tk[2] += 1; }
+      const long long tr = tk && tid == 0 ? wall_clock64() : 0;
+      dlx_l = fmax(dlx_l, dv * dv);   // max d^2: per lane, reduced once per sweep
+      if (bal) {   // R^2, a sequential sum in visit order, while waves 1..7 update
+        const double t = dv * (2.0 * s_log[2 * lane + 1] - dv);
+        double rsq = s_sc[0];
+        for (unsigned long long m = bal; m; m &= m - 1) rsq = rsq + lp_rdlane(t, __builtin_ctzll(m));
+        if (lane == 0) s_sc[0] = rsq;
+      }
+      if (tk && tid == 0) tk[17] += wall_clock64() - tr;
     } else {
       double nx[LP_PF], pv[LP_B];
       bool qon = false;
+      // every load unconditional (clamped to a valid entry, then selected):
+      // no branch between the loads and their use, so all stay in flight
 #pragma unroll
       for (int i = 0; i < LP_PF; ++i) {   // the next block's G_AA block
         const int e = u + (LP_NT - 64) * i, s = e >> 6, t = e & 63;
-        nx[i] = (e < LP_B * LP_B && s < nb1 && t < nb1)
-                    ? GAA[(int64_t)lp_at(ord, b1 + s) * ldaa + lp_at(ord, b1 + t)] : 0.0;
+        const double v =
+            GAA[(int64_t)lp_at<ORD>(ord, b1 + min(s, nb1 - 1)) * ldaa + lp_at<ORD>(ord, b1 + min(t, nb1 - 1))];
+        nx[i] = (e < LP_B * LP_B && s < nb1 && t < nb1) ? v : 0.0;
       }
-      const int q = u;   // gradient (entry position) q: this block's rows of G_AA at column q
+      const int q = u, qq = min(q, n - 1);   // gradient (entry position) q: this block's rows of G_AA at column q
       if (q < n) {
-        const int rq = ord ? s_rank[q] : q;
+        const int rq = ORD ? s_rank[q] : q;
         qon = rq < b0 || rq >= b0 + nb;
       }
 #pragma unroll
       for (int s = 0; s < LP_B; ++s) {   // row base uniform (scalar), column offset per lane
-        const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at(ord, b0 + min(s, nb - 1))) * ldaa;
-        pv[s] = (qon && s < nb) ? row[q] : 0.0;
+        const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s, nb - 1))) * ldaa;
+        pv[s] = (qon && s < nb) ? row[qq] : 0.0;
       }
       __syncthreads();
+      const long long tw = tk && tid == 64 ? wall_clock64() : 0;
       const int nch = (int)s_sc[2];
 #pragma unroll
       for (int i = 0; i < LP_PF; ++i) {
         const int e = u + (LP_NT - 64) * i;
         if (e < LP_B * LP_B) s_gb[e] = nx[i];
       }
-      if (qon && nch) {   // elnet1's eager updates, in visit order
+      if (qon && nch) {   // elnet1's eager updates, in visit order (d = 0: g - G * 0 == g)
         double gq = s_g[u];
 #pragma unroll
-        for (int s = 0; s < LP_B; ++s) {
-          const double d = s_d[s];
-          if (s < nb && d != 0.0) gq = gq - pv[s] * d;
-        }
+        for (int s = 0; s < LP_B; ++s) gq = gq - pv[s] * s_d[s];
         s_g[u] = gq;
       }
+      if (tk && tid == 64) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tk[16] += wall_clock64() - tw; }
     }
     const int nch = (int)s_sc[2];
     if (nch && n > LP_NT - 64) {   // gradients past the prefetched ones: loads after the serial steps
       for (int q = LP_NT - 64 + tid; q < n; q += blockDim.x) {
-        const int rq = ord ? s_rank[q] : q;
+        const int rq = ORD ? s_rank[q] : q;
         if (rq >= b0 && rq < b0 + nb) continue;
         double gq = s_g[q];
         for (int s0 = 0; s0 < nb; s0 += 32) {
           double gv[32];
 #pragma unroll
           for (int w = 0; w < 32; ++w) {
-            const int s = s0 + w;
-            const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at(ord, b0 + min(s, nb - 1))) * ldaa;
-            gv[w] = (s < nb && s_d[s] != 0.0) ? row[q] : 0.0;
+            const double *row =
+                GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s0 + w, nb - 1))) * ldaa;
+            gv[w] = row[q];
           }
 #pragma unroll
-          for (int w = 0; w < 32; ++w) {
-            const int s = s0 + w;
-            if (s < nb && s_d[s] != 0.0) gq = gq - gv[w] * s_d[s];
-          }
+          for (int w = 0; w < 32; ++w) gq = gq - gv[w] * s_d[s0 + w];   // s_d = 0 past the block
         }
         s_g[q] = gq;
       }
@@ -406,11 +442,17 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
     __syncthreads();
     if (tk && tid == 0) { tk[1] += wall_clock64() - t0; tk[3] += nch; }
   }
+  if (wave == 0) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) dlx_l = fmax(dlx_l, __shfl_xor(dlx_l, o));
+    if (lane == 0) s_sc[1] = fmax(s_sc[1], dlx_l);
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[3 * LP_LMAX * 4 + 2 * LP_LMAX * 8];
-  __shared__ double s_d[LP_B], s_sc[4], s_gb[LP_B * LP_B];
+  __shared__ double s_d[LP_B], s_sc[4], s_gb[LP_B * LP_B], s_log[2 * LP_B];
   __shared__ int s_i[8], s_cnt[LP_NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
@@ -419,8 +461,9 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   double *dl = A.dlist + (int64_t)f * LP_LMAX;
   if (role > 0) {   // ------------------------------------------------ helper
     int *hk = (int *)lds;
-    double *hd = (double *)(lds + LP_LMAX * 4);
+    double *hd = (double *)(lds + (LP_LMAX + 2 * LP_U) * 4);   // hk padded by < 2 LP_U
     const int h = role - 1, j0 = (int)((int64_t)h * p / H), j1 = (int)((int64_t)(h + 1) * p / H);
+    long long hb[4] = {0, 0, 0, 0};   // helper 0 diagnostics: busy ticks (FULL), FULL tasks, changes, busy (REFRESH)
     for (int q = 1;; ++q) {
       if (tid == 0) {   // ONE lane polls the task granule, then ONE acquire
         const long long t0 = wall_clock64();
@@ -439,18 +482,28 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       if (tv < 0) break;
       const int type = tv & 3, gcur = (tv >> 2) & 1, nc = tv >> 3;
       if (type == LP_EXIT) break;
+      const long long tb = A.prof && h == 0 && tid == 0 ? wall_clock64() : 0;
       const double lam = __longlong_as_double((long long)lp_ldu(&ctl->lam.v));
+      const int ncp = (nc + 2 * LP_U - 1) / (2 * LP_U) * (2 * LP_U);
       for (int i = tid; i < nc; i += blockDim.x) { hk[i] = lp_ldi(kl + i); hd[i] = lp_ld(dl + i); }
+      __syncthreads();
+      for (int i = nc + tid; i < ncp; i += blockDim.x) { hk[i] = hk[nc - 1]; hd[i] = 0.0; }
       __syncthreads();
       const int first = lp_task_cols(A, f, type, nc, lam, gcur, j0, j1, hk, hd);
       if (first != INT_MAX) atomicMin(&s_i[1], first);   // LDS
       lp_drain();
       __syncthreads();
+      if (A.prof && h == 0 && tid == 0) {
+        const long long dt = wall_clock64() - tb;
+        if (type == LP_FULL) { hb[0] += dt; hb[1] += 1; hb[2] += nc; } else hb[3] += dt;
+      }
       if (tid == 0) {
         lp_release();
         lp_stu(&ctl->done[h].v, lp_gran(q, (unsigned)s_i[1]));
       }
     }
+    if (A.prof && h == 0 && tid == 0)
+      for (int i = 0; i < 4; ++i) A.prof[(int64_t)f * LP_PROF + 20 + i] = hb[i];
     return;
   }
   // ----------------------------------------------------------------- leader
@@ -507,7 +560,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     return s_i[4] != 0;
   };
   long long pt = wall_clock64();
-  long long pacc[16] = {0};
+  long long pacc[LP_PROF] = {0};
   long long *tk = A.prof ? pacc + 8 : nullptr;
   auto ptick = [&](int i) {   // leader phase timing (A.prof): thread 0 only
     if (A.prof && tid == 0) { const long long t = wall_clock64(); pacc[i] += t - pt; pt = t; }
@@ -529,10 +582,10 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           if (tid == 0) { s_sc[1] = 0.0; s_i[1] = 0; }
           __syncthreads();
           ptick(6);
-          lp_sweep(s_srt, nin, lam, true, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_sc,
-                   &s_i[1], kl, dl, tk);
+          lp_sweep<true>(s_srt, nin, lam, true, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
+                   s_sc, &s_i[1], kl, dl, tk);
           ptick(0);
-          if (tid == 0) { pacc[12] += 1; pacc[13] += nin; }
+          if (tid == 0) { pacc[16] += 1; pacc[17] += nin; }
           if (!run_task(LP_FULL, s_i[1], lam)) { st = 3; fail_m = m; break; }
           ptick(1);
           const int v = s_i[3];
@@ -600,10 +653,10 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         if (tid == 0) s_sc[1] = 0.0;
         __syncthreads();
         ptick(6);
-        lp_sweep(nullptr, nin, lam, false, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_sc,
-                 &s_i[1], kl, dl, tk);
+        lp_sweep<false>(nullptr, nin, lam, false, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
+                 s_sc, &s_i[1], kl, dl, tk);
         ptick(2);
-        if (tid == 0) { pacc[14] += 1; pacc[15] += nin; }
+        if (tid == 0) { pacc[18] += 1; pacc[19] += nin; }
         if (s_sc[1] < A.thr) break;
         if (nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
@@ -656,9 +709,11 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   }
   run_task(LP_EXIT, 0, 0.0);
   ptick(6);
+  if (A.prof && tid == 64) A.prof[(int64_t)f * LP_PROF + 24] = pacc[24];
   if (A.prof && tid == 0) {
     pacc[7] = nin;
-    for (int i = 0; i < 16; ++i) A.prof[(int64_t)f * 16 + i] = pacc[i];
+    for (int i = 0; i < 20; ++i) A.prof[(int64_t)f * LP_PROF + i] = pacc[i];
+    A.prof[(int64_t)f * LP_PROF + 25] = pacc[25];
   }
   if (tid == 0) {
     A.status[f] = st;
@@ -750,7 +805,7 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   A.tmo = 2000000000LL;   // 20 s of the 100 MHz wall clock
   // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
   static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
-  if (prof) A.prof = (long long *)alloc((size_t)nprob * 16 * 8);
+  if (prof) A.prof = (long long *)alloc((size_t)nprob * LP_PROF * 8);
   auto cleanup = [&]() { hipStreamSynchronize(st); for (void *b : bufs) hipFree(b); };
   if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA) {
     cleanup();
@@ -764,15 +819,17 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     e = hipLaunchCooperativeKernel((const void *)lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), args, 0, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess && A.prof) {
-    std::vector<long long> hp((size_t)nprob * 16);
+    std::vector<long long> hp((size_t)nprob * LP_PROF);
     hipMemcpy(hp.data(), A.prof, hp.size() * 8, hipMemcpyDeviceToHost);
     for (int f = 0; f < nprob; ++f) {
-      const long long *q = hp.data() + f * 16;
+      const long long *q = hp.data() + f * LP_PROF;
       fprintf(stderr, "[lasso prof] problem %2d H %d: full-pass sweeps %.2f ms, FULL replays %.2f, active passes %.2f, "
               "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
-              "blocks %lld: serial %.2f ms, update %.2f ms, changes %lld\n", f, H, q[0] * 1e-5, q[1] * 1e-5,
-              q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[12], q[13], q[14], q[15], q[10], q[8] * 1e-5, q[9] * 1e-5,
-              q[11]);
+              "blocks %lld: serial %.2f ms (Gr %.2f, chain %.2f, post %.2f, barrier %.2f), update %.2f ms, changes %lld | helper 0: FULL %lld "
+              "tasks, %lld changes, busy %.2f ms, REFRESH busy %.2f ms | wave 1 update %.2f ms, wave 0 R^2 %.2f ms\n", f, H, q[0] * 1e-5,
+              q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10], q[8] * 1e-5,
+              q[12] * 1e-5, q[13] * 1e-5, (q[14] - q[13]) * 1e-5, q[15] * 1e-5, q[9] * 1e-5, q[11], q[21], q[22], q[20] * 1e-5, q[23] * 1e-5, q[24] * 1e-5,
+              q[25] * 1e-5);
     }
   }
   if (e == hipSuccess) {   // a timed-out problem: report its control block
