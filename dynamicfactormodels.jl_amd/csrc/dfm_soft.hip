@@ -143,6 +143,9 @@ constexpr int LP_LMAX = 4096;   // active-set capacity (leader LDS state; glmnet
 constexpr int LP_B = 64;        // coordinate block = one wave
 constexpr int LP_NT = 512;      // threads per workgroup
 constexpr int LP_PROF = 32;     // diagnostics slots per problem
+constexpr int LP_U = 32;        // helper change-list chunk (replay snapshots at every chunk boundary)
+constexpr int LP_NCH = LP_LMAX / LP_U + 2;   // chunk snapshots per column
+constexpr int LP_NBL = LP_LMAX / LP_B + 2;   // block snapshots of the leader's full sweep
 constexpr int LP_PF = (LP_B * LP_B + LP_NT - 64 - 1) / (LP_NT - 64);   // next-block loads per thread of waves 1..7
 enum { LP_FULL = 1, LP_REFRESH = 2, LP_EXIT = 3 };
 
@@ -151,7 +154,7 @@ struct alignas(256) LpLine {   // one granule per 256-B line
   unsigned long long pad[31];
 };
 struct LassoCtl {   // per problem, zeroed before the launch
-  LpLine task;      // {tag = task number, value = type | gcur << 2 | nc << 3}
+  LpLine task;      // {tag = task number, value = type | gcur << 2 | c0 << 3 | nc << 11}
   LpLine lam;       // the task's lambda (payload)
   LpLine done[64];  // helper h: {tag = task number, value = first entering variable (or INT_MAX)}
 };
@@ -170,6 +173,9 @@ struct LassoArgs {
   double *dlist;    // [nprob][LP_LMAX]              deltas
   double *save;     // [nprob][2][LP_LMAX] pass-start a, g (by entry position)
   double *GAA;      // [nprob][ldaa][ldaa] G over the active set, entry order
+  double *snapC;    // [nprob][LP_NCH][p]  FULL replay: gradient of column j after the first LP_U c changes
+  double *snapL;    // [nprob][LP_NBL][2][ldaa] full sweep: active (g, a) at each block start (entry order)
+  double *snapR;    // [nprob][LP_NBL][4]  full sweep: {R^2, changes, active count} at each block start
   double *bpath, *rsq_out;
   int *nlam_out, *status;
   long long tmo;    // spin timeout, wall-clock ticks (100 MHz)
@@ -205,13 +211,16 @@ DFM_DEV double lp_rdlane(double x, int l) {   // l: a compile-time constant insi
 }
 
 // The helpers' share of a task over columns [j0, j1) of problem f.  hk / hd:
-// the task's change list, padded to a multiple of 2 LP_U with a valid row
-// and a zero delta (g - G * 0 == g), so that every load is unconditional and
-// two chunks of LP_U loads stay in flight.  FULL: the list is in coordinate
-// order, so the variable's own visit falls after the pos = #{k < j} first
-// changes.
-constexpr int LP_U = 32;
-DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam, int gcur, int j0, int j1,
+// the task's change list, padded past nc with a valid row and a zero delta
+// (g - G * 0 == g), so that every load is unconditional and two chunks of
+// LP_U loads stay in flight.  FULL: the list is in coordinate order, so the
+// variable's own visit falls after the pos = #{k < j} first changes.  A FULL
+// task resumes at change LP_U c0 from the column's chunk snapshot (the list
+// before it is the one the snapshot was taken on: a restarted pass keeps its
+// prefix) and snapshots every further complete chunk.  A visit inside the
+// kept prefix precedes the entering variable that caused the restart, so it
+// was found not entering and is not checked again.
+DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, int c0, double lam, int gcur, int j0, int j1,
                          const int *hk, const double *hd) {
   const int p = A.p;
   const double *G = A.G + (int64_t)f * A.strideG;
@@ -219,17 +228,20 @@ DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam
   const int *isact = A.isact + (int64_t)f * p;
   double *gin = A.g2 + ((int64_t)f * 2 + gcur) * p;
   double *gout = A.g2 + ((int64_t)f * 2 + (gcur ^ 1)) * p;
+  double *sc = A.snapC + (int64_t)f * LP_NCH * p;
+  const bool full = type == LP_FULL;
+  const int i0s = full ? LP_U * c0 : 0;
   int first = INT_MAX;   // this thread's first entering variable
   for (int j = j0 + (int)threadIdx.x; j < j1; j += blockDim.x) {
     if (!ju[j] || lp_ldi(isact + j)) continue;
     int pos = 0;   // FULL: changes before j's visit (hk ascending)
-    if (type == LP_FULL) {
+    if (full) {
       int lo = 0, hi = nc;
       while (lo < hi) { const int mid = (lo + hi) >> 1; if (hk[mid] < j) lo = mid + 1; else hi = mid; }
       pos = lo;
     }
     const double *Gj = G + j;
-    double s = type == LP_FULL ? lp_ld(gin + j) : 0.0, sv = s;
+    double s = full ? lp_ld(c0 == 0 ? gin + j : sc + (int64_t)c0 * p + j) : 0.0, sv = s;
     double ga[LP_U], gb[LP_U];
     auto ld = [&](double *gv, int i0) {
 #pragma unroll
@@ -238,23 +250,24 @@ DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, double lam
     auto use = [&](const double *gv, int i0) {
 #pragma unroll
       for (int u = 0; u < LP_U; ++u) {
-        if (type == LP_FULL) {   // elnet1's eager updates in visit order
+        if (full) {   // elnet1's eager updates in visit order
           s = s - gv[u] * hd[i0 + u];
           sv = i0 + u < pos ? s : sv;
-        } else {                 // REFRESH: dot(da, c_j,A), a sequential sum in entry order
+        } else {      // REFRESH: dot(da, c_j,A), a sequential sum in entry order
           s = s + hd[i0 + u] * gv[u];
         }
       }
+      if (full && i0 + LP_U <= nc) sc[(int64_t)((i0 + LP_U) / LP_U) * p + j] = s;
     };
-    if (nc > 0) ld(ga, 0);
-    for (int i0 = 0; i0 < nc; i0 += 2 * LP_U) {
+    if (i0s < nc) ld(ga, i0s);
+    for (int i0 = i0s; i0 < nc; i0 += 2 * LP_U) {
       ld(gb, i0 + LP_U);
       use(ga, i0);
       if (i0 + 2 * LP_U < nc) ld(ga, i0 + 2 * LP_U);
       use(gb, i0 + LP_U);
     }
-    if (type == LP_FULL) {
-      if (fabs(sv) - lam > 0.0) first = min(first, j);
+    if (full) {
+      if (pos >= i0s && fabs(sv) - lam > 0.0) first = min(first, j);
       gout[j] = s;
     } else {
       gin[j] = lp_ld(gin + j) - s;
@@ -298,9 +311,11 @@ DFM_DEV void lp_chain(double &g, const double a0, const double *Gr, double lam, 
   }
 }
 
-// One pass over n active positions, in entry order (!ORD) or in
-// coordinate-index order (ORD, ord = s_srt).  rec: append every change
-// (coordinate, delta) to kl / dl in visit order.  All threads call it.
+// One pass over n active positions from block bstart on, in entry order
+// (!ORD) or in coordinate-index order (ORD, ord = s_srt: elnet1's full pass,
+// which appends every change (coordinate, delta) to kl / dl in visit order
+// and snapshots (g, a) of the active set and {R^2, changes, n} at every
+// block start, the restart points of the pass).  All threads call it.
 //
 // Per block of 64 sweep positions: wave 0 runs the serial coordinate steps
 // (lane t = one coordinate, its column of the block's G_AA in registers from
@@ -313,18 +328,20 @@ DFM_DEV void lp_chain(double &g, const double a0, const double *Gr, double lam, 
 // first block of the sweep order `key` when gkey == key (the last block
 // prefetches the next sweep's first).
 template <bool ORD>
-DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int &gkey, const double *GAA, int ldaa,
+DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, int &gkey, const double *GAA, int ldaa,
                       const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_d, double *s_gb,
-                      double *s_log, double *s_sc, int *s_nc, int *kl, double *dl, long long *tk) {
+                      double *s_log, double *s_sc, int *s_nc, int *kl, double *dl, double *snapL, double *snapR,
+                      long long *tk) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), u = tid - 64;
   if (n <= 0) return;
-  if (gkey != key) {
-    lp_gblock_load<ORD>(ord, 0, n, GAA, ldaa, s_gb);
+  if (gkey != key || bstart != 0) {
+    lp_gblock_load<ORD>(ord, LP_B * bstart, n, GAA, ldaa, s_gb);
     __syncthreads();
     gkey = key;
   }
   double dlx_l = 0.0;
-  for (int b0 = 0; b0 < n; b0 += LP_B) {
+  for (int b0 = LP_B * bstart; b0 < n; b0 += LP_B) {
+    const int bn = b0 / LP_B + 1;   // the next block start's snapshot slot
     const int nb = min(LP_B, n - b0);
     const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);
     long long t0 = tk && tid == 0 ? wall_clock64() : 0;
@@ -358,7 +375,7 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
       s_d[lane] = dv;
       const unsigned long long bal = __ballot(ch);
       if (lane == 0) s_sc[2] = (double)__popcll(bal);
-      if (rec) {   // changes in visit order
+      if (ORD) {   // changes in visit order
         const int base = *s_nc;
         if (ch) {
           const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
@@ -375,10 +392,22 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
       const long long tr = tk && tid == 0 ? wall_clock64() : 0;
       dlx_l = fmax(dlx_l, dv * dv);   // max d^2: per lane, reduced once per sweep
       if (bal) {   // R^2, a sequential sum in visit order, while waves 1..7 update
+        // (an unchanged coordinate adds t = 0 * x = +-0: rsq >= 0 is unchanged)
         const double t = dv * (2.0 * s_log[2 * lane + 1] - dv);
         double rsq = s_sc[0];
-        for (unsigned long long m = bal; m; m &= m - 1) rsq = rsq + lp_rdlane(t, __builtin_ctzll(m));
+        const int last = 63 - __builtin_clzll(bal);
+#pragma unroll
+        for (int s0 = 0; s0 < LP_B; s0 += 16) {
+          if (s0 > last) break;
+#pragma unroll
+          for (int s = s0; s < s0 + 16; ++s) rsq = rsq + lp_rdlane(t, s);
+        }
         if (lane == 0) s_sc[0] = rsq;
+      }
+      if (ORD && lane == 0) {
+        snapR[bn * 4 + 0] = s_sc[0];
+        snapR[bn * 4 + 1] = (double)*s_nc;
+        snapR[bn * 4 + 2] = (double)n;
       }
       if (tk && tid == 0) tk[17] += wall_clock64() - tr;
     } else {
@@ -412,18 +441,42 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
         if (e < LP_B * LP_B) s_gb[e] = nx[i];
       }
       if (qon && nch) {   // elnet1's eager updates, in visit order (d = 0: g - G * 0 == g)
+        // products first (the deltas read 16 at a time, 8 wide LDS reads in
+        // flight), then the subtractions in visit order
+        const double2 *sd2 = reinterpret_cast<const double2 *>(s_d);
+#pragma unroll
+        for (int c = 0; c < LP_B / 16; ++c) {
+          double2 dd[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dd[i] = sd2[8 * c + i];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            pv[16 * c + 2 * i] = pv[16 * c + 2 * i] * dd[i].x;
+            pv[16 * c + 2 * i + 1] = pv[16 * c + 2 * i + 1] * dd[i].y;
+          }
+        }
         double gq = s_g[u];
 #pragma unroll
-        for (int s = 0; s < LP_B; ++s) gq = gq - pv[s] * s_d[s];
+        for (int s = 0; s < LP_B; ++s) gq = gq - pv[s];
         s_g[u] = gq;
+      }
+      if (ORD && u < n) {   // this gradient at the next block start
+        snapL[(int64_t)bn * 2 * ldaa + u] = s_g[u];
+        snapL[((int64_t)bn * 2 + 1) * ldaa + u] = s_a[u];
       }
       if (tk && tid == 64) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tk[16] += wall_clock64() - tw; }
     }
     const int nch = (int)s_sc[2];
-    if (nch && n > LP_NT - 64) {   // gradients past the prefetched ones: loads after the serial steps
+    if ((nch || ORD) && n > LP_NT - 64) {   // gradients past the prefetched ones: loads after the serial steps
       for (int q = LP_NT - 64 + tid; q < n; q += blockDim.x) {
         const int rq = ORD ? s_rank[q] : q;
-        if (rq >= b0 && rq < b0 + nb) continue;
+        if (nch == 0 || (rq >= b0 && rq < b0 + nb)) {
+          if (ORD) {
+            snapL[(int64_t)bn * 2 * ldaa + q] = s_g[q];
+            snapL[((int64_t)bn * 2 + 1) * ldaa + q] = s_a[q];
+          }
+          continue;
+        }
         double gq = s_g[q];
         for (int s0 = 0; s0 < nb; s0 += 32) {
           double gv[32];
@@ -437,6 +490,10 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
           for (int w = 0; w < 32; ++w) gq = gq - gv[w] * s_d[s0 + w];   // s_d = 0 past the block
         }
         s_g[q] = gq;
+        if (ORD) {
+          snapL[(int64_t)bn * 2 * ldaa + q] = gq;
+          snapL[((int64_t)bn * 2 + 1) * ldaa + q] = s_a[q];
+        }
       }
     }
     __syncthreads();
@@ -452,7 +509,8 @@ DFM_DEV void lp_sweep(const int *ord, int n, double lam, bool rec, int key, int 
 
 __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[3 * LP_LMAX * 4 + 2 * LP_LMAX * 8];
-  __shared__ double s_d[LP_B], s_sc[4], s_gb[LP_B * LP_B], s_log[2 * LP_B];
+  __shared__ __attribute__((aligned(16))) double s_d[LP_B];
+  __shared__ double s_sc[4], s_gb[LP_B * LP_B], s_log[2 * LP_B];
   __shared__ int s_i[8], s_cnt[LP_NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
@@ -480,16 +538,17 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       __syncthreads();
       const int tv = s_i[0];
       if (tv < 0) break;
-      const int type = tv & 3, gcur = (tv >> 2) & 1, nc = tv >> 3;
+      const int type = tv & 3, gcur = (tv >> 2) & 1, c0 = (tv >> 3) & 255, nc = tv >> 11;
       if (type == LP_EXIT) break;
       const long long tb = A.prof && h == 0 && tid == 0 ? wall_clock64() : 0;
       const double lam = __longlong_as_double((long long)lp_ldu(&ctl->lam.v));
-      const int ncp = (nc + 2 * LP_U - 1) / (2 * LP_U) * (2 * LP_U);
+      const int i0s = type == LP_FULL ? LP_U * c0 : 0;   // the replay's first change
+      const int ncp = nc > i0s ? i0s + (nc - i0s + 2 * LP_U - 1) / (2 * LP_U) * (2 * LP_U) : nc;
       for (int i = tid; i < nc; i += blockDim.x) { hk[i] = lp_ldi(kl + i); hd[i] = lp_ld(dl + i); }
       __syncthreads();
       for (int i = nc + tid; i < ncp; i += blockDim.x) { hk[i] = hk[nc - 1]; hd[i] = 0.0; }
       __syncthreads();
-      const int first = lp_task_cols(A, f, type, nc, lam, gcur, j0, j1, hk, hd);
+      const int first = lp_task_cols(A, f, type, nc, c0, lam, gcur, j0, j1, hk, hd);
       if (first != INT_MAX) atomicMin(&s_i[1], first);   // LDS
       lp_drain();
       __syncthreads();
@@ -517,6 +576,8 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   int *isact = A.isact + (int64_t)f * p;
   double *sv = A.save + (int64_t)f * 2 * LP_LMAX;
   double *GAA = A.GAA + (int64_t)f * ldaa * ldaa;
+  double *snL = A.snapL + (int64_t)f * LP_NBL * 2 * ldaa, *snR = A.snapR + (int64_t)f * LP_NBL * 4;
+  const double *snC = A.snapC + (int64_t)f * LP_NCH * p;
   double *bp = A.bpath + (int64_t)f * nlam * p;
   for (int j = tid; j < p; j += blockDim.x) { lp_st(g2 + j, c[j]); lp_sti(isact + j, 0); }
   if (tid == 0) { s_sc[0] = 0.0; s_sc[1] = 0.0; s_i[1] = 0; s_i[2] = 0; }
@@ -525,14 +586,14 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   // publish a task to the helpers and wait for all of them (H == 0: run it here)
   // publish a task to the helpers (payload: kl, dl, isact, g2, lam) and wait
   // for every helper's done granule; s_i[3] = the first entering variable
-  auto run_task = [&](int type, int nc, double lam) -> bool {   // (H >= 1: the host guarantees it)
+  auto run_task = [&](int type, int nc, double lam, int c0) -> bool {   // (H >= 1: the host guarantees it)
     ++seq;
     if (tid == 0) lp_stu(&ctl->lam.v, (unsigned long long)__double_as_longlong(lam));
     lp_drain();
     __syncthreads();
     if (tid == 0) {
       lp_release();
-      lp_stu(&ctl->task.v, lp_gran(seq, (unsigned)(type | gcur << 2 | nc << 3)));
+      lp_stu(&ctl->task.v, lp_gran(seq, (unsigned)(type | gcur << 2 | c0 << 3 | nc << 11)));
     }
     if (type == LP_EXIT) return true;
     if (wave == 0) {   // lane h polls helper h's granule
@@ -575,25 +636,25 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         // ---------------- full pass (speculative: see the header comment)
         for (int t = tid; t < nin; t += blockDim.x) { lp_st(sv + t, s_a[t]); lp_st(sv + LP_LMAX + t, s_g[t]); }
         const double rsq_save = s_sc[0];
+        const int n_pass = nin;   // active count at the pass start (sv's entries)
+        int rsb = 0, c0 = 0;      // the restart's first block (sweep) and chunk (replay)
         lp_drain();
         ++nlp;
+        if (tid == 0) s_i[1] = 0;
         for (;;) {
           __syncthreads();
-          if (tid == 0) { s_sc[1] = 0.0; s_i[1] = 0; }
-          __syncthreads();
           ptick(6);
-          lp_sweep<true>(s_srt, nin, lam, true, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
-                   s_sc, &s_i[1], kl, dl, tk);
+          lp_sweep<true>(s_srt, nin, rsb, lam, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
+                         s_sc, &s_i[1], kl, dl, snL, snR, tk);
           ptick(0);
-          if (tid == 0) { pacc[16] += 1; pacc[17] += nin; }
-          if (!run_task(LP_FULL, s_i[1], lam)) { st = 3; fail_m = m; break; }
+          if (tid == 0) { pacc[16] += 1; pacc[17] += nin - LP_B * rsb; }
+          if (!run_task(LP_FULL, s_i[1], lam, c0)) { st = 3; fail_m = m; break; }
           ptick(1);
           const int v = s_i[3];
           if (v == INT_MAX) break;
           if (nin >= cap) { st = 2; fail_m = m; break; }
           // ---- variable v enters at entry position nin
           const int pos = nin;
-          const double gvv = lp_ld(g2 + (int64_t)gcur * p + v);   // its pass-start gradient
           for (int t = tid; t <= pos; t += blockDim.x) {
             const int col = t == pos ? v : s_ia[t];
             const double val = G[(int64_t)v * p + col];
@@ -627,14 +688,68 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           }
           __syncthreads();
           for (int t = tid; t <= pos; t += blockDim.x) s_rank[s_srt[t]] = t;
-          // restart the pass from its start state, v included (a = 0, its start gradient)
-          if (tid == 0) { lp_st(sv + pos, 0.0); lp_st(sv + LP_LMAX + pos, gvv); s_sc[0] = rsq_save; }
           nin = pos + 1;
           ++ver;
           lp_drain();
           __syncthreads();
           lp_acquire();   // this CU's L1 drops its G_AA lines (plain loads read the new row / column)
-          for (int t = tid; t < nin; t += blockDim.x) { s_a[t] = lp_ld(sv + t); s_g[t] = lp_ld(sv + LP_LMAX + t); }
+          // ---- restart from the block holding v's slot: the pass up to that
+          // block is unchanged.  Its snapshot (block 0: the pass start) gives
+          // the entries visited before; an entry not in the snapshot (v, or
+          // one that entered later than it was taken) sits past the block
+          // start, so it has a = 0 and the gradient after the first nc_b
+          // changes: its chunk snapshot (chunk 0: the pass-start gradient)
+          // plus the changes left, in visit order.
+          const int bi = ins / LP_B;
+          const double rsq_b = bi == 0 ? rsq_save : lp_ld(snR + bi * 4 + 0);
+          const int nc_b = bi == 0 ? 0 : (int)lp_ld(snR + bi * 4 + 1);
+          const int n_snap = bi == 0 ? n_pass : (int)lp_ld(snR + bi * 4 + 2);
+          const double *snG = bi == 0 ? sv + LP_LMAX : snL + (int64_t)bi * 2 * ldaa;
+          const double *snA = bi == 0 ? sv : snL + ((int64_t)bi * 2 + 1) * ldaa;
+          const double *gin = g2 + (int64_t)gcur * p;
+          const int cb = nc_b / LP_U, nt = nc_b - LP_U * cb;   // chunk snapshot, changes past it (< LP_U)
+          double *s_pd = s_log;                                  // (s_log is free between sweeps)
+          int *s_pk = reinterpret_cast<int *>(s_log + LP_U);
+          for (int i = tid; i < nt; i += blockDim.x) { s_pk[i] = lp_ldi(kl + LP_U * cb + i); s_pd[i] = lp_ld(dl + LP_U * cb + i); }
+          __syncthreads();
+          for (int t = tid; t < nin; t += blockDim.x) {
+            if (t < n_snap) {
+              s_a[t] = lp_ld(snA + t);
+              s_g[t] = lp_ld(snG + t);
+            } else {
+              const int j = s_ia[t];
+              double g = lp_ld(cb == 0 ? gin + j : snC + (int64_t)cb * p + j);
+              if (nt > 0) {
+                double gv[LP_U];
+#pragma unroll
+                for (int i = 0; i < LP_U; ++i) gv[i] = G[(int64_t)s_pk[min(i, nt - 1)] * p + j];
+#pragma unroll
+                for (int i = 0; i < LP_U; ++i)
+                  if (i < nt) g = g - gv[i] * s_pd[i];
+              }
+              s_a[t] = 0.0;
+              s_g[t] = g;
+            }
+          }
+          if (tid == 0) { s_sc[0] = rsq_b; s_i[1] = nc_b; }
+          rsb = bi;
+          c0 = nc_b / LP_U;
+        }
+        if (st) break;
+        {   // the pass's max d^2: over its changes
+          const int nc = s_i[1];
+          double mx = 0.0;
+          for (int i = tid; i < nc; i += blockDim.x) { const double d = lp_ld(dl + i); mx = fmax(mx, d * d); }
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+          __syncthreads();
+          if (lane == 0) s_d[wave] = mx;
+          __syncthreads();
+          if (tid == 0) {
+            double r = 0.0;
+            for (int w2 = 0; w2 < LP_NT / 64; ++w2) r = fmax(r, s_d[w2]);
+            s_sc[1] = r;
+          }
         }
         if (st) break;
         gcur ^= 1;                     // the replay's non-active gradients are current
@@ -653,8 +768,8 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         if (tid == 0) s_sc[1] = 0.0;
         __syncthreads();
         ptick(6);
-        lp_sweep<false>(nullptr, nin, lam, false, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
-                 s_sc, &s_i[1], kl, dl, tk);
+        lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
+                        s_sc, &s_i[1], kl, dl, nullptr, nullptr, tk);
         ptick(2);
         if (tid == 0) { pacc[18] += 1; pacc[19] += nin; }
         if (s_sc[1] < A.thr) break;
@@ -683,7 +798,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         __syncthreads();
       }
       ptick(6);
-      if (!run_task(LP_REFRESH, s_i[1], lam)) { st = 3; fail_m = m; break; }
+      if (!run_task(LP_REFRESH, s_i[1], lam, 0)) { st = 3; fail_m = m; break; }
       ptick(3);
       jz = 0;
     }
@@ -707,7 +822,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       if (Lp > 0 && m + 1 >= Lp) { L = m + 1; break; }
     }
   }
-  run_task(LP_EXIT, 0, 0.0);
+  run_task(LP_EXIT, 0, 0.0, 0);
   ptick(6);
   if (A.prof && tid == 64) A.prof[(int64_t)f * LP_PROF + 24] = pacc[24];
   if (A.prof && tid == 0) {
@@ -801,13 +916,16 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   A.dlist = (double *)alloc((size_t)nprob * LP_LMAX * 8);
   A.save = (double *)alloc((size_t)nprob * 2 * LP_LMAX * 8);
   A.GAA = (double *)alloc((size_t)nprob * ldaa * ldaa * 8);
+  A.snapC = (double *)alloc((size_t)nprob * LP_NCH * p * 8);
+  A.snapL = (double *)alloc((size_t)nprob * LP_NBL * 2 * ldaa * 8);
+  A.snapR = (double *)alloc((size_t)nprob * LP_NBL * 4 * 8);
   A.bpath = bpath; A.rsq_out = rsq; A.nlam_out = nl; A.status = sts;
   A.tmo = 2000000000LL;   // 20 s of the 100 MHz wall clock
   // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
   static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
   if (prof) A.prof = (long long *)alloc((size_t)nprob * LP_PROF * 8);
   auto cleanup = [&]() { hipStreamSynchronize(st); for (void *b : bufs) hipFree(b); };
-  if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA) {
+  if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA || !A.snapC || !A.snapL || !A.snapR) {
     cleanup();
     *why = "out of device memory";
     return hipErrorOutOfMemory;
