@@ -232,40 +232,62 @@ DFM_DEV int lp_task_cols(const LassoArgs &A, int f, int type, int nc, int c0, do
   const bool full = type == LP_FULL;
   const int i0s = full ? LP_U * c0 : 0;
   int first = INT_MAX;   // this thread's first entering variable
-  for (int j = j0 + (int)threadIdx.x; j < j1; j += blockDim.x) {
-    if (!ju[j] || lp_ldi(isact + j)) continue;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform trip count: every lane runs the body (the readlane
+  // broadcasts read all 64 lanes); lanes without a live column compute on a
+  // valid one and store nothing
+  for (int jb = j0 + (int)(threadIdx.x & ~63); jb < j1; jb += blockDim.x) {
+    const int jr = jb + lane, j = min(jr, j1 - 1);
+    const bool live = jr < j1 && ju[j] && !lp_ldi(isact + j);
     int pos = 0;   // FULL: changes before j's visit (hk ascending)
     if (full) {
       int lo = 0, hi = nc;
       while (lo < hi) { const int mid = (lo + hi) >> 1; if (hk[mid] < j) lo = mid + 1; else hi = mid; }
       pos = lo;
     }
-    const double *Gj = G + j;
     double s = full ? lp_ld(c0 == 0 ? gin + j : sc + (int64_t)c0 * p + j) : 0.0, sv = s;
+    // 64 changes at a time, lane u holding change i0 + u: the row and delta of
+    // change u are broadcast by readlane (scalar row base, no LDS round trip
+    // per change); two halves of 32 loads in flight
     double ga[LP_U], gb[LP_U];
-    auto ld = [&](double *gv, int i0) {
-#pragma unroll
-      for (int u = 0; u < LP_U; ++u) gv[u] = Gj[(int64_t)hk[i0 + u] * p];
-    };
-    auto use = [&](const double *gv, int i0) {
+    auto ld = [&](double *gv, int kv, int h0) {
 #pragma unroll
       for (int u = 0; u < LP_U; ++u) {
+        const double *row = G + (int64_t)__builtin_amdgcn_readlane(kv, h0 + u) * p;
+        gv[u] = row[j];
+      }
+    };
+    auto use = [&](const double *gv, double dv, int i0, int h0) {
+#pragma unroll
+      for (int u = 0; u < LP_U; ++u) {
+        const double d = lp_rdlane(dv, h0 + u);
         if (full) {   // elnet1's eager updates in visit order
-          s = s - gv[u] * hd[i0 + u];
-          sv = i0 + u < pos ? s : sv;
+          s = s - gv[u] * d;
+          sv = i0 + h0 + u < pos ? s : sv;
         } else {      // REFRESH: dot(da, c_j,A), a sequential sum in entry order
-          s = s + hd[i0 + u] * gv[u];
+          s = s + d * gv[u];
         }
       }
-      if (full && i0 + LP_U <= nc) sc[(int64_t)((i0 + LP_U) / LP_U) * p + j] = s;
+      if (full && live && i0 + h0 + LP_U <= nc) sc[(int64_t)((i0 + h0 + LP_U) / LP_U) * p + j] = s;
     };
-    if (i0s < nc) ld(ga, i0s);
-    for (int i0 = i0s; i0 < nc; i0 += 2 * LP_U) {
-      ld(gb, i0 + LP_U);
-      use(ga, i0);
-      if (i0 + 2 * LP_U < nc) ld(ga, i0 + 2 * LP_U);
-      use(gb, i0 + LP_U);
+    if (i0s < nc) {
+      int kv = hk[i0s + lane];
+      double dv = hd[i0s + lane];
+      ld(ga, kv, 0);
+      ld(gb, kv, LP_U);
+      for (int i0 = i0s; i0 < nc; i0 += 2 * LP_U) {
+        const bool more = i0 + 2 * LP_U < nc;
+        const int kn = more ? hk[i0 + 2 * LP_U + lane] : kv;
+        const double dn = more ? hd[i0 + 2 * LP_U + lane] : 0.0;
+        use(ga, dv, i0, 0);
+        if (more) ld(ga, kn, 0);
+        use(gb, dv, i0, LP_U);
+        if (more) ld(gb, kn, LP_U);
+        kv = kn;
+        dv = dn;
+      }
     }
+    if (!live) continue;
     if (full) {
       if (pos >= i0s && fabs(sv) - lam > 0.0) first = min(first, j);
       gout[j] = s;
@@ -295,20 +317,33 @@ DFM_DEV void lp_gblock_load(const int *ord, int b, int n, const double *GAA, int
 // start).  Every step is branch-free: an unchanged coordinate gives d = +0,
 // and g - G * 0 == g (a gradient of exactly -0 becomes +0, which no later
 // step can tell apart).  Lanes past the block hold g = a0 = 0 and Gr = 0, so
-// their steps are no-ops.  Lane 0 logs (d, g at the visit) per step for the
-// bookkeeping done off the chain (R^2, max d^2, the new coefficients).
-template <int S>
-DFM_DEV void lp_chain(double &g, const double a0, const double *Gr, double lam, double *s_log, int lane) {
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
+// their steps are no-ops.  Lane s keeps its gradient at its own visit (gm,
+// written from the broadcast value): its delta and new coefficient are
+// recomputed from it off the chain, with the same operations.
+template <int L>
+DFM_DEV double lp_wrlane(double x, double v) {   // x with lane L := v (v uniform)
+  const long long b = __double_as_longlong(x), c = __double_as_longlong(v);
+  int lo = (int)b, hi = (int)(b >> 32);
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((int)c), "i"(L));
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((int)(c >> 32)), "i"(L));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int s, int S>
+DFM_DEV void lp_chain_step(double &g, double &gm, const double a0, const double *Gr, double lam) {
+  if constexpr (s < S) {
     const double gk = lp_rdlane(g, s), ak = lp_rdlane(a0, s);
     const double uu = gk + ak;
     const double v = fabs(uu) - lam;
     const double na = v > 0.0 ? copysign(v, uu) : 0.0;
     const double d = na - ak;
     g = g - Gr[s] * d;
-    if (lane == 0) { s_log[2 * s] = d; s_log[2 * s + 1] = gk; }
+    gm = lp_wrlane<s>(gm, gk);
+    lp_chain_step<s + 1, S>(g, gm, a0, Gr, lam);
   }
+}
+template <int S>
+DFM_DEV void lp_chain(double &g, double &gm, const double a0, const double *Gr, double lam) {
+  lp_chain_step<0, S>(g, gm, a0, Gr, lam);
 }
 
 // One pass over n active positions from block bstart on, in entry order
@@ -356,21 +391,21 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
       for (int s = 0; s < LP_B; ++s) Gr[s] = s_gb[s * LP_B + lane];
       long long ta = 0;
       if (tk && tid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ta = wall_clock64(); tk[4] += ta - t0; }
+      double gm = 0.0;
       switch ((nb + 15) >> 4) {
-        case 1: lp_chain<16>(g, a0, Gr, lam, s_log, lane); break;
-        case 2: lp_chain<32>(g, a0, Gr, lam, s_log, lane); break;
-        case 3: lp_chain<48>(g, a0, Gr, lam, s_log, lane); break;
-        default: lp_chain<64>(g, a0, Gr, lam, s_log, lane); break;
+        case 1: lp_chain<16>(g, gm, a0, Gr, lam); break;
+        case 2: lp_chain<32>(g, gm, a0, Gr, lam); break;
+        case 3: lp_chain<48>(g, gm, a0, Gr, lam); break;
+        default: lp_chain<64>(g, gm, a0, Gr, lam); break;
       }
       if (tk && tid == 0) tk[5] += wall_clock64() - ta;
-      const double dv = on ? s_log[2 * lane] : 0.0;
+      // this lane's step, recomputed from its gradient at the visit (same operations)
+      const double uu = gm + a0;
+      const double vv = fabs(uu) - lam;
+      const double na = vv > 0.0 ? copysign(vv, uu) : 0.0;
+      const double dv = on ? na - a0 : 0.0;
       const bool ch = dv != 0.0;
-      double a = a0;
-      if (ch) {   // the chain's new coefficient, recomputed from the logged gradient
-        const double uu = s_log[2 * lane + 1] + a0;
-        const double v = fabs(uu) - lam;
-        a = v > 0.0 ? copysign(v, uu) : 0.0;
-      }
+      const double a = ch ? na : a0;
       if (on) { s_g[pt] = g; s_a[pt] = a; }
       s_d[lane] = dv;
       const unsigned long long bal = __ballot(ch);
@@ -393,7 +428,7 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
       dlx_l = fmax(dlx_l, dv * dv);   // max d^2: per lane, reduced once per sweep
       if (bal) {   // R^2, a sequential sum in visit order, while waves 1..7 update
         // (an unchanged coordinate adds t = 0 * x = +-0: rsq >= 0 is unchanged)
-        const double t = dv * (2.0 * s_log[2 * lane + 1] - dv);
+        const double t = dv * (2.0 * gm - dv);
         double rsq = s_sc[0];
         const int last = 63 - __builtin_clzll(bal);
 #pragma unroll
@@ -521,7 +556,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     int *hk = (int *)lds;
     double *hd = (double *)(lds + (LP_LMAX + 2 * LP_U) * 4);   // hk padded by < 2 LP_U
     const int h = role - 1, j0 = (int)((int64_t)h * p / H), j1 = (int)((int64_t)(h + 1) * p / H);
-    long long hb[4] = {0, 0, 0, 0};   // helper 0 diagnostics: busy ticks (FULL), FULL tasks, changes, busy (REFRESH)
+    long long hb[6] = {0, 0, 0, 0, 0, 0};   // helper 0 diagnostics: busy (FULL), FULL tasks, changes, busy (REFRESH), staging, replayed changes
     for (int q = 1;; ++q) {
       if (tid == 0) {   // ONE lane polls the task granule, then ONE acquire
         const long long t0 = wall_clock64();
@@ -548,6 +583,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       __syncthreads();
       for (int i = nc + tid; i < ncp; i += blockDim.x) { hk[i] = hk[nc - 1]; hd[i] = 0.0; }
       __syncthreads();
+      if (A.prof && h == 0 && tid == 0) { hb[4] += wall_clock64() - tb; hb[5] += nc - i0s; }
       const int first = lp_task_cols(A, f, type, nc, c0, lam, gcur, j0, j1, hk, hd);
       if (first != INT_MAX) atomicMin(&s_i[1], first);   // LDS
       lp_drain();
@@ -563,6 +599,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     }
     if (A.prof && h == 0 && tid == 0)
       for (int i = 0; i < 4; ++i) A.prof[(int64_t)f * LP_PROF + 20 + i] = hb[i];
+    if (A.prof && h == 0 && tid == 0) { A.prof[(int64_t)f * LP_PROF + 26] = hb[4]; A.prof[(int64_t)f * LP_PROF + 27] = hb[5]; }
     return;
   }
   // ----------------------------------------------------------------- leader
@@ -661,14 +698,17 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
             GAA[(int64_t)pos * ldaa + t] = val;
             GAA[(int64_t)t * ldaa + pos] = val;
           }
-          // index order: v's slot in s_srt (count of active indices below v)
-          int below = 0;
+          // index order: v's slot in s_srt (count of active indices below v),
+          // and v's visit in the change list (count of changes below v)
+          int below = 0, cbelow = 0;
           for (int t = tid; t < pos; t += blockDim.x) below += s_ia[t] < v ? 1 : 0;
+          for (int i = tid; i < s_i[1]; i += blockDim.x) cbelow += lp_ldi(kl + i) < v ? 1 : 0;
           below = (int)wave_sum((double)below);
-          if (lane == 0) s_d[wave] = below;
+          cbelow = (int)wave_sum((double)cbelow);
+          if (lane == 0) { s_d[wave] = below; s_log[wave] = cbelow; }
           __syncthreads();
-          int ins = 0;
-          for (int w2 = 0; w2 < LP_NT / 64; ++w2) ins += (int)s_d[w2];
+          int ins = 0, pos_v = 0;
+          for (int w2 = 0; w2 < LP_NT / 64; ++w2) { ins += (int)s_d[w2]; pos_v += (int)s_log[w2]; }
           int tmp[LP_LMAX / LP_NT];
 #pragma unroll
           for (int i = 0; i < LP_LMAX / LP_NT; ++i) {
@@ -733,7 +773,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           }
           if (tid == 0) { s_sc[0] = rsq_b; s_i[1] = nc_b; }
           rsb = bi;
-          c0 = nc_b / LP_U;
+          c0 = pos_v / LP_U;   // the replay's changes before v's visit are unchanged
         }
         if (st) break;
         {   // the pass's max d^2: over its changes
@@ -944,9 +984,10 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
       fprintf(stderr, "[lasso prof] problem %2d H %d: full-pass sweeps %.2f ms, FULL replays %.2f, active passes %.2f, "
               "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
               "blocks %lld: serial %.2f ms (Gr %.2f, chain %.2f, post %.2f, barrier %.2f), update %.2f ms, changes %lld | helper 0: FULL %lld "
-              "tasks, %lld changes, busy %.2f ms, REFRESH busy %.2f ms | wave 1 update %.2f ms, wave 0 R^2 %.2f ms\n", f, H, q[0] * 1e-5,
+              "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms | wave 1 update %.2f ms, "
+              "wave 0 R^2 %.2f ms\n", f, H, q[0] * 1e-5,
               q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10], q[8] * 1e-5,
-              q[12] * 1e-5, q[13] * 1e-5, (q[14] - q[13]) * 1e-5, q[15] * 1e-5, q[9] * 1e-5, q[11], q[21], q[22], q[20] * 1e-5, q[23] * 1e-5, q[24] * 1e-5,
+              q[12] * 1e-5, q[13] * 1e-5, (q[14] - q[13]) * 1e-5, q[15] * 1e-5, q[9] * 1e-5, q[11], q[21], q[22], q[27], q[20] * 1e-5, q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5,
               q[25] * 1e-5);
     }
   }
