@@ -346,51 +346,109 @@ DFM_DEV void lp_chain(double &g, double &gm, const double a0, const double *Gr, 
   lp_chain_step<0, S>(g, gm, a0, Gr, lam);
 }
 
+// Wave-pipeline state of a sweep (LDS; monotone counters of blocks).
+struct LpPipe {
+  int rdy;                 // wave 1: blocks whose gradients are complete (the next chain may start)
+  int grc;                 // wave 0: blocks whose chain has ended (their s_gb block is no longer read)
+  int pub;                 // wave 0: blocks whose deltas it has published (s_dr / s_gmr slot k & 1)
+  int gbw;                 // waves 2..7: s_gb fills (6 per block)
+  int cons[LP_NT / 64];    // per wave: published blocks it has finished with
+  int nch[2];              // changes in the published block (slot)
+  int err;                 // a spin timed out
+};
+DFM_DEV void lp_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// spin (every lane of the wave) until *f >= target; LDS reads are in order per wave
+DFM_DEV void lp_wait(const int *f, int target, LpPipe *pp, long long tmo) {
+  const volatile int *vf = f;
+  if (*vf < target) {
+    const long long t0 = wall_clock64();
+    while (*vf < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
+    }
+  }
+  asm volatile("" ::: "memory");
+}
+DFM_DEV void lp_post(int *f, int v) {   // after this wave's LDS writes
+  lp_lds_fence();
+  if ((threadIdx.x & 63) == 0) *(volatile int *)f = v;
+}
+DFM_DEV int lp_min_cons(const LpPipe *pp, int w0) {
+  const volatile int *c = pp->cons;
+  int m = INT_MAX;
+  for (int w = w0; w < LP_NT / 64; ++w) m = min(m, c[w]);
+  return m;
+}
+DFM_DEV void lp_wait_cons(LpPipe *pp, int w0, int target, long long tmo) {
+  if (lp_min_cons(pp, w0) < target) {
+    const long long t0 = wall_clock64();
+    while (lp_min_cons(pp, w0) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
+    }
+  }
+  asm volatile("" ::: "memory");
+}
+
 // One pass over n active positions from block bstart on, in entry order
 // (!ORD) or in coordinate-index order (ORD, ord = s_srt: elnet1's full pass,
 // which appends every change (coordinate, delta) to kl / dl in visit order
 // and snapshots (g, a) of the active set and {R^2, changes, n} at every
 // block start, the restart points of the pass).  All threads call it.
 //
-// Per block of 64 sweep positions: wave 0 runs the serial coordinate steps
-// (lane t = one coordinate, its column of the block's G_AA in registers from
-// the LDS copy s_gb, deltas broadcast by readlane); meanwhile waves 1..7 load
-// the NEXT block's G_AA block (-> s_gb after the barrier) and, for their
-// gradient q, this block's 64 G_AA rows, so that the block's changes reach
-// every other active gradient without a memory round trip after the
-// barrier.  G_AA is private to this workgroup: plain loads (its L1 lines are
-// invalidated after every update of G_AA, see the entry step).  s_gb holds the
-// first block of the sweep order `key` when gkey == key (the last block
-// prefetches the next sweep's first).
+// Blocks of 64 sweep positions run as a wave pipeline with LDS counters
+// instead of workgroup barriers:
+//   wave 0     the serial coordinate steps of block k (lane t = one
+//              coordinate, its column of the block's G_AA in registers from
+//              the LDS copy s_gb, deltas broadcast by readlane), then
+//              publishes the block's deltas and visit gradients;
+//   wave 1     applies block k's deltas to the 64 gradients of block k + 1
+//              first (their G_AA rows prefetched during the chain), which
+//              releases wave 0 into block k + 1, then the R^2 bookkeeping;
+//   waves 2..7 refill s_gb with block k + 1's G_AA block as soon as wave 0's
+//              chain of block k ends, and apply block k's deltas to every
+//              other active gradient (rows prefetched) while wave 0 runs
+//              block k + 1.
+// Every gradient receives the blocks' changes in visit order (wave 1 waits
+// for waves 2..7 to finish block k - 1 before it applies block k), so the
+// arithmetic is elnet1's.  G_AA is private to this workgroup: plain loads
+// (its L1 lines are invalidated after every update of G_AA, see the entry
+// step).  s_gb holds the first block of the sweep order `key` when
+// gkey == key (the last block prefetches the next sweep's first).
 template <bool ORD>
 DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, int &gkey, const double *GAA, int ldaa,
-                      const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_d, double *s_gb,
-                      double *s_log, double *s_sc, int *s_nc, int *kl, double *dl, double *snapL, double *snapR,
-                      long long *tk) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), u = tid - 64;
+                      const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_dr, double *s_gmr,
+                      double *s_gb, LpPipe *pp, double *s_sc, int *s_nc, int *kl, double *dl, double *snapL,
+                      double *snapR, long long tmo, long long *tk) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (n <= 0) return;
   if (gkey != key || bstart != 0) {
     lp_gblock_load<ORD>(ord, LP_B * bstart, n, GAA, ldaa, s_gb);
-    __syncthreads();
     gkey = key;
   }
-  double dlx_l = 0.0;
-  for (int b0 = LP_B * bstart; b0 < n; b0 += LP_B) {
-    const int bn = b0 / LP_B + 1;   // the next block start's snapshot slot
-    const int nb = min(LP_B, n - b0);
-    const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);
-    long long t0 = tk && tid == 0 ? wall_clock64() : 0;
-    // wave-uniform branches, each with its own barrier (every wave reaches one)
-    if (wave == 0) {
+  if (tid < (int)(sizeof(LpPipe) / 4)) reinterpret_cast<int *>(pp)[tid] = 0;
+  __syncthreads();
+  const int nbk = (n + LP_B - 1) / LP_B, K = nbk - bstart;
+  double *snG = snapL, *snA = snapL + ldaa;   // + bn * 2 ldaa
+  if (wave == 0) {
+    // ------------------------------------------------ the serial chain
+    for (int k = 0; k < K; ++k) {
+      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
+      long long t0 = tk && tid == 0 ? wall_clock64() : 0;
+      if (k > 0) {
+        lp_wait(&pp->rdy, k, pp, tmo);
+        lp_wait(&pp->gbw, 6 * k, pp, tmo);
+      }
+      long long t1 = 0;
+      if (tk && tid == 0) { t1 = wall_clock64(); tk[0] += t1 - t0; }
       const bool on = lane < nb;
       const int pt = on ? lp_at<ORD>(ord, b0 + lane) : 0;
       double g = on ? s_g[pt] : 0.0;
       const double a0 = on ? s_a[pt] : 0.0;
-      double Gr[LP_B];   // this lane's column of the block (rows: the block's coordinates)
+      double Gr[LP_B];
 #pragma unroll
       for (int s = 0; s < LP_B; ++s) Gr[s] = s_gb[s * LP_B + lane];
-      long long ta = 0;
-      if (tk && tid == 0) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ta = wall_clock64(); tk[4] += ta - t0; }
+      if (tk && tid == 0) { lp_lds_fence(); t0 = wall_clock64(); tk[4] += t0 - t1; }
       double gm = 0.0;
       switch ((nb + 15) >> 4) {
         case 1: lp_chain<16>(g, gm, a0, Gr, lam); break;
@@ -398,7 +456,8 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
         case 3: lp_chain<48>(g, gm, a0, Gr, lam); break;
         default: lp_chain<64>(g, gm, a0, Gr, lam); break;
       }
-      if (tk && tid == 0) tk[5] += wall_clock64() - ta;
+      lp_post(&pp->grc, k + 1);   // (the chain has consumed every Gr read: s_gb may be refilled)
+      if (tk && tid == 0) { t1 = wall_clock64(); tk[5] += t1 - t0; }
       // this lane's step, recomputed from its gradient at the visit (same operations)
       const double uu = gm + a0;
       const double vv = fabs(uu) - lam;
@@ -407,29 +466,86 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
       const bool ch = dv != 0.0;
       const double a = ch ? na : a0;
       if (on) { s_g[pt] = g; s_a[pt] = a; }
-      s_d[lane] = dv;
       const unsigned long long bal = __ballot(ch);
-      if (lane == 0) s_sc[2] = (double)__popcll(bal);
-      if (ORD) {   // changes in visit order
+      if (k >= 2) lp_wait_cons(pp, 1, k - 1, tmo);   // slot k & 1 free: block k - 2 consumed by waves 1..7
+      s_dr[(k & 1) * LP_B + lane] = dv;
+      s_gmr[(k & 1) * LP_B + lane] = gm;
+      if (lane == 0) pp->nch[k & 1] = __popcll(bal);
+      if (ORD) {   // changes in visit order; this block's coordinates at the next block start
         const int base = *s_nc;
         if (ch) {
           const int o = base + __popcll(bal & ((1ull << lane) - 1ull));
           kl[o] = s_ia[pt];
           dl[o] = dv;
         }
-        if (lane == 0) *s_nc = base + __popcll(bal);
+        if (lane == 0) {
+          *s_nc = base + __popcll(bal);
+          snapR[bn * 4 + 1] = (double)(base + __popcll(bal));
+          snapR[bn * 4 + 2] = (double)n;
+        }
+        if (on) {
+          snG[(int64_t)bn * 2 * ldaa + pt] = g;
+          snA[(int64_t)bn * 2 * ldaa + pt] = a;
+        }
       }
-      long long tb = 0;
-      if (tk && tid == 0) { tb = wall_clock64(); tk[6] += tb - ta; }
-      __syncthreads();
-      if (tk && tid == 0) tk[7] += wall_clock64() - tb;
-      if (tk && tid == 0) { const long long t1 = wall_clock64(); tk[0] += t1 - t0; t0 = t1; tk[2] += 1; }
-      const long long tr = tk && tid == 0 ? wall_clock64() : 0;
-      dlx_l = fmax(dlx_l, dv * dv);   // max d^2: per lane, reduced once per sweep
-      if (bal) {   // R^2, a sequential sum in visit order, while waves 1..7 update
-        // (an unchanged coordinate adds t = 0 * x = +-0: rsq >= 0 is unchanged)
-        const double t = dv * (2.0 * gm - dv);
-        double rsq = s_sc[0];
+      lp_post(&pp->pub, k + 1);
+      if (tk && tid == 0) { tk[6] += wall_clock64() - t1; tk[2] += 1; }
+    }
+  } else if (wave == 1) {
+    // ------------------------------------------------ next block first, R^2
+    double rsq = s_sc[0], dlx_l = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
+      const bool urg = k + 1 < K;
+      const int b1 = b0 + LP_B, nb1 = urg ? min(LP_B, n - b1) : 0;
+      const bool qon = lane < nb1;
+      const int qq = urg ? lp_at<ORD>(ord, b1 + min(lane, nb1 - 1)) : 0;   // block k + 1's gradient (entry position)
+      double pv[LP_B];
+      if (urg) {
+#pragma unroll
+        for (int s = 0; s < LP_B; ++s) {
+          const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s, nb - 1))) * ldaa;
+          pv[s] = (qon && s < nb) ? row[qq] : 0.0;
+        }
+      }
+      lp_wait(&pp->pub, k + 1, pp, tmo);
+      const int nch = pp->nch[k & 1];
+      const double *dr = s_dr + (k & 1) * LP_B;
+      if (urg) {
+        lp_wait_cons(pp, 2, k, tmo);   // waves 2..7 have applied block k - 1 to these gradients
+        if (qon) {
+          double gq = s_g[qq];
+          if (nch) {
+            const double2 *d2 = reinterpret_cast<const double2 *>(dr);
+#pragma unroll
+            for (int c = 0; c < LP_B / 16; ++c) {
+              double2 dd[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) dd[i] = d2[8 * c + i];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                pv[16 * c + 2 * i] = pv[16 * c + 2 * i] * dd[i].x;
+                pv[16 * c + 2 * i + 1] = pv[16 * c + 2 * i + 1] * dd[i].y;
+              }
+            }
+#pragma unroll
+            for (int s = 0; s < LP_B; ++s) gq = gq - pv[s];
+            s_g[qq] = gq;
+          }
+          if (ORD) {
+            snG[(int64_t)bn * 2 * ldaa + qq] = gq;
+            snA[(int64_t)bn * 2 * ldaa + qq] = s_a[qq];
+          }
+        }
+        lp_post(&pp->rdy, k + 1);
+      }
+      // R^2, a sequential sum in visit order (an unchanged coordinate adds
+      // t = 0 * x = +-0: rsq >= 0 is unchanged), and max d^2 per lane
+      const double dv = dr[lane];
+      dlx_l = fmax(dlx_l, dv * dv);
+      if (nch) {
+        const double t = dv * (2.0 * s_gmr[(k & 1) * LP_B + lane] - dv);
+        const unsigned long long bal = __ballot(dv != 0.0);
         const int last = 63 - __builtin_clzll(bal);
 #pragma unroll
         for (int s0 = 0; s0 < LP_B; s0 += 16) {
@@ -437,115 +553,110 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
 #pragma unroll
           for (int s = s0; s < s0 + 16; ++s) rsq = rsq + lp_rdlane(t, s);
         }
-        if (lane == 0) s_sc[0] = rsq;
       }
-      if (ORD && lane == 0) {
-        snapR[bn * 4 + 0] = s_sc[0];
-        snapR[bn * 4 + 1] = (double)*s_nc;
-        snapR[bn * 4 + 2] = (double)n;
-      }
-      if (tk && tid == 0) tk[17] += wall_clock64() - tr;
-    } else {
-      double nx[LP_PF], pv[LP_B];
-      bool qon = false;
-      // every load unconditional (clamped to a valid entry, then selected):
-      // no branch between the loads and their use, so all stay in flight
+      if (ORD && lane == 0) snapR[bn * 4 + 0] = rsq;
+      lp_post(&pp->cons[1], k + 1);
+    }
 #pragma unroll
-      for (int i = 0; i < LP_PF; ++i) {   // the next block's G_AA block
-        const int e = u + (LP_NT - 64) * i, s = e >> 6, t = e & 63;
-        const double v =
-            GAA[(int64_t)lp_at<ORD>(ord, b1 + min(s, nb1 - 1)) * ldaa + lp_at<ORD>(ord, b1 + min(t, nb1 - 1))];
-        nx[i] = (e < LP_B * LP_B && s < nb1 && t < nb1) ? v : 0.0;
+    for (int o = 32; o >= 1; o >>= 1) dlx_l = fmax(dlx_l, __shfl_xor(dlx_l, o));
+    if (lane == 0) { s_sc[0] = rsq; s_sc[1] = fmax(s_sc[1], dlx_l); }
+  } else {
+    // ------------------------------------------------ s_gb refill, the other gradients
+    constexpr int NW = LP_NT - 128, PF = (LP_B * LP_B + NW - 1) / NW;
+    const int v = tid - 128;
+    for (int k = 0; k < K; ++k) {
+      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
+      const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);   // (wraps to the next sweep's first)
+      const int u0 = k + 1 < K ? b0 + LP_B : n, u1 = k + 1 < K ? b0 + LP_B + nb1 : n;   // wave 1's block
+      double nx[PF], pv[LP_B];
+#pragma unroll
+      for (int i = 0; i < PF; ++i) {
+        const int e = v + NW * i, s = e >> 6, t = e & 63;
+        nx[i] = (e < LP_B * LP_B && s < nb1 && t < nb1)
+                    ? GAA[(int64_t)lp_at<ORD>(ord, b1 + s) * ldaa + lp_at<ORD>(ord, b1 + t)] : 0.0;
       }
-      const int q = u, qq = min(q, n - 1);   // gradient (entry position) q: this block's rows of G_AA at column q
+      const int q = v, qq = min(q, n - 1);   // gradient (entry position) q
+      bool qon = false;
       if (q < n) {
         const int rq = ORD ? s_rank[q] : q;
-        qon = rq < b0 || rq >= b0 + nb;
+        qon = (rq < b0 || rq >= b0 + nb) && (rq < u0 || rq >= u1);
       }
 #pragma unroll
-      for (int s = 0; s < LP_B; ++s) {   // row base uniform (scalar), column offset per lane
+      for (int s = 0; s < LP_B; ++s) {
         const double *row = GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s, nb - 1))) * ldaa;
         pv[s] = (qon && s < nb) ? row[qq] : 0.0;
       }
-      __syncthreads();
-      const long long tw = tk && tid == 64 ? wall_clock64() : 0;
-      const int nch = (int)s_sc[2];
+      lp_wait(&pp->grc, k + 1, pp, tmo);   // wave 0's chain of block k has ended
 #pragma unroll
-      for (int i = 0; i < LP_PF; ++i) {
-        const int e = u + (LP_NT - 64) * i;
+      for (int i = 0; i < PF; ++i) {
+        const int e = v + NW * i;
         if (e < LP_B * LP_B) s_gb[e] = nx[i];
       }
-      if (qon && nch) {   // elnet1's eager updates, in visit order (d = 0: g - G * 0 == g)
-        // products first (the deltas read 16 at a time, 8 wide LDS reads in
-        // flight), then the subtractions in visit order
-        const double2 *sd2 = reinterpret_cast<const double2 *>(s_d);
-#pragma unroll
-        for (int c = 0; c < LP_B / 16; ++c) {
-          double2 dd[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) dd[i] = sd2[8 * c + i];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            pv[16 * c + 2 * i] = pv[16 * c + 2 * i] * dd[i].x;
-            pv[16 * c + 2 * i + 1] = pv[16 * c + 2 * i + 1] * dd[i].y;
-          }
-        }
-        double gq = s_g[u];
-#pragma unroll
-        for (int s = 0; s < LP_B; ++s) gq = gq - pv[s];
-        s_g[u] = gq;
-      }
-      if (ORD && u < n) {   // this gradient at the next block start
-        snapL[(int64_t)bn * 2 * ldaa + u] = s_g[u];
-        snapL[((int64_t)bn * 2 + 1) * ldaa + u] = s_a[u];
-      }
-      if (tk && tid == 64) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tk[16] += wall_clock64() - tw; }
-    }
-    const int nch = (int)s_sc[2];
-    if ((nch || ORD) && n > LP_NT - 64) {   // gradients past the prefetched ones: loads after the serial steps
-      for (int q = LP_NT - 64 + tid; q < n; q += blockDim.x) {
-        const int rq = ORD ? s_rank[q] : q;
-        if (nch == 0 || (rq >= b0 && rq < b0 + nb)) {
-          if (ORD) {
-            snapL[(int64_t)bn * 2 * ldaa + q] = s_g[q];
-            snapL[((int64_t)bn * 2 + 1) * ldaa + q] = s_a[q];
-          }
-          continue;
-        }
+      lp_lds_fence();
+      if (lane == 0) atomicAdd(&pp->gbw, 1);
+      lp_wait(&pp->pub, k + 1, pp, tmo);
+      const int nch = pp->nch[k & 1];
+      const double *dr = s_dr + (k & 1) * LP_B;
+      if (qon) {
         double gq = s_g[q];
-        for (int s0 = 0; s0 < nb; s0 += 32) {
-          double gv[32];
+        if (nch) {   // elnet1's eager updates, in visit order (d = 0: g - G * 0 == g)
+          const double2 *d2 = reinterpret_cast<const double2 *>(dr);
 #pragma unroll
-          for (int w = 0; w < 32; ++w) {
-            const double *row =
-                GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s0 + w, nb - 1))) * ldaa;
-            gv[w] = row[q];
+          for (int c = 0; c < LP_B / 16; ++c) {
+            double2 dd[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dd[i] = d2[8 * c + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              pv[16 * c + 2 * i] = pv[16 * c + 2 * i] * dd[i].x;
+              pv[16 * c + 2 * i + 1] = pv[16 * c + 2 * i + 1] * dd[i].y;
+            }
           }
 #pragma unroll
-          for (int w = 0; w < 32; ++w) gq = gq - gv[w] * s_d[s0 + w];   // s_d = 0 past the block
+          for (int s = 0; s < LP_B; ++s) gq = gq - pv[s];
+          s_g[q] = gq;
         }
-        s_g[q] = gq;
         if (ORD) {
-          snapL[(int64_t)bn * 2 * ldaa + q] = gq;
-          snapL[((int64_t)bn * 2 + 1) * ldaa + q] = s_a[q];
+          snG[(int64_t)bn * 2 * ldaa + q] = gq;
+          snA[(int64_t)bn * 2 * ldaa + q] = s_a[q];
         }
       }
-    }
-    __syncthreads();
-    if (tk && tid == 0) { tk[1] += wall_clock64() - t0; tk[3] += nch; }
-  }
-  if (wave == 0) {
+      for (int q2 = NW + v; q2 < n; q2 += NW) {   // gradients past the prefetched ones
+        const int rq = ORD ? s_rank[q2] : q2;
+        if ((rq >= b0 && rq < b0 + nb) || (rq >= u0 && rq < u1)) continue;
+        double gq = s_g[q2];
+        if (nch) {
+          for (int s0 = 0; s0 < nb; s0 += 32) {
+            double gv[32];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dlx_l = fmax(dlx_l, __shfl_xor(dlx_l, o));
-    if (lane == 0) s_sc[1] = fmax(s_sc[1], dlx_l);
+            for (int w = 0; w < 32; ++w) {
+              const double *row =
+                  GAA + (int64_t)__builtin_amdgcn_readfirstlane(lp_at<ORD>(ord, b0 + min(s0 + w, nb - 1))) * ldaa;
+              gv[w] = row[q2];
+            }
+#pragma unroll
+            for (int w = 0; w < 32; ++w) gq = gq - gv[w] * dr[s0 + w];   // dr = 0 past the block
+          }
+          s_g[q2] = gq;
+        }
+        if (ORD) {
+          snG[(int64_t)bn * 2 * ldaa + q2] = gq;
+          snA[(int64_t)bn * 2 * ldaa + q2] = s_a[q2];
+        }
+      }
+      lp_post(&pp->cons[wave], k + 1);
+    }
   }
+  long long te = tk && tid == 0 ? wall_clock64() : 0;
   __syncthreads();
+  if (tk && tid == 0) tk[1] += wall_clock64() - te;
 }
 
 __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[3 * LP_LMAX * 4 + 2 * LP_LMAX * 8];
-  __shared__ __attribute__((aligned(16))) double s_d[LP_B];
-  __shared__ double s_sc[4], s_gb[LP_B * LP_B], s_log[2 * LP_B];
+  __shared__ __attribute__((aligned(16))) double s_d[2 * LP_B];   // sweeps: the delta ring
+  __shared__ double s_sc[4], s_gb[LP_B * LP_B], s_log[2 * LP_B];  // sweeps: s_log = the visit-gradient ring
+  __shared__ LpPipe s_pp;
   __shared__ int s_i[8], s_cnt[LP_NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
@@ -617,7 +728,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   const double *snC = A.snapC + (int64_t)f * LP_NCH * p;
   double *bp = A.bpath + (int64_t)f * nlam * p;
   for (int j = tid; j < p; j += blockDim.x) { lp_st(g2 + j, c[j]); lp_sti(isact + j, 0); }
-  if (tid == 0) { s_sc[0] = 0.0; s_sc[1] = 0.0; s_i[1] = 0; s_i[2] = 0; }
+  if (tid == 0) { s_sc[0] = 0.0; s_sc[1] = 0.0; s_i[1] = 0; s_i[2] = 0; s_pp.err = 0; }
   int seq = 0, gcur = 0, nlp = 0, iz = 0, L = nlam, st = 0, fail_m = nlam, nin = 0;
   int ver = 0, gkey = -1;   // active-set version (entries); the sweep order s_gb's block belongs to
   // publish a task to the helpers and wait for all of them (H == 0: run it here)
@@ -681,10 +792,11 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         for (;;) {
           __syncthreads();
           ptick(6);
-          lp_sweep<true>(s_srt, nin, rsb, lam, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
-                         s_sc, &s_i[1], kl, dl, snL, snR, tk);
+          lp_sweep<true>(s_srt, nin, rsb, lam, 2 * ver + 1, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_log, s_gb,
+                         &s_pp, s_sc, &s_i[1], kl, dl, snL, snR, A.tmo, tk);
           ptick(0);
           if (tid == 0) { pacc[16] += 1; pacc[17] += nin - LP_B * rsb; }
+          if (s_pp.err) { st = 3; fail_m = m; break; }
           if (!run_task(LP_FULL, s_i[1], lam, c0)) { st = 3; fail_m = m; break; }
           ptick(1);
           const int v = s_i[3];
@@ -808,10 +920,11 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         if (tid == 0) s_sc[1] = 0.0;
         __syncthreads();
         ptick(6);
-        lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_gb, s_log,
-                        s_sc, &s_i[1], kl, dl, nullptr, nullptr, tk);
+        lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_log, s_gb,
+                        &s_pp, s_sc, &s_i[1], kl, dl, nullptr, nullptr, A.tmo, tk);
         ptick(2);
         if (tid == 0) { pacc[18] += 1; pacc[19] += nin; }
+        if (s_pp.err) { st = 3; fail_m = m; break; }
         if (s_sc[1] < A.thr) break;
         if (nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
@@ -864,11 +977,9 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   }
   run_task(LP_EXIT, 0, 0.0, 0);
   ptick(6);
-  if (A.prof && tid == 64) A.prof[(int64_t)f * LP_PROF + 24] = pacc[24];
   if (A.prof && tid == 0) {
     pacc[7] = nin;
     for (int i = 0; i < 20; ++i) A.prof[(int64_t)f * LP_PROF + i] = pacc[i];
-    A.prof[(int64_t)f * LP_PROF + 25] = pacc[25];
   }
   if (tid == 0) {
     A.status[f] = st;
@@ -983,12 +1094,11 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
       const long long *q = hp.data() + f * LP_PROF;
       fprintf(stderr, "[lasso prof] problem %2d H %d: full-pass sweeps %.2f ms, FULL replays %.2f, active passes %.2f, "
               "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
-              "blocks %lld: serial %.2f ms (Gr %.2f, chain %.2f, post %.2f, barrier %.2f), update %.2f ms, changes %lld | helper 0: FULL %lld "
-              "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms | wave 1 update %.2f ms, "
-              "wave 0 R^2 %.2f ms\n", f, H, q[0] * 1e-5,
-              q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10], q[8] * 1e-5,
-              q[12] * 1e-5, q[13] * 1e-5, (q[14] - q[13]) * 1e-5, q[15] * 1e-5, q[9] * 1e-5, q[11], q[21], q[22], q[27], q[20] * 1e-5, q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5,
-              q[25] * 1e-5);
+              "blocks %lld: wave 0 wait %.2f ms, Gr %.2f, chain %.2f, post %.2f, drain %.2f | helper 0: FULL %lld "
+              "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms\n", f, H,
+              q[0] * 1e-5, q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10],
+              q[8] * 1e-5, q[12] * 1e-5, q[13] * 1e-5, q[14] * 1e-5, q[9] * 1e-5, q[21], q[22], q[27], q[20] * 1e-5,
+              q[26] * 1e-5, q[23] * 1e-5);
     }
   }
   if (e == hipSuccess) {   // a timed-out problem: report its control block
