@@ -508,11 +508,14 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           pv[s] = (qon && s < nb) ? row[qq] : 0.0;
         }
       }
+      long long w0 = tk && tid == 64 ? wall_clock64() : 0;
       lp_wait(&pp->pub, k + 1, pp, tmo);
+      if (tk && tid == 64) { const long long w1 = wall_clock64(); tk[16] += w1 - w0; w0 = w1; }
       const int nch = pp->nch[k & 1];
       const double *dr = s_dr + (k & 1) * LP_B;
       if (urg) {
         lp_wait_cons(pp, 2, k, tmo);   // waves 2..7 have applied block k - 1 to these gradients
+        if (tk && tid == 64) { const long long w1 = wall_clock64(); tk[17] += w1 - w0; w0 = w1; }
         if (qon) {
           double gq = s_g[qq];
           if (nch) {
@@ -538,6 +541,7 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           }
         }
         lp_post(&pp->rdy, k + 1);
+        if (tk && tid == 64) tk[20] += wall_clock64() - w0;
       }
       // R^2, a sequential sum in visit order (an unchanged coordinate adds
       // t = 0 * x = +-0: rsq >= 0 is unchanged), and max d^2 per lane
@@ -977,6 +981,11 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   }
   run_task(LP_EXIT, 0, 0.0, 0);
   ptick(6);
+  if (A.prof && tid == 64) {
+    A.prof[(int64_t)f * LP_PROF + 24] = pacc[24];
+    A.prof[(int64_t)f * LP_PROF + 25] = pacc[25];
+    A.prof[(int64_t)f * LP_PROF + 28] = pacc[28];
+  }
   if (A.prof && tid == 0) {
     pacc[7] = nin;
     for (int i = 0; i < 20; ++i) A.prof[(int64_t)f * LP_PROF + i] = pacc[i];
@@ -1095,10 +1104,11 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
       fprintf(stderr, "[lasso prof] problem %2d H %d: full-pass sweeps %.2f ms, FULL replays %.2f, active passes %.2f, "
               "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
               "blocks %lld: wave 0 wait %.2f ms, Gr %.2f, chain %.2f, post %.2f, drain %.2f | helper 0: FULL %lld "
-              "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms\n", f, H,
+              "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms | wave 1: wait pub %.2f, "
+              "wait bulk %.2f, urgent %.2f\n", f, H,
               q[0] * 1e-5, q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10],
               q[8] * 1e-5, q[12] * 1e-5, q[13] * 1e-5, q[14] * 1e-5, q[9] * 1e-5, q[21], q[22], q[27], q[20] * 1e-5,
-              q[26] * 1e-5, q[23] * 1e-5);
+              q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5, q[25] * 1e-5, q[28] * 1e-5);
     }
   }
   if (e == hipSuccess) {   // a timed-out problem: report its control block
