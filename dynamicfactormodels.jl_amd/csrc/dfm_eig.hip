@@ -1576,10 +1576,6 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
   zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, rep, ab, aacc, sred);
 }
 
-static bool gemm_compact_enabled() {   // DFM_GEMM_COMPACT=0: A/B switch
-  static const bool on = [] { const char *e = getenv("DFM_GEMM_COMPACT"); return !(e && e[0] == '0'); }();
-  return on;
-}
 // Ascending list of the still-active replicates (done == 0) and their count,
 // one 1024-thread workgroup: per-thread chunk counts, an LDS scan, in-order
 // writes.  Feeds the compacted H.Z GEMM of the straggler phase.
@@ -1677,7 +1673,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       // and compact the GEMMs to the stragglers' columns
       const bool tail = (int64_t)a * 8 < nb;
       next_poll = it + (tail ? 1 : poll);
-      if (tail && !cl_on && gemm_compact_enabled()) {
+      if (tail && !cl_on) {
         hipLaunchKernelGGL(active_list_kernel, dim3(1), dim3(1024), 0, st, w.done, nb, alist, acount);
         cl_on = true;
       }
