@@ -26,8 +26,10 @@ step trace_direct 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_dir
 step configs 600 python -u tools/bench_configs.py --configs c1,c2,c4,c5 --reps 3
 cat "$OUT/configs.out"
 step trace_c2 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 2
-step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffic.json"
+# last: rocprofv3 writes this trace's CSVs and then segfaults in its own exit
+# path after the cooperative lasso launch (exit 139, results complete)
+step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
 echo ALLDONE
