@@ -354,6 +354,8 @@ struct LpPipe {
   int gbw;                 // waves 2..7: s_gb fills (6 per block)
   int cons[LP_NT / 64];    // per wave: published blocks it has finished with
   int nch[2];              // changes in the published block (slot)
+  int stop;                // wave 0: 1 + the index of the last block (entry-order passes: dlx < thr or budget)
+  int nsw;                 // wave 0: sweeps done
   int err;                 // a spin timed out
 };
 DFM_DEV void lp_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -419,7 +421,7 @@ template <bool ORD>
 DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, int &gkey, const double *GAA, int ldaa,
                       const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_dr, double *s_gmr,
                       double *s_gb, LpPipe *pp, double *s_sc, int *s_nc, int *kl, double *dl, double *snapL,
-                      double *snapR, long long tmo, long long *tk) {
+                      double *snapR, long long tmo, long long *tk, int maxsw = 1, double thr = 0.0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (n <= 0) return;
   if (gkey != key || bstart != 0) {
@@ -428,15 +430,22 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
   }
   if (tid < (int)(sizeof(LpPipe) / 4)) reinterpret_cast<int *>(pp)[tid] = 0;
   __syncthreads();
-  const int nbk = (n + LP_B - 1) / LP_B, K = nbk - bstart;
+  // ORD: one pass from block bstart.  !ORD: elnet1's passes over the active
+  // set back to back, the pipeline running on across pass boundaries (block
+  // k is block k mod nbk of pass k / nbk), until wave 0 finds a pass with
+  // max d^2 < thr or maxsw passes are done
+  const int nbk = (n + LP_B - 1) / LP_B, K = ORD ? nbk - bstart : INT_MAX;
+  const bool nxt = ORD ? false : nbk > 1;   // !ORD: the next block always exists (and differs)
   double *snG = snapL, *snA = snapL + ldaa;   // + bn * 2 ldaa
   if (wave == 0) {
     // ------------------------------------------------ the serial chain
+    double dlx_s = 0.0;   // !ORD: this pass's max d^2 per lane
+    int sw = 0;
     for (int k = 0; k < K; ++k) {
-      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
+      const int bk = (bstart + k) % nbk, b0 = LP_B * bk, nb = min(LP_B, n - b0), bn = bk + 1;
       long long t0 = tk && tid == 0 ? wall_clock64() : 0;
       if (k > 0) {
-        lp_wait(&pp->rdy, k, pp, tmo);
+        if (ORD || nxt) lp_wait(&pp->rdy, k, pp, tmo);
         lp_wait(&pp->gbw, 6 * k, pp, tmo);
       }
       long long t1 = 0;
@@ -488,16 +497,30 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           snA[(int64_t)bn * 2 * ldaa + pt] = a;
         }
       }
+      bool last = false;
+      if (!ORD) {
+        dlx_s = fmax(dlx_s, dv * dv);
+        if (bk == nbk - 1) {   // end of a pass: converged, or the pass budget spent?
+          double mx = dlx_s;
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+          ++sw;
+          last = mx < thr || sw >= maxsw;
+          if (lane == 0) { s_sc[1] = mx; pp->nsw = sw; if (last) pp->stop = k + 1; }
+          dlx_s = 0.0;
+        }
+      }
       lp_post(&pp->pub, k + 1);
       if (tk && tid == 0) { tk[6] += wall_clock64() - t1; tk[2] += 1; }
+      if (last) break;
     }
   } else if (wave == 1) {
     // ------------------------------------------------ next block first, R^2
     double rsq = s_sc[0], dlx_l = 0.0;
     for (int k = 0; k < K; ++k) {
-      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
-      const bool urg = k + 1 < K;
-      const int b1 = b0 + LP_B, nb1 = urg ? min(LP_B, n - b1) : 0;
+      const int bk = (bstart + k) % nbk, b0 = LP_B * bk, nb = min(LP_B, n - b0), bn = bk + 1;
+      const bool urg = ORD ? k + 1 < K : nxt;
+      const int b1 = LP_B * ((bk + 1) % nbk), nb1 = urg ? min(LP_B, n - b1) : 0;
       const bool qon = lane < nb1;
       const int qq = urg ? lp_at<ORD>(ord, b1 + min(lane, nb1 - 1)) : 0;   // block k + 1's gradient (entry position)
       double pv[LP_B];
@@ -559,19 +582,24 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
         }
       }
       if (ORD && lane == 0) snapR[bn * 4 + 0] = rsq;
+      const bool fin = !ORD && *(volatile int *)&pp->stop == k + 1;   // (set before pub(k + 1))
       lp_post(&pp->cons[1], k + 1);
+      if (fin) break;
     }
+    if (ORD) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dlx_l = fmax(dlx_l, __shfl_xor(dlx_l, o));
-    if (lane == 0) { s_sc[0] = rsq; s_sc[1] = fmax(s_sc[1], dlx_l); }
+      for (int o = 32; o >= 1; o >>= 1) dlx_l = fmax(dlx_l, __shfl_xor(dlx_l, o));
+    }
+    if (lane == 0) { s_sc[0] = rsq; if (ORD) s_sc[1] = fmax(s_sc[1], dlx_l); }
   } else {
     // ------------------------------------------------ s_gb refill, the other gradients
     constexpr int NW = LP_NT - 128, PF = (LP_B * LP_B + NW - 1) / NW;
     const int v = tid - 128;
     for (int k = 0; k < K; ++k) {
-      const int b0 = LP_B * (bstart + k), nb = min(LP_B, n - b0), bn = bstart + k + 1;
-      const int b1 = b0 + LP_B < n ? b0 + LP_B : 0, nb1 = min(LP_B, n - b1);   // (wraps to the next sweep's first)
-      const int u0 = k + 1 < K ? b0 + LP_B : n, u1 = k + 1 < K ? b0 + LP_B + nb1 : n;   // wave 1's block
+      const int bk = (bstart + k) % nbk, b0 = LP_B * bk, nb = min(LP_B, n - b0), bn = bk + 1;
+      const int b1 = LP_B * ((bk + 1) % nbk), nb1 = min(LP_B, n - b1);   // (wraps to the next sweep's first)
+      const bool urg = ORD ? k + 1 < K : nxt;
+      const int u0 = urg ? b1 : n, u1 = urg ? b1 + nb1 : n;   // wave 1's block
       double nx[PF], pv[LP_B];
 #pragma unroll
       for (int i = 0; i < PF; ++i) {
@@ -648,7 +676,9 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           snA[(int64_t)bn * 2 * ldaa + q2] = s_a[q2];
         }
       }
+      const bool fin = !ORD && *(volatile int *)&pp->stop == k + 1;   // (set before pub(k + 1))
       lp_post(&pp->cons[wave], k + 1);
+      if (fin) break;
     }
   }
   long long te = tk && tid == 0 ? wall_clock64() : 0;
@@ -806,6 +836,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           const int v = s_i[3];
           if (v == INT_MAX) break;
           if (nin >= cap) { st = 2; fail_m = m; break; }
+          const long long te0 = A.prof && tid == 0 ? wall_clock64() : 0;
           // ---- variable v enters at entry position nin
           const int pos = nin;
           for (int t = tid; t <= pos; t += blockDim.x) {
@@ -890,6 +921,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           if (tid == 0) { s_sc[0] = rsq_b; s_i[1] = nc_b; }
           rsb = bi;
           c0 = pos_v / LP_U;   // the replay's changes before v's visit are unchanged
+          if (A.prof && tid == 0) { pacc[29] += wall_clock64() - te0; pacc[30] += 1; }
         }
         if (st) break;
         {   // the pass's max d^2: over its changes
@@ -918,21 +950,24 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       // ---------------- passes over the active set (entry order)
       for (int t = tid; t < nin; t += blockDim.x) lp_st(sv + t, s_a[t]);   // da start
       lp_drain();
-      for (;;) {
-        ++nlp;
+      {   // the passes until max d^2 < thr, as one pipelined run (nlp: elnet1's pass count)
         __syncthreads();
         if (tid == 0) s_sc[1] = 0.0;
-        __syncthreads();
         ptick(6);
-        lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_log, s_gb,
-                        &s_pp, s_sc, &s_i[1], kl, dl, nullptr, nullptr, A.tmo, tk);
+        if (nin > 0) {
+          lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_log, s_gb,
+                          &s_pp, s_sc, &s_i[1], kl, dl, nullptr, nullptr, A.tmo, tk, A.maxit + 1 - nlp, A.thr);
+        } else {
+          if (tid == 0) s_pp.nsw = 1;   // (no active variable: one empty pass, max d^2 = 0)
+          __syncthreads();
+        }
         ptick(2);
-        if (tid == 0) { pacc[18] += 1; pacc[19] += nin; }
+        const int nsw = s_pp.nsw;
+        nlp += nsw;
+        if (tid == 0) { pacc[18] += nsw; pacc[19] += (long long)nsw * nin; }
         if (s_pp.err) { st = 3; fail_m = m; break; }
-        if (s_sc[1] < A.thr) break;
-        if (nlp > A.maxit) { st = 1; fail_m = m; break; }
+        if (!(s_sc[1] < A.thr) && nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
-      if (st) break;
       // ---------------- refresh: g_j -= dot(da, c_j,A) over the non-active j
       if (tid == 0) s_i[1] = 0;
       __syncthreads();
@@ -986,6 +1021,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     A.prof[(int64_t)f * LP_PROF + 25] = pacc[25];
     A.prof[(int64_t)f * LP_PROF + 28] = pacc[28];
   }
+  if (A.prof && tid == 0) { A.prof[(int64_t)f * LP_PROF + 29] = pacc[29]; A.prof[(int64_t)f * LP_PROF + 30] = pacc[30]; }
   if (A.prof && tid == 0) {
     pacc[7] = nin;
     for (int i = 0; i < 20; ++i) A.prof[(int64_t)f * LP_PROF + i] = pacc[i];
@@ -1105,10 +1141,10 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
               "REFRESH %.2f, other %.2f; final |A| %lld | full sweeps %lld (sum n %lld), active sweeps %lld (sum n %lld), "
               "blocks %lld: wave 0 wait %.2f ms, Gr %.2f, chain %.2f, post %.2f, drain %.2f | helper 0: FULL %lld "
               "tasks, %lld changes (%lld replayed), busy %.2f ms (staging %.2f), REFRESH busy %.2f ms | wave 1: wait pub %.2f, "
-              "wait bulk %.2f, urgent %.2f\n", f, H,
+              "wait bulk %.2f, urgent %.2f | entries %lld: %.2f ms\n", f, H,
               q[0] * 1e-5, q[1] * 1e-5, q[2] * 1e-5, q[3] * 1e-5, q[6] * 1e-5, q[7], q[16], q[17], q[18], q[19], q[10],
               q[8] * 1e-5, q[12] * 1e-5, q[13] * 1e-5, q[14] * 1e-5, q[9] * 1e-5, q[21], q[22], q[27], q[20] * 1e-5,
-              q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5, q[25] * 1e-5, q[28] * 1e-5);
+              q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5, q[25] * 1e-5, q[28] * 1e-5, q[30], q[29] * 1e-5);
     }
   }
   if (e == hipSuccess) {   // a timed-out problem: report its control block
