@@ -837,25 +837,49 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
           if (v == INT_MAX) break;
           if (nin >= cap) { st = 2; fail_m = m; break; }
           const long long te0 = A.prof && tid == 0 ? wall_clock64() : 0;
-          // ---- variable v enters at entry position nin
-          const int pos = nin;
-          for (int t = tid; t <= pos; t += blockDim.x) {
-            const int col = t == pos ? v : s_ia[t];
-            const double val = G[(int64_t)v * p + col];
-            GAA[(int64_t)pos * ldaa + t] = val;
-            GAA[(int64_t)t * ldaa + pos] = val;
-          }
-          // index order: v's slot in s_srt (count of active indices below v),
-          // and v's visit in the change list (count of changes below v)
-          int below = 0, cbelow = 0;
+          // ---- variable v enters at entry position nin; the pass restarts
+          // from the block holding v's slot (the pass up to that block is
+          // unchanged).  Its snapshot (block 0: the pass start) gives the
+          // entries visited before; an entry not in the snapshot (v, or one
+          // that entered later than it was taken) sits past the block start,
+          // so it has a = 0 and the gradient after the first nc_b changes: its
+          // chunk snapshot (chunk 0: the pass-start gradient) plus the changes
+          // left, in visit order.  Three rounds of global loads: (1) v's row
+          // of G, the change list (counts below v and below the restart
+          // block's first coordinate) and the block record; (2) the
+          // snapshots and the changes past the chunk snapshot; (3) their G
+          // entries.
+          const int pos = nin, nc = s_i[1];
+          int below = 0;   // v's slot in the index order: active indices below v (LDS only)
           for (int t = tid; t < pos; t += blockDim.x) below += s_ia[t] < v ? 1 : 0;
-          for (int i = tid; i < s_i[1]; i += blockDim.x) cbelow += lp_ldi(kl + i) < v ? 1 : 0;
           below = (int)wave_sum((double)below);
-          cbelow = (int)wave_sum((double)cbelow);
-          if (lane == 0) { s_d[wave] = below; s_log[wave] = cbelow; }
+          if (lane == 0) s_d[wave] = below;
           __syncthreads();
-          int ins = 0, pos_v = 0;
-          for (int w2 = 0; w2 < LP_NT / 64; ++w2) { ins += (int)s_d[w2]; pos_v += (int)s_log[w2]; }
+          int ins = 0;
+          for (int w2 = 0; w2 < LP_NT / 64; ++w2) ins += (int)s_d[w2];
+          const int bi = ins / LP_B;
+          // the restart block's first coordinate (v's slot at the end of a full block: past every change)
+          const int cbi = bi == 0 ? 0 : (LP_B * bi < pos ? s_ia[s_srt[LP_B * bi]] : INT_MAX);
+          double rsq_b = rsq_save;
+          int n_snap = n_pass;
+          if (bi > 0) { rsq_b = lp_ld(snR + bi * 4 + 0); n_snap = (int)lp_ld(snR + bi * 4 + 2); }
+          int cbelow = 0, cblk = 0;
+          for (int t = tid; t <= pos || t < nc; t += blockDim.x) {
+            const double val = t <= pos ? G[(int64_t)v * p + (t == pos ? v : s_ia[t])] : 0.0;
+            const int kk = t < nc ? lp_ldi(kl + t) : INT_MAX;
+            if (t <= pos) {
+              GAA[(int64_t)pos * ldaa + t] = val;
+              GAA[(int64_t)t * ldaa + pos] = val;
+            }
+            cbelow += kk < v ? 1 : 0;
+            cblk += bi > 0 && kk < cbi ? 1 : 0;
+          }
+          cbelow = (int)wave_sum((double)cbelow);
+          cblk = (int)wave_sum((double)cblk);
+          if (lane == 0) { s_log[wave] = cbelow; s_log[8 + wave] = cblk; }
+          __syncthreads();
+          int pos_v = 0, nc_b = 0;   // changes before v's visit / before the restart block
+          for (int w2 = 0; w2 < LP_NT / 64; ++w2) { pos_v += (int)s_log[w2]; nc_b += (int)s_log[8 + w2]; }
           int tmp[LP_LMAX / LP_NT];
 #pragma unroll
           for (int i = 0; i < LP_LMAX / LP_NT; ++i) {
@@ -873,51 +897,47 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
             s_ia[pos] = v;
             lp_sti(isact + v, 1);
           }
-          __syncthreads();
-          for (int t = tid; t <= pos; t += blockDim.x) s_rank[s_srt[t]] = t;
           nin = pos + 1;
           ++ver;
-          lp_drain();
-          __syncthreads();
-          lp_acquire();   // this CU's L1 drops its G_AA lines (plain loads read the new row / column)
-          // ---- restart from the block holding v's slot: the pass up to that
-          // block is unchanged.  Its snapshot (block 0: the pass start) gives
-          // the entries visited before; an entry not in the snapshot (v, or
-          // one that entered later than it was taken) sits past the block
-          // start, so it has a = 0 and the gradient after the first nc_b
-          // changes: its chunk snapshot (chunk 0: the pass-start gradient)
-          // plus the changes left, in visit order.
-          const int bi = ins / LP_B;
-          const double rsq_b = bi == 0 ? rsq_save : lp_ld(snR + bi * 4 + 0);
-          const int nc_b = bi == 0 ? 0 : (int)lp_ld(snR + bi * 4 + 1);
-          const int n_snap = bi == 0 ? n_pass : (int)lp_ld(snR + bi * 4 + 2);
           const double *snG = bi == 0 ? sv + LP_LMAX : snL + (int64_t)bi * 2 * ldaa;
           const double *snA = bi == 0 ? sv : snL + ((int64_t)bi * 2 + 1) * ldaa;
           const double *gin = g2 + (int64_t)gcur * p;
           const int cb = nc_b / LP_U, nt = nc_b - LP_U * cb;   // chunk snapshot, changes past it (< LP_U)
           double *s_pd = s_log;                                  // (s_log is free between sweeps)
           int *s_pk = reinterpret_cast<int *>(s_log + LP_U);
-          for (int i = tid; i < nt; i += blockDim.x) { s_pk[i] = lp_ldi(kl + LP_U * cb + i); s_pd[i] = lp_ld(dl + LP_U * cb + i); }
           __syncthreads();
-          for (int t = tid; t < nin; t += blockDim.x) {
-            if (t < n_snap) {
-              s_a[t] = lp_ld(snA + t);
-              s_g[t] = lp_ld(snG + t);
-            } else {
-              const int j = s_ia[t];
-              double g = lp_ld(cb == 0 ? gin + j : snC + (int64_t)cb * p + j);
-              if (nt > 0) {
-                double gv[LP_U];
-#pragma unroll
-                for (int i = 0; i < LP_U; ++i) gv[i] = G[(int64_t)s_pk[min(i, nt - 1)] * p + j];
-#pragma unroll
-                for (int i = 0; i < LP_U; ++i)
-                  if (i < nt) g = g - gv[i] * s_pd[i];
-              }
-              s_a[t] = 0.0;
-              s_g[t] = g;
-            }
+          // (2) the snapshots, the entries past them, the changes past the chunk snapshot
+          double ra = 0.0, rg = 0.0;
+          const int t1 = tid < nin ? tid : nin - 1;   // nin <= LP_NT here: one entry per thread, else the loop below
+          if (tid < nt) { s_pk[tid] = lp_ldi(kl + LP_U * cb + tid); s_pd[tid] = lp_ld(dl + LP_U * cb + tid); }
+          if (t1 < n_snap) { ra = lp_ld(snA + t1); rg = lp_ld(snG + t1); }
+          else rg = lp_ld(cb == 0 ? gin + s_ia[t1] : snC + (int64_t)cb * p + s_ia[t1]);
+          for (int t = tid + LP_NT; t < nin; t += blockDim.x) {   // (more than LP_NT active)
+            if (t < n_snap) { s_a[t] = lp_ld(snA + t); s_g[t] = lp_ld(snG + t); }
+            else { s_a[t] = 0.0; s_g[t] = lp_ld(cb == 0 ? gin + s_ia[t] : snC + (int64_t)cb * p + s_ia[t]); }
           }
+          __syncthreads();
+          // (3) the entries past the snapshot: the changes left, in visit order
+          for (int t = tid; t < nin; t += blockDim.x) {
+            double g = t == tid ? rg : s_g[t];
+            const bool fresh = t >= n_snap;
+            if (fresh && nt > 0) {
+              const int j = s_ia[t];
+              double gv[LP_U];
+#pragma unroll
+              for (int i = 0; i < LP_U; ++i) gv[i] = G[(int64_t)s_pk[min(i, nt - 1)] * p + j];
+#pragma unroll
+              for (int i = 0; i < LP_U; ++i)
+                if (i < nt) g = g - gv[i] * s_pd[i];
+            }
+            if (t == tid) s_a[t] = fresh ? 0.0 : ra;
+            else if (fresh) s_a[t] = 0.0;
+            s_g[t] = g;
+          }
+          for (int t = tid; t <= nin - 1; t += blockDim.x) s_rank[s_srt[t]] = t;
+          lp_drain();
+          __syncthreads();
+          lp_acquire();   // this CU's L1 drops its G_AA lines (plain loads read the new row / column)
           if (tid == 0) { s_sc[0] = rsq_b; s_i[1] = nc_b; }
           rsb = bi;
           c0 = pos_v / LP_U;   // the replay's changes before v's visit are unchanged
