@@ -25,6 +25,8 @@
 namespace dfm {
 
 constexpr int EROWS = 64;  // rows per workgroup in gq/apply
+typedef double dv4 __attribute__((ext_vector_type(4)));
+DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
 struct EigWork {
   double *Q, *Y, *U;       // nb x m x P
@@ -392,19 +394,29 @@ DFM_DEV void wave_trinv(const double *Lo, const double *dinv, double *Li, const 
   __syncthreads();
 }
 
-// C = op(A) op(B) for P x P LDS matrices (TA/TB transpose flags); padded
-// entries are zero so the full P x P product is exact.
+// C = op(A) op(B) for P x P LDS matrices (TA/TB transpose flags; C distinct
+// from A and B); padded entries are zero so the full P x P product is exact.
+// One wave of v_mfma_f64_16x16x4 per 16 x 16 output tile: A operand = row
+// (lane & 15), k (lane >> 4); B operand = k (lane >> 4), column (lane & 15);
+// accumulator register g = row 4g + (lane >> 4), column (lane & 15).
 template <int P, bool TA, bool TB>
 DFM_DEV void wave_mm(const double *A, const double *B, double *C) {
-  constexpr int S = P + 1;
-  for (int e = threadIdx.x; e < P * P; e += 64) {
-    const int i = e / P, j = e % P;
-    double acc = 0.0;
+  constexpr int S = P + 1, NT = P / 16;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
-    for (int q = 0; q < P; ++q)
-      acc = fma(TA ? A[q * S + i] : A[i * S + q], TB ? B[j * S + q] : B[q * S + j], acc);
-    C[i * S + j] = acc;
-  }
+  for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) {
+      const int i = 16 * rt + li, j = 16 * ct + li;
+      dv4 acc = dv4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < P / 4; ++kk) {
+        const int q = 4 * kk + lk;
+        acc = mfma16(TA ? A[q * S + i] : A[i * S + q], TB ? B[j * S + q] : B[q * S + j], acc);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) C[(16 * rt + 4 * g + lk) * S + 16 * ct + li] = acc[g];
+    }
   __syncthreads();
 }
 
@@ -933,8 +945,6 @@ size_t fact_workspace_bytes(int T, int nb, int P) {
 // 4g .. 4g+3 in exactly the B-operand layout, so Q'Y etc. need no lane movement.
 // Reductions over waves run in a fixed order: bit-reproducible, batch-invariant.
 constexpr int F2_T_MAX = 4096;   // dynamic LDS of ap2: 16 T + 4 bytes
-typedef double dv4 __attribute__((ext_vector_type(4)));
-DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
 // Convergence verdict from per-column squared residuals res2[j] (j < k), on
 // one whole wave (same rules as check_converged: strict eigenvector-residual
