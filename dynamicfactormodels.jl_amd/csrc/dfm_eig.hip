@@ -394,6 +394,64 @@ DFM_DEV void wave_trinv(const double *Lo, const double *dinv, double *Li, const 
   __syncthreads();
 }
 
+DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compile-time constant in unrolled loops)
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Li = Lo^-1 of the lower Cholesky factor M = Lo Lo' (p x p), in registers:
+// lane i < P holds row i.  Right-looking factorisation (step j: pivot by
+// readlane, column j scaled by one reciprocal square root, the trailing rows
+// updated with the column broadcast lane by lane), then lane c forward-
+// substitutes column c of the inverse with the rows of Lo broadcast the same
+// way — no LDS round trip per step.  Tiny pivots -> dead (unit diagonal, zero
+// column, zero row of Li), as the LDS form it replaces.
+template <int P>
+DFM_DEV void wave_chol_inv(const double *M, double *Li, int *dead, int p) {
+  constexpr int S = P + 1;
+  const int lane = threadIdx.x;
+  double mx = 0.0;
+  for (int j = lane; j < p; j += 64) mx = fmax(mx, fabs(M[j * S + j]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  const double thresh = 1e-22 * mx;
+  double r[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) r[k] = (lane < p && k < p) ? M[min(lane, P - 1) * S + k] : 0.0;
+  double inv_l = 1.0;
+  int dead_l = 0;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    if (j < p) {
+      const double sj = rl64(r[j], j);
+      const bool dd = !(sj > thresh);
+      const double inv = dd ? 1.0 : rsqrt(sj);
+      double lij = (lane > j && lane < p) ? (dd ? 0.0 : r[j] * inv) : 0.0;
+      if (lane == j) { lij = dd ? 1.0 : sj * inv; inv_l = inv; dead_l = dd; }
+      r[j] = lij;
+#pragma unroll
+      for (int k = j + 1; k < P; ++k) r[k] = r[k] - lij * rl64(lij, k);
+    }
+  }
+  if (lane < P) dead[lane] = lane < p ? dead_l : 0;
+  double x[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    double sacc = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int q = 0; q < i; ++q) sacc = sacc - rl64(r[q], i) * x[q];
+    x[i] = (i < p) ? sacc * rl64(inv_l, i) : 0.0;
+  }
+  const bool dl = lane < p;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const bool di = __shfl(dead_l, i) != 0;
+    if (lane < P) Li[i * S + lane] = (i < p && dl && !di) ? x[i] : 0.0;
+  }
+  __syncthreads();
+}
+
 // C = op(A) op(B) for P x P LDS matrices (TA/TB transpose flags; C distinct
 // from A and B); padded entries are zero so the full P x P product is exact.
 // One wave of v_mfma_f64_16x16x4 per 16 x 16 output tile: A operand = row
@@ -463,9 +521,8 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   SMALL_STAMP(1);
   wave_sym<P>(sm.Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
-  wave_chol<P>(sm.Qq, sm.L, sm.dinv, sm.dead1, p);
+  wave_chol_inv<P>(sm.Qq, sm.Li, sm.dead1, p);
   SMALL_STAMP(2);
-  wave_trinv<P>(sm.L, sm.dinv, sm.Li, sm.dead1, p);
   SMALL_STAMP(3);
   wave_mm<P, false, false>(sm.Li, sm.Hq, sm.W);
   wave_mm<P, false, true>(sm.W, sm.Li, sm.Hq);
@@ -560,9 +617,8 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   wave_mm<P, true, false>(sm.A, sm.W, sm.Qq);
   wave_sym<P>(sm.Qq);
   SMALL_STAMP(7);
-  wave_chol<P>(sm.Qq, sm.L, sm.dinv, sm.dead2, p);
+  wave_chol_inv<P>(sm.Qq, sm.Li, sm.dead2, p);
   SMALL_STAMP(8);
-  wave_trinv<P>(sm.L, sm.dinv, sm.Li, sm.dead2, p);
   SMALL_STAMP(9);
   wave_mm<P, false, true>(sm.A, sm.Li, sm.W);   // Bm = A Li'
   for (int e = lane; e < P * P; e += 64) {
