@@ -33,6 +33,11 @@ DFM_DEV double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f64_16x16x4: A[i][k] at lane i + 16k, B[k][j] at lane j + 16k,
+// C[row][col] at lane col + 16 (row % 4), register row / 4 (tools/mfma16_layout.hip).
+typedef double dv4 __attribute__((ext_vector_type(4)));
+DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
 DFM_DEV double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);

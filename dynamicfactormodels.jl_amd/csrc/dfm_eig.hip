@@ -25,8 +25,6 @@
 namespace dfm {
 
 constexpr int EROWS = 64;  // rows per workgroup in gq/apply
-typedef double dv4 __attribute__((ext_vector_type(4)));
-DFM_DEV dv4 mfma16(double a, double b, dv4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
 struct EigWork {
   double *Q, *Y, *U;       // nb x m x P

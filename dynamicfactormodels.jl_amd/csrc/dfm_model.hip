@@ -367,12 +367,181 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel_t(const double *__restrict
   if (tid == 0 && status) status[rep] = sbad ? 2 : 0;
 }
 
-// LDS sized to the design width: d <= 16 (every bootstrap fit at r <= 15
-// with one regressor) fits 5 workgroups per CU instead of 2.
+// One-wave form of the same regression for d + 1 <= 16 (every bootstrap fit
+// at r <= 14 with one regressor): the augmented design [D y] (T x 16, zero
+// columns past d) runs through v_mfma_f64_16x16x4 chains instead of 256
+// threads of LDS dot products, so a replicate is one wave and a CU holds
+// ~14 of them.
+//   pass 1  [D y]'[D y] over 4-row chunks: lane l holds element (t0 + (l >> 4),
+//           l & 15), which is its own A and B operand; four accumulators
+//           summed in fixed order -> D'D, D'y (column d), y'y;
+//   Cholesky D'D = L L', Inv = L^-T L^-1, beta = Inv D'y (as ols_hc2_kernel_t);
+//   pass 2  per 16-row tile D [Inv | beta] on MFMA (A: row l & 15, column
+//           4s + (l >> 4)); h_t = sum_j (D Inv)_tj D_tj by xor shuffles over the
+//           16 lanes of a row, u_t = y_t - D_t beta, sigma2_t = u_t^2 / (1 - h_t);
+//           the meat D' diag(sigma2) D on MFMA in the pass-1 layout (the tile's
+//           accumulator register g holds rows t0 + 4g + (l >> 4)).
+// The row sums run in MFMA order (not ols_hc2_kernel_t's serial order):
+// results agree to rounding, and are per-replicate (batch-invariant).
+__global__ __launch_bounds__(64, 3) void ols_hc2_wave_kernel(const double *__restrict__ y, const double *__restrict__ w,
+                                                         int q, const double *__restrict__ F, int Tphys, int kF,
+                                                         const int *__restrict__ Tn, const int *__restrict__ kr,
+                                                         double *__restrict__ coef, double *__restrict__ tstat,
+                                                         double *__restrict__ cov_out, double *__restrict__ resid_out,
+                                                         int *__restrict__ status) {
+  constexpr int S = 17;
+  __shared__ double M[16 * S], Li[16 * S], Inv[16 * S], Tmp[16 * S];
+  __shared__ double sb[16];
+  __shared__ int sbad;
+  const int tid = threadIdx.x, rep = blockIdx.x, li = tid & 15, lk = tid >> 4;
+  const int T = Tn ? Tn[rep] : Tphys;
+  const int k = kr ? kr[rep] : kF;
+  const int d = q + k, dstr = q + kF;
+  const double *Fr = F + (int64_t)rep * Tphys * kF;
+  // column j of [D y] as (base, row stride); columns past d read nothing
+  struct Col { const double *p; int st; bool on; };
+  auto col = [&](int j) -> Col {
+    if (j < q) return {w + (int64_t)j * Tphys, 1, true};
+    if (j < d) return {Fr + (j - q), kF, true};
+    return {y, 1, j == d};
+  };
+  auto ld = [&](const Col &c, int t) -> double { return (c.on && t < T) ? c.p[(int64_t)t * c.st] : 0.0; };
+  const Col cl = col(li);
+  // ---- pass 1
+  dv4 a4[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a4[u] = dv4{0.0, 0.0, 0.0, 0.0};
+  for (int t0 = 0; t0 < T; t0 += 64) {   // 16 loads in flight per lane
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = ld(cl, t0 + 4 * u + lk);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a4[u & 3] = mfma16(v[u], v[u], a4[u & 3]);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) M[(4 * g + lk) * S + li] = ((a4[0][g] + a4[1][g]) + a4[2][g]) + a4[3][g];
+  for (int e = tid; e < 16 * S; e += 64) Li[e] = 0.0;
+  if (tid == 0) sbad = 0;
+  __syncthreads();
+  // ---- Cholesky, inverse, beta (ols_hc2_kernel_t's arithmetic)
+  for (int j = 0; j < d; ++j) {
+    if (tid == 0) {
+      double s = M[j * S + j];
+      for (int p = 0; p < j; ++p) s -= Li[j * S + p] * Li[j * S + p];
+      if (!(s > 0.0)) { sbad = 1; s = 1.0; }
+      Li[j * S + j] = sqrt(s);
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < d; i += 64) {
+      double s = M[i * S + j];
+      for (int p = 0; p < j; ++p) s -= Li[i * S + p] * Li[j * S + p];
+      Li[i * S + j] = s / Li[j * S + j];
+    }
+    __syncthreads();
+  }
+  for (int c = tid; c < d; c += 64)
+    for (int i = 0; i < d; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int p = c; p < i; ++p) s -= Li[i * S + p] * Tmp[p * S + c];
+      Tmp[i * S + c] = i < c ? 0.0 : s / Li[i * S + i];
+    }
+  __syncthreads();
+  for (int e = tid; e < 16 * 16; e += 64) {
+    const int a = e >> 4, c = e & 15;
+    double s = 0.0;
+    if (a < d && c < d)
+      for (int p = max(a, c); p < d; ++p) s = fma(Tmp[p * S + a], Tmp[p * S + c], s);
+    Inv[a * S + c] = s;   // zero outside d x d
+  }
+  __syncthreads();
+  if (tid < d) {
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Inv[tid * S + p], M[p * S + d], s);
+    sb[tid] = s;
+  }
+  __syncthreads();
+  // ---- pass 2: B operand [Inv | beta] (row k = 4s + (l >> 4), column l & 15)
+  double Bm[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int kk = 4 * s + lk;
+    Bm[s] = li < d ? Inv[kk * S + li] : ((li == d && kk < d) ? sb[kk] : 0.0);
+  }
+  Col ca[4];   // A-operand columns 4s + (l >> 4) of D (the y column excluded)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { ca[s] = col(4 * s + lk); ca[s].on = 4 * s + lk < d; }
+  dv4 mt[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) mt[u] = dv4{0.0, 0.0, 0.0, 0.0};
+  const int src = (tid & 48) | d;   // lane of this row group holding column d
+  for (int tb = 0; tb < T; tb += 32) {   // two 16-row tiles, 16 loads in flight per lane
+    double av[2][4], dgt[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) av[h][s] = ld(ca[s], tb + 16 * h + li);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dgt[h][g] = ld(cl, tb + 16 * h + 4 * g + lk);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+    const int t0 = tb + 16 * h;
+    const double *dg = dgt[h];
+    dv4 out = dv4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) out = mfma16(av[h][s], Bm[s], out);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int t = t0 + 4 * g + lk;
+      double h = li < d ? out[g] * dg[g] : 0.0;
+      h += __shfl_xor(h, 8);
+      h += __shfl_xor(h, 4);
+      h += __shfl_xor(h, 2);
+      h += __shfl_xor(h, 1);
+      const double u = __shfl(dg[g] - out[g], src);   // y_t - D_t beta (lane d of the row)
+      const double sig = t < T ? u * u / (1.0 - h) : 0.0;
+      if (resid_out && li == d && t < T) resid_out[t] = u;
+      const double dm = li < d ? dg[g] : 0.0;
+      mt[g] = mfma16(dm * sig, dm, mt[g]);
+    }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) Tmp[(4 * g + lk) * S + li] = ((mt[0][g] + mt[1][g]) + mt[2][g]) + mt[3][g];
+  __syncthreads();
+  // ---- sandwich Inv Meat Inv, outputs (ols_hc2_kernel_t's arithmetic)
+  for (int e = tid; e < d * d; e += 64) {
+    const int a = e / d, c = e % d;
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Tmp[a * S + p], Inv[p * S + c], s);
+    Li[a * S + c] = s;
+  }
+  __syncthreads();
+  for (int e = tid; e < d * d; e += 64) {
+    const int a = e / d, c = e % d;
+    double s = 0.0;
+    for (int p = 0; p < d; ++p) s = fma(Inv[a * S + p], Li[p * S + c], s);
+    M[a * S + c] = s;   // coefficient covariance
+  }
+  __syncthreads();
+  if (tid < dstr) {
+    coef[(int64_t)rep * dstr + tid] = tid < d ? sb[tid] : NAN;
+    tstat[(int64_t)rep * dstr + tid] = tid < d ? sb[tid] / sqrt(M[tid * S + tid]) : NAN;
+  }
+  if (cov_out)
+    for (int e = tid; e < d * d; e += 64) cov_out[(int64_t)rep * d * d + (e % d) * d + e / d] = M[(e / d) * S + e % d];
+  if (tid == 0 && status) status[rep] = sbad ? 2 : 0;
+}
+
+// d + 1 <= 16: one wave per replicate (ols_hc2_wave_kernel); else LDS sized
+// to the design width: d <= 16 fits 5 workgroups per CU instead of 2.
 hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, int q, const double *F, int Tphys,
                       int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
                       double *resid_out, int *status) {
-  if (q + kF <= 16)
+  if (q + kF + 1 <= 16)
+    hipLaunchKernelGGL(ols_hc2_wave_kernel, dim3(nb), dim3(64), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef, tstat,
+                       cov_out, resid_out, status);
+  else if (q + kF <= 16)
     hipLaunchKernelGGL(ols_hc2_kernel_t<16>, dim3(nb), dim3(256), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef, tstat,
                        cov_out, resid_out, status);
   else
