@@ -40,8 +40,14 @@ DFM_DEV int lds_off(int a, int kc) {
 template <int ORIENT, bool HAS_C, bool HAS_ETA, bool HAS_IDX>
 __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K, int T,
                                                       double *__restrict__ G, int64_t ldg,
-                                                      int64_t strideG, int ksteps, int64_t strideZ) {
+                                                      int64_t strideG, int ksteps, int64_t strideZ, int kpre) {
   __shared__ __attribute__((aligned(16))) double lds[2][2][GT * KS];
+  // COLS with kpre = K: the replicate's eta / idx rows staged in dynamic LDS
+  // up front, so a k-row's gather is one load (E[idx_t]) instead of two
+  // dependent ones (idx_t, then the row) per stage
+  extern __shared__ double s_pre[];
+  double *s_et = s_pre;
+  int *s_ix = (int *)(s_pre + kpre);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int rep = blockIdx.y;
@@ -100,8 +106,8 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
           const bool ok = (t < K) && (col < ld);
           rowok[op][h] = ok;
           if (ok) {
-            const int er = HAS_IDX ? idx[t] : t;
-            ev[op][h] = HAS_ETA ? eta[t] : 1.0;
+            const int er = HAS_IDX ? (kpre ? s_ix[t] : idx[t]) : t;
+            ev[op][h] = HAS_ETA ? (kpre ? s_et[t] : eta[t]) : 1.0;
             re[op][h] = *reinterpret_cast<const double2 *>(src.E + (int64_t)er * ld + col);
             if (HAS_C) rc[op][h] = *reinterpret_cast<const double2 *>(src.C + (int64_t)t * ld + col);
           }
@@ -140,6 +146,13 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
   // own partial image (strideZ apart); launch_gram sums them in fixed order
   const int s0 = blockIdx.z * ksteps;
   const int nst = min((K + KS - 1) / KS, s0 + ksteps);
+  if (ORIENT == ORIENT_COLS && kpre) {
+    for (int e = tid; e < kpre; e += 256) {
+      if (HAS_ETA) s_et[e] = eta[e];
+      if (HAS_IDX) s_ix[e] = idx[e];
+    }
+    __syncthreads();
+  }
   load_stage(s0 * KS);
   store_stage(0);
   __syncthreads();
@@ -272,8 +285,12 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
   if (e) sub.eta = src.eta + (int64_t)r0 * src.rs;
   double *Gout = S > 1 ? Gk : G + (int64_t)r0 * strideG;
   dim3 grid(nt * (nt + 1) / 2, nr, S), block(256);
+  // COLS gather rows staged in LDS when they fit (C2: K = 600, 7.2 KB)
+  const int kpre = (orient == ORIENT_COLS && (e || x) && K <= 2048) ? K : 0;
+  const size_t dyn = (size_t)kpre * 12;
 #define DFM_GRAM_L(O, C_, E_, X_) \
-  hipLaunchKernelGGL((gram_kernel<O, C_, E_, X_>), grid, block, 0, st, sub, m, K, T, Gout, ldg, sG, ksteps, sZ)
+  hipLaunchKernelGGL((gram_kernel<O, C_, E_, X_>), grid, block, dyn, st, sub, m, K, T, Gout, ldg, sG, ksteps, sZ, \
+                     kpre)
   if (orient == ORIENT_ROWS) {
     if (c && e && x) DFM_GRAM_L(ORIENT_ROWS, true, true, true);
     else if (c && !e && x) DFM_GRAM_L(ORIENT_ROWS, true, false, true);
