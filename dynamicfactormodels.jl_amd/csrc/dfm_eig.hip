@@ -689,13 +689,13 @@ template <int P>
 __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
                                                         double *__restrict__ Uk, int *__restrict__ status) {
   // one pass over U: each thread keeps the running max |U[r][j]| (first row
-  // on ties) of its rows for every column j, then one tree reduction over the
-  // block for all columns at once (smaller row index wins ties: same pick as
-  // a serial scan)
-  __shared__ double sv[P][256];
-  __shared__ int si[P][256];
+  // on ties) of its rows for every column j, then a shuffle reduction per
+  // wave and a fixed-order combine of the four waves (smaller row index wins
+  // ties: the same pick as a serial scan)
+  __shared__ double sv[P][4];
+  __shared__ int si[P][4];
   __shared__ double ssign[P];
-  const int tid = threadIdx.x, rep = blockIdx.x;
+  const int tid = threadIdx.x, rep = blockIdx.x, wv = tid >> 6;
   const double *Ur = w.U + (int64_t)rep * m * P;
   const double *theta = w.small + (int64_t)rep * small_stride<P>() + 2 * P * P;
   double best[P];
@@ -716,19 +716,27 @@ __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k,
     }
   }
 #pragma unroll
-  for (int j = 0; j < P; ++j) { sv[j][tid] = best[j]; si[j][tid] = bi[j]; }
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o)
+  for (int j = 0; j < P; ++j) {
+    if (j >= k) continue;
+    double a = best[j];
+    int ai = bi[j];
 #pragma unroll
-      for (int j = 0; j < P; ++j) {
-        if (j >= k) continue;
-        const double a = sv[j][tid + o];
-        const int ai = si[j][tid + o];
-        if (a > sv[j][tid] || (a == sv[j][tid] && ai < si[j][tid])) { sv[j][tid] = a; si[j][tid] = ai; }
-      }
-    __syncthreads();
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double b = __shfl_xor(a, o);
+      const int bj = __shfl_xor(ai, o);
+      if (b > a || (b == a && bj < ai)) { a = b; ai = bj; }
+    }
+    if ((tid & 63) == 0) { sv[j][wv] = a; si[j][wv] = ai; }
   }
+  __syncthreads();
+  if (tid < k) {
+    double a = sv[tid][0];
+    int ai = si[tid][0];
+    for (int q = 1; q < 4; ++q)
+      if (sv[tid][q] > a || (sv[tid][q] == a && si[tid][q] < ai)) { a = sv[tid][q]; ai = si[tid][q]; }
+    si[tid][0] = ai;
+  }
+  __syncthreads();
   if (tid < k) ssign[tid] = Ur[(int64_t)si[tid][0] * P + tid] < 0.0 ? -1.0 : 1.0;
   __syncthreads();
   if (tid < k) lam[(int64_t)rep * k + tid] = theta[tid];
@@ -967,8 +975,8 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   if (tid == 0) trace[rep] = red[0];
 }
 
-hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, double invT, double *Lout, hipStream_t st, int Ncv);
+hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int Kp, int rp, int N, int nrep,
+                                int K, int r, double invT, double *Lout, hipStream_t st);
 hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1, bool b_padded = false,
@@ -1789,30 +1797,39 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
 int fact_t_max() { return F2_T_MAX; }
 
 // ---- factored loadings pass: L* = X*' F* / T = (L (F'F*) + E' P' D F*) / T
-// boot_zf: ZF[s][rep*r + j] = sum_{t in bucket s} eta_t F*[t][j]  and
-//          M1[rep] = F' F* (r x r);  F* = sqrt(T) U*  written to Fout.
+// boot_zf: replicate rep's block ZB = ZF + rep Kp rp (Kp x rp, row-major):
+//          ZB[s][j] = sum_{t in bucket s} eta_t F*[t][j]   (s < T)
+//          ZB[T + i][j] = M1[rep][i][j] = (F' F*)[i][j]    (i < r)
+//          zero rows T + r .. Kp - 1 and zero column r when rp > r;
+//          F* = sqrt(T) U* written to Fout.
+// The block is contiguous, so every row segment lands in whole lines.
 __global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double *__restrict__ Uk,
                                                       const double *__restrict__ eta,
                                                       const int *__restrict__ off, const int *__restrict__ lst,
-                                                      double *__restrict__ Fout, double *__restrict__ ZF,
-                                                      int64_t ldzf, double *__restrict__ M1) {
+                                                      double *__restrict__ Fout, double *__restrict__ ZF, int Kp,
+                                                      int rp, double *__restrict__ M1) {
   const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
   const double sT = sqrt((double)T);
   const double *U = Uk + (int64_t)rep * T * r;
   double *Fr = Fout + (int64_t)rep * T * r;
-  for (int e = tid; e < T * r; e += 256) Fr[e] = sT * U[e];
+  double *ZB = ZF + (int64_t)rep * Kp * rp;
   const double *et = eta ? eta + (int64_t)rep * T : nullptr;
   const int *o = off + (int64_t)rep * (T + 1);
   const int *L = lst + (int64_t)rep * T;
-  for (int e = tid; e < T * r; e += 256) {
-    const int sI = e / r, j = e % r;
+  for (int e = tid; e < T * r; e += 256) Fr[e] = sT * U[e];
+  for (int e = tid; e < T * rp; e += 256) {
+    const int sI = e / rp, j = e - sI * rp;
     double z = 0.0;
-    for (int q = o[sI]; q < o[sI + 1]; ++q) {
-      const int t = L[q];
-      z = fma(et ? et[t] : 1.0, sT * U[(int64_t)t * r + j], z);
-    }
-    ZF[(int64_t)sI * ldzf + (int64_t)rep * r + j] = z;
+    if (j < r)
+      for (int q = o[sI]; q < o[sI + 1]; ++q) {
+        const int t = L[q];
+        z = fma(et ? et[t] : 1.0, sT * U[(int64_t)t * r + j], z);
+      }
+    ZB[e] = z;
   }
+  for (int e = (T + r) * rp + tid; e < Kp * rp; e += 256) ZB[e] = 0.0;
+  if (rp > r)
+    for (int i = tid; i < r; i += 256) ZB[(int64_t)(T + i) * rp + r] = 0.0;
   // M1 = F' F*: 4 row-interleaved partial sums per entry (four independent
   // chains of T/4 instead of one of T), combined in a fixed order
   __shared__ double m1p[4][256];
@@ -1830,7 +1847,7 @@ __global__ __launch_bounds__(256) void boot_zf_kernel(FactBase fb, const double 
       const double v = (m1p[0][tid] + m1p[1][tid]) + (m1p[2][tid] + m1p[3][tid]);
       M1[(int64_t)rep * r * r + e] = v;
       // the same block as k-rows T..T+r-1 of the loadings GEMM's B operand
-      ZF[(int64_t)(T + e / r) * ldzf + (int64_t)rep * r + e % r] = v;
+      ZB[(int64_t)(T + e / r) * rp + e % r] = v;
     }
     __syncthreads();
   }
@@ -1844,36 +1861,30 @@ __global__ void eaug_tail_kernel(const double *__restrict__ Lb, int N, int r, in
   tail[(int64_t)i * ld + n] = (i < r && n < N) ? Lb[n * r + i] : 0.0;
 }
 
+static int zf_rp(int r) { return (r + 1) / 2 * 2; }
+static int zf_kp(int T, int r) { return (T + r + 15) / 16 * 16; }
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
                   const double *Uk, const double *eta, const int *off, const int *lst, int nb,
                   double *Fout, double *Lout, char *ws, hipStream_t st) {
-  const int T = fb.T, r = fb.r;
-  const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
-  // ZF: Kp rows — F-scatter rows 0..T-1, the M1 = F'F* blocks as rows
-  // T..T+r-1 (written by boot_zf), zero rows up to Kp (the GEMM's k padding)
-  const int Kp = (T + r + 15) / 16 * 16;
-  double *ZF = (double *)ws;
-  double *M1 = ZF + (size_t)Kp * ldzf;
-  double *Eaug = M1 + (size_t)nb * r * r;   // [E; L'; 0]: Kp x ld
-  hipMemsetAsync(ZF + (size_t)T * ldzf, 0, (size_t)(Kp - T) * ldzf * 8, st);
-  // the pad column of an odd nb r is streamed by the GEMM (its products are
-  // discarded): keep it finite
-  if (ldzf != (int64_t)nb * r) hipMemset2DAsync(ZF + ldzf - 1, (size_t)ldzf * 8, 0, 8, T, st);
-  hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, ldzf, M1);
+  const int T = fb.T, r = fb.r, rp = zf_rp(r), Kp = zf_kp(T, r);
+  double *ZF = (double *)ws;                       // nb blocks of Kp x rp
+  double *M1 = ZF + (size_t)nb * Kp * rp;
+  double *Eaug = M1 + (size_t)nb * r * r;          // [E; L'; 0]: Kp x ld
+  // (staging U*, eta and the CSR in LDS first measured slower: 0.62 -> 0.76 ms at C3)
+  hipLaunchKernelGGL(boot_zf_kernel, dim3(nb), dim3(256), 0, st, fb, Uk, eta, off, lst, Fout, ZF, Kp, rp, M1);
   // one GEMM of depth T + r does the whole finish (see gemm_loadings_kernel),
   // for every batch size: the same arithmetic for every replicate whatever
   // the batch composition (batch- and shard-invariant loadings)
   hipMemcpy2DAsync(Eaug, (size_t)ld * 8, Ep, (size_t)ld * 8, (size_t)ld * 8, T, hipMemcpyDeviceToDevice, st);
   hipLaunchKernelGGL(eaug_tail_kernel, dim3((unsigned)((ld + 255) / 256), Kp - T), dim3(256), 0, st, Lb, N, r, ld,
                      Eaug + (size_t)T * ld);
-  const hipError_t e = launch_gemm_loadings(Eaug, ld, ZF, ldzf, N, (int)ldzf, T + r, r, 1.0 / T, Lout, st, nb * r);
+  const hipError_t e = launch_gemm_loadings(Eaug, ld, ZF, Kp, rp, N, nb, T + r, r, 1.0 / T, Lout, st);
   return e == hipSuccess ? 0 : 1000 + (int)e;
 }
 size_t fact_loadings_bytes(int T, int N, int r, int nb) {
-  const int64_t ldzf = ((int64_t)nb * r + 1) / 2 * 2;
-  const int Kp = (T + r + 15) / 16 * 16;
   const int64_t ld = ((int64_t)N + 15) / 16 * 16;
-  return ((size_t)Kp * ldzf + (size_t)nb * r * r + (size_t)Kp * ld) * 8 + 1024;
+  const int Kp = zf_kp(T, r);
+  return ((size_t)nb * Kp * zf_rp(r) + (size_t)nb * r * r + (size_t)Kp * ld) * 8 + 1024;
 }
 
 // ---- model-level precompute: EL = E L (T x r), S = L'L, cF, hd

@@ -341,13 +341,17 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 
 // ---------------------------------------------------------------------------
 // Loadings GEMM of the factored bootstrap:
-//   L*[rep][n][j] = ( [E' | L] [ZF ; M1] )[n][rep r + j] / T
+//   L*[rep][n][j] = ( [E' | L] [ZF ; M1] )[n][rep rp + j] / T
 // (src/DynamicFactorModel.jl:90 for every replicate: L* = X*' F* / T with
 // X*' F* = E' P' D F* + L (F'F*)): the r x r blocks M1 = F'F* sit under ZF
 // as r extra k-rows and L' under E, so the whole finish is K = T + r MFMA
 // depth (+1.6 %) and the epilogue a plain scaled store.  A^T operand
-// [E; L'] (Kpad x lda) and B operand [ZF; M1; 0] (Kpad x ldb, Kpad =
-// round_up(T + r, 16), zero rows past T + r) staged by LDS-DMA into [k][a]
+// [E; L'] (Kpad x lda, Kpad = round_up(T + r, 16), zero rows past T + r).
+// B operand replicate-major: replicate rep's [ZF; M1; 0] is one contiguous
+// Kpad x rp block (rp = r rounded up to even, column r zero when r is odd),
+// so boot_zf writes whole lines; column x of the GEMM is (rep, j) =
+// (x / rp, x % rp), and a lane's 16-B DMA pair (x, x + 1), x even, never
+// straddles two replicates.  Both operands staged by LDS-DMA into [k][a]
 // images (4-deep ring as gemmh_kernel).  Grid: the row blocks (64 variables)
 // are spread over the XCDs — XCD x owns row blocks x, x+8, ... whose E slabs
 // (64 x T x 8 B each) stay in its L2 — and every XCD walks the column blocks
@@ -355,9 +359,9 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 // other XCDs from the Infinity Cache.
 template <int NBUF, int MINB>
 __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *__restrict__ A, int64_t lda,
-                                                                  const double *__restrict__ B, int64_t ldb, int M,
+                                                                  const double *__restrict__ B, int Kp, int rp, int M,
                                                                   int Nc, int K, int nrb, int ncb, int r, double invT,
-                                                                  double *__restrict__ Lout, int Ncv) {
+                                                                  double *__restrict__ Lout, int nrep) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -381,9 +385,10 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
     const int kc = 2 * (2 * wave + h) + (lane >> 5);
     const int sw = (2 * (lane & 31)) ^ ((kc & 7) << 2);
     pa[h] = A + (int64_t)kc * lda + min(abase + sw, (int)lda - 2);
-    pb[h] = B + (int64_t)kc * ldb + min(bbase + sw, Nc - 2);
+    const int x = min(bbase + sw, Nc - 2), rep = x / rp;   // past Nc: finite, discarded
+    pb[h] = B + ((int64_t)rep * Kp + kc) * rp + (x - rep * rp);
   }
-  const int64_t astep = (int64_t)G2_KS * lda, bstep = (int64_t)G2_KS * ldb;
+  const int64_t astep = (int64_t)G2_KS * lda, bstep = (int64_t)G2_KS * rp;
   auto issue = [&](int s) {
     double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
 #pragma unroll
@@ -429,24 +434,21 @@ __global__ __launch_bounds__(256, MINB) void gemm_loadings_kernel(const double *
       const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
       const int n = abase + wr * 32 + 4 * fa + oi;
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
-      if (n < M && col < Ncv) {
-        const int rep = col / r, jj = col - rep * r;
-        Lout[((int64_t)rep * M + n) * r + jj] = v * invT;
-      }
+      const int rep = col / rp, jj = col - rep * rp;
+      if (n < M && rep < nrep && jj < r) Lout[((int64_t)rep * M + n) * r + jj] = v * invT;
     }
 }
 
-// Nc: columns of ZF streamed (even: the 16-B DMA pairs never straddle the
-// valid range), Ncv <= Nc: columns stored (nb r).
-hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int64_t ldb, int N, int Nc, int K,
-                                int r, double invT, double *Lout, hipStream_t st, int Ncv) {
+// ZF: nrep replicate blocks of Kp x rp (see gemm_loadings_kernel); K = T + r.
+hipError_t launch_gemm_loadings(const double *Eaug, int64_t lda, const double *ZF, int Kp, int rp, int N, int nrep,
+                                int K, int r, double invT, double *Lout, hipStream_t st) {
+  const int Nc = nrep * rp;
   const int nrb = (N + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
   const int nrb8 = (nrb + 7) / 8;
   // (the 3-deep ring at 3 workgroups per CU measured 20 % slower here, with
   // running pointers still 23 % slower: 4-deep at 2 per CU stays)
-  // running DMA pointers over the zero k-padding of both operands
-  hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, ldb, N,
-                     Nc, K, nrb, ncb, r, invT, Lout, Ncv);
+  hipLaunchKernelGGL((gemm_loadings_kernel<4, 2>), dim3(8 * nrb8 * ncb), dim3(256), 0, st, Eaug, lda, ZF, Kp, rp, N,
+                     Nc, K, nrb, ncb, r, invT, Lout, nrep);
   return hipGetLastError();
 }
 
