@@ -398,3 +398,32 @@ def test_errors_are_reported(dfm, oracle):
         dfm.targeted_predictors(y, w, np.random.default_rng(0).standard_normal((50, 60)))
     with pytest.raises(dfm.DFMError):
         dfm.wild_bootstrap(g, 1, dfm.Stat.V(), idx=np.full((1, 50), 99, dtype=np.int32), eta=eta[:1])
+
+
+@pytest.mark.parametrize("r,mode", [(11, "direct"), (11, "factored"), (12, "direct"), (12, "factored")])
+def test_ols_width_boundary(dfm, oracle, r, mode):
+    """OLS + HC2 (src/DynamicFactorModel.jl:40-48) at the boundary of the
+    one-wave MFMA kernel: q + r = 15 (d + 1 = 16 columns with y: one wave)
+    and q + r = 16 (the 256-thread LDS kernel), in the base fit and in
+    bootstrap replicates — every coefficient and t-statistic."""
+    T, N, q = 140, 90 if mode == "direct" else 260, 4
+    rng = np.random.default_rng(40 + r)
+    y, x, *_ = oracle.factor_model_DGP(T + 3, N, 12, rng)
+    x = oracle.normalize(x)[3:]
+    w = np.hstack([np.ones((T, 1)), np.column_stack([y[3 - k:len(y) - k] for k in range(1, 4)])])
+    y = y[3:]
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    g.set_bootstrap_mode(mode)
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    assert_fit_matches(g, o, oracle, q=q)
+    B = 3
+    idx, eta = oracle.draw_wild(np.random.default_rng(5), B, T)
+    S = dfm.Stat
+    d = q + r
+    out = dfm.wild_bootstrap(g, B, [S.coefficient(j) for j in range(1, d + 1)] +
+                             [S.t_stat(j) for j in range(1, d + 1)], idx=idx, eta=eta)
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        ob = oracle.DynamicFactorModel(y, w, xs, r, "ICp2")
+        assert rel(out[b, :d], ob.coefficients) < 1e-9
+        assert rel(out[b, d:], ob.t_stats) < 1e-9
