@@ -101,6 +101,9 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
                   const double *Uk, const double *eta, const int *off, const int *lst, int nb,
                   double *Fout, double *Lout, char *ws, hipStream_t st);
 size_t fact_loadings_bytes(int T, int N, int r, int nb);
+hipError_t launch_fact_fsf(int T, int r, const double *Fb, const double *S, double *FSF, int64_t ldH, hipStream_t st);
+hipError_t launch_gram_fact(const FactBase &fb, const double *FSF, const int32_t *idx, const double *eta, int nb,
+                            double *G, int64_t ldg, int64_t strideG, hipStream_t st);
 int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
                     const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st);
 hipError_t launch_targeted(int mode, const double *y, const double *w, int q, const double *Xp,
@@ -156,6 +159,7 @@ struct dfm_model {
   bool fact_ready = false;
   int64_t ldH = 0;
   double *H = nullptr, *EL = nullptr, *S = nullptr, *cF = nullptr, *hd = nullptr;
+  double *FSF = nullptr;   // F S F' (T x ldH): the direct path's identity-based replicate Grams
   // break blocks (src/DynamicFactorModel.jl:73, :98): first row, rows, Gram
   // size, per-block eigenvectors (Gram size x r) and loadings (N x r); block 0's
   // are aliased by Ub and L
@@ -423,7 +427,7 @@ int dfm_model_destroy(dfm_model *m) {
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
   for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->Lall, m->Ub, m->colssr, m->H, m->EL, m->S,
-                    m->cF, m->hd})
+                    m->cF, m->hd, m->FSF})
     hipFree(p);
   for (size_t j = 1; j < m->Ubs.size(); ++j) hipFree(m->Ubs[j]);
   hipFree(m->ws);
@@ -960,6 +964,9 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   // PCp reads each replicate's full spectrum, so its Gram is formed: direct path
   const bool fact = (M->orient == 0) && (M->mode != 1) && r <= 16 && T <= fact_t_max() && M->nblk == 1 && !pcp &&
                     !wide;
+  // direct path, N > T, no breaks: the replicate Grams by the factored
+  // identity (gram_fact_kernel, 2 T^2 r flop each) instead of the SYRK
+  const bool gid = !fact && (M->orient == 0) && M->nblk == 1 && r >= 1 && r <= 16 && T <= 4096;
   if (pcp && m > spectrum_any_max())
     return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
                           "supported for min(T,N) <= %d", spectrum_any_max());
@@ -983,7 +990,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     nb = (B + nbat - 1) / nbat;
   }
   nb = std::min<int64_t>(nb, B);
-  if (fact && !M->fact_ready) {
+  if ((fact || gid) && !M->fact_ready) {
     // H = E E' by the MFMA Gram kernel (K1), then EL, S, cF, diag(H)
     M->ldH = round_up(T, 16);
     HIPCHK(ctx, dalloc(&M->H, (size_t)T * M->ldH));
@@ -1001,6 +1008,10 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     if (rc0) return fail(ctx, rc0, "factored precompute failed");
     HIPCHK(ctx, hipStreamSynchronize(st));
     M->fact_ready = true;
+  }
+  if (gid && !M->FSF) {
+    HIPCHK(ctx, dalloc(&M->FSF, (size_t)T * M->ldH));
+    HIPCHK(ctx, launch_fact_fsf(T, r, M->F, M->S, M->FSF, M->ldH, st));
   }
   const size_t need = boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, nullptr, nullptr);
   if (need > M->ws_bytes) {
@@ -1099,7 +1110,11 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     } else {
       {
         Scope sc(ctx, DFM_KC_GRAM);
-        HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
+        if (gid)
+          HIPCHK(ctx, launch_gram_fact(fb, M->FSF, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, n,
+                                       w.G, m, (int64_t)m * m, st));
+        else
+          HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
       }
       int rc = eig_any(w.G, m, n, M->Ub, w.lam, w.Uk, w.trace, b0);
       if (rc) return rc;

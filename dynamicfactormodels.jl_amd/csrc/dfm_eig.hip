@@ -1920,6 +1920,114 @@ __global__ void fact_cf_kernel(int T, int r, const double *__restrict__ Fb, cons
   }
   cF[t] = acc;
 }
+// FSF = F S F' (T x T, ldH), the common-component Gram C C' of the base fit
+// (C = F L', S = L'L): entry (s, t >= s) computed once and mirrored, so the
+// matrix is exactly symmetric.
+__global__ void fact_fsf_kernel(int T, int r, const double *__restrict__ Fb, const double *__restrict__ S,
+                                double *__restrict__ FSF, int64_t ldH) {
+  const int t = blockIdx.x * 256 + threadIdx.x, s = blockIdx.y;
+  if (t >= T || t < s) return;
+  double acc = 0.0;
+  for (int i = 0; i < r; ++i) {
+    double u = 0.0;
+    for (int j = 0; j < r; ++j) u = fma(S[i * r + j], Fb[(int64_t)t * r + j], u);
+    acc = fma(Fb[(int64_t)s * r + i], u, acc);
+  }
+  FSF[(int64_t)s * ldH + t] = acc;
+  FSF[(int64_t)t * ldH + s] = acc;
+}
+hipError_t launch_fact_fsf(int T, int r, const double *Fb, const double *S, double *FSF, int64_t ldH, hipStream_t st) {
+  hipLaunchKernelGGL(fact_fsf_kernel, dim3((T + 255) / 256, T), dim3(256), 0, st, T, r, Fb, S, FSF, ldH);
+  return hipGetLastError();
+}
+
+// Replicate Grams of the direct (Gram-forming) path for N > T without
+// breaks, by the factored identity instead of the T x T x N SYRK:
+//   X* = F L' + D P E  =>  G* = X* X*' = F S F' + F c' + c F' + D P H P' D,
+//   c_t = eta_t EL[idx_t]  (EL = E L, H = E E', S = L'L: model precompute),
+// i.e. G*[s][t] = FSF[s][t] + sum_j (F_sj c_tj + c_sj F_tj)
+//                 + (eta_s eta_t) H[idx_s][idx_t]          (2 T^2 r flop, not T^2 N).
+// Each term is symmetric in (s, t) operation by operation (separately rounded
+// products and sums — no contraction — in a fixed order), so G* is exactly
+// symmetric.
+// One workgroup per (replicate, GF_R rows): the rows' H rows H[idx_s][:]
+// staged in LDS (gathered by idx_t from there), one thread per column t
+// holding F_t and c_t in registers.
+constexpr int GF_R = 8;
+template <int RM>
+__global__ __launch_bounds__(256) void gram_fact_kernel(FactBase fb, const double *__restrict__ FSF,
+                                                        const int32_t *__restrict__ idx,
+                                                        const double *__restrict__ eta, int R,
+                                                        double *__restrict__ G, int64_t ldg, int64_t strideG) {
+  extern __shared__ double gdyn[];
+  const int T = fb.T, r = fb.r, tid = threadIdx.x, rep = blockIdx.y, s0 = blockIdx.x * R;
+  const int ns = min(R, T - s0);
+  double *sH = gdyn;                       // R x T: H[idx_s][:]
+  double *sFc = sH + (size_t)R * T;        // R x 2 RM: F_s, c_s
+  const int32_t *ix = idx + (int64_t)rep * T;
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  for (int e = tid; e < ns * T; e += 256) {
+    const int i = e / T, t = e - i * T;
+    sH[e] = fb.H[(int64_t)ix[s0 + i] * fb.ldH + t];
+  }
+  for (int e = tid; e < ns * RM; e += 256) {
+    const int i = e / RM, j = e - i * RM, sI = s0 + i;
+    const double es = et ? et[sI] : 1.0;
+    sFc[i * 2 * RM + j] = j < r ? fb.F[(int64_t)sI * r + j] : 0.0;
+    sFc[i * 2 * RM + RM + j] = j < r ? es * fb.EL[(int64_t)ix[sI] * r + j] : 0.0;
+  }
+  __syncthreads();
+  double *Gr = G + (int64_t)rep * strideG;
+  for (int t = tid; t < T; t += 256) {
+    const int it = ix[t];
+    const double eT = et ? et[t] : 1.0;
+    double Ft[RM], ct[RM];
+#pragma unroll
+    for (int j = 0; j < RM; ++j) {
+      Ft[j] = j < r ? fb.F[(int64_t)t * r + j] : 0.0;
+      ct[j] = j < r ? eT * fb.EL[(int64_t)it * r + j] : 0.0;
+    }
+    // GF_R rows at a time: every row's FSF entry and H gather issued before the sums
+    for (int i0 = 0; i0 < ns; i0 += GF_R) {
+      double fsf[GF_R], hv[GF_R], es[GF_R];
+#pragma unroll
+      for (int u = 0; u < GF_R; ++u) {
+        const int i = min(i0 + u, ns - 1), sI = s0 + i;
+        fsf[u] = FSF[(int64_t)sI * fb.ldH + t];
+        hv[u] = sH[i * T + it];
+        es[u] = et ? et[sI] : 1.0;
+      }
+#pragma unroll
+      for (int u = 0; u < GF_R; ++u) {
+        const int i = i0 + u;
+        if (i >= ns) break;
+        const double *fc = sFc + i * 2 * RM;
+        double x = 0.0;
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+          if (j < r) x = __dadd_rn(x, __dadd_rn(__dmul_rn(fc[j], ct[j]), __dmul_rn(fc[RM + j], Ft[j])));
+        Gr[(int64_t)(s0 + i) * ldg + t] = __dadd_rn(__dadd_rn(fsf[u], x), __dmul_rn(__dmul_rn(es[u], eT), hv[u]));
+      }
+    }
+  }
+}
+int gram_fact_rows(int T) { return std::max(1, std::min(GF_R, 4096 / std::max(T, 1))); }
+size_t gram_fact_lds(int T, int r) {
+  const int R = gram_fact_rows(T), RM = r <= 8 ? 8 : 16;
+  return (size_t)R * T * 8 + (size_t)R * 2 * RM * 8;
+}
+hipError_t launch_gram_fact(const FactBase &fb, const double *FSF, const int32_t *idx, const double *eta, int nb,
+                            double *G, int64_t ldg, int64_t strideG, hipStream_t st) {
+  const int R = gram_fact_rows(fb.T);
+  const size_t lds = gram_fact_lds(fb.T, fb.r);
+  dim3 grid((fb.T + R - 1) / R, nb);
+  if (fb.r <= 8)
+    hipLaunchKernelGGL(gram_fact_kernel<8>, grid, dim3(256), lds, st, fb, FSF, idx, eta, R, G, ldg, strideG);
+  else
+    hipLaunchKernelGGL(gram_fact_kernel<16>, grid, dim3(256), lds, st, fb, FSF, idx, eta, R, G, ldg, strideG);
+  return hipGetLastError();
+}
+
 int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
                     const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st) {
   hipLaunchKernelGGL(fact_pre_kernel, dim3((T + 3) / 4), dim3(256), 0, st, Ep, ld, T, N, r, Lb, Fb, H, ldH,
