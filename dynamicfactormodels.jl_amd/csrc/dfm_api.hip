@@ -101,6 +101,14 @@ int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const
                   const double *Uk, const double *eta, const int *off, const int *lst, int nb,
                   double *Fout, double *Lout, char *ws, hipStream_t st);
 size_t fact_loadings_bytes(int T, int N, int r, int nb);
+hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
+                              double *K, double *A0, hipStream_t st);
+size_t gram_wk_work(int T, int N, int r, int nb);
+int64_t gram_wk_ldk(int N);
+int gram_wk_tp(int T);
+hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
+                          const double *K, const double *A0, const int32_t *idx, const double *eta, int64_t rs,
+                          int nb, double *work, double *G, hipStream_t st);
 hipError_t launch_fact_fsf(int T, int r, const double *Fb, const double *S, double *FSF, int64_t ldH, hipStream_t st);
 hipError_t launch_gram_fact(const FactBase &fb, const double *FSF, const int32_t *idx, const double *eta, int nb,
                             double *G, int64_t ldg, int64_t strideG, hipStream_t st);
@@ -160,6 +168,9 @@ struct dfm_model {
   int64_t ldH = 0;
   double *H = nullptr, *EL = nullptr, *S = nullptr, *cF = nullptr, *hd = nullptr;
   double *FSF = nullptr;   // F S F' (T x ldH): the direct path's identity-based replicate Grams
+  // T >= N bootstrap Grams by one weighted-outer-product GEMM (gram_wk_*):
+  // K = [E_s' E_s] lower-triangle pairs (Tp x ldk) and A0 = C'C (N x N)
+  double *Kwk = nullptr, *A0wk = nullptr;
   // break blocks (src/DynamicFactorModel.jl:73, :98): first row, rows, Gram
   // size, per-block eigenvectors (Gram size x r) and loadings (N x r); block 0's
   // are aliased by Ub and L
@@ -427,7 +438,7 @@ int dfm_model_destroy(dfm_model *m) {
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
   for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->Lall, m->Ub, m->colssr, m->H, m->EL, m->S,
-                    m->cF, m->hd, m->FSF})
+                    m->cF, m->hd, m->FSF, m->Kwk, m->A0wk})
     hipFree(p);
   for (size_t j = 1; j < m->Ubs.size(); ++j) hipFree(m->Ubs[j]);
   hipFree(m->ws);
@@ -967,6 +978,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   // direct path, N > T, no breaks: the replicate Grams by the factored
   // identity (gram_fact_kernel, 2 T^2 r flop each) instead of the SYRK
   const bool gid = !fact && (M->orient == 0) && M->nblk == 1 && r >= 1 && r <= 16 && T <= 4096;
+  // T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk)
+  const bool gwk = (M->orient == 1) && M->nblk == 1 && N <= 256 && r >= 1 && r <= 16 && T <= 8192;
   if (pcp && m > spectrum_any_max())
     return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
                           "supported for min(T,N) <= %d", spectrum_any_max());
@@ -1009,6 +1022,11 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     HIPCHK(ctx, hipStreamSynchronize(st));
     M->fact_ready = true;
   }
+  if (gwk && !M->Kwk) {
+    HIPCHK(ctx, dalloc(&M->Kwk, (size_t)gram_wk_tp(T) * gram_wk_ldk(N)));
+    HIPCHK(ctx, dalloc(&M->A0wk, (size_t)N * N));
+    HIPCHK(ctx, gram_wk_precompute(M->Ep, M->ld, T, N, r, M->F, M->L, M->Kwk, M->A0wk, st));
+  }
   if (gid && !M->FSF) {
     HIPCHK(ctx, dalloc(&M->FSF, (size_t)T * M->ldH));
     HIPCHK(ctx, launch_fact_fsf(T, r, M->F, M->S, M->FSF, M->ldH, st));
@@ -1031,7 +1049,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, &w, M->ws);
   // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
   // src/criteria.jl:18), its spectrum, sigma^2 per replicate
-  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc;
+  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc, wGk;
+  if (gwk) HIPCHK(ctx, dalloc(&wGk.p, gram_wk_work(T, N, r, (int)nb)));
   if (wide) {
     HIPCHK(ctx, dalloc(&wDe.p, (size_t)nb * dense_eig_work(m, r)));
     if (q + r > 32) HIPCHK(ctx, dalloc(&wOls.p, (size_t)nb * ols_wide_work(T, q + r)));
@@ -1113,6 +1132,9 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
         if (gid)
           HIPCHK(ctx, launch_gram_fact(fb, M->FSF, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, n,
                                        w.G, m, (int64_t)m * m, st));
+        else if (gwk)
+          HIPCHK(ctx, launch_gram_wk(M->Ep, M->ld, T, N, r, M->F, M->L, M->Kwk, M->A0wk, idx + b0 * T,
+                                     kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, wGk.p, w.G, st));
         else
           HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
       }

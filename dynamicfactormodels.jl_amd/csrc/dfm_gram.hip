@@ -317,3 +317,215 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
 }
 
 }  // namespace dfm
+
+namespace dfm {
+
+// ---------------------------------------------------------------------------
+// T >= N bootstrap Grams without the per-replicate SYRK (C2: 130 x 130 Grams
+// of 600 resampled rows, where 64 x 64 tiles waste 65 % of the MFMA work).
+// With X* = C + D P E (C = F L' the base common component, D = diag(eta),
+// P the row selection idx):
+//   X*'X* = C'C + L B + (L B)' + E' diag(w) E,
+//   B = F' D P E (r x N),  w_s = sum_{t : idx_t = s} eta_t^2,
+// and E' diag(w) E = sum_s w_s vec(E_s' E_s): for the whole batch ONE MFMA
+// GEMM  Q (nb x NP) = W (nb x T) K (T x NP), K[s][(n, m)] = E[s][n] E[s][m]
+// over the NP = N(N+1)/2 lower-triangle pairs (precomputed once per model).
+// Every replicate's Gram is then A0 + L B + (L B)' + unpack(Q), each lower
+// tile computed once and stored with its transpose (exactly symmetric).
+// Per-replicate sums run in a fixed order: results are batch-invariant.
+
+// K[s][n(n+1)/2 + m] = E[s][n] E[s][m] (m <= n); rows T..Tp-1 and pad column zero
+__global__ void gram_wk_kmat_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N, int64_t ldk,
+                                    double *__restrict__ K) {
+  const int s = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= ldk) return;
+  double v = 0.0;
+  const int64_t NP = (int64_t)N * (N + 1) / 2;
+  if (s < T && e < NP) {
+    int n = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+    while ((int64_t)(n + 1) * (n + 2) / 2 <= e) ++n;
+    while ((int64_t)n * (n + 1) / 2 > e) --n;
+    const int m = (int)(e - (int64_t)n * (n + 1) / 2);
+    v = Ep[(int64_t)s * ld + n] * Ep[(int64_t)s * ld + m];
+  }
+  K[(int64_t)s * ldk + e] = v;
+}
+
+// A0 = L (F'F) L' (the common-component Gram C'C), lower triangle mirrored
+__global__ void gram_wk_a0_kernel(const double *__restrict__ F, const double *__restrict__ L, int T, int N, int r,
+                                  double *__restrict__ A0) {
+  __shared__ double FF[32 * 32];
+  for (int e = threadIdx.x; e < r * r; e += 256) {
+    const int i = e / r, j = e % r;
+    double acc = 0.0;
+    for (int t = 0; t < T; ++t) acc = fma(F[(int64_t)t * r + i], F[(int64_t)t * r + j], acc);
+    FF[e] = acc;
+  }
+  __syncthreads();
+  const int n = blockIdx.x;
+  for (int m = threadIdx.x; m <= n; m += 256) {
+    double acc = 0.0;
+    for (int i = 0; i < r; ++i) {
+      double u = 0.0;
+      for (int j = 0; j < r; ++j) u = fma(FF[i * r + j], L[(int64_t)m * r + j], u);
+      acc = fma(L[(int64_t)n * r + i], u, acc);
+    }
+    A0[(int64_t)n * N + m] = acc;
+    A0[(int64_t)m * N + n] = acc;
+  }
+}
+
+// Per replicate: w (row rep of W, zero-padded to Tp) and B = F' D P E (r x N).
+// idx / eta of the replicate staged in LDS; w_s by a scan over t (fixed order).
+template <int RM>
+__global__ __launch_bounds__(256) void gram_wk_prep_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N,
+                                                           int r, const double *__restrict__ F,
+                                                           const int32_t *__restrict__ idx,
+                                                           const double *__restrict__ eta, int64_t rs, int Tp,
+                                                           double *__restrict__ W, double *__restrict__ Bo) {
+  extern __shared__ double pdyn[];
+  double *se = pdyn;                 // eta_t
+  double *sF = pdyn + T;             // F (T x r)
+  int *sx = (int *)(sF + (int64_t)T * r);   // idx_t
+  const int rep = blockIdx.x, tid = threadIdx.x;
+  const int32_t *ix = idx + (int64_t)rep * rs;
+  const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
+  for (int t = tid; t < T; t += 256) { sx[t] = ix[t]; se[t] = et ? et[t] : 1.0; }
+  for (int e = tid; e < T * r; e += 256) sF[e] = F[e];
+  __syncthreads();
+  // w_s = sum over t ascending of eta_t^2 [idx_t == s]: branch-free (adding
+  // +0 leaves the sum unchanged), 8 rows per round from LDS (broadcast reads)
+  double *se2 = pdyn + T + (int64_t)T * r + ((T + 7) & ~7) / 2;   // eta_t^2 (after sx: round_up(T, 8) ints)
+  for (int t = tid; t < T; t += 256) se2[t] = se[t] * se[t];
+  for (int t = T + tid; t < ((T + 7) & ~7); t += 256) { sx[t] = -1; se2[t] = 0.0; }
+  __syncthreads();
+  double *Wr = W + (int64_t)rep * Tp;
+  for (int s = tid; s < Tp; s += 256) {
+    double acc = 0.0;
+    if (s < T)
+      for (int t0 = 0; t0 < T; t0 += 8) {
+        int xv[8];
+        double ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { xv[u] = sx[t0 + u]; ev[u] = se2[t0 + u]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + (xv[u] == s ? ev[u] : 0.0);
+      }
+    Wr[s] = acc;
+  }
+  double *Br = Bo + (int64_t)rep * r * N;
+  constexpr int TU = 16;   // rows gathered per round: TU loads in flight per thread
+  for (int n = tid; n < N; n += 256) {
+    double acc[RM];
+#pragma unroll
+    for (int j = 0; j < RM; ++j) acc[j] = 0.0;
+    for (int t0 = 0; t0 < T; t0 += TU) {
+      double xv[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int t = min(t0 + u, T - 1);
+        xv[u] = Ep[(int64_t)sx[t] * ld + n];
+      }
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int t = t0 + u;
+        if (t >= T) break;
+        const double x = se[t] * xv[u];
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+          if (j < r) acc[j] = fma(sF[t * r + j], x, acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RM; ++j)
+      if (j < r) Br[(int64_t)j * N + n] = acc[j];
+  }
+}
+
+// G[rep] (N x N, row-major, stride N*N) = A0 + L B + (L B)' + unpack(Q[rep]),
+// one workgroup per (lower 32 x 32 tile (I, J), replicate): the tile is
+// computed once (rows n of block I read their contiguous packed Q ranges),
+// staged in LDS, and written as tile (I, J) and, transposed, (J, I) — both
+// coalesced, G exactly symmetric.
+constexpr int WK_TILE = 32;
+__global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__restrict__ A0,
+                                                              const double *__restrict__ L,
+                                                              const double *__restrict__ Bo,
+                                                              const double *__restrict__ Q, int64_t ldk, int N, int r,
+                                                              double *__restrict__ G) {
+  __shared__ double tile[WK_TILE][WK_TILE + 1];
+  const int rep = blockIdx.y, tid = threadIdx.x;
+  int I = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= (int)blockIdx.x) ++I;
+  while (I * (I + 1) / 2 > (int)blockIdx.x) --I;
+  const int J = blockIdx.x - I * (I + 1) / 2;
+  const double *Br = Bo + (int64_t)rep * r * N;
+  const double *Qr = Q + (int64_t)rep * ldk;
+  double *Gr = G + (int64_t)rep * N * N;
+  for (int e = tid; e < WK_TILE * WK_TILE; e += 256) {
+    const int a = e / WK_TILE, b = e % WK_TILE, n = I * WK_TILE + a, m = J * WK_TILE + b;
+    double v = 0.0;
+    if (n < N && m <= n) {
+      double x = 0.0, y = 0.0;   // x: L[n] . B[:, m],  y: L[m] . B[:, n]
+      for (int j = 0; j < r; ++j) {
+        x = fma(L[(int64_t)n * r + j], Br[(int64_t)j * N + m], x);
+        y = fma(L[(int64_t)m * r + j], Br[(int64_t)j * N + n], y);
+      }
+      v = (A0[(int64_t)n * N + m] + (x + y)) + Qr[(int64_t)n * (n + 1) / 2 + m];
+    }
+    tile[a][b] = v;
+  }
+  __syncthreads();
+  for (int e = tid; e < WK_TILE * WK_TILE; e += 256) {
+    const int a = e / WK_TILE, b = e % WK_TILE;
+    const int n = I * WK_TILE + a, m = J * WK_TILE + b;
+    if (n < N && m <= n) Gr[(int64_t)n * N + m] = tile[a][b];
+    const int n2 = J * WK_TILE + a, m2 = I * WK_TILE + b;   // transposed tile (J, I): entry (n2, m2) = (m2, n2)
+    if (m2 < N && n2 < m2) Gr[(int64_t)n2 * N + m2] = tile[b][a];
+  }
+}
+
+hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double *B, int64_t ldb,
+                       double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
+                       const int *col_done, int col_group, bool b_padded, const int *clist, const int *ccount);
+
+int64_t gram_wk_ldk(int N) { return ((int64_t)N * (N + 1) / 2 + 1) / 2 * 2; }
+int gram_wk_tp(int T) { return (T + 15) / 16 * 16; }
+// model-level: K (Tp x ldk) and A0 (N x N)
+hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
+                              double *K, double *A0, hipStream_t st) {
+  const int64_t ldk = gram_wk_ldk(N);
+  hipLaunchKernelGGL(gram_wk_kmat_kernel, dim3((unsigned)((ldk + 255) / 256), gram_wk_tp(T)), dim3(256), 0, st, Ep,
+                     ld, T, N, ldk, K);
+  hipLaunchKernelGGL(gram_wk_a0_kernel, dim3(N), dim3(256), 0, st, F, L, T, N, r, A0);
+  return hipGetLastError();
+}
+// workspace doubles for nb replicates: W (nb x Tp), B (nb x r x N), Q (nb x ldk)
+size_t gram_wk_work(int T, int N, int r, int nb) {
+  return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N));
+}
+// nb replicate Grams X*'X* (N x N each, stride N*N) of src (C + diag(eta) E[idx]).
+hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
+                          const double *K, const double *A0, const int32_t *idx, const double *eta, int64_t rs,
+                          int nb, double *work, double *G, hipStream_t st) {
+  const int Tp = gram_wk_tp(T);
+  const int64_t ldk = gram_wk_ldk(N);
+  double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)nb * r * N;
+  const int T8 = (T + 7) & ~7;
+  const size_t lds = (size_t)T * 8 + (size_t)T * r * 8 + (size_t)T8 * 4 + (size_t)T8 * 8;   // se, sF, sx, se2
+  if (r <= 8)
+    hipLaunchKernelGGL(gram_wk_prep_kernel<8>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, r, F, idx, eta, rs, Tp, W,
+                       Bo);
+  else
+    hipLaunchKernelGGL(gram_wk_prep_kernel<16>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, r, F, idx, eta, rs, Tp,
+                       W, Bo);
+  hipError_t e = launch_gemm(false, W, Tp, K, ldk, Q, ldk, nb, (int)ldk, T, st, nullptr, 1, true, nullptr, nullptr);
+  if (e != hipSuccess) return e;
+  const int nt = (N + WK_TILE - 1) / WK_TILE;
+  hipLaunchKernelGGL(gram_wk_combine_kernel, dim3(nt * (nt + 1) / 2, nb), dim3(256), 0, st, A0, L, Bo, Q, ldk, N, r,
+                     G);
+  return hipGetLastError();
+}
+
+}  // namespace dfm
