@@ -101,12 +101,15 @@ def c2(D, ctx, args):
                                        f"LR/LM/Wald all variables at bp={bp} + V + ICp2 (inputs resident)",
            "value": round(B / s, 1), "unit": "replicates/s", "ms_per_job": round(s * 1e3, 3),
            "kernels_ms_per_job": {k: round(v[0] / (args.reps + 1), 4) for k, v in tm.items() if v[1]}}
-    # K1 roofline: the fused-gather Gram X*'X* (130 x 130 over T = 600) per
-    # replicate, SYRK count N (N + 1) T, over its HIP-event time
+    # Gram roofline: the replicate Grams X*'X* (130 x 130 over T = 600), SYRK
+    # count N (N + 1) T per replicate (the weighted GEMM Q = W K
+    # of the gram_wk path does 2 T N (N + 1) / 2, the same count), over the
+    # HIP-event time of the whole Gram phase (prep + GEMM + combine)
     gms, gn = tm.get("gram", (0.0, 0))
     if gn:
         flop = B * (args.reps + 1) * N * (N + 1) * T
-        rec["roofline_gram"] = {"kernel": "gram_kernel<COLS> (fused resample gather, v_mfma_f64_4x4x4_4b)",
+        rec["roofline_gram"] = {"kernel": "gram_wk: prep (w, B = F'DPE) + ONE batch GEMM Q = W K on gemmh_kernel_t "
+                                          "(v_mfma_f64_4x4x4_4b) + tiled symmetric combine",
                                 "bound": "mfma", "achieved": round(flop / (gms * 1e-3) / 1e12, 3), "peak": 78.6,
                                 "unit": "TFLOP/s", "frac": round(flop / (gms * 1e-3) / 1e12 / 78.6, 4),
                                 "avg_launch_ms": round(gms / gn, 4), "flop_per_replicate": N * (N + 1) * T}
