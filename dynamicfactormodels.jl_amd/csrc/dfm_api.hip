@@ -94,7 +94,7 @@ struct FactBase {
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst);
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr);
 size_t fact_workspace_bytes(int T, int nb, int P);
 int fact_t_max();
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
@@ -145,6 +145,9 @@ struct dfm_ctx {
   double ms[DFM_KC_COUNT] = {};
   int64_t launches[DFM_KC_COUNT] = {};
   int64_t eig_batches = 0, eig_iters = 0, eig_iters_max = 0, rep_iters = 0, gemm_products = 0;
+  // factored runs accumulate {replicate-iterations, GEMM replicate-products}
+  // here on the device (no host sync after the eigen loop); read on query
+  long long *cnt_dev = nullptr;
 };
 
 struct dfm_model {
@@ -261,6 +264,12 @@ int dfm_ctx_create(int device, dfm_ctx **out) {
   if (hipSetDevice(device) != hipSuccess) { delete c; return -3; }
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return -4; }
   c->stream = c->own;
+  if (hipMalloc((void **)&c->cnt_dev, 2 * sizeof(long long)) != hipSuccess ||
+      hipMemsetAsync(c->cnt_dev, 0, 2 * sizeof(long long), c->stream) != hipSuccess) {
+    hipStreamDestroy(c->own);
+    delete c;
+    return -4;
+  }
   {   // stream-ordered scratch (split-K Gram partials) stays mapped between calls
     hipMemPool_t pool;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
@@ -285,6 +294,7 @@ static void ctx_release(dfm_ctx *ctx) {
   hipStreamSynchronize(ctx->stream);
   harvest(ctx);
   for (auto e : ctx->pool) hipEventDestroy(e);
+  hipFree(ctx->cnt_dev);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -333,7 +343,16 @@ int dfm_ctx_reset_timing(dfm_ctx *ctx) {
   harvest(ctx);
   for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
   ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = ctx->rep_iters = ctx->gemm_products = 0;
+  hipMemsetAsync(ctx->cnt_dev, 0, 2 * sizeof(long long), ctx->stream);
   return 0;
+}
+// host totals + the device-side counters of factored runs (one sync, on query)
+static void read_counts(dfm_ctx *ctx, int64_t *rep_iters, int64_t *products) {
+  long long c[2] = {0, 0};
+  hipMemcpyAsync(c, ctx->cnt_dev, sizeof(c), hipMemcpyDeviceToHost, ctx->stream);
+  hipStreamSynchronize(ctx->stream);
+  if (rep_iters) *rep_iters = ctx->rep_iters + c[0];
+  if (products) *products = ctx->gemm_products + c[1];
 }
 int dfm_ctx_eig_stats(dfm_ctx *ctx, int64_t *batches, int64_t *iters_total, int64_t *iters_max) {
   if (!ctx) return -1;
@@ -351,12 +370,12 @@ static void note_iters(dfm_ctx *ctx) {
 }
 int dfm_ctx_gemm_products(dfm_ctx *ctx, int64_t *products) {
   if (!ctx || !products) return -1;
-  *products = ctx->gemm_products;
+  read_counts(ctx, nullptr, products);
   return 0;
 }
 int dfm_ctx_rep_iters(dfm_ctx *ctx, int64_t *rep_iters) {
   if (!ctx || !rep_iters) return -1;
-  *rep_iters = ctx->rep_iters;
+  read_counts(ctx, rep_iters, nullptr);
   return 0;
 }
 const char *dfm_kernel_class_name(int cls) {
@@ -1102,7 +1121,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     if (fact) {
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
-                                w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst);
+                                w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst,
+                                ctx->cnt_dev);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);

@@ -802,6 +802,19 @@ int64_t g_last_gemm_products = 0;   // replicate-products H . Z of the last fact
 // Sum of the unconverged-replicate counts seen by the products of iterations
 // 0..last (shift = 1: the product of iteration it runs before that
 // iteration's convergence check, so it sees active[it-1]; active[-1] = nb).
+// Device-side form of count_rep_iters for the factored run: adds the
+// replicate-iterations (GEMM launches 0..last_gemm, shift 1) and the GEMM
+// replicate-products (those plus the Chebyshev GEMMs 0..last_cheb, shift 0)
+// to cnt[0], cnt[1] — no host synchronisation after the eigen loop.
+__global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm, int last_cheb, int nb,
+                                   long long *cnt) {
+  if (threadIdx.x != 0) return;
+  long long a = 0, b = 0;
+  for (int it = 0; it <= last_gemm; ++it) a += it - 1 < 0 ? nb : active[it - 1];
+  for (int it = 0; it <= last_cheb; ++it) b += active[it];
+  cnt[0] += a;       // one thread; launches on the context's stream are ordered
+  cnt[1] += a + b;
+}
 static int64_t count_rep_iters(const int *active_dev, int last, int shift, int nb, hipStream_t st) {
   if (last < 0) return 0;
   std::vector<int> a((size_t)last + 2, 0);
@@ -1676,7 +1689,7 @@ template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                            char *fws, double *lam, double *Uk, double *trace_out, int *status,
-                           hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst) {
+                           hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst, long long *cnt) {
   const int m = fb.T;
   EigWork w = carve(ws, m, nb, P, maxit);
   const int64_t ldz = (int64_t)nb * P;
@@ -1770,9 +1783,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     qs = (int64_t)m * P;
   }
   g_last_iters = it;
-  g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
   // the Chebyshev GEMM of iteration it runs after that iteration's check
-  g_last_gemm_products = g_last_rep_iters + count_rep_iters(w.active, last_cheb, 0, nb, st);
+  if (cnt) {
+    hipLaunchKernelGGL(count_iters_kernel, dim3(1), dim3(64), 0, st, w.active, last_gemm, last_cheb, nb, cnt);
+    g_last_rep_iters = g_last_gemm_products = 0;
+  } else {
+    g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
+    g_last_gemm_products = g_last_rep_iters + count_rep_iters(w.active, last_cheb, 0, nb, st);
+  }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
   if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
@@ -1785,14 +1803,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst) {
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
   if (fb.r > 16 || fb.T > F2_T_MAX) return -1;   // callers take the direct path
   if (p <= 16)
     return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                               trace_out, status, st, tf, tctx, off, lst);
+                               trace_out, status, st, tf, tctx, off, lst, cnt);
   return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                             trace_out, status, st, tf, tctx, off, lst);
+                             trace_out, status, st, tf, tctx, off, lst, cnt);
 }
 int fact_t_max() { return F2_T_MAX; }
 
