@@ -148,6 +148,10 @@ struct dfm_ctx {
   // factored runs accumulate {replicate-iterations, GEMM replicate-products}
   // here on the device (no host sync after the eigen loop); read on query
   long long *cnt_dev = nullptr;
+  // expanding-windows scratch: one arena reused call to call (stream-ordered),
+  // grown to the largest call's need — no per-call pool malloc/free on the host
+  char *warena = nullptr;
+  size_t warena_cap = 0, warena_need = 0;
 };
 
 struct dfm_model {
@@ -295,6 +299,7 @@ static void ctx_release(dfm_ctx *ctx) {
   harvest(ctx);
   for (auto e : ctx->pool) hipEventDestroy(e);
   hipFree(ctx->cnt_dev);
+  hipFree(ctx->warena);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -884,8 +889,12 @@ int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
 }
 
 // Per-batch device workspace layout for the bootstrap.
+// T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk)
+static bool use_gram_wk(const dfm_model *M) {
+  return M->orient == 1 && M->nblk == 1 && M->N <= 256 && M->r >= 1 && M->r <= 16 && M->T <= 8192;
+}
 struct BootWs {
-  double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat, *blam, *btr;
+  double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat, *blam, *btr, *gwk;
   int *status, *ost, *off, *lst;
   char *eig, *chow, *fact, *fload;
   size_t eig_bytes, chow_bytes, fact_bytes, fload_bytes;
@@ -919,6 +928,7 @@ static size_t boot_ws_bytes(const dfm_model *M, int nb, int P, int maxit, bool c
   w.fload = take(w.fload_bytes);
   w.off = (int *)take(fact ? (size_t)nb * (T + 1) * 4 : 4);
   w.lst = (int *)take(fact ? (size_t)nb * T * 4 : 4);
+  w.gwk = (double *)take(use_gram_wk(M) ? gram_wk_work(T, N, r, nb) * 8 : 8);
   if (o) *o = w;
   return off;
 }
@@ -998,7 +1008,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   // identity (gram_fact_kernel, 2 T^2 r flop each) instead of the SYRK
   const bool gid = !fact && (M->orient == 0) && M->nblk == 1 && r >= 1 && r <= 16 && T <= 4096;
   // T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk)
-  const bool gwk = (M->orient == 1) && M->nblk == 1 && N <= 256 && r >= 1 && r <= 16 && T <= 8192;
+  const bool gwk = use_gram_wk(M);
   if (pcp && m > spectrum_any_max())
     return fail(ctx, -31, "PCp criteria inside the bootstrap need each replicate's full spectrum: "
                           "supported for min(T,N) <= %d", spectrum_any_max());
@@ -1012,6 +1022,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       nb = (int64_t)std::max(1.0, std::min(16384.0, std::floor(16e9 / per)));
     } else {
       double gbytes = (double)m * m * 8 * (pcp ? 3 : 1);
+      if (gwk) gbytes += 8.0 * (double)gram_wk_work(T, N, r, 1);
       if (wide)
         gbytes += 8.0 * ((double)dense_eig_work(m, r) + (double)T * M->ld + (double)ols_wide_work(T, q + r));
       if (chow_wide) gbytes += 8.0 * ((double)chow_wide_work(T, N, r) + (double)T * M->ld + 3.0 * N);
@@ -1068,8 +1079,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
   boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, &w, M->ws);
   // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
   // src/criteria.jl:18), its spectrum, sigma^2 per replicate
-  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc, wGk;
-  if (gwk) HIPCHK(ctx, dalloc(&wGk.p, gram_wk_work(T, N, r, (int)nb)));
+  DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc;
   if (wide) {
     HIPCHK(ctx, dalloc(&wDe.p, (size_t)nb * dense_eig_work(m, r)));
     if (q + r > 32) HIPCHK(ctx, dalloc(&wOls.p, (size_t)nb * ols_wide_work(T, q + r)));
@@ -1154,7 +1164,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
                                        w.G, m, (int64_t)m * m, st));
         else if (gwk)
           HIPCHK(ctx, launch_gram_wk(M->Ep, M->ld, T, N, r, M->F, M->L, M->Kwk, M->A0wk, idx + b0 * T,
-                                     kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, wGk.p, w.G, st));
+                                     kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, w.gwk, w.G, st));
         else
           HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? N : T, T, w.G, m, (int64_t)m * m, n, st));
       }
@@ -1660,10 +1670,30 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   int rc = upload_panel(ctx, X, T, N, ldx, dp, dev);
   if (rc) return rc;
   std::vector<int> hTn(P), hkr(P);
-  // scratch: stream-ordered pool allocations (no device-wide sync on free)
+  // scratch: bump allocation from the context's arena (sized by the largest
+  // earlier call; stream-ordered reuse), overflow from the stream-ordered pool
+  if (ctx->warena_need > ctx->warena_cap) {
+    hipStreamSynchronize(st);
+    hipFree(ctx->warena);
+    ctx->warena = nullptr;
+    ctx->warena_cap = 0;
+    if (hipMalloc((void **)&ctx->warena, ctx->warena_need) == hipSuccess) ctx->warena_cap = ctx->warena_need;
+  }
   std::vector<void *> frees;
-  auto dal = [&](size_t bytes) -> void * { void *ptr = nullptr; if (hipMallocAsync(&ptr, std::max<size_t>(bytes, 8), st) != hipSuccess) return nullptr; frees.push_back(ptr); return ptr; };
-  struct Freer { std::vector<void *> &v; hipStream_t s; ~Freer() { for (void *x : v) hipFreeAsync(x, s); } } freer{frees, st};
+  size_t aoff = 0, aneed = 0;
+  auto dal = [&](size_t bytes) -> void * {
+    const size_t b = (std::max<size_t>(bytes, 8) + 255) & ~size_t(255);
+    aneed += b;
+    if (aoff + b <= ctx->warena_cap) { void *ptr = ctx->warena + aoff; aoff += b; return ptr; }
+    void *ptr = nullptr;
+    if (hipMallocAsync(&ptr, b, st) != hipSuccess) return nullptr;
+    frees.push_back(ptr);
+    return ptr;
+  };
+  struct Freer {
+    std::vector<void *> &v; hipStream_t s; dfm_ctx *c; size_t &need;
+    ~Freer() { for (void *x : v) hipFreeAsync(x, s); c->warena_need = std::max(c->warena_need, need); }
+  } freer{frees, st, ctx, aneed};
   // window w as a "replicate" of the panel: identity rows, row mask t < n0 + w
   int32_t *didx = (int32_t *)dal((size_t)P * T * 4);
   double *deta = (double *)dal((size_t)P * T * 8);
