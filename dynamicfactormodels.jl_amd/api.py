@@ -400,7 +400,7 @@ def principal_components(x, k: int, *, ctx: Optional[Context] = None):
 
 def gram_spectrum(x, *, ctx: Optional[Context] = None):
     """All eigenvalues (descending) of the smaller Gram, min(T,N) <=
-    ``dfm_full_spectrum_max()`` (4096): Jacobi in LDS up to 140, Householder
+    ``dfm_full_spectrum_max()`` (4096): Jacobi in LDS up to 32, Householder
     tridiagonalisation + bisection beyond."""
     ctx = ctx or default_context()
     x = _f64(x, 2)
