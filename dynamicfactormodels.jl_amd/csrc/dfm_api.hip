@@ -63,6 +63,9 @@ hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m,
 // dfm_model.hip
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
 __global__ void colmajor_from_rows_kernel(const double *, int64_t, int, int, double *);
+bool launch_factors_cols_fact(const double *Ep, int64_t ld, int T, int N, int k, const double *Fb, const double *Lb,
+                              int rb, const int32_t *idx, const double *eta, int64_t rs, int nb, const double *Uk,
+                              double *F, double *L, int64_t fstride, hipStream_t st);
 int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb, const double *Uk,
                    double *F, double *L, double *colssr, hipStream_t st, double Ts = 0, int64_t fstride = 0);
 __global__ void colssr_cols_kernel(const double *, int64_t, int64_t, int, int, const double *,
@@ -1170,7 +1173,14 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       }
       int rc = eig_any(w.G, m, n, M->Ub, w.lam, w.Uk, w.trace, b0);
       if (rc) return rc;
-      if ((rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
+      bool done_f = false;
+      if (gwk) {   // T >= N: F* = (F (L' L*) + D P (E L*)) / N, no pass over the resampled panel
+        Scope sc(ctx, DFM_KC_FACTORS);
+        done_f = launch_factors_cols_fact(M->Ep, M->ld, T, N, r, M->F, M->L, r, idx + b0 * T,
+                                          kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, w.Uk, w.F, w.L,
+                                          (int64_t)T * r, st);
+      }
+      if (!done_f && (rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
     }
     if (q + r <= 32) {
       Scope sc(ctx, DFM_KC_OLS);

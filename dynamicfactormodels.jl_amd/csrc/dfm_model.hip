@@ -645,6 +645,84 @@ int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb,
 
 
 
+// T >= N bootstrap factors by the same identity as the replicate Grams
+// (dfm_gram.hip gram_wk_*): with X* = C + D P E, C = F L' (base fit) and the
+// replicate loadings L* = sqrt(N) U*,
+//   F* = X* L* / N = ( F (L' L*) + D P (E L*) ) / N,
+// so a replicate needs E L* (T x N x k, E shared and L2-resident) and the
+// k x k block L' L* instead of a pass over its resampled panel.  One
+// workgroup per replicate: L* and E L* staged in LDS (the gather idx_t is then
+// an LDS read), L = L* written.  Requirements: k <= KM, (T + N) KM doubles of LDS.
+template <int KM>
+__global__ __launch_bounds__(256) void factors_cols_fact_kernel(const double *__restrict__ Ep, int64_t ld, int T,
+                                                                int N, int k, const double *__restrict__ Fb,
+                                                                const double *__restrict__ Lb, int rb,
+                                                                const int32_t *__restrict__ idx,
+                                                                const double *__restrict__ eta, int64_t rs,
+                                                                const double *__restrict__ Uk,
+                                                                double *__restrict__ F, double *__restrict__ L,
+                                                                int64_t fstride) {
+  extern __shared__ double fdyn[];
+  double *sL = fdyn;                        // N x KM: L* = sqrt(N) U*
+  double *sEL = sL + (size_t)N * KM;        // T x KM: E L*
+  __shared__ double sM[32 * KM];            // rb x k: L' L*
+  const int rep = blockIdx.x, tid = threadIdx.x;
+  const double sN = sqrt((double)N);
+  const double *U = Uk + (int64_t)rep * N * k;
+  double *Lr = L + (int64_t)rep * N * k;
+  for (int e = tid; e < N * KM; e += 256) {
+    const int n = e / KM, j = e - n * KM;
+    const double v = j < k ? sN * U[(int64_t)n * k + j] : 0.0;
+    sL[e] = v;
+    if (j < k) Lr[(int64_t)n * k + j] = v;
+  }
+  __syncthreads();
+  // M = L' L* (rb x k): one dot product of length N per entry, in n order
+  for (int e = tid; e < rb * k; e += 256) {
+    const int i = e / k, j = e - i * k;
+    double acc = 0.0;
+    for (int n = 0; n < N; ++n) acc = fma(Lb[(int64_t)n * rb + i], sL[n * KM + j], acc);
+    sM[i * KM + j] = acc;
+  }
+  // E L*: row s per thread, n in order (the row stays in L1 across n)
+  for (int s0 = tid; s0 < T; s0 += 256) {
+    double acc[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) acc[j] = 0.0;
+    const double *er = Ep + (int64_t)s0 * ld;
+    for (int n = 0; n < N; ++n) {
+      const double x = er[n];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) acc[j] = fma(x, sL[n * KM + j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) sEL[s0 * KM + j] = acc[j];
+  }
+  __syncthreads();
+  const int32_t *ix = idx + (int64_t)rep * rs;
+  const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
+  double *Fr = F + (int64_t)rep * fstride;
+  const double invN = 1.0 / N;
+  for (int e = tid; e < T * k; e += 256) {
+    const int t = e / k, j = e - t * k;
+    double c = 0.0;   // (F (L' L*))[t][j]
+    for (int i = 0; i < rb; ++i) c = fma(Fb[(int64_t)t * rb + i], sM[i * KM + j], c);
+    const double x = fma(et ? et[t] : 1.0, sEL[ix[t] * KM + j], c);
+    Fr[(int64_t)t * k + j] = x * invN;
+  }
+}
+// nb replicates; false when the shape does not fit (caller keeps launch_factors)
+bool launch_factors_cols_fact(const double *Ep, int64_t ld, int T, int N, int k, const double *Fb, const double *Lb,
+                              int rb, const int32_t *idx, const double *eta, int64_t rs, int nb, const double *Uk,
+                              double *F, double *L, int64_t fstride, hipStream_t st) {
+  if (k < 1 || k > 8 || rb < 1 || rb > 32) return false;
+  const size_t lds = (size_t)(T + N) * 8 * 8;
+  if (lds > 64 * 1024) return false;
+  hipLaunchKernelGGL(factors_cols_fact_kernel<8>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, k, Fb, Lb, rb, idx, eta,
+                     rs, Uk, F, L, fstride);
+  return hipGetLastError() == hipSuccess;
+}
+
 // ------------------------------------------------------------ break blocks
 // Per-variable ||E_n||^2 of a row-major residual panel, rows summed in order
 // (the per-variable SSR the Chow LR test reads, for a model fitted per break
