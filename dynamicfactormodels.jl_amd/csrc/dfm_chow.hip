@@ -123,6 +123,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
                                                        double *__restrict__ WD) {
   constexpr int TR = 64;
   constexpr int RR = CH_RMAX;
+  constexpr int CU = 16;   // rows whose gathered values are in flight together
   __shared__ double sF[TR * R], sZ[TR * R], sE[TR];
   __shared__ int sI[TR];
   __shared__ ChowPrep P;
@@ -172,10 +173,20 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    for (int rr = 0; rr < tn; ++rr) {
+    // CU rows per round: every row's gathered x loaded before the sums
+    // (CU loads in flight per thread instead of one dependent load per row);
+    // the arithmetic and its order are unchanged
+    for (int rb = 0; rb < tn; rb += CU) {
+    double xs[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) { const int rq = min(rb + u, tn - 1); xs[u] = xval(rq, t0 + rq); }
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const int rr = rb + u;
+      if (rr >= tn) break;
       const int t = t0 + rr;
       if (BRK && t == next) { ++cb; next = blk.a[cb + 1]; load_l(cb); }
-      const double x = xval(rr, t);
+      const double x = xs[u];
       double ev = x;
 #pragma unroll
       for (int j = 0; j < R; ++j) ev -= sF[rr * R + j] * l[j];
@@ -191,6 +202,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
 #pragma unroll
         for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[rr * R + j], g2[j]);
       }
+    }
     }
   }
   // subperiod OLS coefficients gamma_j = A_j^-1 g_j, Wald beta = M^-1 [g1+g2; g2],
@@ -227,9 +239,16 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    for (int rr = 0; rr < tn; ++rr) {
+    for (int rb = 0; rb < tn; rb += CU) {
+    double xs[CU];
+#pragma unroll
+    for (int uq = 0; uq < CU; ++uq) { const int rq = min(rb + uq, tn - 1); xs[uq] = xval(rq, t0 + rq); }
+#pragma unroll
+    for (int uq = 0; uq < CU; ++uq) {
+      const int rr = rb + uq;
+      if (rr >= tn) break;
       const int t = t0 + rr;
-      const double x = xval(rr, t);
+      const double x = xs[uq];
       const bool post = t >= bp;
       double u = x, rs = x;
 #pragma unroll
@@ -248,6 +267,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
       for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[rr * R + c2], S[e]); ++e; }
+    }
     }
   }
   if (!ok) return;
