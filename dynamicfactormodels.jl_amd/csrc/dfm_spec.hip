@@ -158,6 +158,13 @@ __global__ __launch_bounds__(TRI_THREADS) void tridiag_kernel(const double *__re
 
 // Eigenvalue j (descending) of the symmetric tridiagonal (d, e) by bisection
 // on the Sturm count (LAPACK dlaebz's recurrence with its pivmin guard).
+// Multisection (Sturm counts at BS_G points per eigenvalue, one per lane of
+// a BS_G-lane group): the interval shrinks (BS_G + 1)-fold per count instead
+// of 2-fold, so an eigenvalue needs ~13 sequential O(m) counts instead of
+// ~53.  Every lane of a group computes the same new interval from the group's
+// ballot (no data exchange beyond it): deterministic.  Same tolerance as the
+// bisection it replaces: eps * ||T|| (+ 4 pivmin).
+constexpr int BS_G = 16;
 __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ din,
                                                      const double *__restrict__ ein, int mst, int m0, int dm,
                                                      int nev, double *__restrict__ ev) {
@@ -188,29 +195,38 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double *__restrict__ 
     e2[m] = fmax(2.2e-308, emax * 2.2e-308);   // pivmin (slot m: LDS holds 2m+1)
   }
   __syncthreads();
-  const int j = blockIdx.x * 256 + tid;
-  if (j >= nev) return;
+  const int g = tid % BS_G, j = blockIdx.x * (256 / BS_G) + tid / BS_G;
+  const bool live = j < nev;   // the whole group agrees (j is per group)
   const double pivmin = e2[m];
-  const int kth = m - 1 - j;   // ascending index of eigenvalue j (descending)
+  const int kth = m - 1 - (live ? j : 0);   // ascending index of eigenvalue j (descending)
   double lo = bnd[0], hi = bnd[1];
   // absolute accuracy eps * ||T||: what the reduction itself guarantees
   const double tol = 2.2e-16 * fmax(fabs(lo), fabs(hi));
-  for (int it = 0; it < 160; ++it) {
-    const double mid = 0.5 * (lo + hi);
-    if (hi - lo <= tol + 4.0 * pivmin || mid <= lo || mid >= hi) break;
-    // number of eigenvalues < mid
+  const int gshift = (threadIdx.x & 63) & ~(BS_G - 1);
+  for (int it = 0; it < 64; ++it) {
+    if (hi - lo <= tol + 4.0 * pivmin) break;   // group-uniform
+    const double w = (hi - lo) / (BS_G + 1);
+    const double x = lo + w * (g + 1);
+    // number of eigenvalues < x
     int cnt = 0;
-    double q = d[0] - mid;
+    double q = d[0] - x;
     if (fabs(q) < pivmin) q = -pivmin;
     cnt += q < 0.0;
     for (int i = 1; i < m; ++i) {
-      q = d[i] - mid - e2[i - 1] / q;
+      q = d[i] - x - e2[i - 1] / q;
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
     }
-    if (cnt > kth) hi = mid; else lo = mid;
+    // first point above eigenvalue kth: lanes with cnt > kth
+    const unsigned long long above = (__ballot(cnt > kth) >> gshift) & ((1ull << BS_G) - 1);
+    const int gs = above ? __builtin_ctzll(above) : BS_G;
+    const double nlo = gs > 0 ? lo + w * gs : lo;
+    const double nhi = gs < BS_G ? lo + w * (gs + 1) : hi;
+    if (!(nlo > lo || nhi < hi)) break;   // no representable progress
+    lo = fmax(lo, nlo);
+    hi = fmin(hi, nhi);
   }
-  ev[(int64_t)rep * (dm ? mst : nev) + j] = 0.5 * (lo + hi);
+  if (live && g == 0) ev[(int64_t)rep * (dm ? mst : nev) + j] = 0.5 * (lo + hi);
 }
 
 // Jacobi (LDS-resident, 1 WG per CU) only for small matrices: from m ~ 40 on
@@ -233,8 +249,8 @@ hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, in
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
   hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
                      strideG, m, m0, dm, 0, S, d, e, (double *)nullptr);
-  hipLaunchKernelGGL(bisect_kernel, dim3((m + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
-                     d, e, m, m0, dm, 0, ev);
+  hipLaunchKernelGGL(bisect_kernel, dim3((m * BS_G + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double),
+                     st, d, e, m, m0, dm, 0, ev);
   return hipGetLastError();
 }
 hipError_t launch_spectrum(const double *G, int64_t ldg, int64_t strideG, int m, int nb, double *ev,
@@ -493,8 +509,8 @@ hipError_t launch_dense_eig_batched(const double *G, int64_t ldg, int64_t stride
   const int pad = (dmv != 0 || mv0 != m) ? 1 : 0;
   hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
                      strideG, m, mv0, dmv, pad, S, d, e, taus);
-  hipLaunchKernelGGL(bisect_kernel, dim3((k + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double), st,
-                     d, e, m, m, 0, k, lam);
+  hipLaunchKernelGGL(bisect_kernel, dim3((k * BS_G + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double),
+                     st, d, e, m, m, 0, k, lam);
   hipLaunchKernelGGL(stein_shifts_kernel, dim3(nb), dim3(64), 0, st, d, e, m, lam, k, sig, tn);
   hipLaunchKernelGGL(invit_kernel, dim3((k + 63) / 64, nb), dim3(64), 0, st, d, e, m, k, sig, tn, ua, ub, uc, ud, piv,
                      Z);
