@@ -238,6 +238,78 @@ int64_t spectrum_work(int m, int nb) {
 }
 int spectrum_any_max() { return SPEC_ANY_MAX; }
 
+// Tridiagonal form (d, e) only, for m <= TRI_LDS_MAX: the whole symmetric
+// matrix resident in LDS (row stride m + 1), LAPACK dsytd2 (lower) step by
+// step: reflector of column k, p = tau A22 v with one thread per row (no
+// cross-lane reductions per row), w = p - (tau/2)(p'v) v, A22 -= v w' + w v'.
+// Single fits (C1's PCp sigma^2, m = 100): 529 -> 477 us per matrix — the
+// step sequence (two block reductions and three barriers per reflector), not
+// the memory level, bounds both forms.
+constexpr int TRI_LDS_MAX = 128;
+constexpr int TRL_THREADS = 256;
+DFM_DEV double trl_sum(double v, double *red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < TRL_THREADS / 64; ++i) s += red[i];
+  return s;
+}
+__global__ __launch_bounds__(TRL_THREADS) void tridiag_lds_kernel(const double *__restrict__ G, int64_t ldg,
+                                                                  int64_t strideG, int mst, int m0, int dm,
+                                                                  double *__restrict__ dout,
+                                                                  double *__restrict__ eout) {
+  extern __shared__ double sm[];
+  __shared__ double red[TRL_THREADS / 64];
+  const int tid = threadIdx.x, rep = blockIdx.x;
+  const int m = m0 + dm * rep, S = m + 1;
+  double *A = sm, *v = A + (size_t)m * S, *p = v + m;
+  const double *g = G + (int64_t)rep * strideG;
+  double *d = dout + (int64_t)rep * mst, *e = eout + (int64_t)rep * mst;
+  for (int x = tid; x < m * m; x += TRL_THREADS) {
+    const int a = x / m, b = x - a * m;
+    A[a * S + b] = 0.5 * (g[(int64_t)a * ldg + b] + g[(int64_t)b * ldg + a]);
+  }
+  __syncthreads();
+  for (int k = 0; k + 1 < m; ++k) {
+    double ss = 0.0;
+    for (int i = k + 2 + tid; i < m; i += TRL_THREADS) ss += A[i * S + k] * A[i * S + k];
+    const double xn2 = trl_sum(ss, red);
+    const double alpha = A[(k + 1) * S + k];
+    double beta = alpha, tau = 0.0, scale = 0.0;
+    if (xn2 > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+      tau = (beta - alpha) / beta;
+      scale = 1.0 / (alpha - beta);
+    }
+    if (tid == 0) { d[k] = A[k * S + k]; e[k] = beta; }
+    for (int i = k + 1 + tid; i < m; i += TRL_THREADS) v[i] = i == k + 1 ? 1.0 : A[i * S + k] * scale;
+    __syncthreads();
+    if (tau == 0.0) continue;   // column already reduced (uniform)
+    double pv = 0.0;
+    for (int a = k + 1 + tid; a < m; a += TRL_THREADS) {
+      double acc = 0.0;
+      for (int b = k + 1; b < m; ++b) acc = fma(A[a * S + b], v[b], acc);
+      acc *= tau;
+      p[a] = acc;
+      pv += acc * v[a];
+    }
+    const double K = 0.5 * tau * trl_sum(pv, red);   // (syncs: p visible)
+    for (int a = k + 1 + tid; a < m; a += TRL_THREADS) p[a] -= K * v[a];   // w
+    __syncthreads();
+    const int n2 = m - k - 1;
+    for (int x = tid; x < n2 * n2; x += TRL_THREADS) {
+      const int a = k + 1 + x / n2, b = k + 1 + x % n2;
+      A[a * S + b] -= v[a] * p[b] + p[a] * v[b];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) d[m - 1] = A[(m - 1) * S + m - 1];
+}
+
 // All eigenvalues (descending) of nb symmetric matrices G + rep * strideG;
 // matrix rep has size m0 + dm * rep <= m (dm = 0: all m x m), ev rows stride m.
 // work: spectrum_work(m, nb) doubles (none for m <= SPEC_MAX).
@@ -247,8 +319,18 @@ hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, in
   if (m <= JACOBI_MAX) return launch_spectrum_jacobi(G, ldg, strideG, m, m0, dm, nb, ev, st);
   if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
-  hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
-                     strideG, m, m0, dm, 0, S, d, e, (double *)nullptr);
+  static const bool lds_attr = hipFuncSetAttribute((const void *)tridiag_lds_kernel,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (TRI_LDS_MAX * (TRI_LDS_MAX + 1) + 2 * TRI_LDS_MAX) * 8) ==
+                               hipSuccess;
+  // the LDS form holds one workgroup per CU: only when the matrices do not
+  // outnumber the CUs (single fits); large batches keep the global-memory form
+  if (m <= TRI_LDS_MAX && nb <= 256 && lds_attr)
+    hipLaunchKernelGGL(tridiag_lds_kernel, dim3(nb), dim3(TRL_THREADS), (size_t)(m * (m + 1) + 2 * m) * sizeof(double),
+                       st, G, ldg, strideG, m, m0, dm, d, e);
+  else
+    hipLaunchKernelGGL(tridiag_kernel, dim3(nb), dim3(TRI_THREADS), (size_t)4 * m * sizeof(double), st, G, ldg,
+                       strideG, m, m0, dm, 0, S, d, e, (double *)nullptr);
   hipLaunchKernelGGL(bisect_kernel, dim3((m * BS_G + 255) / 256, nb), dim3(256), (size_t)(2 * m + 1) * sizeof(double),
                      st, d, e, m, m0, dm, 0, ev);
   return hipGetLastError();
