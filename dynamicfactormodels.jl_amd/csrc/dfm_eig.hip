@@ -33,7 +33,7 @@ struct EigWork {
   double *small;           // nb x SMALL_STRIDE (A, Bm, theta, dead)
   int *done, *iters, *active;
   double *trace;           // nb
-  long long *dbg;          // debug phase stamps of replicate 0 (DFM_SMALL_STAMPS), else null
+  long long *dbg;          // phase stamps of replicate 0 (SMALL_STAMP) when a diagnostic build points it at a buffer; null
 };
 #define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
@@ -313,84 +313,26 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
 
 // ---------------------------------------------------------------- small
 // One wave per replicate, all p x p algebra in LDS, written for latency:
-// Cholesky with the pivot broadcast by a lane shuffle, explicit triangular
-// inverses (so every solve becomes a parallel matrix product), and a parallel
-// cyclic Jacobi whose round is ONE phase: with the pairs of a round disjoint,
-// every 2x2 block (pair s1 rows, pair s2 cols) is rotated J1' B J2 by one lane.
+// Cholesky + triangular inverse in registers (every solve becomes a parallel
+// matrix product), and a parallel cyclic Jacobi whose round is ONE phase: with
+// the pairs of a round disjoint, every 2x2 block (pair s1 rows, pair s2 cols)
+// is rotated J1' B J2 by one lane.
 template <int P>
 struct SmallLds {
   static constexpr int S = P + 1;
-  // A is first written after the last read of H~ (the sorted Ritz values),
-  // and the Cholesky factor L is dead while the Jacobi vectors V live:
-  // aliasing them cuts the image from 8 to 6 P x (P+1) matrices (more
-  // workgroups per CU for this latency-bound kernel)
-  union { double Hq[P * S]; double A[P * S]; };
-  union { double L[P * S]; double V[P * S]; };
-  double Yq[P * S], Qq[P * S], Li[P * S], W[P * S];
+  // four P x (P+1) regions, reused as the matrices' lifetimes end (the
+  // kernel is latency-bound and one wave per workgroup, so the LDS image sets
+  // the occupancy: 4 regions = 9.2 KB at P = 16, 16 waves per CU, where the 6
+  // of the unshared layout held it to 11):
+  //   R1  H~ (Q'Y, then Li Q'Y Li', Jacobi)      -> W = V[:, perm] -> Y'Y A -> Bm
+  //   R2  Q'Q -> Li Q'Y -> V (Jacobi vectors)    -> A = Li' W
+  //   R3  Y'Y                                    -> Z'Z = A' Y'Y A
+  //   R4  Li = chol(Q'Q)^-1                      -> chol(Z'Z)^-1
+  double R1[P * S], R2[P * S], R3[P * S], R4[P * S];
   double rc[P / 2], rs[P / 2];
-  double dinv[P];   // 1 / L[j][j] of the last Cholesky (1 for dead pivots)
   int ra[P / 2], rb[P / 2], perm[P];
-  int dead1[P], dead2[P];
+  int dead[P];
 };
-
-// lower Cholesky M = Lo Lo' (p x p), tiny pivots -> dead (unit diagonal, zero column);
-// dinv[j] = 1 / Lo[j][j].  One reciprocal square root per pivot (no divide).
-template <int P>
-DFM_DEV void wave_chol(const double *M, double *Lo, double *dinv, int *dead, int p) {
-  constexpr int S = P + 1;
-  const int lane = threadIdx.x;
-  double mx = 0.0;
-  for (int j = lane; j < p; j += 64) mx = fmax(mx, fabs(M[j * S + j]));
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-  for (int e = lane; e < P * S; e += 64) Lo[e] = 0.0;
-  __syncthreads();
-  const double thresh = 1e-22 * mx;
-  for (int j = 0; j < p; ++j) {
-    const int i = lane;
-    double s0 = 0.0, s1 = 0.0;
-    if (i >= j && i < p) {
-      s0 = M[i * S + j];
-      int q = 0;
-      for (; q + 1 < j; q += 2) {   // two accumulators: half the dependent chain
-        s0 -= Lo[i * S + q] * Lo[j * S + q];
-        s1 -= Lo[i * S + q + 1] * Lo[j * S + q + 1];
-      }
-      if (q < j) s0 -= Lo[i * S + q] * Lo[j * S + q];
-    }
-    const double sv = s0 + s1;
-    const double sj = __shfl(sv, j);
-    const bool dd = !(sj > thresh);
-    const double inv = dd ? 1.0 : rsqrt(sj);
-    if (i == j) { Lo[j * S + j] = dd ? 1.0 : sj * inv; dead[j] = dd; dinv[j] = inv; }
-    else if (i > j && i < p) Lo[i * S + j] = dd ? 0.0 : sv * inv;
-    __syncthreads();
-  }
-}
-
-// Li = Lo^-1 (lower), column c per lane in registers; rows of dead pivots zeroed.
-template <int P>
-DFM_DEV void wave_trinv(const double *Lo, const double *dinv, double *Li, const int *dead, int p) {
-  constexpr int S = P + 1;
-  const int c = threadIdx.x;
-  if (c < P) {
-    double x[P];
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      double s0 = (i == c) ? 1.0 : 0.0, s1 = 0.0;
-#pragma unroll
-      for (int q = 0; q + 1 < i; q += 2) {
-        s0 -= Lo[i * S + q] * x[q];
-        s1 -= Lo[i * S + q + 1] * x[q + 1];
-      }
-      if (i & 1) s0 -= Lo[i * S + i - 1] * x[i - 1];
-      x[i] = (i < p) ? (s0 + s1) * dinv[i] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < P; ++i) Li[i * S + c] = (i < p && c < p && !dead[i]) ? x[i] : 0.0;
-  }
-  __syncthreads();
-}
 
 DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compile-time constant in unrolled loops)
   const long long b = __double_as_longlong(x);
@@ -490,6 +432,7 @@ template <int P>
 __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb, int jsweeps) {
   constexpr int S = P + 1;
   __shared__ SmallLds<P> sm;
+  double *const Hq = sm.R1, *const Yq = sm.R3;   // region map: SmallLds
   const int lane = threadIdx.x, rep = blockIdx.x;
   if (w.done[rep]) return;
   SMALL_STAMP(0);
@@ -511,23 +454,24 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
     for (int u = 0; u < PER; ++u) {
       const int e = lane + 64 * u;
       const int which = e / (P * P), a = (e / P) % P, c = e % P;
-      double *M = which == 0 ? sm.Hq : (which == 1 ? sm.Yq : sm.Qq);
+      double *M = which == 0 ? sm.R1 : (which == 1 ? sm.R3 : sm.R2);
       M[a * S + c] = acc[u];
     }
   }
   __syncthreads();
   SMALL_STAMP(1);
-  wave_sym<P>(sm.Hq);
+  wave_sym<P>(Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
-  wave_chol_inv<P>(sm.Qq, sm.Li, sm.dead1, p);
+  wave_chol_inv<P>(sm.R2, sm.R4, sm.dead, p);
   SMALL_STAMP(2);
   SMALL_STAMP(3);
-  wave_mm<P, false, false>(sm.Li, sm.Hq, sm.W);
-  wave_mm<P, false, true>(sm.W, sm.Li, sm.Hq);
-  wave_sym<P>(sm.Hq);
+  wave_mm<P, false, false>(sm.R4, Hq, sm.R2);   // Q'Q is dead once Li is formed
+  wave_mm<P, false, true>(sm.R2, sm.R4, Hq);
+  wave_sym<P>(Hq);
   SMALL_STAMP(4);
-  for (int e = lane; e < P * S; e += 64) sm.V[e] = ((e / S) == (e % S)) ? 1.0 : 0.0;
+  for (int e = lane; e < P * S; e += 64) sm.R2[e] = ((e / S) == (e % S)) ? 1.0 : 0.0;   // V
   __syncthreads();
+  double *const V = sm.R2;
   // 3. parallel cyclic Jacobi (circle-method pairs; index p is a dummy when p is odd)
   const int n = p + (p & 1), h = n / 2;
   // A pair is rotated only while |h_ab| > 4 eps sqrt(|h_aa h_bb|) (the classic
@@ -535,18 +479,38 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   // O(eps^2)); the sweep loop ends at the first sweep that rotates nothing.
   // (A Frobenius off-diagonal test sits at the rounding floor for these
   // matrices and ran every sweep to the cap.)
+  // every lane's 2x2 blocks and V entries are the same in every round: their
+  // (s1, s2) and (k, sI) indices are computed once here, and the circle-method
+  // positions advance by a wrapped increment (no integer division per round)
+  constexpr int NHB = ((P / 2) * (P / 2) + 63) / 64, NVE = (P * (P / 2) + 63) / 64;
+  int hb1[NHB], hb2[NHB], vk[NVE], vs[NVE];
+#pragma unroll
+  for (int u = 0; u < NHB; ++u) {
+    const int e = lane + 64 * u;
+    hb1[u] = (h > 0 && e < h * h) ? e / h : -1;
+    hb2[u] = (h > 0 && e < h * h) ? e % h : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < NVE; ++u) {
+    const int e = lane + 64 * u;
+    vk[u] = (h > 0 && e < p * h) ? e / h : -1;
+    vs[u] = (h > 0 && e < p * h) ? e % h : 0;
+  }
+  const int n1 = n - 1, pa = lane, pb = n - 1 - lane;
   for (int sweep = 0; sweep < jsweeps; ++sweep) {
     bool rotated = false;
-    for (int r = 0; r < n - 1; ++r) {
+    int xa = pa - 1, xb = pb - 1;   // position - 1 + r, wrapped into [0, n - 1)
+    for (int r = 0; r < n1; ++r, ++xa, ++xb) {
+      if (xa >= n1) xa -= n1;
+      if (xb >= n1) xb -= n1;
       bool rot = false;
       if (lane < h) {
-        const int pa = lane, pb = n - 1 - lane;
-        int a = pa == 0 ? 0 : 1 + (pa - 1 + r) % (n - 1);
-        int b = pb == 0 ? 0 : 1 + (pb - 1 + r) % (n - 1);
+        int a = pa == 0 ? 0 : 1 + xa;
+        int b = pb == 0 ? 0 : 1 + xb;
         if (a > b) { const int t = a; a = b; b = t; }
         double c = 1.0, sn = 0.0;
         if (b < p) {
-          const double hab = sm.Hq[a * S + b], haa = sm.Hq[a * S + a], hbb = sm.Hq[b * S + b];
+          const double hab = Hq[a * S + b], haa = Hq[a * S + a], hbb = Hq[b * S + b];
           if (fabs(hab) > 1e-300 && fabs(hab) > 8.9e-16 * sqrt(fabs(haa) * fabs(hbb))) {
             const double zeta = (hbb - haa) / (2.0 * hab);
             const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
@@ -562,26 +526,30 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
       if (!any) continue;   // wave-uniform: nothing to apply this round
       __syncthreads();
       // H <- J' H J by 2x2 blocks; V <- V J
-      for (int e = lane; e < h * h; e += 64) {
-        const int s1 = e / h, s2 = e % h;
+#pragma unroll
+      for (int u = 0; u < NHB; ++u) {
+        if (hb1[u] < 0) continue;
+        const int s1 = hb1[u], s2 = hb2[u];
         const int i0 = sm.ra[s1], i1 = sm.rb[s1], j0 = sm.ra[s2], j1 = sm.rb[s2];
         const double c1 = sm.rc[s1], n1 = sm.rs[s1], c2 = sm.rc[s2], n2 = sm.rs[s2];
-        const double b00 = sm.Hq[i0 * S + j0], b01 = sm.Hq[i0 * S + j1];
-        const double b10 = sm.Hq[i1 * S + j0], b11 = sm.Hq[i1 * S + j1];
+        const double b00 = Hq[i0 * S + j0], b01 = Hq[i0 * S + j1];
+        const double b10 = Hq[i1 * S + j0], b11 = Hq[i1 * S + j1];
         const double t00 = c1 * b00 - n1 * b10, t01 = c1 * b01 - n1 * b11;
         const double t10 = n1 * b00 + c1 * b10, t11 = n1 * b01 + c1 * b11;
-        sm.Hq[i0 * S + j0] = c2 * t00 - n2 * t01;
-        sm.Hq[i0 * S + j1] = n2 * t00 + c2 * t01;
-        sm.Hq[i1 * S + j0] = c2 * t10 - n2 * t11;
-        sm.Hq[i1 * S + j1] = n2 * t10 + c2 * t11;
+        Hq[i0 * S + j0] = c2 * t00 - n2 * t01;
+        Hq[i0 * S + j1] = n2 * t00 + c2 * t01;
+        Hq[i1 * S + j0] = c2 * t10 - n2 * t11;
+        Hq[i1 * S + j1] = n2 * t10 + c2 * t11;
       }
-      for (int e = lane; e < p * h; e += 64) {
-        const int k = e / h, sI = e % h;
+#pragma unroll
+      for (int u = 0; u < NVE; ++u) {
+        if (vk[u] < 0) continue;
+        const int k = vk[u], sI = vs[u];
         const int a = sm.ra[sI], b = sm.rb[sI];
         const double c = sm.rc[sI], sn = sm.rs[sI];
-        const double va = sm.V[k * S + a], vb = sm.V[k * S + b];
-        sm.V[k * S + a] = c * va - sn * vb;
-        sm.V[k * S + b] = sn * va + c * vb;
+        const double va = V[k * S + a], vb = V[k * S + b];
+        V[k * S + a] = c * va - sn * vb;
+        V[k * S + b] = sn * va + c * vb;
       }
       __syncthreads();
     }
@@ -591,40 +559,43 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   SMALL_STAMP(5);
   // 4. sort descending (stable): lane j computes the rank of diagonal j
   for (int j = lane; j < p; j += 64) {
-    const double v = sm.Hq[j * S + j];
+    const double v = Hq[j * S + j];
     int rank = 0;
     for (int i = 0; i < p; ++i) {
-      const double u = sm.Hq[i * S + i];
+      const double u = Hq[i * S + i];
       rank += (u > v || (u == v && i < j)) ? 1 : 0;
     }
     sm.perm[rank] = j;
   }
   __syncthreads();
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  for (int j = lane; j < P; j += 64) small[2 * P * P + j] = j < p ? sm.Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
-  // W = V[:, perm] (zero-padded)
+  for (int j = lane; j < P; j += 64) small[2 * P * P + j] = j < p ? Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
+  __syncthreads();   // the Ritz values are read from R1 before W overwrites it
+  // W = V[:, perm] (zero-padded), into R1
+  double *const W = sm.R1;
   for (int e = lane; e < P * P; e += 64) {
     const int i = e / P, c = e % P;
-    sm.W[i * S + c] = (i < p && c < p) ? sm.V[i * S + sm.perm[c]] : 0.0;
+    W[i * S + c] = (i < p && c < p) ? V[i * S + sm.perm[c]] : 0.0;
   }
   __syncthreads();
   SMALL_STAMP(6);
   // 5. A = L^-T Vs = Li' W ;  Z'Z = A' (Y'Y) A ;  L2 = chol ;  Bm = A L2^-T
-  wave_mm<P, true, false>(sm.Li, sm.W, sm.A);
-  wave_mm<P, false, false>(sm.Yq, sm.A, sm.W);
-  wave_mm<P, true, false>(sm.A, sm.W, sm.Qq);
-  wave_sym<P>(sm.Qq);
+  double *const A = sm.R2;
+  wave_mm<P, true, false>(sm.R4, W, A);       // V is dead once permuted
+  wave_mm<P, false, false>(Yq, A, sm.R1);     // Y'Y A (W is dead)
+  wave_mm<P, true, false>(A, sm.R1, sm.R3);   // Z'Z (Y'Y is dead)
+  wave_sym<P>(sm.R3);
   SMALL_STAMP(7);
-  wave_chol_inv<P>(sm.Qq, sm.Li, sm.dead2, p);
+  wave_chol_inv<P>(sm.R3, sm.R4, sm.dead, p);
   SMALL_STAMP(8);
   SMALL_STAMP(9);
-  wave_mm<P, false, true>(sm.A, sm.Li, sm.W);   // Bm = A Li'
+  wave_mm<P, false, true>(A, sm.R4, sm.R1);   // Bm = A Li'
   for (int e = lane; e < P * P; e += 64) {
     const int a = e / P, c = e % P;
-    small[e] = (a < p && c < p) ? sm.A[a * S + c] : 0.0;
-    small[P * P + e] = (a < p && c < p) ? sm.W[a * S + c] : 0.0;
+    small[e] = (a < p && c < p) ? A[a * S + c] : 0.0;
+    small[P * P + e] = (a < p && c < p) ? sm.R1[a * S + c] : 0.0;
   }
-  for (int j = lane; j < P; j += 64) small[2 * P * P + P + j] = (j < p && sm.dead2[j]) ? 1.0 : 0.0;
+  for (int j = lane; j < P; j += 64) small[2 * P * P + P + j] = (j < p && sm.dead[j]) ? 1.0 : 0.0;
   SMALL_STAMP(10);
 }
 
