@@ -340,15 +340,18 @@ DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compil
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Li = Lo^-1 of the lower Cholesky factor M = Lo Lo' (p x p), in registers:
-// lane i < P holds row i.  Right-looking factorisation (step j: pivot by
+// Li = Lo^-1 of the lower Cholesky factor M = Lo Lo' (p x p): lane i < P
+// holds row i in registers.  Right-looking factorisation (step j: pivot by
 // readlane, column j scaled by one reciprocal square root, the trailing rows
-// updated with the column broadcast lane by lane), then lane c forward-
-// substitutes column c of the inverse with the rows of Lo broadcast the same
-// way — no LDS round trip per step.  Tiny pivots -> dead (unit diagonal, zero
-// column, zero row of Li), as the LDS form it replaces.
+// updated), then lane c forward-substitutes column c of the inverse.  M is
+// dead once its rows are in registers, so it holds the columns of Lo as they
+// are formed (column j in M's row j): every lane reads the values it needs
+// from there as same-address LDS broadcasts, one instruction per double
+// where a readlane pair plus its hazard wait took three or four (this
+// wave's own writes, in LDS order).  Tiny pivots -> dead (unit diagonal,
+// zero column, zero row of Li).
 template <int P>
-DFM_DEV void wave_chol_inv(const double *M, double *Li, int *dead, int p) {
+DFM_DEV void wave_chol_inv(double *M, double *Li, int *dead, int p) {
   constexpr int S = P + 1;
   const int lane = threadIdx.x;
   double mx = 0.0;
@@ -359,6 +362,7 @@ DFM_DEV void wave_chol_inv(const double *M, double *Li, int *dead, int p) {
   double r[P];
 #pragma unroll
   for (int k = 0; k < P; ++k) r[k] = (lane < p && k < p) ? M[min(lane, P - 1) * S + k] : 0.0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // M's rows are in registers before M is overwritten
   double inv_l = 1.0;
   int dead_l = 0;
 #pragma unroll
@@ -370,23 +374,27 @@ DFM_DEV void wave_chol_inv(const double *M, double *Li, int *dead, int p) {
       double lij = (lane > j && lane < p) ? (dd ? 0.0 : r[j] * inv) : 0.0;
       if (lane == j) { lij = dd ? 1.0 : sj * inv; inv_l = inv; dead_l = dd; }
       r[j] = lij;
+      if (lane < P) M[j * S + lane] = lij;          // column j of Lo
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int k = j + 1; k < P; ++k) r[k] = r[k] - lij * rl64(lij, k);
+      for (int k = j + 1; k < P; ++k) r[k] = r[k] - lij * M[j * S + k];
     }
   }
   if (lane < P) dead[lane] = lane < p ? dead_l : 0;
+  if (lane < P) M[(P - 1) * S + lane] = inv_l;   // 1 / Lo[i][i], over column P-1 of Lo (the substitution never reads it)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   double x[P];
 #pragma unroll
   for (int i = 0; i < P; ++i) {
     double sacc = (i == lane) ? 1.0 : 0.0;
 #pragma unroll
-    for (int q = 0; q < i; ++q) sacc = sacc - rl64(r[q], i) * x[q];
-    x[i] = (i < p) ? sacc * rl64(inv_l, i) : 0.0;
+    for (int q = 0; q < i; ++q) sacc = sacc - M[q * S + i] * x[q];
+    x[i] = (i < p) ? sacc * M[(P - 1) * S + i] : 0.0;
   }
   const bool dl = lane < p;
 #pragma unroll
   for (int i = 0; i < P; ++i) {
-    const bool di = __shfl(dead_l, i) != 0;
+    const bool di = dead[i] != 0;
     if (lane < P) Li[i * S + lane] = (i < p && dl && !di) ? x[i] : 0.0;
   }
   __syncthreads();
