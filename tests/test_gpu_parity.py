@@ -234,6 +234,33 @@ def test_wild_bootstrap_matches_oracle(dfm, oracle, T, N, r, mode):
         assert rel(out[b, 6:], ref[6:]) < 1e-9      # w-column coef/t: sign-invariant
 
 
+@pytest.mark.parametrize("mode", ["factored", "direct"])
+def test_wild_bootstrap_exact_rank_panel(dfm, oracle, mode):
+    """Replicates of an exact rank-3 panel: the factor residuals vanish, so every
+    replicate Gram has rank 3 and the Rayleigh-Ritz block (width > 3) runs
+    on rank-deficient Q'Q — the dead-pivot path of the in-register Cholesky and
+    its random refill.  Eigenvalues against the oracle; V at the rounding floor."""
+    rng = np.random.default_rng(31)
+    T, N, r = 60, 40, 3
+    x = rng.standard_normal((T, r)) @ rng.standard_normal((N, r)).T
+    y, w = rng.standard_normal(T), np.ones((T, 1))
+    g = dfm.DynamicFactorModel(y, w, x, r)
+    g.set_bootstrap_mode(mode)
+    o = oracle.DynamicFactorModel(y, w, x, r)
+    B = 4
+    idx, eta = oracle.draw_wild(np.random.default_rng(6), B, T)
+    S = dfm.Stat
+    out = dfm.wild_bootstrap(g, B, [S.V(), S.eigenvalue(1), S.eigenvalue(r), S.trace()], idx=idx, eta=eta)
+    assert np.all(np.isfinite(out))
+    for b in range(B):
+        xs = o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]]
+        d = oracle.DynamicFactorModel(y, w, xs, r)
+        tr = np.sum(xs * xs)
+        assert abs(out[b, 0]) < 1e-12 * tr / (N * T)
+        assert rel(out[b, 1:3], [d.eigenvalues[0][0], d.eigenvalues[0][r - 1]]) < STAT_RTOL
+        assert rel(out[b, 3], tr) < 1e-12
+
+
 @pytest.mark.parametrize("T,N", [(150, 70), (70, 150)])
 def test_residual_bootstrap_matches_oracle(dfm, oracle, T, N):
     y, x, w = panel(oracle, T, N, 2, 16)
