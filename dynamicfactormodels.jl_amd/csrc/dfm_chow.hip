@@ -112,9 +112,21 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
   }
 }
 
-template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK>
+// FLAT = false: one thread per variable, grid (variable blocks, replicate);
+// the block is sized to the panel width (64 .. 256) and the replicate's
+// ChowPrep is staged in LDS.  FLAT = true (N >= CH_FLAT_MIN_N, R <= 8): one
+// thread per (replicate, variable) pair in replicate-major order, so the lanes
+// of a 256-thread block run on into the next replicate's variables instead of
+// idling at the panel edge (C2, N = 130: 3 waves per replicate of which 62
+// lanes idle -> 2.03 waves); a block spans at most CH_FLAT_REPS replicates,
+// each with its own staged F, Z, eta and idx rows, and reads the small
+// ChowPrep matrices from global memory (L2).  Per (replicate, variable) the
+// arithmetic and its order are the same in both forms.
+constexpr int CH_FLAT_REPS = 4, CH_FLAT_MIN_N = 86;   // ceil(256 / 86) + 1 <= 4
+
+template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK, bool FLAT = false>
 __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
-                                                       const double *__restrict__ F,
+                                                       int nb, const double *__restrict__ F,
                                                        const double *__restrict__ Z,
                                                        const ChowPrep *__restrict__ prep,
                                                        const double *__restrict__ Lm,
@@ -124,33 +136,48 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
   constexpr int TR = 64;
   constexpr int RR = CH_RMAX;
   constexpr int CU = 16;   // rows whose gathered values are in flight together
-  __shared__ double sF[TR * R], sZ[TR * R], sE[TR];
-  __shared__ int sI[TR];
-  __shared__ ChowPrep P;
-  // one thread per variable; the block is sized to the panel width (64 .. 256)
-  const int tid = threadIdx.x, nth = blockDim.x, rep = blockIdx.y, i = blockIdx.x * nth + tid;
-  for (int e = tid; e < (int)(sizeof(ChowPrep) / 8); e += nth)
-    reinterpret_cast<double *>(&P)[e] = reinterpret_cast<const double *>(prep + rep)[e];
-  const double *Fr = F + (int64_t)rep * T * r;
-  const double *Zr = Z + (int64_t)rep * T * r;
-  const int32_t *idx = HAS_IDX ? src.idx + (int64_t)rep * src.rs : nullptr;
-  const double *eta = HAS_ETA ? src.eta + (int64_t)rep * src.rs : nullptr;
-  const bool ok = i < N;
+  constexpr int NR = FLAT ? CH_FLAT_REPS : 1;   // replicates staged per block
+  __shared__ double sF[NR][TR * R], sZ[NR][TR * R], sE[NR][TR];
+  __shared__ int sI[NR][TR];
+  const int tid = threadIdx.x, nth = blockDim.x;
+  int rep, i, rep0, nrw;
+  if constexpr (FLAT) {
+    const int64_t g = (int64_t)blockIdx.x * nth + tid, g0 = (int64_t)blockIdx.x * nth;
+    rep = (int)(g / N); i = (int)(g % N);
+    rep0 = (int)(g0 / N);
+    nrw = min(nb - 1, (int)((g0 + nth - 1) / N)) - rep0 + 1;
+  } else {
+    rep = blockIdx.y; i = blockIdx.x * nth + tid; rep0 = rep; nrw = 1;
+  }
+  const bool ok = FLAT ? rep < nb : i < N;
+  const int lr = FLAT ? (ok ? rep - rep0 : 0) : 0;   // this thread's staged replicate
+  const ChowPrep *Pp;
+  if constexpr (FLAT) {
+    Pp = prep + (ok ? rep : rep0);
+  } else {
+    __shared__ ChowPrep sP;
+    for (int e = tid; e < (int)(sizeof(ChowPrep) / 8); e += nth)
+      reinterpret_cast<double *>(&sP)[e] = reinterpret_cast<const double *>(prep + rep)[e];
+    Pp = &sP;
+  }
+  const ChowPrep &P = *Pp;
   auto stage = [&](int t0) {
-    for (int e = tid; e < TR * R; e += nth) {
-      const int rr = e / R, j = e % R, t = t0 + rr;
-      sF[e] = (t < T && j < r) ? Fr[(int64_t)t * r + j] : 0.0;
-      sZ[e] = (t < T && j < r) ? Zr[(int64_t)t * r + j] : 0.0;
+    for (int e = tid; e < nrw * TR * R; e += nth) {
+      const int q = e / (TR * R), f = e % (TR * R), rr = f / R, j = f % R, t = t0 + rr;
+      const int64_t base = (int64_t)(rep0 + q) * T * r;
+      sF[q][f] = (t < T && j < r) ? F[base + (int64_t)t * r + j] : 0.0;
+      sZ[q][f] = (t < T && j < r) ? Z[base + (int64_t)t * r + j] : 0.0;
     }
-    if (tid < TR) {
-      const int t = t0 + tid;
-      sE[tid] = (HAS_ETA && t < T) ? eta[t] : 1.0;
-      sI[tid] = t < T ? (HAS_IDX ? idx[t] : t) : 0;
+    for (int e = tid; e < nrw * TR; e += nth) {
+      const int q = e / TR, rr = e % TR, t = t0 + rr;
+      const int64_t ro = (int64_t)(rep0 + q) * src.rs;
+      sE[q][rr] = (HAS_ETA && t < T) ? src.eta[ro + t] : 1.0;
+      sI[q][rr] = t < T ? (HAS_IDX ? src.idx[ro + t] : t) : 0;
     }
   };
   auto xval = [&](int rr, int t) {
-    double x = src.E[(int64_t)sI[rr] * src.ld + i];
-    if (HAS_ETA) x *= sE[rr];
+    double x = src.E[(int64_t)sI[lr][rr] * src.ld + i];
+    if (HAS_ETA) x *= sE[lr][rr];
     if (HAS_C) x += src.C[(int64_t)t * src.ld + i];
     return x;
   };
@@ -189,18 +216,18 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
       const double x = xs[u];
       double ev = x;
 #pragma unroll
-      for (int j = 0; j < R; ++j) ev -= sF[rr * R + j] * l[j];
+      for (int j = 0; j < R; ++j) ev -= sF[lr][rr * R + j] * l[j];
       e2 = fma(ev, ev, e2);
       if (BRK && t >= bp) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[rr * R + j], cx[j]);
+        for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[lr][rr * R + j], cx[j]);
       }
       if (t < bp) {
 #pragma unroll
-        for (int j = 0; j < R; ++j) g1[j] = fma(x, sF[rr * R + j], g1[j]);
+        for (int j = 0; j < R; ++j) g1[j] = fma(x, sF[lr][rr * R + j], g1[j]);
       } else {
 #pragma unroll
-        for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[rr * R + j], g2[j]);
+        for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[lr][rr * R + j], g2[j]);
       }
     }
     }
@@ -253,7 +280,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
       double u = x, rs = x;
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        const double f = sF[rr * R + j];
+        const double f = sF[lr][rr * R + j];
         u -= f * (post ? b1[j] + b2[j] : b1[j]);
         rs -= f * (post ? ga2[j] : ga1[j]);
       }
@@ -261,12 +288,12 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
       const double u2 = u * u;
       double zs[R];
 #pragma unroll
-      for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[rr * R + j];
+      for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[lr][rr * R + j];
       int e = 0;
 #pragma unroll
       for (int a = 0; a < R; ++a)
 #pragma unroll
-        for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[rr * R + c2], S[e]); ++e; }
+        for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
     }
     }
   }
@@ -308,12 +335,20 @@ static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int
                           const double *F, const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
                           double *LM, double *WD, hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
-  // narrow panels (C2: N = 130) get a 192-thread block, not a half-idle 256
-  const int nth = std::min(256, (N + 63) / 64 * 64);
-  dim3 grid((N + nth - 1) / nth, nb), block(nth);
-#define DFM_CH(C_, E_, X_, B_)                                                                          \
-  hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_>), grid, block, 0, st, src, blk, T, N, r, bp, F, Z, \
-                     prep, Lm, LR, LM, WD)
+  const bool flat = R <= 8 && N >= CH_FLAT_MIN_N;
+  // non-flat: narrow panels get a block of round_up(N, 64) threads, not a half-idle 256
+  const int nth = flat ? 256 : std::min(256, (N + 63) / 64 * 64);
+  dim3 grid(flat ? (unsigned)(((int64_t)nb * N + 255) / 256) : (unsigned)((N + nth - 1) / nth), flat ? 1 : nb),
+      block(nth);
+#define DFM_CH(C_, E_, X_, B_)                                                                                  \
+  do {                                                                                                          \
+    if (flat)                                                                                                   \
+      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, (R <= 8)>), grid, block, 0, st, src, blk, T, N, r, \
+                         bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                   \
+    else                                                                                                        \
+      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_>), grid, block, 0, st, src, blk, T, N, r, bp, nb,   \
+                         F, Z, prep, Lm, LR, LM, WD);                                                           \
+  } while (0)
   if (blk.n > 1) {
     if (c && e && x) DFM_CH(true, true, true, true);
     else if (c && !e && x) DFM_CH(true, false, true, true);

@@ -272,23 +272,26 @@ def test_residual_bootstrap_matches_oracle(dfm, oracle, T, N):
     assert rel(out[:, 0], ref) < STAT_RTOL
 
 
-@pytest.mark.parametrize("T,N", [(160, 24), (80, 120)])
+# N = 24: one thread per variable per replicate block; N = 90, 120: the flat
+# (replicate, variable) mapping, blocks spanning up to 4 replicates (dfm_chow.hip)
+@pytest.mark.parametrize("T,N", [(160, 24), (80, 120), (100, 90)])
 def test_bootstrap_chow_all_matches_oracle(dfm, oracle, T, N):
     y, x, w = panel(oracle, T, N, 2, 17, model="Breitung_Eickmeier_2011", b=0.5)
     g = dfm.DynamicFactorModel(y, w, x, 2)
     o = oracle.DynamicFactorModel(y, w, x, 2)
-    idx, eta = oracle.draw_wild(np.random.default_rng(5), 3, T)
+    B = 6   # N = 90: the second 256-thread block spans replicates 2..5
+    idx, eta = oracle.draw_wild(np.random.default_rng(5), B, T)
     S = dfm.Stat
     bp = T // 2
-    out = dfm.wild_bootstrap(g, 3, [S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp)], idx=idx, eta=eta)
-    nv = min(N, 24)
-    for b in range(3):
+    out = dfm.wild_bootstrap(g, B, [S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp)], idx=idx, eta=eta)
+    vs = np.array(sorted(set(range(min(N, 12))) | set(range(max(0, N - 12), N))))   # both panel edges
+    for b in range(B):
         d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]], 2)
         ref = np.array([[oracle.LR_test(d, bp, i), oracle.LM_test(d, bp, i), oracle.Wald_test(d, bp, i)]
-                        for i in range(nv)])
-        assert rel(out[b, :nv], ref[:, 0]) < 1e-9
-        assert rel(out[b, N:N + nv], ref[:, 1]) < 1e-9
-        assert rel(out[b, 2 * N:2 * N + nv], ref[:, 2]) < 1e-9
+                        for i in vs])
+        assert rel(out[b, vs], ref[:, 0]) < 1e-9
+        assert rel(out[b, N + vs], ref[:, 1]) < 1e-9
+        assert rel(out[b, 2 * N + vs], ref[:, 2]) < 1e-9
 
 
 # -------------------------------------- full-size (C3) size-independent props
