@@ -62,8 +62,22 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
   for (int e = tid; e < 2 * r * r; e += 256) {
     const int which = e / (r * r), a = (e / r) % r, c = e % r;
     const int t0 = which ? bp : 0, t1 = which ? T : bp;
+    // 16 rows' operands loaded before their (in-order) products: the sum is
+    // the same dependent chain, without one load latency per row
+    constexpr int PU = 16;
     double s = 0.0;
-    for (int t = t0; t < t1; ++t) s = fma(Fr[(int64_t)t * r + a], Fr[(int64_t)t * r + c], s);
+    for (int tb = t0; tb < t1; tb += PU) {
+      double fa[PU], fc[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int t = min(tb + u, t1 - 1);
+        fa[u] = Fr[(int64_t)t * r + a];
+        fc[u] = Fr[(int64_t)t * r + c];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u)
+        if (tb + u < t1) s = fma(fa[u], fc[u], s);
+    }
     (which ? A2s : A1)[a * S + c] = s;
   }
   __syncthreads();
