@@ -195,6 +195,9 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < EROWS / 16; ++ks) {
+      // wave-uniform: rows past m (m = 130: 3 of 12 waves) and k steps past m
+      // only ever added zero products
+      if (row0 >= m || kc0 + ks * 16 >= m) continue;
       const int kg = kc0 + ks * 16 + fkc;
       double af[4], bf[P / 4];
 #pragma unroll
@@ -272,6 +275,9 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < EROWS / 16; ++ks) {
+      // wave-uniform: rows past m (m = 130: 3 of 12 waves) and k steps past m
+      // only ever added zero products
+      if (row0 >= m || kc0 + ks * 16 >= m) continue;
       const int kg = kc0 + ks * 16 + fkc;
       double af[4], bf[P / 4];
 #pragma unroll
