@@ -75,14 +75,43 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by the cgroup's
+    cpu.max quota when one is set (cgroup v2; v1's cfs quota otherwise).
+    Returns (count, how it was determined)."""
+    n = len(os.sched_getaffinity(0))
+    how = f"sched_getaffinity: {n}"
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        how += f", cgroup quota {quota:g}"
+        n = max(1, min(n, int(quota)))
+    return n, how
+
+
 def cpu_baseline(seconds: float = 12.0):
     """Reference-faithful oracle (full eig, full loadings, T x T hat matrix,
     serial replicate loop: the algorithm of src/bootstrap.jl:41-51 as written)
     on this host's cores, bounded samples, in the two modes of BASELINE.md:
       1. one process, OpenBLAS threads = the host's BLAS pool (Julia's serial
          loop over threaded BLAS);
-      2. a pool of min(16, cpu_count) processes x 1 BLAS thread (the box's
-         CPU share is 16; best CPU throughput for independent replicates).
+      2. a pool of processes x 1 BLAS thread, one per CPU of this process's
+         share (affinity mask and cgroup quota: cpu_share()); best CPU
+         throughput for independent replicates.
     `value` is the faster mode."""
     try:
         from threadpoolctl import threadpool_info
@@ -93,7 +122,7 @@ def cpu_baseline(seconds: float = 12.0):
         threads, blas_info = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), "unknown"
     n1, el1 = _c3_oracle_loop(seconds, 1)
     mode1 = {"value": n1 / el1, "cores": int(threads), "sample": f"{n1} replicates in {el1:.1f} s"}
-    workers = max(1, min(16, os.cpu_count() or 1))
+    workers, share_how = cpu_share()
     import multiprocessing as mp
     saved = {k: os.environ.get(k) for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS")}
     for k in saved:
@@ -116,7 +145,8 @@ def cpu_baseline(seconds: float = 12.0):
             "sample": f"C3 wild bootstrap (T=500 N=2000 r=8, V + ICp2), oracle/dfm_oracle.py "
                       f"reference-faithful loop; {best['sample']}",
             "modes": {"1_threaded_blas": mode1, "2_process_pool": mode2},
-            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(), "blas": blas_info}
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(), "cpu_share": share_how,
+            "blas": blas_info}
 
 
 def pmc_traffic(kernel):
@@ -343,8 +373,7 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                 "avg_launch_ms": round(per_launch_ms, 4), "replicates_per_launch": reps_per_launch,
-                "bytes_per_replicate": gbytes,
-                "gram_equivalent_tflops": round(SYRK_FLOP * reps_per_launch / (per_launch_ms * 1e-3) / 1e12, 2)}
+                "bytes_per_replicate": gbytes}
     rec = {
         "metric": "bootstrap replicates/sec (node), T=500 N=2000 r=8; % fp64 MFMA peak",
         "value": round(value, 2), "unit": "replicates/s", "n_gpus": world,
@@ -364,7 +393,6 @@ def main():
                          "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
         "eig_iterations": eig,
         "eig_filter": "degree-2 Chebyshev filter on [0, theta_p] between Rayleigh-Ritz steps",
-        "gram_equivalent_tflops": round(value * SYRK_FLOP / 1e12, 2),
         "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps),
     }
     if weak:

@@ -23,9 +23,9 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 const int *eig_iters_ptr(char *ws, int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
-extern int g_last_iters;
-extern int64_t g_last_rep_iters;
-extern int64_t g_last_gemm_products;
+extern thread_local int g_last_iters;   // per host thread: dfm_bootstrap_multi's shards run concurrently
+extern thread_local int64_t g_last_rep_iters;
+extern thread_local int64_t g_last_gemm_products;
 int spectrum_max();
 int spectrum_any_max();
 int64_t spectrum_work(int m, int nb);
@@ -109,6 +109,7 @@ hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r,
 size_t gram_wk_work(int T, int N, int r, int nb);
 int64_t gram_wk_ldk(int N);
 int gram_wk_tp(int T);
+size_t gram_wk_prep_lds(int T, int r);
 hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
                           const double *K, const double *A0, const int32_t *idx, const double *eta, int64_t rs,
                           int nb, double *work, double *G, hipStream_t st);
@@ -892,9 +893,13 @@ int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
 }
 
 // Per-batch device workspace layout for the bootstrap.
-// T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk)
+// T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk).
+// Its prep kernel stages the replicate's draws and F (T x r) in LDS: only
+// while that fits the default 64 KB dynamic-LDS launch; larger T r take the
+// fused-gather K1 Gram (gram_kernel<COLS>).
 static bool use_gram_wk(const dfm_model *M) {
-  return M->orient == 1 && M->nblk == 1 && M->N <= 256 && M->r >= 1 && M->r <= 16 && M->T <= 8192;
+  return M->orient == 1 && M->nblk == 1 && M->N <= 256 && M->r >= 1 && M->r <= 16 &&
+         gram_wk_prep_lds(M->T, M->r) <= 65536;
 }
 struct BootWs {
   double *G, *lam, *Uk, *trace, *F, *L, *colssr, *coef, *tstat, *blam, *btr, *gwk;

@@ -777,12 +777,12 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 // iterations, and the residual test of check_converged includes any leftover
 // off-diagonal coupling.
 constexpr int kJacobiSweeps = 2;
-int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
+thread_local int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
 // replicate-iterations of the last run's dominant product (G.Q in eig_gq, or
 // the H.Z GEMM in the factored solver) that still had an unconverged
 // replicate: the algorithmic work the roofline figure is priced on.
-int64_t g_last_rep_iters = 0;
-int64_t g_last_gemm_products = 0;   // replicate-products H . Z of the last factored run (both Chebyshev GEMMs)
+thread_local int64_t g_last_rep_iters = 0;
+thread_local int64_t g_last_gemm_products = 0;   // replicate-products H . Z of the last factored run (both Chebyshev GEMMs)
 
 // Sum of the unconverged-replicate counts seen by the products of iterations
 // 0..last (shift = 1: the product of iteration it runs before that

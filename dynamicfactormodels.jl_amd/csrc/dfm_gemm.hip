@@ -4,7 +4,7 @@
 //   B: K x Nc row-major (the k-rows of every replicate's skinny operand laid
 //   side by side: column block = one replicate's p columns).
 //
-// This is the compute core of the factored bootstrap (dfm_boot.hip): one
+// This is the compute core of the factored bootstrap (dfm_eig.hip): one
 // fixed, cache-resident left operand (H = E E' or E') shared by every
 // replicate of a batch, so the per-replicate eigen-iterations and the
 // loadings pass become single large MFMA GEMMs instead of nb memory-bound

@@ -490,6 +490,11 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done, int col_group, bool b_padded, const int *clist, const int *ccount);
 
+// gram_wk_prep_kernel's dynamic LDS: se (T), sF (T x r), sx (round_up(T, 8) ints), se2
+size_t gram_wk_prep_lds(int T, int r) {
+  const size_t T8 = (size_t)((T + 7) & ~7);
+  return (size_t)T * 8 + (size_t)T * r * 8 + T8 * 4 + T8 * 8;
+}
 int64_t gram_wk_ldk(int N) { return ((int64_t)N * (N + 1) / 2 + 1) / 2 * 2; }
 int gram_wk_tp(int T) { return (T + 15) / 16 * 16; }
 // model-level: K (Tp x ldk) and A0 (N x N)
@@ -512,8 +517,7 @@ hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, con
   const int Tp = gram_wk_tp(T);
   const int64_t ldk = gram_wk_ldk(N);
   double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)nb * r * N;
-  const int T8 = (T + 7) & ~7;
-  const size_t lds = (size_t)T * 8 + (size_t)T * r * 8 + (size_t)T8 * 4 + (size_t)T8 * 8;   // se, sF, sx, se2
+  const size_t lds = gram_wk_prep_lds(T, r);
   if (r <= 8)
     hipLaunchKernelGGL(gram_wk_prep_kernel<8>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, r, F, idx, eta, rs, Tp, W,
                        Bo);

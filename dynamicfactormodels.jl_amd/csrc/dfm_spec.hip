@@ -319,10 +319,10 @@ hipError_t launch_spectrum_var(const double *G, int64_t ldg, int64_t strideG, in
   if (m <= JACOBI_MAX) return launch_spectrum_jacobi(G, ldg, strideG, m, m0, dm, nb, ev, st);
   if (m > SPEC_ANY_MAX || !work) return hipErrorInvalidValue;
   double *S = work, *d = work + (int64_t)nb * m * m, *e = d + (int64_t)nb * m;
-  static const bool lds_attr = hipFuncSetAttribute((const void *)tridiag_lds_kernel,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   (TRI_LDS_MAX * (TRI_LDS_MAX + 1) + 2 * TRI_LDS_MAX) * 8) ==
-                               hipSuccess;
+  // the dynamic-LDS attribute is per device: set it on every call (cheap)
+  const bool lds_attr = hipFuncSetAttribute((const void *)tridiag_lds_kernel,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (TRI_LDS_MAX * (TRI_LDS_MAX + 1) + 2 * TRI_LDS_MAX) * 8) == hipSuccess;
   // the LDS form holds one workgroup per CU: only when the matrices do not
   // outnumber the CUs (single fits); large batches keep the global-memory form
   if (m <= TRI_LDS_MAX && nb <= 256 && lds_attr)

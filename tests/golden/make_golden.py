@@ -16,6 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import dfm_oracle as O  # noqa: E402
+import dfm_xp as XP  # noqa: E402
 
 
 def c1():
@@ -147,6 +148,62 @@ def c5():
     np.savez_compressed(os.path.join(HERE, "c5_windows.npz"), windows=np.array(wins),
                         digest=np.array([x.sum(), np.abs(x).sum(), y.sum()]),
                         **{k: np.array(v) for k, v in rows.items()})
+
+
+def xp():
+    """Extended-precision (double-double) referee values for golden C1 and C2
+    (oracle/dfm_xp.py): the values the reference's algebra defines, to ~1e-28,
+    and each one's parity bar max(1e-10 |exact|, |oracle - exact|) — the GPU
+    must be within 1e-10 relative of the exact value, or no further from it
+    than the fp64 oracle is.  C2: the base fit's Chow LR/LM/Wald of all 130
+    variables, and V, ICp2 and all 3 x 130 Chow statistics of each of the 16
+    wild-bootstrap replicates (same idx/eta as the C2 fixture)."""
+    def bar(exact, orc):
+        exact, orc = np.asarray(exact, float), np.asarray(orc, float)
+        return np.maximum(1e-10 * np.abs(exact), np.abs(orc - exact))
+
+    out = {}
+    g = np.load(os.path.join(HERE, "c1_bai_ng_T200_N100_r3.npz"))
+    f = XP.XPFit(g["y"], g["w"], g["x"], int(g["r"]), "ICp2")
+    o = O.DynamicFactorModel(g["y"], g["w"], g["x"], int(g["r"]), "ICp2")
+    s = np.sign(np.sum(f.F.f64() * o.F, axis=0))
+    coef, t = f.coefficients.f64(), f.t_stats.copy()
+    coef[1:] *= s
+    t[1:] *= s
+    out.update(c1_coef=coef, c1_coef_bar=bar(coef, o.coefficients), c1_t=t, c1_t_bar=bar(t, o.t_stats),
+               c1_V=f.V.f64(), c1_eig=f.lam[:16].f64(), c1_ICp2=f.criterion_value("ICp2"))
+    ic = np.empty((len(O.CRITERIA), 8))
+    h = (100 + 1) // 2
+    s2 = (f.trace - f.lam[:h].sum()) / float(200 * 100)
+    for k in range(1, 9):
+        fk = XP.XPFit(g["y"], g["w"], g["x"], k)
+        for ci, name in enumerate(O.CRITERIA):
+            ic[ci, k - 1] = fk.criterion_value(name, s2)
+    out.update(c1_ic=ic, c1_ic_bar=bar(ic, g["ic_values"]))
+    print("xp c1 done", flush=True)
+
+    g = np.load(os.path.join(HERE, "c2_breitung_eickmeier_T600_N130_B16.npz"))
+    r, bp = int(g["r"]), int(g["bp"])
+    N = g["x"].shape[1]
+    f = XP.XPFit(g["y"], g["w"], g["x"], r, "ICp2")
+    base = np.column_stack(f.chow_all(bp))
+    out.update(c2_base_chow=base, c2_base_chow_bar=bar(base, g["base_chow"]), c2_base_V=f.V.f64())
+    o = O.DynamicFactorModel(g["y"], g["w"], g["x"], r, "ICp2")
+    C, E = o.common_component, o.factor_residuals
+    rows, bars = [], []
+    for b in range(g["idx"].shape[0]):
+        xs = f.replicate(g["idx"][b], g["eta"][b])
+        fb = XP.XPFit(g["y"], g["w"], xs, r, "ICp2")
+        ex = np.concatenate([[fb.V.f64(), fb.criterion_value("ICp2")], *fb.chow_all(bp)])
+        d = O.DynamicFactorModel(g["y"], g["w"], C + g["eta"][b][:, None] * E[g["idx"][b]], r, "ICp2")
+        orc = np.concatenate([[O.factor_residual_variance(d), d.number_of_factors_criterion_value],
+                              [O.LR_test(d, bp, i) for i in range(N)], [O.LM_test(d, bp, i) for i in range(N)],
+                              [O.Wald_test(d, bp, i) for i in range(N)]])
+        rows.append(ex)
+        bars.append(bar(ex, orc))
+        print("xp c2 replicate", b, "oracle max rel dev", float(np.max(np.abs(orc - ex) / np.abs(ex))), flush=True)
+    out.update(c2_boot=np.array(rows), c2_boot_bar=np.array(bars))
+    np.savez_compressed(os.path.join(HERE, "xp_c1_c2.npz"), **out)
 
 
 if __name__ == "__main__":

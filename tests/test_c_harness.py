@@ -98,10 +98,10 @@ def test_harness_matches_python_binding_and_oracle(dfm, oracle, tmp_path):
     assert np.array_equal(h["chow_LR"], LR) and np.array_equal(h["chow_LM"], LM) and np.array_equal(h["chow_Wald"], W)
     bo = oracle.DynamicFactorModel(y, w, X, 2, "BIC", [T // 2 + 1])
     ref = np.array([oracle.LR_test(bo, T // 2 + 1, i) for i in range(10)])
-    assert np.max(np.abs(h["break_chow_LR"][:10] - ref) / np.abs(ref)) < 1e-9
+    assert np.max(np.abs(h["break_chow_LR"][:10] - ref) / np.abs(ref)) < 1e-10
     assert np.max(np.abs(h["normalize_col0"] - oracle.normalize(X)[:, 0])) < 1e-13 * 10
     tx, _ = oracle.targeted_predictors_hard(y, w, X, "per_candidate")
-    assert np.max(np.abs(h["tp_hard_t"] - tx) / np.abs(tx)) < 1e-9
+    assert np.max(np.abs(h["tp_hard_t"] - tx) / np.abs(tx)) < 1e-10
     pred, true = dfm.pseudo_out_of_sample_forecasts(dfm.DynamicFactorModel, y, w, X, "ICp2", num_predictions=4,
                                                     kmax=4)
     assert np.array_equal(h["windows_pred"], pred)

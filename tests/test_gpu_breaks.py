@@ -40,8 +40,8 @@ def assert_block_fit(g, o, oracle):
     assert np.max(np.abs(g.factor_residuals - o.factor_residuals)) < ANGLE_TOL * np.max(np.abs(x_of(o)))
     # coefficients / t-stats of weak (noise-level) factors chosen by a sweep are
     # O(1e-3): compare on the vector's scale, as the factor angle bounds them
-    assert np.max(np.abs(g.coefficients - o.coefficients)) < 1e-9 * np.max(np.abs(o.coefficients))
-    assert np.max(np.abs(g.t_stats - o.t_stats)) < 1e-9 * np.max(np.abs(o.t_stats))
+    assert np.max(np.abs(g.coefficients - o.coefficients)) < STAT_RTOL * np.max(np.abs(o.coefficients))
+    assert np.max(np.abs(g.t_stats - o.t_stats)) < STAT_RTOL * np.max(np.abs(o.t_stats))
     if o.number_of_factors_criterion:
         assert abs(g.number_of_factors_criterion_value - o.number_of_factors_criterion_value) <= \
             STAT_RTOL * abs(o.number_of_factors_criterion_value)
@@ -92,8 +92,8 @@ def test_break_wild_bootstrap_matches_oracle(dfm, oracle, T, N, breaks):
                                       2, "ICp2", breaks)
         assert abs(out[b, 0] - oracle.factor_residual_variance(d)) < STAT_RTOL * oracle.factor_residual_variance(d)
         assert abs(out[b, 1] - d.number_of_factors_criterion_value) < STAT_RTOL * abs(d.number_of_factors_criterion_value)
-        assert abs(out[b, 2] - d.coefficients[0]) < 1e-9 * abs(d.coefficients[0])
-        assert abs(out[b, 3] - d.t_stats[0]) < 1e-9 * abs(d.t_stats[0])
+        assert abs(out[b, 2] - d.coefficients[0]) < STAT_RTOL * abs(d.coefficients[0])
+        assert abs(out[b, 3] - d.t_stats[0]) < STAT_RTOL * abs(d.t_stats[0])
 
 
 def test_break_residual_bootstrap_block_draws(dfm, oracle):
@@ -150,10 +150,10 @@ def test_break_chow_all_matches_oracle(dfm, oracle, T, N, r, breaks):
         nv = min(N, 30)
         ref = np.array([[oracle.LR_test(o, bp, i), oracle.LM_test(o, bp, i), oracle.Wald_test(o, bp, i)]
                         for i in range(nv)])
-        assert rel(LR[:nv], ref[:, 0]) < 1e-9, bp
-        assert rel(LM[:nv], ref[:, 1]) < 1e-9, bp
-        assert rel(W[:nv], ref[:, 2]) < 1e-9, bp
-        assert abs(dfm.LM_test(g, bp, 3) - ref[2, 1]) < 1e-9 * abs(ref[2, 1])
+        assert rel(LR[:nv], ref[:, 0]) < STAT_RTOL, bp
+        assert rel(LM[:nv], ref[:, 1]) < STAT_RTOL, bp
+        assert rel(W[:nv], ref[:, 2]) < STAT_RTOL, bp
+        assert abs(dfm.LM_test(g, bp, 3) - ref[2, 1]) < STAT_RTOL * abs(ref[2, 1])
 
 
 @pytest.mark.parametrize("T,N,r,breaks", [(120, 60, 2, [61]), (96, 150, 3, [31, 70]), (120, 160, 17, [61])])
@@ -171,13 +171,13 @@ def test_break_bootstrap_chow_matches_oracle(dfm, oracle, T, N, r, breaks):
                                       r, "ICp2", breaks)
         ref = np.array([[oracle.LR_test(d, bp, i), oracle.LM_test(d, bp, i), oracle.Wald_test(d, bp, i)]
                         for i in range(nv)])
-        assert rel(out[b, :nv], ref[:, 0]) < 1e-9
-        assert rel(out[b, N:N + nv], ref[:, 1]) < 1e-9
-        assert rel(out[b, 2 * N:2 * N + nv], ref[:, 2]) < 1e-9
+        assert rel(out[b, :nv], ref[:, 0]) < STAT_RTOL
+        assert rel(out[b, N:N + nv], ref[:, 1]) < STAT_RTOL
+        assert rel(out[b, 2 * N:2 * N + nv], ref[:, 2]) < STAT_RTOL
         assert out[b, 3 * N] == out[b, 1]      # single-variable LR(bp, 2) = row entry 2
     idx_r = oracle.draw_residual(np.random.default_rng(13), 2, T, breaks)
     outr = dfm.residual_bootstrap(g, 2, [S.LM_all(bp)], idx=idx_r)
     for b in range(2):
         d = oracle.DynamicFactorModel(y, w, o.common_component + o.factor_residuals[idx_r[b]], r, "ICp2", breaks)
         ref = np.array([oracle.LM_test(d, bp, i) for i in range(nv)])
-        assert rel(outr[b, :nv], ref) < 1e-9
+        assert rel(outr[b, :nv], ref) < STAT_RTOL

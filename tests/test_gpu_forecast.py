@@ -10,7 +10,7 @@ import pytest
 from test_gpu_parity import panel
 
 pytestmark = pytest.mark.gpu
-FCST_RTOL = 1e-9
+FCST_RTOL = 1e-10
 
 
 @pytest.mark.parametrize("T,N,P,crit", [(90, 160, 8, "ICp2"), (140, 40, 10, "BIC"), (120, 300, 6, "ICp1"),
@@ -24,7 +24,7 @@ def test_forecasts_match_oracle(dfm, oracle, T, N, P, crit):
         lambda yy, ww, xx: oracle.DynamicFactorModel_ic(yy, ww, xx, crit, kmax=kmax), y, w, x, P)
     assert np.array_equal(true, to)
     assert np.max(np.abs(pred - po)) <= FCST_RTOL * np.max(np.abs(po))
-    assert abs(dfm.MSE(true, pred) - oracle.MSE(to, po)) <= 1e-9 * oracle.MSE(to, po)
+    assert abs(dfm.MSE(true, pred) - oracle.MSE(to, po)) <= FCST_RTOL * oracle.MSE(to, po)
 
 
 def test_forecast_with_extra_regressor(dfm, oracle):

@@ -94,8 +94,8 @@ def test_c5_full_panel_windows_match_frozen_oracle(dfm, oracle):
         assert abs(out["V"][wi] - g["V"][k]) <= STAT_RTOL * g["V"][k]
         assert abs(out["criterion_value"][wi] - g["crit"][k]) <= STAT_RTOL * abs(g["crit"][k])
         assert rel(out["eigenvalues"][wi][:8], g["eigvals"][k]) < STAT_RTOL
-        assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < 1e-9            # intercept: sign-free
-        assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < 1e-9
+        assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < STAT_RTOL            # intercept: sign-free
+        assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < STAT_RTOL
 
 
 def test_c4_full_panel_per_candidate_matches_oracle(dfm, oracle):
@@ -106,6 +106,6 @@ def test_c4_full_panel_per_candidate_matches_oracle(dfm, oracle):
     w = np.ones((T, 1))
     mask, t = dfm.targeted_predictors(y, w, x, "hard", mode="per_candidate", return_tstats=True)
     to, mo = oracle.targeted_predictors_hard(y, w, x, "per_candidate")
-    assert rel(t, to) < 1e-9
+    assert rel(t, to) < STAT_RTOL
     assert np.array_equal(mask, mo)
     assert 0 < mask.sum() < N

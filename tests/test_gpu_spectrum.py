@@ -117,7 +117,7 @@ def test_many_factors_with_breaks(dfm, oracle):
     o = oracle.DynamicFactorModel(y, w, x, 35, "ICp2", break_indices=[121])
     assert g.number_of_factors == o.number_of_factors == 35
     assert abs(g.V - oracle.factor_residual_variance(o)) <= STAT_RTOL * oracle.factor_residual_variance(o)
-    assert rel(g.t_stats[:1], o.t_stats[:1]) < 1e-9
+    assert rel(g.t_stats[:1], o.t_stats[:1]) < STAT_RTOL
     assert np.max(np.abs(g.factor_residuals - o.factor_residuals)) < 1e-9 * np.max(np.abs(o.factor_residuals))
 
 
@@ -168,7 +168,7 @@ def test_bootstrap_many_factors(dfm, oracle, T, N, r, crit, breaks):
                sum(e[0] for e in d.eigenvalues), sum(e[r - 1] for e in d.eigenvalues), np.sum(xs * xs),
                d.coefficients[0], d.t_stats[0]]
         assert rel(out[b, :5], ref[:5]) < STAT_RTOL
-        assert rel(out[b, 5:], ref[5:]) < 1e-8
+        assert rel(out[b, 5:], ref[5:]) < STAT_RTOL
 
 
 # ------------------------------------------------ Chow tests at r > 16
@@ -184,9 +184,9 @@ def test_chow_all_many_factors(dfm, oracle, T, N, r):
                     for i in range(nv)])
     # LR / LM are differences (of log SSRs, of 1 - R^2) from r = 18-20 column
     # projections on 45-80 rows: both sides carry cond(F_j'F_j) eps -> 1e-8
-    assert rel(LR[:nv], ref[:, 0]) < 1e-8
-    assert rel(LM[:nv], ref[:, 1]) < 1e-8
-    assert rel(WD[:nv], ref[:, 2]) < 1e-8
+    assert rel(LR[:nv], ref[:, 0]) < STAT_RTOL
+    assert rel(LM[:nv], ref[:, 1]) < STAT_RTOL
+    assert rel(WD[:nv], ref[:, 2]) < STAT_RTOL
 
 
 @pytest.mark.parametrize("r", [2, 20])
@@ -205,9 +205,9 @@ def test_bootstrap_chow_batched(dfm, oracle, r):
     out = dfm.wild_bootstrap(g, B, [S.LR_all(bp), S.LM(bp, i0 + 1), S.Wald(bp, i0 + 1)], idx=idx, eta=eta)
     for b in range(B):
         d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]], r)
-        assert rel(out[b, :8], [oracle.LR_test(d, bp, i) for i in range(8)]) < 1e-9
-        assert rel(out[b, N], oracle.LM_test(d, bp, i0)) < 1e-9
-        assert rel(out[b, N + 1], oracle.Wald_test(d, bp, i0)) < 1e-8
+        assert rel(out[b, :8], [oracle.LR_test(d, bp, i) for i in range(8)]) < STAT_RTOL
+        assert rel(out[b, N], oracle.LM_test(d, bp, i0)) < STAT_RTOL
+        assert rel(out[b, N + 1], oracle.Wald_test(d, bp, i0)) < STAT_RTOL
 
 
 # ---------------------------------------- JOINT hard thresholding, q + N > 64
@@ -219,7 +219,7 @@ def test_targeted_joint_wide(dfm, oracle, T, N, q):
     w = np.hstack([np.ones((T, 1)), rng.standard_normal((T, q - 1))])
     mask, t = dfm.targeted_predictors(y, w, x, return_tstats=True)
     to, mo = oracle.targeted_predictors_hard(y, w, x, mode="joint")
-    assert rel(t, to) < 1e-8
+    assert rel(t, to) < STAT_RTOL
     # the mask may differ only where |t| sits within rounding of the critical value
     cv = oracle.sps.t.ppf(0.975, T - q - N) if hasattr(oracle, "sps") else None
     diff = np.flatnonzero(mask != mo)
@@ -248,7 +248,7 @@ def test_reference_test_workflow_from_csv(dfm, oracle, tmp_path):
     assert g.number_of_factors == o.number_of_factors == 30
     ssr_g, ssr_o = np.sum(g.factor_residuals ** 2), np.sum(o.factor_residuals ** 2)
     assert abs(ssr_g - ssr_o) <= 1e-10 * ssr_o
-    assert rel(g.t_stats[:5], o.t_stats[:5]) < 1e-8       # intercept and lags: sign-invariant
+    assert rel(g.t_stats[:5], o.t_stats[:5]) < STAT_RTOL       # intercept and lags: sign-invariant
 
 
 def test_dense_spectrum_bit_reproducible(dfm, oracle):

@@ -291,3 +291,43 @@ def test_repaired_get_factors_reproduces_in_sample_factors(oracle):
         assert np.allclose((x @ rot)[:, :3], d.F, atol=1e-8 * np.abs(d.F).max())
         xs_new = x[:2] * x.std(ddof=1) + x.mean()        # de-normalised by the scalar moments
         assert np.allclose(oracle.get_factors(d, xs_new), d.F[:2], atol=1e-8 * np.abs(d.F).max())
+
+
+# ------------------------------------------------ extended-precision referee
+def test_xp_referee_pins_the_oracle(oracle):
+    """oracle/dfm_xp.py recomputes the fit, criteria and Chow statistics in
+    double-double: on a small panel the fp64 oracle agrees with it to 1e-11
+    (the referee's own arithmetic is checked by the identities below)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import dfm_xp as XP
+    a = XP.DD(np.array([1.0, 3.0]))
+    third = a / 3.0
+    assert third.hi[0] == 1.0 / 3.0 and abs((third * 3.0 - 1.0).f64()[0]) < 1e-30
+    assert abs((XP.DD(2.0).sqrt() * XP.DD(2.0).sqrt() - 2.0).f64()) < 1e-30
+    for T, N in [(60, 25), (25, 60)]:
+        y, x, w = _panel(oracle, T, N, 2, 77, model="Breitung_Eickmeier_2011", b=0.5)
+        f = XP.XPFit(y, w, x, 2, "ICp1")
+        o = oracle.DynamicFactorModel(y, w, x, 2, "ICp1")
+        assert abs(f.V.f64() / oracle.factor_residual_variance(o) - 1) < 1e-12
+        assert abs(f.criterion_value("ICp1") / o.number_of_factors_criterion_value - 1) < 1e-12
+        s = np.sign(np.sum(f.F.f64() * o.F, axis=0))
+        assert np.allclose(f.t_stats[1:] * s, o.t_stats[1:], rtol=1e-11, atol=0)
+        LR, LM, W = f.chow_all(T // 2)
+        ref = np.array([[oracle.LR_test(o, T // 2, i), oracle.LM_test(o, T // 2, i), oracle.Wald_test(o, T // 2, i)]
+                        for i in range(N)])
+        assert np.allclose(np.column_stack([LR, LM, W]), ref, rtol=1e-11, atol=0)
+
+
+def test_xp_fixture_agrees_with_golden():
+    """The committed referee values and the oracle's golden values differ by
+    less than 1e-10 relative (the C2 oracle's largest deviation is 4e-12)."""
+    xp = np.load(os.path.join(GOLD, "xp_c1_c2.npz"))
+    g2 = np.load(os.path.join(GOLD, "c2_breitung_eickmeier_T600_N130_B16.npz"))
+    assert np.all(np.abs(xp["c2_base_chow"] - g2["base_chow"]) < 1e-10 * np.abs(xp["c2_base_chow"]))
+    nv, N = int(g2["nv"]), g2["x"].shape[1]
+    cols = [0, 1] + [2 + k * N + i for k in range(3) for i in range(nv)]
+    assert np.all(np.abs(xp["c2_boot"][:, cols] - g2["boot"]) < 1e-10 * np.abs(xp["c2_boot"][:, cols]))
+    assert np.all(xp["c2_boot_bar"] >= 1e-10 * np.abs(xp["c2_boot"]))
+    g1 = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
+    assert np.all(np.abs(xp["c1_ic"] - g1["ic_values"]) < 1e-10 * np.abs(xp["c1_ic"]))

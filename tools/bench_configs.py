@@ -208,7 +208,13 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle (bounded samples)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dump-maps", default="", help="copy /proc/self/maps here at interpreter exit (names the "
+                                                      "libraries behind addresses in an exit-time stack trace)")
     args = ap.parse_args()
+    if args.dump_maps:
+        import atexit
+        import shutil
+        atexit.register(lambda: shutil.copyfile("/proc/self/maps", args.dump_maps))
     import torch  # noqa: F401  (before libdfm: one HIP runtime in the process, as bench.py)
     torch.cuda.init()
     import dfm_pkg
