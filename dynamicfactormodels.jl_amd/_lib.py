@@ -24,6 +24,11 @@ class dfm_stat(C.Structure):
     _fields_ = [("kind", C.c_int32), ("arg0", C.c_int32), ("arg1", C.c_int32), ("pad", C.c_int32)]
 
 
+class dfm_window_spec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("length", C.c_int32), ("r", C.c_int32), ("crit", C.c_int32),
+                ("kmax", C.c_int32), ("nbreaks", C.c_int32), ("breaks", C.POINTER(C.c_int64))]
+
+
 # (name, restype, argtypes) — one row per symbol of include/dfm.h
 SIGNATURES = [
     ("dfm_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -75,6 +80,10 @@ SIGNATURES = [
     ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
     ("dfm_model_set_mode", C.c_int, [C.c_void_p, C.c_int]),
     ("dfm_chow_all", C.c_int, [C.c_void_p, C.c_int64, c_double_p, c_double_p, c_double_p]),
+    ("dfm_chow", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_double_p, c_double_p, c_double_p]),
+    ("dfm_model_criterion", C.c_int, [C.c_void_p, C.c_int, c_double_p]),
+    ("dfm_get_factors", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, c_double_p]),
+    ("dfm_predict", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, c_double_p]),
     ("dfm_windows", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
                               C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
                               c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
@@ -84,6 +93,10 @@ SIGNATURES = [
     ("dfm_windows_forecast", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64, c_double_p,
                                        C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, c_int64_p,
                                        c_double_p, c_double_p]),
+    ("dfm_windows_ex", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                                 C.c_int64, C.c_int64, C.c_int64, C.c_int, C.POINTER(dfm_window_spec), C.c_int,
+                                 c_int64_p, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                 c_double_p, c_double_p]),
     ("dfm_targeted_hard", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_int, C.c_int64,
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                     C.c_double, c_double_p, c_uint8_p]),

@@ -458,19 +458,16 @@ def calculate_criterion(dfm: DynamicFactorModelResult) -> DynamicFactorModelResu
 
 
 def criterion_value(name: str, dfm: DynamicFactorModelResult) -> float:
-    """``criterion_<name>`` (``src/criteria.jl:17-53``) for the fitted r."""
+    """``criterion_<name>(dfm)`` (``src/criteria.jl:17-53``) of the fitted model
+    at its r (``dfm_model_criterion``: PCp's unrestricted sigma^2 from the
+    resident panel's full spectrum)."""
     if name == dfm.number_of_factors_criterion:
         return dfm.number_of_factors_criterion_value
-    T, N = dfm.x.shape
-    k, V = dfm.number_of_factors, dfm.V
-    c, m = (N + T) / (N * T), min(T, N)
-    if name in ("PCp1", "PCp2", "PCp3"):
-        ev, tr = gram_spectrum(dfm.x, ctx=dfm._ctx)
-        s2 = (tr - ev[:int(math.ceil(m / 2))].sum()) / (N * T)
-        g = {"PCp1": c * math.log(1 / c), "PCp2": c * math.log(m), "PCp3": math.log(m) / m}[name]
-        return V + k * s2 * g
-    return {"ICp1": math.log(V) + k * c * math.log(1 / c), "ICp2": math.log(V) + k * c * math.log(m),
-            "ICp3": math.log(V) + k * math.log(m) / m, "BIC": V + k * math.log(T) / T}[name]
+    if name not in _CRIT_CODE:
+        raise KeyError(f"criterion_{name} is not defined")
+    v = C.c_double()
+    dfm._ctx.check(dfm._ctx.lib.dfm_model_criterion(dfm.handle, _CRIT_CODE[name], C.byref(v)))
+    return float(v.value)
 
 
 for _n in CRITERIA:
@@ -565,6 +562,36 @@ def residual_bootstrap(dfm, B: int, stat, *, idx=None, rng: Optional[np.random.G
     return _run_bootstrap(dfm, 1, B, stat, idx, None)
 
 
+# ------------------------------------------------------ get_factors / predict
+def get_factors(dfm: DynamicFactorModelResult, x_new) -> np.ndarray:
+    """``src/DynamicFactorModel.jl:125-128`` with defect D4 repaired
+    (``dfm_get_factors``): the new rows' active factors, (n_new, r)."""
+    x_new = np.atleast_2d(_f64(x_new))
+    n, N = x_new.shape
+    if N != dfm.x.shape[1]:
+        raise ValueError("x_new must have the model's N columns")
+    xc = _colmajor(x_new)
+    F = np.zeros((n, dfm.number_of_factors), order="F")
+    dfm._ctx.check(dfm._ctx.lib.dfm_get_factors(dfm.handle, n, xc.ctypes.data, n, F.ctypes.data_as(_lib.c_double_p)))
+    return np.ascontiguousarray(F)
+
+
+def predict(dfm: DynamicFactorModelResult, w_new, x_new) -> np.ndarray:
+    """``src/DynamicFactorModel.jl:152-155``: [w_new get_factors(dfm, x_new)]
+    coefficients (``dfm_predict``); one prediction per new row."""
+    x_new = np.atleast_2d(_f64(x_new))
+    n, N = x_new.shape
+    q = dfm.w.shape[1]
+    w_new = np.asarray(w_new, dtype=np.float64).reshape(n, q)
+    if N != dfm.x.shape[1]:
+        raise ValueError("x_new must have the model's N columns")
+    xc, wc = _colmajor(x_new), _colmajor(w_new)
+    out = np.zeros(n)
+    dfm._ctx.check(dfm._ctx.lib.dfm_predict(dfm.handle, n, wc.ctypes.data if q else None, n, xc.ctypes.data, n,
+                                            _lib.ptr(out)))
+    return out
+
+
 # --------------------------------------------------------------- Chow tests
 def chow_all(dfm: DynamicFactorModelResult, break_period: int):
     """LR, LM, Wald for every variable (N-vectors)."""
@@ -576,19 +603,30 @@ def chow_all(dfm: DynamicFactorModelResult, break_period: int):
     return LR, LM, W
 
 
+def _chow_one(dfm, break_period: int, variable_index: int):
+    """(LR, LM, Wald) of one variable (1-based) through ``dfm_chow``: the model
+    keeps the all-variables results of the last break period, so a loop over
+    the variables costs one pass over the panel."""
+    ctx = dfm._ctx
+    v = [C.c_double(), C.c_double(), C.c_double()]
+    ctx.check(ctx.lib.dfm_chow(dfm.handle, int(break_period), _one_based(variable_index),
+                               *[C.byref(a) for a in v]))
+    return [a.value for a in v]
+
+
 def LR_test(dfm, break_period: int, variable_index: int) -> float:
     """``src/chowtest.jl:19-23`` (variable_index 1-based)."""
-    return float(chow_all(dfm, break_period)[0][variable_index - 1])
+    return float(_chow_one(dfm, break_period, variable_index)[0])
 
 
 def LM_test(dfm, break_period: int, variable_index: int) -> float:
     """``src/chowtest.jl:35-42``."""
-    return float(chow_all(dfm, break_period)[1][variable_index - 1])
+    return float(_chow_one(dfm, break_period, variable_index)[1])
 
 
 def Wald_test(dfm, break_period: int, variable_index: int) -> float:
     """``src/chowtest.jl:25-33``."""
-    return float(chow_all(dfm, break_period)[2][variable_index - 1])
+    return float(_chow_one(dfm, break_period, variable_index)[2])
 
 
 # ------------------------------------------------------- targeted predictors
@@ -761,17 +799,125 @@ def pseudo_out_of_sample_refits_dev(y, w, x, criterion: str = "ICp2", num_predic
             "criterion_value": cv, "eigenvalues": ev, "coefficients": coef, "t_stats": ts}
 
 
+def _parse_model_args(model_args):
+    """``model_args`` of ``pseudo_out_of_sample_forecasts`` (src/utils.jl:64-65)
+    as the DynamicFactorModel constructors read them: (criterion, factor_type,
+    targeted_predictors, number_of_lags, break_indices) for the IC sweep (:53),
+    (r, criterion, factor_type, targeted_predictors, number_of_factor_lags,
+    break_indices) for the workhorse (:28), () for the 3-arg default (D2).
+    Returns (r: >0 fixed / 0 sweep / -1 default, criterion, break_indices)."""
+    args = list(model_args)
+    if not args:
+        return -1, "", ()
+    if isinstance(args[0], str):
+        r, crit, rest = 0, args[0], args[1:]
+        brk_pos = 3
+    else:
+        r = int(args[0])
+        if r < 1:
+            raise ValueError("number_of_factors must be >= 1")
+        crit = args[1] if len(args) > 1 else ""
+        rest = args[2:]
+        brk_pos = 3
+    if len(rest) > 0 and rest[0] not in (None, "principal components"):
+        raise NotImplementedError(f"factor_type {rest[0]!r}: broken in the reference (D6)")
+    if len(rest) > 1 and rest[1] is not None and not np.all(np.asarray(rest[1], dtype=bool)):
+        raise NotImplementedError("targeted_predictors masks other than all-true are not read by the refit")
+    if len(rest) > 2 and rest[2]:
+        raise NotImplementedError("factor lags are unfinished in the reference (:35-37)")
+    brk = tuple(rest[brk_pos]) if len(rest) > brk_pos else ()
+    if crit and crit not in _CRIT_CODE:
+        raise KeyError(f"criterion_{crit} is not defined")
+    return r, crit, brk
+
+
+def _windows_K(T: int, N: int, P: int, r: int, kmax, rolling) -> int:
+    """Row width of the per-window eigenvalue / coefficient outputs: the widest
+    window's bound on r_w (include/dfm.h, dfm_windows_ex)."""
+    n = int(rolling) if rolling else T - 1
+    kd = int(math.ceil(min(n, N) / 2))
+    if r > 0:
+        return min(r, kd)
+    if r < 0:
+        return kd
+    return min(int(kmax), kd) if kmax else kd
+
+
+def pseudo_out_of_sample_windows(y, w, x, *model_args, num_predictions: int = 200, kmax: Optional[int] = None,
+                                 rolling: Optional[int] = None, forecast: bool = False,
+                                 ctx: Optional[Context] = None):
+    """Every window's refit (and, with ``forecast``, its one-step prediction)
+    of ``pseudo_out_of_sample_forecasts(DynamicFactorModel, y, w, x,
+    model_args...)`` (src/utils.jl:54-72) through ``dfm_windows_ex``:
+    expanding windows as the reference, or ``rolling=L`` windows of the last
+    L rows.  ``y``/``w``/``x`` may be host arrays or GPU tensors (column-major
+    w, x, as ``pseudo_out_of_sample_refits_dev``).  Returns a dict of
+    per-window arrays."""
+    ctx = ctx or default_context()
+    r, crit, brk = _parse_model_args(model_args)
+    dev = _is_device_tensor(x)
+    if dev:
+        T, N = int(x.shape[0]), int(x.shape[1])
+        if x.stride(0) != 1:
+            raise ValueError("x must be column-major (stride (1, ldx >= T))")
+        if w.dim() == 1:
+            w = w.reshape(-1, 1)
+        q = int(w.shape[1])
+        ldw, ldx = (int(w.stride(1)) if q > 1 else T), int(x.stride(1))
+        yp, wp, xp = y.data_ptr(), w.data_ptr(), x.data_ptr()
+        keep = None
+    else:
+        y = _f64(y).ravel()
+        w = _f64(w, 2)
+        x = _f64(x, 2)
+        T, N = x.shape
+        q = w.shape[1]
+        xc, wc = _colmajor(x), _colmajor(w)
+        keep = (y, xc, wc)
+        ldw = ldx = T
+        yp, wp, xp = y.ctypes.data, wc.ctypes.data, xc.ctypes.data
+    P = int(num_predictions)
+    K = _windows_K(T, N, P, r, kmax, rolling)
+    bk = np.asarray([int(b) - 1 for b in brk], dtype=np.int64)   # 1-based -> 0-based rows
+    spec = _lib.dfm_window_spec(1 if rolling else 0, int(rolling or 0), r, _CRIT_CODE[crit] if crit else -1,
+                                int(kmax) if kmax else 0, len(bk),
+                                bk.ctypes.data_as(_lib.c_int64_p) if len(bk) else None)
+    rr = np.zeros(P, dtype=np.int64)
+    V, cv = np.zeros(P), np.zeros(P)
+    ev = np.zeros((P, K))
+    coef, ts = np.zeros((P, q + K)), np.zeros((P, q + K))
+    pred = np.zeros(P) if forecast else None
+    true = np.zeros(P) if forecast else None
+    ctx.check(ctx.lib.dfm_windows_ex(ctx.h, yp, wp, q, ldw, xp, T, N, ldx, P, C.byref(spec), int(dev),
+                                     rr.ctypes.data_as(_lib.c_int64_p), _lib.ptr(V), _lib.ptr(cv), _lib.ptr(ev),
+                                     _lib.ptr(coef), _lib.ptr(ts), _lib.ptr(pred), _lib.ptr(true)))
+    del keep
+    out = {"window_rows": np.arange(T - P, T) if not rolling else np.full(P, int(rolling)),
+           "window_first_row": np.zeros(P, dtype=np.int64) if not rolling else np.arange(T - P - int(rolling),
+                                                                                         T - int(rolling)),
+           "number_of_factors": rr, "V": V, "criterion_value": cv, "eigenvalues": ev, "coefficients": coef,
+           "t_stats": ts}
+    if forecast:
+        out["predictions"], out["true_values"] = pred, true
+    return out
+
+
 def pseudo_out_of_sample_forecasts(model, y, w, x, *model_args, num_predictions: int = 200,
-                                   kmax: Optional[int] = None, ctx: Optional[Context] = None):
+                                   kmax: Optional[int] = None, rolling: Optional[int] = None,
+                                   ctx: Optional[Context] = None):
     """``src/utils.jl:54-72``: one-step-ahead pseudo out-of-sample forecasts.
-    For date_index = T-P+1..T the model is refit on rows 1..date_index-1 and
-    row date_index is predicted with ``predict`` (``src/DynamicFactorModel.jl:152``)
-    through ``get_factors`` repaired (defect D4: the local rotation of ``:126``).
-    ``model`` is ``DynamicFactorModel`` with a criterion name as its first extra
-    argument (the IC-sweep constructor, ``:53``).  Returns (predictions,
-    true_values)."""
-    if model is not DynamicFactorModel or not model_args or not isinstance(model_args[0], str):
-        raise NotImplementedError("the device path refits DynamicFactorModel(y, w, x, criterion) per window")
+    For date_index = T-P+1..T the model is refit on rows 1..date_index-1 (or,
+    with ``rolling=L``, on the L rows before date_index) with ``model_args``
+    (an IC criterion name, a fixed r with an optional criterion, break_indices,
+    or nothing for the 3-arg default r, D2) and row date_index is predicted
+    with ``predict`` (``src/DynamicFactorModel.jl:152``) through
+    ``get_factors`` repaired (defect D4).  Returns (predictions, true_values)."""
+    if model is not DynamicFactorModel:
+        raise NotImplementedError("the device path refits the DynamicFactorModel constructors per window")
+    if not model_args or not isinstance(model_args[0], str) or len(model_args) > 1 or rolling:
+        res = pseudo_out_of_sample_windows(y, w, x, *model_args, num_predictions=num_predictions, kmax=kmax,
+                                           rolling=rolling, forecast=True, ctx=ctx)
+        return res["predictions"], res["true_values"]
     ctx = ctx or default_context()
     crit = model_args[0]
     y = _f64(y).ravel()

@@ -78,7 +78,8 @@ __global__ void block_accum_kernel(const double *, const double *, int, int, dou
 __global__ void ordered_sum_kernel(const double *, int, double *);
 hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, int q, const double *F, int Tphys,
                       int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
-                      double *resid_out, int *status);
+                      double *resid_out, int *status,
+                      const int *R0 = nullptr);
 struct StatDesc { int kind, arg0, arg1, off; };
 __global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *, const double *,
                              const double *, const double *, const int *, const StatDesc *, int, double *, int64_t);
@@ -116,6 +117,9 @@ hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, con
 hipError_t launch_fact_fsf(int T, int r, const double *Fb, const double *S, double *FSF, int64_t ldH, hipStream_t st);
 hipError_t launch_gram_fact(const FactBase &fb, const double *FSF, const int32_t *idx, const double *eta, int nb,
                             double *G, int64_t ldg, int64_t strideG, hipStream_t st);
+hipError_t launch_predict(const double *Xp, int64_t ld, int T, int N, const double *L, int r, const double *x_dev,
+                          int64_t ldx, int64_t nn, const double *w_dev, int64_t ldw, int q, const double *beta_dev,
+                          double *work, double *F_out, double *yhat, hipStream_t st);
 int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
                     const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st);
 hipError_t launch_targeted(int mode, const double *y, const double *w, int q, const double *Xp,
@@ -190,6 +194,9 @@ struct dfm_model {
   std::vector<double *> Ubs, Ls;   // Ls[j] = Lall + j N r (contiguous: the Chow kernels index blocks)
   double *Lall = nullptr;
   std::vector<std::vector<double>> blam;
+  // dfm_chow: the all-variables statistics of the last break period asked for
+  int64_t chow_bp = -1;
+  std::vector<double> chow_cache;   // LR (N), LM (N), Wald (N)
 };
 
 static int fail(dfm_ctx *ctx, int code, const char *fmt, ...) {
@@ -256,6 +263,21 @@ static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 static bool chow_stat(int k) { return k >= DFM_STAT_LR && k <= DFM_STAT_WALD_ALL; }
 static bool all_var_stat(int k) { return k >= DFM_STAT_LR_ALL && k <= DFM_STAT_WALD_ALL; }
 static int ceil_half(int m) { return (m + 1) / 2; }
+// src/criteria.jl:17-53 at k factors: V(k), PCp's sigma^2 (V of the
+// unrestricted fit), c = (N + T) / (N T), m = min(T, N)
+static double crit_formula(int crit, double V, int k, double sigma2, int T, int N) {
+  const double NT = (double)N * (double)T, c = (double)(N + T) / NT, m = (double)std::min(T, N);
+  switch (crit) {
+    case 0: return V + k * sigma2 * c * std::log(1.0 / c);
+    case 1: return V + k * sigma2 * c * std::log(m);
+    case 2: return V + k * sigma2 * std::log(m) / m;
+    case 3: return std::log(V) + k * c * std::log(1.0 / c);
+    case 4: return std::log(V) + k * c * std::log(m);
+    case 5: return std::log(V) + k * std::log(m) / m;
+    case 6: return V + k * std::log((double)T) / T;
+  }
+  return NAN;
+}
 
 template <class T>
 static hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
@@ -542,9 +564,10 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   CK(dalloc(&M->w, (size_t)T * std::max(q, 1)));
   double *Xraw = nullptr;
   TALLOC(Xraw, (size_t)T * N);
-  CK(hipMemcpy2DAsync(Xraw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N, hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(M->y, y, (size_t)T * 8, hipMemcpyHostToDevice, st));
-  if (q > 0) CK(hipMemcpy2DAsync(M->w, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyHostToDevice, st));
+  // host or device inputs (hipMemcpyDefault: the windows driver refits from a resident panel)
+  CK(hipMemcpy2DAsync(Xraw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N, hipMemcpyDefault, st));
+  CK(hipMemcpyAsync(M->y, y, (size_t)T * 8, hipMemcpyDefault, st));
+  if (q > 0) CK(hipMemcpy2DAsync(M->w, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, hipMemcpyDefault, st));
   {
     Scope sc(ctx, DFM_KC_MISC);
     hipLaunchKernelGGL(panel_from_colmajor_kernel, dim3((unsigned)((M->ld + 31) / 32), (T + 31) / 32),
@@ -778,18 +801,7 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
   if (ols_bad) return bail(fail(ctx, 3, "singular design matrix D'D"));
   M->trace = trace;
   M->V = essq / NT;
-  if (crit >= 0) {
-    const double c = (double)(N + T) / NT;
-    switch (crit) {
-      case 0: M->critval = M->V + r * M->sigma2 * c * std::log(1.0 / c); break;
-      case 1: M->critval = M->V + r * M->sigma2 * c * std::log((double)m); break;
-      case 2: M->critval = M->V + r * M->sigma2 * std::log((double)m) / m; break;
-      case 3: M->critval = std::log(M->V) + r * c * std::log(1.0 / c); break;
-      case 4: M->critval = std::log(M->V) + r * c * std::log((double)m); break;
-      case 5: M->critval = std::log(M->V) + r * std::log((double)m) / m; break;
-      case 6: M->critval = M->V + r * std::log((double)T) / T; break;
-    }
-  }
+  if (crit >= 0) M->critval = crit_formula(crit, M->V, r, M->sigma2, T, N);
   CK(dalloc(&M->flag_dev, 4));
   *out = M;
   return 0;
@@ -1424,6 +1436,64 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
   return 0;
 }
 
+// criterion_<name>(dfm) of a fitted model (src/criteria.jl:17-53) at its r:
+// V(r) is the model's; PCp's sigma^2 is V(ceil(m/2)) of the unrestricted
+// 3-arg fit DynamicFactorModel(y, w, x) (:18, :23, :28; no breaks, D2): the
+// spectral tail of the resident panel's full Gram spectrum, computed once.
+int dfm_model_criterion(dfm_model *M, int crit, double *value) {
+  if (!M || !value) return -1;
+  dfm_ctx *ctx = M->ctx;
+  if (crit < 0 || crit > 6) return fail(ctx, -31, "unknown criterion %d", crit);
+  if (crit <= 2 && std::isnan(M->sigma2)) {
+    const int m = M->m;
+    if (m > spectrum_any_max())
+      return fail(ctx, -30, "PCp criteria need the full spectrum: supported for min(T,N) <= %d", spectrum_any_max());
+    hipSetDevice(ctx->device);
+    hipStream_t st = ctx->stream;
+    DevBuf Gb, evb, wk;
+    HIPCHK(ctx, dalloc(&Gb.p, (size_t)m * m));
+    HIPCHK(ctx, dalloc(&evb.p, m));
+    if (spectrum_work(m, 1) > 0) HIPCHK(ctx, dalloc(&wk.p, (size_t)spectrum_work(m, 1)));
+    PanelSrc src{nullptr, M->Xp, nullptr, nullptr, M->ld, 0};
+    {
+      Scope sc(ctx, DFM_KC_GRAM);
+      HIPCHK(ctx, launch_gram(M->orient, src, m, M->orient == 0 ? M->N : M->T, M->T, Gb.p, m, (int64_t)m * m, 1, st));
+    }
+    {
+      Scope sc(ctx, DFM_KC_EIG_OTHER);
+      HIPCHK(ctx, launch_spectrum(Gb.p, m, (int64_t)m * m, m, 1, evb.p, wk.p, st));
+    }
+    std::vector<double> ev(m);
+    HIPCHK(ctx, hipMemcpyAsync(ev.data(), evb.p, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    double s = 0.0;   // trace minus the top ceil(m/2), as the fit's sigma^2
+    for (double v : ev) s += v;
+    for (int j = 0; j < ceil_half(m); ++j) s -= ev[j];
+    M->sigma2 = s / ((double)M->N * M->T);
+  }
+  *value = crit_formula(crit, M->V, M->r, M->sigma2, M->T, M->N);
+  return 0;
+}
+
+// One variable's LR / LM / Wald (src/chowtest.jl:19-42): the all-variables
+// kernel runs once per break period and the model keeps its N x 3 results,
+// so a caller's loop over the variables costs one pass over the panel.
+int dfm_chow(dfm_model *M, int64_t bp, int64_t i, double *LR, double *LM, double *Wald) {
+  if (!M) return -1;
+  if (i < 0 || i >= M->N) return fail(M->ctx, -2, "variable index %lld out of range", (long long)i);
+  if (M->chow_bp != bp) {
+    std::vector<double> c((size_t)3 * M->N);
+    int rc = dfm_chow_all(M, bp, c.data(), c.data() + M->N, c.data() + 2 * M->N);
+    if (rc) return rc;
+    M->chow_cache.swap(c);
+    M->chow_bp = bp;
+  }
+  if (LR) *LR = M->chow_cache[(size_t)i];
+  if (LM) *LM = M->chow_cache[(size_t)M->N + i];
+  if (Wald) *Wald = M->chow_cache[(size_t)2 * M->N + i];
+  return 0;
+}
+
 int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald) {
   if (!M) return -1;
   dfm_ctx *ctx = M->ctx;
@@ -1524,12 +1594,12 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
 //  T >= N: per-window Grams X_w' X_w from the masked fused-gather Gram kernel.
 // Each window runs the IC sweep k = 1..kmax (the refit is the IC-sweep
 // constructor, :53-66), picks r_w, and fits OLS+HC2 on [w F_r] over its rows.
-__global__ void window_scale_kernel(const double *__restrict__ Uk, int T, int k, int Tfirst,
+__global__ void window_scale_kernel(const double *__restrict__ Uk, int T, int k, int Tfirst, int dn,
                                     double *__restrict__ F) {
   const int rep = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)T * k) return;
-  const int t = (int)(e / k), n = Tfirst + rep;
+  const int t = (int)(e / k), n = Tfirst + dn * rep;
   F[(int64_t)rep * T * k + e] = t < n ? sqrt((double)n) * Uk[(int64_t)rep * T * k + e] : 0.0;
 }
 
@@ -1560,7 +1630,7 @@ __global__ void panel_row_sums_kernel(const double *__restrict__ P, int64_t ld, 
 }
 
 __global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp, int64_t ld, int T, int N, int n0,
-                                       int q, int kmax, const double *__restrict__ H, int64_t ldH,
+                                       int len, int q, int kmax, const double *__restrict__ H, int64_t ldH,
                                        const double *__restrict__ F, const double *__restrict__ Uk,
                                        const double *__restrict__ lam, const double *__restrict__ rs,
                                        const double *__restrict__ ss, const int *__restrict__ kr,
@@ -1569,11 +1639,13 @@ __global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp
                                        double *__restrict__ truev) {
   __shared__ double red[256];
   __shared__ double smom[2];
-  const int wi = blockIdx.x, tid = threadIdx.x, n = n0 + wi, r = kr[wi], d = q + kmax;
-  if (tid == 0) {   // scalar moments of the window's n x N entries (fixed order)
+  // the window's rows a0 .. n - 1 (expanding: a0 = 0; rolling: the last len
+  // rows before n, relocated to rows 0 .. len - 1 of F)
+  const int wi = blockIdx.x, tid = threadIdx.x, n = n0 + wi, a0 = len > 0 ? n - len : 0, r = kr[wi], d = q + kmax;
+  if (tid == 0) {   // scalar moments of the window's (n - a0) x N entries (fixed order)
     double a = 0.0, b = 0.0;
-    for (int s = 0; s < n; ++s) { a += rs[s]; b += ss[s]; }
-    const double cnt = (double)n * N, mu = a / cnt;
+    for (int s = a0; s < n; ++s) { a += rs[s]; b += ss[s]; }
+    const double cnt = (double)(n - a0) * N, mu = a / cnt;
     smom[0] = mu;
     smom[1] = sqrt((b - cnt * mu * mu) / (cnt - 1.0));
   }
@@ -1585,7 +1657,8 @@ __global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp
     if (orient == 0) {
       const double *Hn = H + (int64_t)n * ldH;
       const double *Fw = F + (int64_t)wi * T * kmax;
-      for (int s = tid; s < n; s += 256) part = fma((Hn[s] - mu * rs[s]) / sd, Fw[(int64_t)s * kmax + j], part);
+      for (int s = a0 + tid; s < n; s += 256)
+        part = fma((Hn[s] - mu * rs[s]) / sd, Fw[(int64_t)(s - a0) * kmax + j], part);
     } else {
       const double *xn = Xp + (int64_t)n * ld;
       const double *V = Uk + (int64_t)wi * N * kmax;
@@ -1608,23 +1681,45 @@ __global__ void window_forecast_kernel(int orient, const double *__restrict__ Xp
   }
 }
 
-__global__ void window_draws_kernel(int T, int n0, int32_t *__restrict__ idx, double *__restrict__ eta) {
+// window wi as a masked "replicate" of the panel: rows t < n_w are panel rows
+// a_w + t (expanding: a_w = 0, n_w = n0 + wi; rolling: n_w = len, a_w = n0 +
+// wi - len), rows past n_w carry eta = 0
+__global__ void window_draws_kernel(int T, int n0, int len, int32_t *__restrict__ idx, double *__restrict__ eta) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x, wi = blockIdx.y;
   if (t >= T) return;
-  idx[(int64_t)wi * T + t] = t;
-  eta[(int64_t)wi * T + t] = t < n0 + wi ? 1.0 : 0.0;
+  const int nw = len > 0 ? len : n0 + wi, aw = len > 0 ? n0 + wi - len : 0;
+  idx[(int64_t)wi * T + t] = t < nw ? aw + t : t;
+  eta[(int64_t)wi * T + t] = t < nw ? 1.0 : 0.0;
 }
+// The refit of each window (pseudo_out_of_sample_forecasts' model_args,
+// src/utils.jl:64-65): len = 0 expanding windows (rows 0 .. T-P+w-1), len > 0
+// rolling windows of len rows ending at T-P+w-1; r > 0 the workhorse
+// constructor at fixed r (:28, clamped to ceil(m_w/2), :116-119), r = 0 the
+// IC-sweep constructor (:53) by crit over k <= kmax_w, r < 0 the 3-arg default
+// r = ceil(m_w/2) (D2); breaks: model_args' break_indices, the same rows for
+// every (expanding) window.
+struct WinSpec {
+  int len = 0, r = 0, crit = -1, kmax = 0;
+  const int64_t *breaks = nullptr;
+  int nbreaks = 0;
+};
 static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
-                        int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
+                        int64_t T64, int64_t N64, int64_t ldx, int P, const WinSpec &ws, int64_t *r_out,
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
                         double *pred_out, double *true_out, bool dev);
+static int windows_breaks_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
+                               int T, int N, int64_t ldx, int P, const WinSpec &ws, int K, int64_t *r_out,
+                               double *V_out, double *crit_out, double *eig_out, double *coef_out,
+                               double *tstat_out, double *pred_out, double *true_out);
 #define LCKW(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(ctx, 1000 + (int)e_, "%s", hipGetErrorString(e_)); } while (0)
 
 extern "C" int dfm_windows(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
                            const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
                            int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                            double *coef_out, double *tstat_out) {
-  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, V_out, crit_out, eig_out,
+  WinSpec ws;
+  ws.crit = crit; ws.kmax = kmax;
+  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, ws, r_out, V_out, crit_out, eig_out,
                       coef_out, tstat_out, nullptr, nullptr, false);
 }
 
@@ -1632,7 +1727,9 @@ extern "C" int dfm_windows_dev(dfm_ctx *ctx, const double *y_dev, const double *
                                const double *X_dev, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
                                int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                                double *coef_out, double *tstat_out) {
-  return windows_impl(ctx, y_dev, w_dev, q, ldw, X_dev, T64, N64, ldx, P, crit, kmax, r_out, V_out, crit_out,
+  WinSpec ws;
+  ws.crit = crit; ws.kmax = kmax;
+  return windows_impl(ctx, y_dev, w_dev, q, ldw, X_dev, T64, N64, ldx, P, ws, r_out, V_out, crit_out,
                       eig_out, coef_out, tstat_out, nullptr, nullptr, true);
 }
 
@@ -1640,12 +1737,46 @@ extern "C" int dfm_windows_forecast(dfm_ctx *ctx, const double *y, const double 
                                     const double *X, int64_t T64, int64_t N64, int64_t ldx, int P, int crit,
                                     int kmax, int64_t *r_out, double *pred_out, double *true_out) {
   if (!pred_out || !true_out) return fail(ctx, -2, "dfm_windows_forecast: output pointers required");
-  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, crit, kmax, r_out, nullptr, nullptr, nullptr,
+  WinSpec ws;
+  ws.crit = crit; ws.kmax = kmax;
+  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, ws, r_out, nullptr, nullptr, nullptr,
                       nullptr, nullptr, pred_out, true_out, false);
 }
 
+extern "C" int dfm_windows_ex(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
+                              int64_t T64, int64_t N64, int64_t ldx, int P, const dfm_window_spec *spec, int dev,
+                              int64_t *r_out, double *V_out, double *crit_out, double *eig_out, double *coef_out,
+                              double *tstat_out, double *pred_out, double *true_out) {
+  if (!ctx) return -1;
+  if (!spec) return fail(ctx, -2, "dfm_windows_ex: spec required");
+  if (spec->kind != DFM_WIN_EXPANDING && spec->kind != DFM_WIN_ROLLING)
+    return fail(ctx, -2, "dfm_windows_ex: unknown window kind %d", spec->kind);
+  if ((pred_out == nullptr) != (true_out == nullptr))
+    return fail(ctx, -2, "dfm_windows_ex: pred_out and true_out go together");
+  WinSpec ws;
+  ws.len = spec->kind == DFM_WIN_ROLLING ? spec->length : 0;
+  if (spec->kind == DFM_WIN_ROLLING && spec->length < 2) return fail(ctx, -2, "dfm_windows_ex: rolling length < 2");
+  ws.r = spec->r; ws.crit = spec->crit; ws.kmax = spec->kmax;
+  ws.breaks = spec->breaks; ws.nbreaks = spec->nbreaks;
+  return windows_impl(ctx, y, w, q, ldw, X, T64, N64, ldx, P, ws, r_out, V_out, crit_out, eig_out, coef_out,
+                      tstat_out, pred_out, true_out, dev != 0);
+}
+
+// Masked explicit window Grams for N > T windows past the factored solver's
+// T range: G_w[i][j] = eta_i eta_j H[idx_i][idx_j] (H = X X', the prefix Gram)
+__global__ void window_gram_kernel(const double *__restrict__ H, int64_t ldH, const int32_t *__restrict__ idx,
+                                   const double *__restrict__ eta, int T, double *__restrict__ G) {
+  const int i = blockIdx.y, wi = blockIdx.z;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= T) return;
+  const int32_t *ix = idx + (int64_t)wi * T;
+  const double *et = eta + (int64_t)wi * T;
+  const double ei = et[i], ej = et[j];
+  G[((int64_t)wi * T + i) * T + j] = (ei != 0.0 && ej != 0.0) ? ei * ej * H[(int64_t)ix[i] * ldH + ix[j]] : 0.0;
+}
+
 static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
-                        int64_t T64, int64_t N64, int64_t ldx, int P, int crit, int kmax, int64_t *r_out,
+                        int64_t T64, int64_t N64, int64_t ldx, int P, const WinSpec &ws, int64_t *r_out,
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
                         double *pred_out, double *true_out, bool dev) {
   if (!ctx) return -1;
@@ -1653,38 +1784,55 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
       !r_out)
     return fail(ctx, -2, "dfm_windows: bad arguments");
-  if (crit < 0 || crit > 6) return fail(ctx, -31, "dfm_windows: unknown criterion %d", crit);
-  const bool pcp = crit <= 2;
+  const int crit = ws.crit, len = ws.len;
+  if (crit < -1 || crit > 6 || (ws.r == 0 && crit < 0))
+    return fail(ctx, -31, "dfm_windows: unknown criterion %d (the IC sweep needs one)", crit);
+  const bool pcp = crit >= 0 && crit <= 2;
   const int n0 = T - P;
-  const int orient = (N > T) ? 0 : 1;
-  if (orient == 1 && N > n0) return fail(ctx, -2, "dfm_windows: windows straddle the T >= N / N > T branches");
-  // window w sweeps k = 1..kmax_w, kmax_w = ceil(m_w / 2) (the IC-sweep
-  // constructor's default, src/DynamicFactorModel.jl:54) capped by the
-  // caller's kmax (D11); m_w = min(n0 + w, N) grows with the window
-  const int kreq = kmax;
+  if (len > n0) return fail(ctx, -2, "dfm_windows: rolling length %d exceeds the %d rows before the first window", len, n0);
+  if (ws.nbreaks < 0 || (ws.nbreaks > 0 && !ws.breaks)) return fail(ctx, -2, "dfm_windows: bad break list");
+  if (ws.nbreaks > 0 && len > 0)
+    return fail(ctx, -2, "dfm_windows: break_indices apply to expanding windows (the same rows in every refit, "
+                         "src/utils.jl:64)");
+  // window wi: rows aw(wi) .. aw(wi) + nw(wi) - 1 (relocated to rows 0 .. nw - 1)
+  auto nw = [&](int wi) { return len > 0 ? len : n0 + wi; };
+  auto aw = [&](int wi) { return len > 0 ? n0 + wi - len : 0; };
+  const int orient = len > 0 ? (N > len ? 0 : 1) : (N > T ? 0 : 1);
+  if (orient == 1 && len == 0 && N > n0)
+    return fail(ctx, -2, "dfm_windows: windows straddle the T >= N / N > T branches");
+  // window w's factor count: the sweep k = 1..kmax_w, kmax_w = ceil(m_w / 2)
+  // (the IC-sweep constructor's default, src/DynamicFactorModel.jl:54) capped
+  // by the caller's kmax (D11); fixed r clamped to ceil(m_w/2) (:116-119);
+  // the 3-arg default ceil(m_w/2) (D2); m_w = min(n_w, N)
+  auto kd_w = [&](int wi) { return (std::min(nw(wi), N) + 1) / 2; };
   auto kmax_w = [&](int wi) {
-    const int kd = (std::min(n0 + wi, N) + 1) / 2;
-    return kreq > 0 ? std::min(kreq, kd) : kd;
+    const int kd = kd_w(wi);
+    if (ws.r > 0) return std::min(ws.r, kd);
+    if (ws.r < 0) return kd;
+    return ws.kmax > 0 ? std::min(ws.kmax, kd) : kd;
   };
-  kmax = kmax_w(P - 1);   // the widest window's: row stride of eig_out / coef_out
+  int kmax = kmax_w(P - 1);   // the widest window's: row stride of eig_out / coef_out
+  if (ws.nbreaks > 0)
+    return windows_breaks_impl(ctx, y, w, q, ldw, X, T, N, ldx, P, ws, kmax, r_out, V_out, crit_out, eig_out,
+                               coef_out, tstat_out, pred_out, true_out);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   const int m = orient == 0 ? T : N;
   // kmax beyond the subspace block (or a design wider than 32): each window's
   // sweep reads its full spectrum, the r_w eigenvectors come from the dense
-  // batched eigensolver (prefix blocks of H zero-padded to T x T for N > T)
+  // batched eigensolver (diagonal blocks of H zero-padded to T x T for N > T)
   const int p = eig_block_p(m, kmax, ctx->block);
   const bool wide = p > 32 || p < kmax || q + kmax > 32;
   if ((pcp || wide) && m > std::min(spectrum_any_max(), dense_eig_max()))
     return fail(ctx, -31, "dfm_windows: PCp / kmax > 24 need each window's full spectrum: supported for "
                           "min(T,N) <= %d", std::min(spectrum_any_max(), dense_eig_max()));
   const int Pb = (p <= 16 || wide) ? 16 : 32;
-  if (orient == 0 && !wide && T > fact_t_max())
-    return fail(ctx, -20, "dfm_windows: N > T windows need T <= %d (got %d)", fact_t_max(), T);
+  // N > T past the factored solver's T range: per-window masked Grams, explicit-Gram solver
+  const bool explicit_gram = orient == 0 && !wide && T > fact_t_max();
   DevPanel dp;
   int rc = upload_panel(ctx, X, T, N, ldx, dp, dev);
   if (rc) return rc;
-  std::vector<int> hTn(P), hkr(P);
+  std::vector<int> hTn(P), hkr(P), hR0(P);
   // scratch: bump allocation from the context's arena (sized by the largest
   // earlier call; stream-ordered reuse), overflow from the stream-ordered pool
   if (ctx->warena_need > ctx->warena_cap) {
@@ -1709,21 +1857,23 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     std::vector<void *> &v; hipStream_t s; dfm_ctx *c; size_t &need;
     ~Freer() { for (void *x : v) hipFreeAsync(x, s); c->warena_need = std::max(c->warena_need, need); }
   } freer{frees, st, ctx, aneed};
-  // window w as a "replicate" of the panel: identity rows, row mask t < n0 + w
+  // window w as a "replicate" of the panel: relocated rows, row mask t < n_w
   int32_t *didx = (int32_t *)dal((size_t)P * T * 4);
   double *deta = (double *)dal((size_t)P * T * 8);
   double *dy = (double *)dal((size_t)T * 8), *dw = (double *)dal((size_t)T * std::max(q, 1) * 8);
   double *tr = (double *)dal((size_t)P * 8);
   int *stt = (int *)dal((size_t)P * 4), *ost = (int *)dal((size_t)P * 4);
-  int *dTn = (int *)dal((size_t)P * 4), *dkr = (int *)dal((size_t)P * 4);
-  if (!didx || !deta || !dy || !dw || !tr || !stt || !ost || !dTn || !dkr)
+  int *dTn = (int *)dal((size_t)P * 4), *dkr = (int *)dal((size_t)P * 4), *dR0 = (int *)dal((size_t)P * 4);
+  if (!didx || !deta || !dy || !dw || !tr || !stt || !ost || !dTn || !dkr || !dR0)
     return fail(ctx, 1002, "dfm_windows: out of device memory");
-  hipLaunchKernelGGL(window_draws_kernel, dim3((unsigned)((T + 255) / 256), P), dim3(256), 0, st, T, n0, didx, deta);
+  hipLaunchKernelGGL(window_draws_kernel, dim3((unsigned)((T + 255) / 256), P), dim3(256), 0, st, T, n0, len, didx,
+                     deta);
   const hipMemcpyKind yk = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIPCHK(ctx, hipMemcpyAsync(dy, y, (size_t)T * 8, yk, st));
   if (q > 0) HIPCHK(ctx, hipMemcpy2DAsync(dw, (size_t)T * 8, w, (size_t)ldw * 8, (size_t)T * 8, q, yk, st));
-  PanelSrc msrc{nullptr, dp.P, didx, deta, dp.ld, T};   // window w = rows < n0 + w of X
-  // ---- the windows' Grams: N > T one prefix Gram H; T >= N per-window G
+  PanelSrc msrc{nullptr, dp.P, didx, deta, dp.ld, T};   // window w = its rows of X, relocated
+  // ---- the windows' Grams: N > T one Gram H = X X' (every window's Gram is a
+  // diagonal block of it); T >= N per-window G
   double *H = nullptr, *G = nullptr;
   int64_t ldH = 0;
   if (orient == 0) {
@@ -1740,15 +1890,20 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     Scope sc(ctx, DFM_KC_GRAM);
     HIPCHK(ctx, launch_gram(1, msrc, N, T, T, G, N, (int64_t)N * N, P, st));
   }
+  // N > T windows as diagonal blocks of H: expanding = leading (n0 + w) blocks,
+  // rolling = the len x len block at row/column n0 + w - len
+  const double *Hb = H ? (len > 0 ? H + (int64_t)(n0 - len) * (ldH + 1) : H) : nullptr;
+  const int64_t sHb = len > 0 ? ldH + 1 : 0;
+  const int mv0 = len > 0 ? len : n0, dmv = len > 0 ? 0 : 1;
   // ---- full spectra (PCp's sigma^2, and the whole sweep when wide)
   double *pev = nullptr;   // P x pst
-  const int pst = orient == 0 ? T - 1 : N;
+  const int pst = orient == 0 ? (len > 0 ? len : T - 1) : N;
   if (pcp || wide) {
     pev = (double *)dal((size_t)P * pst * 8);
     double *pwk = spectrum_work(pst, P) > 0 ? (double *)dal((size_t)spectrum_work(pst, P) * 8) : nullptr;
     if (!pev || (spectrum_work(pst, P) > 0 && !pwk)) return fail(ctx, 1002, "dfm_windows: out of device memory");
     Scope sc(ctx, DFM_KC_EIG_OTHER);
-    if (orient == 0) HIPCHK(ctx, launch_spectrum_var(H, ldH, 0, pst, n0, 1, P, pev, pwk, st));
+    if (orient == 0) HIPCHK(ctx, launch_spectrum_var(Hb, ldH, sHb, pst, mv0, dmv, P, pev, pwk, st));
     else HIPCHK(ctx, launch_spectrum(G, N, (int64_t)N * N, N, P, pev, pwk, st));
   }
   std::vector<double> hev;
@@ -1763,13 +1918,13 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   if (!wide) {
     lam = (double *)dal((size_t)P * kmax * 8); Uk = (double *)dal((size_t)P * m * kmax * 8);
     F = (double *)dal((size_t)P * T * kmax * 8);
-    char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
-    if (!lam || !Uk || !F || !ews) return fail(ctx, 1002, "dfm_windows: out of device memory");
-    if (orient == 0) {
+    if (!lam || !Uk || !F) return fail(ctx, 1002, "dfm_windows: out of device memory");
+    if (orient == 0 && !explicit_gram) {
+      char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
       double *zero = (double *)dal((size_t)T * 8), *hd = (double *)dal((size_t)T * 8);
       char *fws = (char *)dal(fact_workspace_bytes(T, P, Pb));
       int *off = (int *)dal((size_t)P * (T + 1) * 4), *lst = (int *)dal((size_t)P * T * 4);
-      if (!zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      if (!ews || !zero || !hd || !fws || !off || !lst) return fail(ctx, 1002, "dfm_windows: out of device memory");
       HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
       rc = fact_precompute(dp.P, dp.ld, T, N, 0, nullptr, nullptr, H, ldH, zero, zero, zero, hd, st);
       if (rc) return fail(ctx, rc, "precompute");
@@ -1778,17 +1933,41 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
       rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
                             lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
-      Scope sc(ctx, DFM_KC_FACTORS);
-      hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kmax + 255) / 256), P), dim3(256), 0,
-                         st, Uk, T, kmax, n0, F);
+    } else if (orient == 0) {
+      // T > the factored solver's range: the windows' masked T x T Grams in
+      // chunks (<= 2 GB), each chunk by the explicit-Gram subspace solver
+      const int64_t per = (int64_t)T * T * 8;
+      const int Pc = (int)std::max<int64_t>(1, std::min<int64_t>(P, (int64_t)(2LL << 30) / per));
+      double *Gc = (double *)dal((size_t)Pc * per);
+      char *ews = (char *)dal(eig_workspace_bytes_padded(m, Pc, Pb, ctx->maxit));
+      if (!Gc || !ews) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      for (int c0 = 0; c0 < P; c0 += Pc) {
+        const int pc = std::min(Pc, P - c0);
+        {
+          Scope sc(ctx, DFM_KC_GRAM);
+          hipLaunchKernelGGL(window_gram_kernel, dim3((unsigned)((T + 255) / 256), T, pc), dim3(256), 0, st, H, ldH,
+                             didx + (size_t)c0 * T, deta + (size_t)c0 * T, T, Gc);
+          HIPCHK(ctx, hipGetLastError());
+        }
+        rc = eig_run(Gc, T, (int64_t)T * T, T, pc, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews,
+                     lam + (size_t)c0 * kmax, Uk + (size_t)c0 * T * kmax, tr + c0, stt + c0, nullptr, st, timer_cb,
+                     ctx, 0);
+        if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
+      }
     } else {
+      char *ews = (char *)dal(eig_workspace_bytes_padded(m, P, Pb, ctx->maxit));
       double *Ld = (double *)dal((size_t)P * N * kmax * 8);
-      if (!Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
+      if (!ews || !Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
       rc = eig_run(G, N, (int64_t)N * N, N, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, lam, Uk,
                    tr, stt, nullptr, st, timer_cb, ctx, 0);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       Scope sc(ctx, DFM_KC_FACTORS);
       launch_factors(1, msrc, T, N, kmax, P, Uk, F, Ld, nullptr, st);
+    }
+    if (orient == 0) {
+      Scope sc(ctx, DFM_KC_FACTORS);
+      hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kmax + 255) / 256), P), dim3(256), 0,
+                         st, Uk, T, kmax, mv0, dmv, F);
     }
     std::vector<int> hs(P);
     HIPCHK(ctx, hipMemcpyAsync(hl.data(), lam, hl.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1800,17 +1979,18 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   } else {
     HIPCHK(ctx, hipStreamSynchronize(st));
     for (int wi = 0; wi < P; ++wi) {   // eigenvalues and trace from the window's spectrum
-      const int mw = orient == 0 ? n0 + wi : N;
+      const int mw = orient == 0 ? nw(wi) : N;
       double s = 0.0;
       for (int j = mw - 1; j >= 0; --j) s += hev[(size_t)wi * pst + j];
       ht[wi] = s;
       for (int j = 0; j < kmax; ++j) hl[(size_t)wi * kmax + j] = hev[(size_t)wi * pst + j];
     }
   }
-  // ---- IC sweep per window on the host (arithmetic only)
+  // ---- per window on the host (arithmetic only): the IC sweep and r_w, or
+  // the fixed / default r_w and its criterion value
   std::vector<double> ic(7 * (size_t)kmax);
   for (int wi = 0; wi < P; ++wi) {
-    const int n = n0 + wi;
+    const int n = nw(wi);
     double s2 = NAN;
     if (pcp) {   // src/criteria.jl:18: V(ceil(m_w/2)) of the window's unrestricted fit = spectral tail
       const int mw = std::min(n, N), h = (mw + 1) / 2;
@@ -1819,23 +1999,34 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
       s2 = s / ((double)N * n);
     }
     const int kw = kmax_w(wi);
-    dfm_ic_sweep(&hl[(size_t)wi * kmax], kw, kw, ht[wi], n, N, s2, ic.data());
-    int best = 0;
-    for (int k = 1; k < kw; ++k)
-      if (ic[(size_t)crit * kw + k] < ic[(size_t)crit * kw + best]) best = k;
+    int rsel = kw;
+    double cv = NAN;
+    if (ws.r == 0) {
+      dfm_ic_sweep(&hl[(size_t)wi * kmax], kw, kw, ht[wi], n, N, s2, ic.data());
+      int best = 0;
+      for (int k = 1; k < kw; ++k)
+        if (ic[(size_t)crit * kw + k] < ic[(size_t)crit * kw + best]) best = k;
+      rsel = best + 1;
+      cv = ic[(size_t)crit * kw + best];
+    } else if (crit >= 0) {   // the workhorse constructor's criterion at r_w (:50)
+      dfm_ic_sweep(&hl[(size_t)wi * kmax], kw, kw, ht[wi], n, N, s2, ic.data());
+      cv = ic[(size_t)crit * kw + kw - 1];
+    }
     hTn[wi] = n;
-    hkr[wi] = best + 1;
-    r_out[wi] = best + 1;
-    if (crit_out) crit_out[wi] = ic[(size_t)crit * kw + best];
+    hkr[wi] = rsel;
+    hR0[wi] = aw(wi);
+    r_out[wi] = rsel;
+    if (crit_out) crit_out[wi] = cv;
     if (V_out) {
       double sacc = ht[wi];
-      for (int j = 0; j <= best; ++j) sacc -= hl[(size_t)wi * kmax + j];
+      for (int j = 0; j < rsel; ++j) sacc -= hl[(size_t)wi * kmax + j];
       V_out[wi] = sacc / ((double)N * n);
     }
   }
   if (eig_out) std::copy(hl.begin(), hl.end(), eig_out);
   HIPCHK(ctx, hipMemcpyAsync(dTn, hTn.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(dkr, hkr.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(dR0, hR0.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
   // ---- wide: the r_w eigenvectors (kv = max_w r_w) and factors of every window
   if (wide) {
     kv = *std::max_element(hkr.begin(), hkr.end());
@@ -1846,14 +2037,14 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     hipError_t e;
     {
       Scope sc(ctx, DFM_KC_EIG_OTHER);
-      e = orient == 0 ? launch_dense_eig_batched(H, ldH, 0, T, n0, 1, P, kv, lam, Uk, tr, stt, dwk, st)
+      e = orient == 0 ? launch_dense_eig_batched(Hb, ldH, sHb, T, mv0, dmv, P, kv, lam, Uk, tr, stt, dwk, st)
                       : launch_dense_eig_batched(G, N, (int64_t)N * N, N, N, 0, P, kv, lam, Uk, tr, stt, dwk, st);
     }
     if (e != hipSuccess) return fail(ctx, 1000 + (int)e, "dense eigensolver: %s", hipGetErrorString(e));
     Scope sc(ctx, DFM_KC_FACTORS);
     if (orient == 0) {
       hipLaunchKernelGGL(window_scale_kernel, dim3((unsigned)(((int64_t)T * kv + 255) / 256), P), dim3(256), 0, st,
-                         Uk, T, kv, n0, F);
+                         Uk, T, kv, mv0, dmv, F);
     } else {
       double *Ld = (double *)dal((size_t)P * N * kv * 8);
       if (!Ld) return fail(ctx, 1002, "dfm_windows: out of device memory");
@@ -1875,16 +2066,16 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
   if (!coef || !tst) return fail(ctx, 1002, "dfm_windows: out of device memory");
   if (dv <= 32) {
     Scope sc(ctx, DFM_KC_OLS);
-    launch_ols(P, st, dy, dw, q, F, T, kv, dTn, dkr, coef, tst, nullptr, nullptr, ost);
+    launch_ols(P, st, dy, dw, q, F, T, kv, dTn, dkr, coef, tst, nullptr, nullptr, ost, len > 0 ? dR0 : nullptr);
   } else {   // per window: its own width q + r_w
     const int dmax = q + kv;
     double *owk = (double *)dal((size_t)ols_wide_work(T, dmax) * 8);
     if (!owk) return fail(ctx, 1002, "dfm_windows: out of device memory");
     Scope sc(ctx, DFM_KC_OLS);
     for (int wi = 0; wi < P; ++wi)
-      HIPCHK(ctx, launch_ols_wide_batched(1, dy, dw, q, F + (size_t)wi * T * kv, T, kv, hkr[wi], dTn + wi,
-                                          coef + (size_t)wi * dv, tst + (size_t)wi * dv, nullptr, nullptr, ost + wi,
-                                          owk, st));
+      HIPCHK(ctx, launch_ols_wide_batched(1, dy + hR0[wi], dw + hR0[wi], q, F + (size_t)wi * T * kv, T, kv, hkr[wi],
+                                          dTn + wi, coef + (size_t)wi * dv, tst + (size_t)wi * dv, nullptr, nullptr,
+                                          ost + wi, owk, st));
   }
   {
     std::vector<int> ho(P);
@@ -1916,14 +2107,112 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     if (!rs || !ss || !dp_ || !dt_) return fail(ctx, 1002, "dfm_windows: out of device memory");
     Scope sc(ctx, DFM_KC_MISC);
     hipLaunchKernelGGL(panel_row_sums_kernel, dim3(T), dim3(256), 0, st, dp.P, dp.ld, N, rs, ss);
-    hipLaunchKernelGGL(window_forecast_kernel, dim3(P), dim3(256), 0, st, orient, dp.P, dp.ld, T, N, n0, q, kv, H,
-                       ldH, F, Uk, lam, rs, ss, dkr, coef, dy, dw, dp_, dt_);
+    hipLaunchKernelGGL(window_forecast_kernel, dim3(P), dim3(256), 0, st, orient, dp.P, dp.ld, T, N, n0, len, q, kv,
+                       H, ldH, F, Uk, lam, rs, ss, dkr, coef, dy, dw, dp_, dt_);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(pred_out, dp_, (size_t)P * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(true_out, dt_, (size_t)P * 8, hipMemcpyDeviceToHost, st));
   }
   HIPCHK(ctx, hipStreamSynchronize(st));
   return 0;
+}
+
+// Expanding windows of a model with structural breaks (model_args'
+// break_indices, src/utils.jl:64 -> src/DynamicFactorModel.jl:73, :98): each
+// window is the break-aware fit of dfm_model_fit_breaks on its leading rows
+// (per-block PCA with the window's full-sample T, N, D7), read back, and —
+// for the forecast step — dfm_predict on the next row.  X, y, w host or
+// device memory (the fit copies with hipMemcpyDefault).
+static int windows_breaks_impl(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw, const double *X,
+                               int T, int N, int64_t ldx, int P, const WinSpec &ws, int K, int64_t *r_out,
+                               double *V_out, double *crit_out, double *eig_out, double *coef_out,
+                               double *tstat_out, double *pred_out, double *true_out) {
+  const int n0 = T - P;
+  for (int j = 0; j < ws.nbreaks; ++j)
+    if (ws.breaks[j] >= n0)
+      return fail(ctx, -9, "dfm_windows: break row %lld is not inside the first window (%d rows)",
+                  (long long)ws.breaks[j], n0);
+  for (int wi = 0; wi < P; ++wi) {
+    const int n = n0 + wi;
+    const int kd = (std::min(n, N) + 1) / 2;
+    const int rarg = ws.r > 0 ? ws.r : (ws.r < 0 ? kd : 0);
+    dfm_model *M = nullptr;
+    int rc = dfm_model_fit_breaks(ctx, y, w, q, ldw, X, n, N, ldx, rarg, ws.crit, ws.kmax, ws.breaks, ws.nbreaks,
+                                  &M);
+    if (rc) return rc;
+    struct Kill { dfm_model *m; ~Kill() { dfm_model_destroy(m); } } kill{M};
+    int64_t r = 0, kmx = 0, ne = 0;
+    double V = 0, cv = 0, tr = 0;
+    dfm_model_scalars(M, &r, &V, &cv, &tr);
+    dfm_model_dims(M, &r, &kmx, &ne);
+    const int d = q + (int)r;
+    std::vector<double> ev(ne), co(d), ts(d);
+    if ((rc = dfm_model_read(M, ev.data(), co.data(), ts.data(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr)))
+      return rc;
+    r_out[wi] = r;
+    if (V_out) V_out[wi] = V;
+    if (crit_out) crit_out[wi] = ws.crit >= 0 ? cv : NAN;
+    if (eig_out)
+      for (int j = 0; j < K; ++j) eig_out[(size_t)wi * K + j] = j < ne ? ev[j] : NAN;
+    const int dk = q + K;
+    for (int c = 0; c < dk; ++c) {
+      if (coef_out) coef_out[(size_t)wi * dk + c] = c < d ? co[c] : NAN;
+      if (tstat_out) tstat_out[(size_t)wi * dk + c] = c < d ? ts[c] : NAN;
+    }
+    if (pred_out) {   // predict row n from this window's fit (D4-repaired get_factors)
+      if ((rc = dfm_predict(M, 1, q > 0 ? w + n : nullptr, ldw, X + n, ldx, pred_out + wi))) return rc;
+      HIPCHK(ctx, hipMemcpy(true_out + wi, y + n, 8, hipMemcpyDefault));
+    }
+  }
+  return 0;
+}
+
+// ---- get_factors / predict on new rows (src/DynamicFactorModel.jl:125-128,
+// :152-155; D4 repaired, dfm_predict.hip).  x_new (nn x N) and w_new (nn x q)
+// column-major, host or device memory (hipMemcpyDefault); outputs host.
+static int predict_impl(dfm_model *M, int64_t nn, const double *w_new, int64_t ldw, const double *x_new,
+                        int64_t ldx, double *F_out, double *yhat) {
+  if (!M) return -1;
+  dfm_ctx *ctx = M->ctx;
+  const int q = M->q, r = M->r, N = M->N, T = M->T;
+  if (nn < 1 || !x_new || ldx < nn || (yhat && q > 0 && (!w_new || ldw < nn)) || (!F_out && !yhat))
+    return fail(ctx, -2, "dfm_predict: bad arguments");
+  hipSetDevice(ctx->device);
+  hipStream_t st = ctx->stream;
+  double *xd = nullptr, *wd = nullptr, *bd = nullptr, *wk = nullptr, *Fd = nullptr, *yd = nullptr;
+  struct Fr { std::vector<double *> v; ~Fr() { for (double *p : v) hipFree(p); } } fr;
+  auto al = [&](double **p, size_t n) { hipError_t e = dalloc(p, n); if (e == hipSuccess) fr.v.push_back(*p); return e; };
+  HIPCHK(ctx, al(&xd, (size_t)nn * N));
+  HIPCHK(ctx, al(&wd, (size_t)nn * std::max(q, 1)));
+  HIPCHK(ctx, al(&bd, (size_t)q + r));
+  HIPCHK(ctx, al(&wk, (size_t)T + 2));
+  HIPCHK(ctx, al(&Fd, (size_t)nn * std::max(r, 1)));
+  HIPCHK(ctx, al(&yd, (size_t)nn));
+  HIPCHK(ctx, hipMemcpy2DAsync(xd, (size_t)nn * 8, x_new, (size_t)ldx * 8, (size_t)nn * 8, N, hipMemcpyDefault, st));
+  if (yhat && q > 0)
+    HIPCHK(ctx, hipMemcpy2DAsync(wd, (size_t)nn * 8, w_new, (size_t)ldw * 8, (size_t)nn * 8, q, hipMemcpyDefault, st));
+  HIPCHK(ctx, hipMemcpyAsync(bd, M->coef.data(), (size_t)(q + r) * 8, hipMemcpyHostToDevice, st));
+  {
+    Scope sc(ctx, DFM_KC_MISC);
+    HIPCHK(ctx, launch_predict(M->Xp, M->ld, T, N, M->L, r, xd, nn, nn, wd, nn, q, yhat ? bd : nullptr, wk, Fd, yd,
+                               st));
+  }
+  if (F_out) HIPCHK(ctx, hipMemcpyAsync(F_out, Fd, (size_t)nn * r * 8, hipMemcpyDeviceToHost, st));
+  if (yhat) HIPCHK(ctx, hipMemcpyAsync(yhat, yd, (size_t)nn * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return 0;
+}
+
+extern "C" int dfm_get_factors(dfm_model *m, int64_t n_new, const double *x_new, int64_t ldx, double *F_out) {
+  if (!F_out) return m ? fail(m->ctx, -2, "dfm_get_factors: output required") : -1;
+  return predict_impl(m, n_new, nullptr, 0, x_new, ldx, F_out, nullptr);
+}
+
+extern "C" int dfm_predict(dfm_model *m, int64_t n_new, const double *w_new, int64_t ldw, const double *x_new,
+                           int64_t ldx, double *out) {
+  if (!out) return m ? fail(m->ctx, -2, "dfm_predict: output required") : -1;
+  return predict_impl(m, n_new, w_new, ldw, x_new, ldx, nullptr, out);
 }
 
 // ------------------------------------------------------------------ normalize

@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel_t(const double *__restrict
                                                       double *__restrict__ tstat,
                                                       double *__restrict__ cov_out,
                                                       double *__restrict__ resid_out,
-                                                      int *__restrict__ status) {
+                                                      int *__restrict__ status,
+                                                      const int *__restrict__ R0) {
   constexpr int S = DMAX + 1;
   __shared__ double sD[OLS_TR * S];
   __shared__ double sy[OLS_TR], ssig[OLS_TR];
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(256) void ols_hc2_kernel_t(const double *__restrict
   const int k = kr ? kr[rep] : kF;
   const int d = q + k, dstr = q + kF;
   const double *Fr = F + (int64_t)rep * Tphys * kF;
+  if (R0) { y += R0[rep]; w += R0[rep]; }   // rolling windows: rows R0 .. R0 + T - 1 of y, w
   auto stage = [&](int t0) {
     for (int e = tid; e < OLS_TR * d; e += 256) {
       const int r = e / d, c = e % d, t = t0 + r;
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(64, 3) void ols_hc2_wave_kernel(const double *__res
                                                          const int *__restrict__ Tn, const int *__restrict__ kr,
                                                          double *__restrict__ coef, double *__restrict__ tstat,
                                                          double *__restrict__ cov_out, double *__restrict__ resid_out,
-                                                         int *__restrict__ status) {
+                                                         int *__restrict__ status, const int *__restrict__ R0) {
   constexpr int S = 17;
   __shared__ double M[16 * S], Li[16 * S], Inv[16 * S], Tmp[16 * S];
   __shared__ double sb[16];
@@ -398,6 +400,7 @@ __global__ __launch_bounds__(64, 3) void ols_hc2_wave_kernel(const double *__res
   const int k = kr ? kr[rep] : kF;
   const int d = q + k, dstr = q + kF;
   const double *Fr = F + (int64_t)rep * Tphys * kF;
+  if (R0) { y += R0[rep]; w += R0[rep]; }   // rolling windows: rows R0 .. R0 + T - 1 of y, w
   // column j of [D y] as (base, row stride); columns past d read nothing
   struct Col { const double *p; int st; bool on; };
   auto col = [&](int j) -> Col {
@@ -537,16 +540,16 @@ __global__ __launch_bounds__(64, 3) void ols_hc2_wave_kernel(const double *__res
 // to the design width: d <= 16 fits 5 workgroups per CU instead of 2.
 hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, int q, const double *F, int Tphys,
                       int kF, const int *Tn, const int *kr, double *coef, double *tstat, double *cov_out,
-                      double *resid_out, int *status) {
+                      double *resid_out, int *status, const int *R0) {
   if (q + kF + 1 <= 16)
     hipLaunchKernelGGL(ols_hc2_wave_kernel, dim3(nb), dim3(64), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef, tstat,
-                       cov_out, resid_out, status);
+                       cov_out, resid_out, status, R0);
   else if (q + kF <= 16)
     hipLaunchKernelGGL(ols_hc2_kernel_t<16>, dim3(nb), dim3(256), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef, tstat,
-                       cov_out, resid_out, status);
+                       cov_out, resid_out, status, R0);
   else
     hipLaunchKernelGGL(ols_hc2_kernel_t<OLS_DMAX>, dim3(nb), dim3(256), 0, st, y, w, q, F, Tphys, kF, Tn, kr, coef,
-                       tstat, cov_out, resid_out, status);
+                       tstat, cov_out, resid_out, status, R0);
   return hipGetLastError();
 }
 

@@ -180,6 +180,17 @@ int dfm_model_read(const dfm_model *m, double *eigvals, double *coef, double *ts
                    double *coef_cov, double *ols_resid, double *F, double *L,
                    double *E, double *ic_values);
 
+/* get_factors (src/DynamicFactorModel.jl:125-128) and predict (:152-155) of a
+ * fitted model on n_new new rows, defect D4 repaired: rotation = L (L'L)^-1 of
+ * the first break block's loadings (D1), first r columns ("active"); the new
+ * rows normalised by the scalar mean and sample std of all T N entries of the
+ * fitted x (:127).  x_new: n_new x N column-major (ldx >= n_new), w_new: n_new x q
+ * column-major (ldw >= n_new; unused when q = 0); host or device memory.
+ * F_out: n_new x r column-major (host); out: n_new predictions (host). */
+int dfm_get_factors(dfm_model *m, int64_t n_new, const double *x_new, int64_t ldx, double *F_out);
+int dfm_predict(dfm_model *m, int64_t n_new, const double *w_new, int64_t ldw, const double *x_new, int64_t ldx,
+                double *out);
+
 /* ------------------------------------------------------------- bootstrap
  * wild_bootstrap (src/bootstrap.jl:41-51) / residual_bootstrap (:21-39):
  * for b < B: X*_b = F_r L_r' + diag(eta_b) E[idx_b, :]  (eta == NULL for
@@ -223,6 +234,18 @@ int dfm_model_set_mode(dfm_model *m, int mode);
  * Any output pointer may be NULL. */
 int dfm_chow_all(dfm_model *m, int64_t bp, double *LR, double *LM, double *Wald);
 
+/* One variable's LR_test / LM_test / Wald_test (src/chowtest.jl:19-42), i
+ * 0-based.  The model keeps the all-variables results of the last break
+ * period asked for, so a loop over i = 0..N-1 costs one dfm_chow_all. */
+int dfm_chow(dfm_model *m, int64_t bp, int64_t i, double *LR, double *LM, double *Wald);
+
+/* criterion_<name>(dfm) (src/criteria.jl:17-53) of a fitted model at its r,
+ * for any criterion code (not only the one it was fitted with).  PCp's sigma^2
+ * = V(ceil(m/2)) of the unrestricted fit DynamicFactorModel(y, w, x)
+ * (:18, :23, :28) comes from the resident panel's full spectrum (min(T,N) <=
+ * dfm_full_spectrum_max()), computed once per model. */
+int dfm_model_criterion(dfm_model *m, int crit, double *value);
+
 /* ---------------------------------------------------- expanding windows
  * The refits of pseudo_out_of_sample_forecasts (src/utils.jl:54-72): window
  * w = 0..P-1 refits the IC-sweep constructor (src/DynamicFactorModel.jl:53)
@@ -258,6 +281,34 @@ int dfm_windows_dev(dfm_ctx *ctx, const double *y_dev, const double *w_dev, int 
                     const double *X_dev, int64_t T, int64_t N, int64_t ldx, int P, int crit,
                     int kmax, int64_t *r_out, double *V_out, double *crit_out, double *eig_out,
                     double *coef_out, double *tstat_out);
+
+/* pseudo_out_of_sample_forecasts(model, y, w, x, model_args...) (src/utils.jl:54-72)
+ * for every model_args form of the DynamicFactorModel constructors, and rolling
+ * windows (BASELINE configs[4]: "rolling-window factor re-estimation").
+ *   kind DFM_WIN_EXPANDING: window w = rows 0 .. T-P+w-1 (the reference's loop);
+ *   kind DFM_WIN_ROLLING:   window w = the `length` rows T-P+w-length .. T-P+w-1.
+ *   r > 0:  the workhorse constructor at fixed r (src/DynamicFactorModel.jl:28),
+ *           r_w = min(r, ceil(m_w/2)) (:116-119), criterion value of crit at r_w
+ *           (crit = DFM_CRIT_NONE: NaN, D3);
+ *   r == 0: the IC-sweep constructor (:53-66) by crit over k = 1..kmax_w (as dfm_windows);
+ *   r < 0:  the 3-arg constructor's default r_w = ceil(m_w/2) (D2).
+ *   breaks (nbreaks > 0, expanding windows only): model_args' break_indices
+ *           (0-based first rows of blocks 2..; all inside the first window), the
+ *           same rows in every refit; each window is then a break-aware fit
+ *           (dfm_model_fit_breaks on its rows, D7) and forecasts through dfm_predict.
+ * dev != 0: y, w, X are device pointers (as dfm_windows_dev).  Outputs as
+ * dfm_windows with K = the widest window's r_w bound; pred_out / true_out (P
+ * each, both or neither) add the forecast step (as dfm_windows_forecast). */
+enum dfm_window_kind { DFM_WIN_EXPANDING = 0, DFM_WIN_ROLLING = 1 };
+typedef struct dfm_window_spec {
+  int32_t kind, length, r, crit, kmax, nbreaks;
+  const int64_t *breaks;
+} dfm_window_spec;
+int dfm_windows_ex(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
+                   const double *X, int64_t T, int64_t N, int64_t ldx, int P,
+                   const dfm_window_spec *spec, int dev, int64_t *r_out, double *V_out,
+                   double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
+                   double *pred_out, double *true_out);
 
 /* --------------------------------------------------- targeted predictors
  * targeted_predictors(..., thresholding="hard") (src/targeted_predictors.jl:9-30).

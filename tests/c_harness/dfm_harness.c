@@ -180,6 +180,44 @@ int main(int argc, char **argv) {
   puti("windows_r", rw, 4);
   put("windows_pred", pred, 4);
 
+  /* predict / get_factors on the last two rows (src/DynamicFactorModel.jl:125-128,
+   * :152-155, D4 repaired): the model fitted on rows 0..T-3 */
+  {
+    dfm_model *mp = NULL;
+    double pr[2], Fn[2 * 8], lr1, lm1, wd1, cr[7];
+    int c;
+    CHECK(ctx, dfm_model_fit(ctx, y, w, 1, T, X, T - 2, N, T, 3, DFM_CRIT_ICP2, 0, &mp));
+    CHECK(ctx, dfm_predict(mp, 2, w + T - 2, T, X + T - 2, T, pr));
+    CHECK(ctx, dfm_get_factors(mp, 2, X + T - 2, T, Fn));
+    put("predict", pr, 2);
+    put("get_factors", Fn, 2 * 3);
+    /* one variable's Chow statistics (cached all-variables pass) */
+    CHECK(ctx, dfm_chow(mp, (T - 2) / 2, 4, &lr1, &lm1, &wd1));
+    {
+      double c3[3];
+      c3[0] = lr1; c3[1] = lm1; c3[2] = wd1;
+      put("chow_one", c3, 3);
+    }
+    /* criterion_<name>(dfm) for every name on the fitted model */
+    for (c = 0; c < 7; ++c) CHECK(ctx, dfm_model_criterion(mp, c, &cr[c]));
+    put("model_criteria", cr, 7);
+    dfm_model_destroy(mp);
+  }
+
+  /* rolling windows (len T/2) of the workhorse at r = 2 with BIC, forecasts */
+  {
+    dfm_window_spec sp;
+    int64_t rr[4];
+    double Vw[4], cw[4], ew[4 * 2], co[4 * 3], tw[4 * 3], pw[4], tv[4];
+    sp.kind = DFM_WIN_ROLLING; sp.length = (int32_t)(T / 2); sp.r = 2; sp.crit = DFM_CRIT_BIC; sp.kmax = 0;
+    sp.nbreaks = 0; sp.breaks = NULL;
+    CHECK(ctx, dfm_windows_ex(ctx, y, w, 1, T, X, T, N, T, 4, &sp, 0, rr, Vw, cw, ew, co, tw, pw, tv));
+    puti("rolling_r", rr, 4);
+    put("rolling_V", Vw, 4);
+    put("rolling_crit", cw, 4);
+    put("rolling_pred", pw, 4);
+  }
+
   /* error behaviour: a status code and a message, nothing thrown */
   {
     int rc = dfm_chow_all(m, 0, LR, LM, WD);

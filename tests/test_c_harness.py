@@ -106,3 +106,23 @@ def test_harness_matches_python_binding_and_oracle(dfm, oracle, tmp_path):
                                                     kmax=4)
     assert np.array_equal(h["windows_pred"], pred)
     assert h["error_rc"][0] < 0 and h["error_msg_nonempty"][0] == 1
+    # predict / get_factors / per-variable Chow / model criteria on rows 0..T-3
+    gp = dfm.DynamicFactorModel(y[:T - 2], w[:T - 2], X[:T - 2], 3, "ICp2")
+    assert np.array_equal(h["predict"], dfm.predict(gp, w[T - 2:], X[T - 2:]))
+    assert np.array_equal(h["get_factors"], dfm.get_factors(gp, X[T - 2:]).ravel(order="F"))
+    op = oracle.DynamicFactorModel(y[:T - 2], w[:T - 2], X[:T - 2], 3, "ICp2")
+    po = oracle.predict(op, w[T - 2:], X[T - 2:])
+    assert np.max(np.abs(h["predict"] - po)) <= 1e-10 * np.max(np.abs(po))
+    bp = (T - 2) // 2
+    assert h["chow_one"][0] == dfm.LR_test(gp, bp, 5)
+    assert abs(h["chow_one"][2] - oracle.Wald_test(op, bp, 4)) <= 1e-10 * abs(oracle.Wald_test(op, bp, 4))
+    for c, name in enumerate(dfm.CRITERIA):
+        ref = oracle.criterion_value(name, op)
+        assert abs(h["model_criteria"][c] - ref) <= 1e-10 * abs(ref), name
+    # rolling windows, workhorse r = 2 with BIC
+    res = dfm.pseudo_out_of_sample_windows(y, w, X, 2, "BIC", num_predictions=4, rolling=T // 2, forecast=True)
+    assert np.array_equal(h["rolling_r"], res["number_of_factors"])
+    assert np.array_equal(h["rolling_V"], res["V"]) and np.array_equal(h["rolling_pred"], res["predictions"])
+    ro, _, _ = oracle.rolling_window_forecasts(lambda yy, ww, xx: oracle.DynamicFactorModel(yy, ww, xx, 2, "BIC"),
+                                               y, w, X, 4, T // 2)
+    assert np.max(np.abs(h["rolling_pred"] - ro)) <= 1e-10 * np.max(np.abs(ro))
