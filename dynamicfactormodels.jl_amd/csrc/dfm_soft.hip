@@ -17,7 +17,7 @@
 //   gram_kernel (K1)    G_f = Zs_f' Zs_f over each problem's training rows,
 //                       gathered by row index (zero row pads ragged folds):
 //                       (K+1) p^2 n MACs on MFMA              (MFMA-bound)
-//   lasso_coop_kernel   one cooperative launch, 1 leader + H helper
+//   lasso_coop_kernel   one co-resident launch, 1 leader + H helper
 //                       workgroups per problem: glmnet's elnet1 path (the
 //                       serial coordinate descent over the active set on the
 //                       leader, the O(p |A|) full-pass replays and gradient
@@ -101,7 +101,7 @@ __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64
 }
 
 // ------------------------------------------------------------- lasso path
-// glmnet's elnet1 (covariance updating) for K + 1 problems in ONE cooperative
+// glmnet's elnet1 (covariance updating) for K + 1 problems in ONE co-resident
 // launch.  The loop order is elnet1's (the parity checker's lasso_path_cd):
 // per lambda a full cyclic pass over every variable in index order with
 // in-pass entry and eager gradient updates g_j -= c_jk d, then passes over
@@ -1098,7 +1098,7 @@ hipStream_t ctx_stream(dfm_ctx *ctx);
 int ctx_device(dfm_ctx *ctx);
 }  // namespace dfm
 
-// Every problem's path in one cooperative launch (lasso_coop_kernel): nprob
+// Every problem's path in one co-resident launch (lasso_coop_kernel): nprob
 // groups of 1 leader + H helper workgroups, H as large as the chip's
 // co-resident workgroups allow (<= one per 256 columns, <= 64).  Scratch is
 // allocated here; outputs: bpath [nprob][nlam][p], rsq [nprob][nlam], nl
@@ -1148,9 +1148,18 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   }
   e = hipMemsetAsync(A.ctl, 0, (size_t)nprob * sizeof(LassoCtl), st);
   if (e == hipSuccess) e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
-  void *args[] = {&A};
-  if (e == hipSuccess)
-    e = hipLaunchCooperativeKernel((const void *)lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), args, 0, st);
+  // A plain launch sized to the co-resident capacity (occupancy API above):
+  // the kernel needs every workgroup resident (leader/helper hand-offs), not
+  // a grid barrier, and every spin is bounded by the wall-clock timeout.  A
+  // cooperative launch (hipLaunchCooperativeKernel) guarantees the same on an
+  // idle device but makes rocprofv3 (ROCm 7.2) fault in its exit path: a bare
+  // cooperative launch of a trivial kernel reproduces that SIGSEGV while the
+  // same kernel launched plainly exits cleanly (tools/coop_exit_probe.hip,
+  // profiles/r03_coop_exit_probe.txt).
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), 0, st, A);
+    e = hipGetLastError();
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess && A.prof) {
     std::vector<long long> hp((size_t)nprob * LP_PROF);

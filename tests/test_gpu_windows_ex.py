@@ -124,7 +124,7 @@ def test_windows_beyond_factored_T(dfm, oracle):
     explicit window Grams (diagonal blocks of the prefix Gram) on the explicit
     Gram solver; eigenvalues and V against LAPACK on the windows' rows."""
     import scipy.linalg as sla
-    T, N, P, k = 4200, 4300, 2, 3
+    T, N, P, k = 4200, 4300, 1, 3
     rng = np.random.default_rng(77)
     f = rng.standard_normal((T, 3))
     x = f @ rng.standard_normal((3, N)) * 2.0 + rng.standard_normal((T, N))
