@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
                     help="c3 (default, the metric's config) or c5: 200 expanding windows x ICp2 sweep at "
                          "T=2000 N=20000, windows sharded over the ranks (strong scaling)")
+    ap.add_argument("--rolling", type=int, default=0,
+                    help="c5: rolling windows of this many rows instead of expanding windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling extra field (N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -415,9 +417,10 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     holds it); a step = all 200 windows, sharded over the ranks as contiguous
     window blocks (parallel.window_shard: a rank reads only the leading rows its
     windows reach) + one all-gather of the per-window rows.  Strong scaling."""
-    from dfm_amd.parallel import window_shard, _pack_windows, gather_rows
-    from dfm_amd.api import _window_kmax
+    from dfm_amd.parallel import window_rows, _pack_windows, gather_rows
+    from dfm_amd.api import _window_kmax, _windows_K
     T5, N5, P5, km = C5_T, C5_N, C5_P, C5_KMAX
+    L = int(args.rolling) or None
     rng = np.random.default_rng(20261015 + 5)
     y, x, *_ = D.factor_model_DGP(T5, N5, 8, rng=rng)
     x = D.normalize(x)
@@ -425,13 +428,19 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     wd = torch.ones((T5, 1), dtype=torch.float64, device=dev)
     xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major T x N in HBM
     del x
-    w0, w1, rows = window_shard(T5, P5, world, rank)
-    K = _window_kmax(T5, N5, km)
+    w0, w1, a0, rows = window_rows(T5, P5, world, rank, L)
+    K = _windows_K(T5, N5, P5, 0, km, L) if L else _window_kmax(T5, N5, km)
     holder = {}
 
     def step():
-        res = D.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=w1 - w0, kmax=km,
-                                                rows=rows, ctx=ctx) if w1 > w0 else {}
+        if w1 <= w0:
+            res = {}
+        elif L:   # rolling: this rank's row slice [a0, rows), a zero-copy column-major view
+            res = D.pseudo_out_of_sample_windows(yd[a0:rows], wd[a0:rows], xd[a0:rows], "ICp2",
+                                                 num_predictions=w1 - w0, kmax=km, rolling=L, ctx=ctx)
+        else:
+            res = D.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=w1 - w0, kmax=km,
+                                                    rows=rows, ctx=ctx)
         loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, 1)).to(dev)
         holder["all"] = gather_rows(loc, P5) if world > 1 else loc
 
@@ -460,22 +469,25 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     allrows = holder["all"].cpu().numpy()
     gram_ms, gram_n = timing.get("gram", (0.0, 0))
     roof = None
-    if gram_n:   # rank-local prefix Gram of the rows its windows reach: rows (rows+1) N flop (SYRK count)
+    if gram_n:   # rank-local prefix Gram of the rows its windows reach: m (m+1) N flop (SYRK count)
         per = gram_ms / gram_n
-        ach = rows * (rows + 1) * N5 / (per * 1e-3) / 1e12
+        m_rows = rows - a0
+        ach = m_rows * (m_rows + 1) * N5 / (per * 1e-3) / 1e12
         roof = {"kernel": "gram_dma_kernel (prefix Gram X X' of the leading rows: LDS-DMA ring, v_mfma_f64_4x4x4_4b)",
                 "bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_F64_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(per, 4),
-                "flop_per_launch": rows * (rows + 1) * N5}
+                "flop_per_launch": m_rows * (m_rows + 1) * N5}
+    kind = f"rolling ({L} rows)" if L else "expanding"
     rec = {
-        "metric": "expanding-window refits/sec (node), T=2000 N=20000, 200 windows x ICp2 sweep kmax 8",
+        "metric": f"{kind}-window refits/sec (node), T=2000 N=20000, 200 windows x ICp2 sweep kmax 8",
         "value": round(P5 * args.steps / el, 2), "unit": "windows/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C5: pseudo_out_of_sample_forecasts refits, Bai-Ng DGP T=2000 N=20000 r=8, "
-                               "P=200 windows per step (all ranks together), panel resident in HBM",
-                   "T": T5, "N": N5, "P": P5, "kmax": km, "parallelism": f"window-sharded x{world}"},
+        "config": {"workload": f"C5: pseudo_out_of_sample_forecasts refits, {kind} windows, Bai-Ng DGP "
+                               f"T=2000 N=20000 r=8, P=200 windows per step (all ranks together), panel "
+                               f"resident in HBM",
+                   "T": T5, "N": N5, "P": P5, "kmax": km, "rolling": L, "parallelism": f"window-sharded x{world}"},
         "roofline": roof,
         "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},

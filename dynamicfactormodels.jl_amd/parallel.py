@@ -107,6 +107,19 @@ def window_shard(T: int, P: int, world: int, rank: int) -> Tuple[int, int, int]:
     return w0, w1, T - P + w1
 
 
+def window_rows(T: int, P: int, world: int, rank: int, rolling: Optional[int] = None) -> Tuple[int, int, int, int]:
+    """(w0, w1, a, b): this rank's windows [w0, w1) and the panel rows [a, b)
+    they read.  Expanding windows read from row 0 (a = 0); rolling windows of
+    L rows (window w = rows T-P+w-L .. T-P+w-1) read only [T-P+w0-L, T-P+w1),
+    so a rank runs the (b - a, w1 - w0) rolling problem on that row slice (a
+    zero-copy view of a column-major panel: pointer + a, same leading
+    dimension) — its own diagonal block of the prefix Gram, no exchange."""
+    w0, w1 = shard_range(P, world, rank)
+    b = T - P + w1
+    a = T - P + w0 - int(rolling) if rolling else 0
+    return w0, w1, a, b
+
+
 def _pack_windows(res: dict, n: int, K: int, q: int) -> np.ndarray:
     """One (n, 3 + K + 2 (q + K)) float64 row block per shard; columns past the
     shard's own sweep bound are NaN."""

@@ -68,6 +68,53 @@ def test_c3_full_batch_sampled_replicates_match_oracle(dfm, oracle):
         assert rel(got, ref) < STAT_RTOL, (b, its[b])
 
 
+def test_c3_full_batch_coefficients_loadings_chow_match_oracle(dfm, oracle):
+    """The B = 9999 C3 job with the fit's regression outputs requested (every
+    OLS coefficient and HC2 t-statistic, src/DynamicFactorModel.jl:40-48) and
+    the Chow LR of every variable (src/chowtest.jl:19-23, which reads each
+    replicate's loadings through E* = X* - F* L*'): the strict eigenvector
+    stopping rule, the factored loadings GEMM, OLS and Chow kernels at full
+    size, sampled replicates against the oracle at 1e-10.  Factor columns'
+    coefficients are compared in absolute value (eigenvector signs are
+    arbitrary; both sides canonicalise them), the intercept's exactly."""
+    import torch
+    T, N, r, B = 500, 2000, 8, 9999
+    rng = np.random.default_rng(20261015 + 3)
+    y, x, *_ = oracle.factor_model_DGP(T, N, r, rng)
+    x = oracle.normalize(x)
+    w = np.ones((T, 1))
+    ctx = dfm.Context(0)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2", ctx=ctx)
+    S = dfm.Stat
+    d = 1 + r
+    bp = 250
+    stats = [S.coefficient(j) for j in range(1, d + 1)] + [S.t_stat(j) for j in range(1, d + 1)] + [S.LR_all(bp)]
+    arr = dfm.api._stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(g.handle, arr, len(stats)))
+    assert width == 2 * d + N
+    idx, eta = dfm.draw_wild_fast(1_000_004, B, T)
+    dev = torch.device("cuda", 0)
+    idx_d, eta_d = torch.from_numpy(idx).to(dev), torch.from_numpy(eta).to(dev)
+    out = torch.empty((B, width), dtype=torch.float64, device=dev)
+    ctx.check(ctx.lib.dfm_bootstrap_dev(g.handle, 0, B, idx_d.data_ptr(), eta_d.data_ptr(), arr, len(stats),
+                                        out.data_ptr()))
+    ctx.synchronize()
+    res = out.cpu().numpy()
+    del out
+    assert np.all(np.isfinite(res))
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    common, E = o.common_component, o.factor_residuals
+    vs = [0, 1, 977, N - 1]
+    for b in sorted(set([0, B - 1] + list(np.random.default_rng(2).integers(1, B - 1, 4)))):
+        xs = common + eta[b][:, None] * E[idx[b]]
+        dd = oracle.DynamicFactorModel(y, w, xs, r, "ICp2")
+        assert rel(res[b, 0], dd.coefficients[0]) < STAT_RTOL and rel(res[b, d], dd.t_stats[0]) < STAT_RTOL, b
+        assert rel(np.abs(res[b, 1:d]), np.abs(dd.coefficients[1:])) < STAT_RTOL, b
+        assert rel(np.abs(res[b, d + 1:2 * d]), np.abs(dd.t_stats[1:])) < STAT_RTOL, b
+        ref = [oracle.LR_test(dd, bp, i) for i in vs]
+        assert rel(res[b, 2 * d + np.array(vs)], ref) < STAT_RTOL, b
+
+
 def c5_panel(oracle):
     rng = np.random.default_rng(20261015 + 5)
     y, x, *_ = oracle.factor_model_DGP(2000, 20000, 8, rng)

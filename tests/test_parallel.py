@@ -152,3 +152,24 @@ def test_gloo_world2_windows_sharded(dfm):
         got = res[r][0]
         for f in ("number_of_factors", "V", "criterion_value", "eigenvalues", "coefficients", "t_stats"):
             assert np.array_equal(got[f], ref[f], equal_nan=True), f
+
+
+def test_rolling_window_rows_cover_each_window():
+    """Rolling windows (L rows before each forecast date) shard by row slices:
+    rank's slice [a, b) holds exactly the rows its windows read, and window
+    w0 + j of the full problem is window j of the (b - a, w1 - w0) problem."""
+    from dfm_amd.parallel import window_rows
+    T, P, L = 2000, 200, 700
+    for world in (1, 2, 3, 8):
+        seen = []
+        for rank in range(world):
+            w0, w1, a, b = window_rows(T, P, world, rank, L)
+            Tl, Pl = b - a, w1 - w0
+            for j in range(Pl):
+                g_lo, g_hi = T - P + w0 + j - L, T - P + w0 + j          # full problem's window rows
+                l_lo, l_hi = Tl - Pl + j - L, Tl - Pl + j                 # the slice problem's
+                assert (a + l_lo, a + l_hi) == (g_lo, g_hi)
+                assert 0 <= l_lo and l_hi <= Tl
+                seen.append(w0 + j)
+        assert seen == list(range(P))
+    assert window_rows(T, P, 4, 1, None)[2] == 0                          # expanding: from row 0
