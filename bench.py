@@ -213,6 +213,8 @@ def main():
     ap.add_argument("--replicates", type=int, default=B)
     ap.add_argument("--mode", default="auto", choices=["auto", "direct", "factored"])
     ap.add_argument("--eig-tol", type=float, default=-1.0, help="eigensolver gap tolerance (default 1e-12)")
+    ap.add_argument("--value-tol", type=float, default=-1.0,
+                    help="Kato-Temple eigenvalue tolerance of eigenvalue-only stats (default: the library's)")
     ap.add_argument("--strict", action="store_true",
                     help="eigenvector-residual stopping rule even for eigenvalue-only stats")
     ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
@@ -243,6 +245,8 @@ def main():
         return bench_windows(args, D, ctx, torch, dist, world, rank, dev)
     if args.eig_tol > 0:
         ctx.set_eig_params(tol=args.eig_tol)
+    if args.value_tol > 0:
+        ctx.set_value_tol(args.value_tol)
     if args.strict:
         ctx.set_value_tol(0.0)
     Bn = args.replicates

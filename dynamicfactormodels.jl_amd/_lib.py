@@ -12,7 +12,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdfm.so")
+# DFM_LIB_PATH: load another build of the same library (A/B timing of a
+# variant built by the csrc Makefile's BUILD/LIB/EXTRA; tools/ab_bench.sh)
+LIB_PATH = os.environ.get("DFM_LIB_PATH") or os.path.join(_HERE, "libdfm.so")
 
 c_double_p = C.POINTER(C.c_double)
 c_int32_p = C.POINTER(C.c_int32)

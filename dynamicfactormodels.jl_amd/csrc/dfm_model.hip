@@ -626,8 +626,12 @@ static void launch_factors_km(int orient, const PanelSrc &src, int T, int N, int
   else                                                                                             \
     hipLaunchKernelGGL((factors_cols_kernel<KM, C_, E_, X_>), dim3((T + 3) / 4, nb), dim3(256), 0, \
                        st, src, T, N, k, Uk, F, L, fs);
+  // every PanelSrc form the callers build (as launch_gram): wild / residual
+  // replicates, plain panels, and masked relocated windows (no C; idx, eta)
   if (c && e && x) { DFM_FR(true, true, true) }
   else if (c && !e && x) { DFM_FR(true, false, true) }
+  else if (!c && e && x) { DFM_FR(false, true, true) }
+  else if (!c && !e && x) { DFM_FR(false, false, true) }
   else { DFM_FR(false, false, false) }
 #undef DFM_FR
 }

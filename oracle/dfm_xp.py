@@ -336,3 +336,23 @@ class XPFit:
         b2 = DD(bX.hi[r:].T.copy(), bX.lo[r:].T.copy())      # (N, r)
         W = (b2[:, None, :] @ dd_inv(S22) @ b2[:, :, None])
         return LR, LM, W[:, 0, 0].f64()
+
+
+def lm_referee(F, Ei, bp: int) -> float:
+    """LM_test (src/chowtest.jl:35-42) of one variable in double-double from
+    fp64 inputs F (T x r, the fit's vcat(F_j)) and E_i (the factor residual
+    column): T (|E_i|^2 - |v|^2) / |E_i|^2, v = E_i - D (D'D)^-1 D'E_i,
+    D = [F, F .* d], d_t = 1{t > bp}.  The reference's fp64 form
+    T (1 - |v|^2/|E_i|^2) loses ~eps / R^2 relative when the uncentred R^2 is
+    small; here the difference is formed exactly (inputs perturbed at eps
+    move the value by ~eps / sqrt(R^2) relative)."""
+    F = np.asarray(F, dtype=np.float64)
+    T, r = F.shape
+    d = np.r_[np.zeros(bp), np.ones(T - bp)][:, None]
+    D = DD(np.hstack([F, F * d]))
+    E = DD(np.asarray(Ei, dtype=np.float64)[:, None])
+    b = dd_inv(D.T @ D) @ (D.T @ E)
+    v = E - D @ b
+    ee = (E * E).sum()
+    vv = (v * v).sum()
+    return float((((ee - vv) / ee) * float(T)).f64())

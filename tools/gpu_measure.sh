@@ -29,7 +29,9 @@ step trace_c2 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c2" -o 
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffic.json"
-# last: rocprofv3 writes this trace's CSVs and then segfaults in its own exit
-# path after the cooperative lasso launch (exit 139, results complete)
+# C2's Chow / Gram / eigen kernels (the bench passes above never launch them)
+step pmc_fetch_c2 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "chow|gram_wk|gemmh|eig_|factors" -f csv -d "$OUT/pmc_fetch_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 1
+step pmc_write_c2 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "chow|gram_wk|gemmh|eig_|factors" -f csv -d "$OUT/pmc_write_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 1
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch_c2" "$OUT/pmc_write_c2" > "$OUT/pmc_traffic_c2.json"
 step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
 echo ALLDONE

@@ -13,8 +13,6 @@ step() {   # name, timeout, command...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 "$OUT/$name.err"; exit $rc; fi
   return 0
 }
-step bigT 150 python -u tools/windows_bigT_probe.py 4200
-cat "$OUT/bigT.out"
 step pytest 1500 python -u -m pytest tests -m gpu -v -rf --maxfail=200 --timeout 300 --timeout-method thread -p no:cacheprovider -k "not beyond_factored"
 grep -E "FAILED|passed|failed" "$OUT/pytest.out" | tail -40
 step iters 200 python -u tools/c3_iters.py 2000
@@ -23,4 +21,8 @@ step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o 
 cat "$OUT/trace_c4.out"
 step bench 300 python -u bench.py --steps 10 --warmup 3 --cpu-seconds 5
 cat "$OUT/bench.out"
+step bigT_pca 100 python -u tools/windows_bigT_probe.py pca 4200
+cat "$OUT/bigT_pca.out"
+step bigT_win 100 python -u tools/windows_bigT_probe.py windows 4200
+cat "$OUT/bigT_win.out"
 echo ALLDONE
