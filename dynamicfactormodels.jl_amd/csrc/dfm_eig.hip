@@ -117,13 +117,16 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
     } else
     for (int j0 = 0; j0 < k; j0 += 64) {
       // lanes: j = j0 + lane / G, r = lane % G   with G = power of two >= nrb
+      // (capped at 64: past 64 row blocks — m > 4096 — lane r also sums
+      // blocks r + 64, r + 128, ... in order before the shuffle tree)
       int G = 1;
-      while (G < nrb) G <<= 1;
+      while (G < nrb && G < 64) G <<= 1;
       const int per = 64 / G;   // residual columns handled per pass
       for (int jj = 0; jj < 64 && j0 + jj < k; jj += per) {
         const int j = j0 + jj + lane / G, r = lane % G;
         double v = 0.0;
-        if (j < k && r < nrb) v = w.rpart[((int64_t)rep * nrb + r) * P + j];
+        if (j < k)
+          for (int rr = r; rr < nrb; rr += G) v += w.rpart[((int64_t)rep * nrb + rr) * P + j];
         for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
         // lanes with r == 0 hold the column sums
         bool okj = true;
