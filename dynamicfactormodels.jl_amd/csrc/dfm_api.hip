@@ -19,7 +19,7 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
             const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
-            timer_fn tf, void *tctx, int64_t rep0);
+            timer_fn tf, void *tctx, int64_t rep0, int subspace = 0);
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 const int *eig_iters_ptr(char *ws, int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
@@ -98,7 +98,7 @@ struct FactBase {
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr);
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr, int subspace = 0);
 size_t fact_workspace_bytes(int T, int nb, int P);
 int fact_t_max();
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
@@ -1013,6 +1013,21 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
                                   stats[i].kind == DFM_STAT_EIGVAL || stats[i].kind == DFM_STAT_TRACE ||
                                   stats[i].kind == DFM_STAT_ITERS);
   const double etol = (values_only && ctx->tol_values > 0) ? -ctx->tol_values : ctx->tol;
+  // Statistics invariant to rotations within span(F_r) — the Chow tests
+  // (src/chowtest.jl reads F only through projections on it), V, criteria,
+  // eigenvalues, and the w-columns' coefficients / t-statistics (the factor
+  // block of the design spans the same space) — need the wanted SUBSPACE, not
+  // each eigenvector: the strict rule then measures every wanted residual
+  // against the gap to the first unwanted Ritz value (EigWork::subspace).
+  // Factor-column coefficients / t-statistics keep the per-vector gap.
+  bool subspace_only = ns > 0;
+  for (int i = 0; i < ns; ++i) {
+    const int kd = stats[i].kind;
+    subspace_only = subspace_only && (kd == DFM_STAT_V || kd == DFM_STAT_CRIT || kd == DFM_STAT_EIGVAL ||
+                                      kd == DFM_STAT_TRACE || kd == DFM_STAT_ITERS || chow_stat(kd) ||
+                                      ((kd == DFM_STAT_COEF || kd == DFM_STAT_TSTAT) && stats[i].arg0 < q));
+  }
+  const int esub = (subspace_only && !values_only) ? 1 : 0;
   const int p = eig_block_p(m, r, ctx->block);
   // r beyond the subspace eigensolver's block: dense batched eigenpairs,
   // materialised replicate panels for the factor GEMMs, GEMM-built OLS
@@ -1115,7 +1130,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
     if (!wide) {
       const int pj = eig_block_p(mm, r, ctx->block);
       int rc = eig_run(G, mm, (int64_t)mm * mm, mm, n, r, pj, warm, r, etol, ctx->maxit, ctx->poll, w.eig, lam, Uk,
-                       tr, w.status, nullptr, st, timer_cb, ctx, b0);
+                       tr, w.status, nullptr, st, timer_cb, ctx, b0, esub);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       return 0;
@@ -1152,7 +1167,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst,
-                                ctx->cnt_dev);
+                                ctx->cnt_dev, esub);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);

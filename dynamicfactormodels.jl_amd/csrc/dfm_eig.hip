@@ -34,6 +34,11 @@ struct EigWork {
   int *done, *iters, *active;
   double *trace;           // nb
   long long *dbg;          // phase stamps of replicate 0 (SMALL_STAMP) when a diagnostic build points it at a buffer; null
+  // strict rule's gap: 0 = distance to the neighbouring Ritz values (every
+  // wanted eigenVECTOR converged); 1 = distance to the first unwanted Ritz
+  // value theta_k (the wanted SUBSPACE converged: for statistics invariant to
+  // rotations within span(F_r) — Chow tests, V, criteria, eigenvalues)
+  int subspace;
 };
 #define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
@@ -133,8 +138,12 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
         if (j < k && r == 0) {
           const double res = sqrt(v);
           double gap = INFINITY;
-          if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
-          if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+          if (w.subspace) {
+            if (k < p) gap = fabs(th[j] - th[k]);
+          } else {
+            if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+            if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+          }
           const bool stagn = it > 2 && res <= 1e-11 * th0 && res > 0.5 * prev[j];
           okj = (res <= tol * gap || res <= 2e-14 * th0 || stagn);
           if (rb == 0) next[j] = res;
@@ -763,6 +772,7 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   w.iters = (int *)take((size_t)nb * 4);
   w.active = (int *)take((size_t)(maxit + 2) * 4);
   w.dbg = nullptr;
+  w.subspace = 0;
   return w;
 }
 
@@ -819,9 +829,10 @@ template <int P>
 static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                      double *lam, double *Uk, double *trace_out, int *status, int *iters_host,
-                     hipStream_t st, timer_fn tf, void *tctx, int64_t rep0) {
+                     hipStream_t st, timer_fn tf, void *tctx, int64_t rep0, int subspace) {
   const int nrb = (m + EROWS - 1) / EROWS;
   EigWork w = carve(ws, m, nb, P, maxit);
+  w.subspace = subspace;
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
@@ -888,13 +899,13 @@ int eig_block_p(int m, int k, int req) {
 int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
             const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
-            timer_fn tf, void *tctx, int64_t rep0) {
+            timer_fn tf, void *tctx, int64_t rep0, int subspace) {
   if (p < k || p > 32 || p > m) return -1;
   if (p <= 16)
     return eig_run_t<16>(G, ldg, strideG, m, nb, k, p, warm, kw, tol, maxit, poll, ws, lam, Uk,
-                         trace_out, status, iters_host, st, tf, tctx, rep0);
+                         trace_out, status, iters_host, st, tf, tctx, rep0, subspace);
   return eig_run_t<32>(G, ldg, strideG, m, nb, k, p, warm, kw, tol, maxit, poll, ws, lam, Uk,
-                       trace_out, status, iters_host, st, tf, tctx, rep0);
+                       trace_out, status, iters_host, st, tf, tctx, rep0, subspace);
 }
 
 
@@ -1013,7 +1024,7 @@ constexpr int F2_T_MAX = 4096;   // dynamic LDS of ap2: 16 T + 4 bytes
 // one whole wave (same rules as check_converged: strict eigenvector-residual
 // test, or for tol < 0 the Kato-Temple eigenvalue bound).
 DFM_DEV bool decide_converged(const double *res2, const double *th, const double *prev, double *next,
-                              int k, int p, double tol, double trace, int itc) {
+                              int k, int p, double tol, double trace, int itc, int subspace) {
   const int lane = threadIdx.x & 63;
   const double th0 = fabs(th[0]);
   bool okall = true, floor_ok = true;
@@ -1021,8 +1032,12 @@ DFM_DEV bool decide_converged(const double *res2, const double *th, const double
   for (int j = lane; j < k; j += 64) {
     const double rs = res2[j], res = sqrt(rs);
     double gap = INFINITY;
-    if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
-    if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+    if (subspace && tol >= 0.0) {   // strict rule, subspace form (EigWork::subspace)
+      if (k < p) gap = fabs(th[j] - th[k]);
+    } else {
+      if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
+      if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
+    }
     bool okj;
     if (tol < 0.0) {
       const double bnd = rs / (0.5 * gap);
@@ -1496,7 +1511,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
       const int itc = it + 1;
       const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
       double *next = small + 2 * P * P + 2 * P + (itc & 1) * P;
-      conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc) ? 1 : 0;
+      conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc, w.subspace) ? 1 : 0;
     }
     if (lane == 0) {
       s_conv = conv;
@@ -1677,9 +1692,11 @@ template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                            char *fws, double *lam, double *Uk, double *trace_out, int *status,
-                           hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst, long long *cnt) {
+                           hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst, long long *cnt,
+                           int subspace) {
   const int m = fb.T;
   EigWork w = carve(ws, m, nb, P, maxit);
+  w.subspace = subspace;
   const int64_t ldz = (int64_t)nb * P;
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)z_rows(m) * ldz;
@@ -1791,14 +1808,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt) {
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt, int subspace) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
   if (fb.r > 16 || fb.T > F2_T_MAX) return -1;   // callers take the direct path
   if (p <= 16)
     return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                               trace_out, status, st, tf, tctx, off, lst, cnt);
+                               trace_out, status, st, tf, tctx, off, lst, cnt, subspace);
   return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                             trace_out, status, st, tf, tctx, off, lst, cnt);
+                             trace_out, status, st, tf, tctx, off, lst, cnt, subspace);
 }
 int fact_t_max() { return F2_T_MAX; }
 
