@@ -7,13 +7,15 @@
 //   A1 = F1'F1, A2 = F2'F2, D'D = M = [[A1+A2, A2], [A2, A2]]      (shared)
 //   per variable i (one thread): g_j = F_j' x_i^(j), two passes over x_i
 //   LR  = T (ln ||E_i||^2 - ln(SSR_1 + SSR_2)), SSR_j of x_i on F_j     (:19-23)
-//   LM  = T c' [M^-1]_22 c / ||E_i||^2 with D'E_i = [0; c], c = g2 - A2 l_i
-//         (F'E_i = 0 for PCA loadings): the uncentred R^2 of :35-42
+//   LM  = T (D'E_i)' M^-1 (D'E_i) / ||E_i||^2, D'E_i = [F'E_i; c],
+//         c = g2 - A2 l_i: the uncentred R^2 of :35-42.  F'E_i = 0 only for
+//         exact eigenvectors; the eigensolver leaves a residual, so the
+//         first block is kept (cf = g1 + g2 - (A1 + A2) l_i)
 //   ||E_i||^2 and the subperiod SSRs are summed explicitly (no cancellation)
 //   A model fitted with break_indices (src/DynamicFactorModel.jl:73, :98)
 //   has one loadings matrix per break block: E_i = x_i - F_t l_i^(block(t)),
-//   and F = vcat(F_j) (defect D1).  F_j'E_ij = 0 still holds block by block,
-//   so D'E_i = [0; c] with c = sum_{t >= bp} f_t e_ti, summed explicitly.
+//   and F = vcat(F_j) (defect D1): D'E_i = [sum_t f_t e_ti; sum_{t >= bp}
+//   f_t e_ti], both summed explicitly.
 //   Wald: beta = M^-1 [g1+g2; g2]; HC0 meat; with W = M^-1[:, r:] = [Wa; Wb]
 //         Cov22 = sum_t u_t^2 z_t z_t',  z_t = Wa'f_t (t < bp), (Wa+Wb)'f_t
 //         (t >= bp) — one r x r accumulator per variable instead of the
@@ -189,11 +191,27 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
       sI[q][rr] = t < T ? (HAS_IDX ? src.idx[ro + t] : t) : 0;
     }
   };
-  auto xval = [&](int rr, int t) {
-    double x = src.E[(int64_t)sI[lr][rr] * src.ld + i];
-    if (HAS_ETA) x *= sE[lr][rr];
-    if (HAS_C) x += src.C[(int64_t)t * src.ld + i];
-    return x;
+  // CU rows' gathered values x = C + eta E[idx]: the staged row indices
+  // first, then every row's loads, then the arithmetic — all 2 CU loads in
+  // flight together (computing each row's x as its loads arrive made the
+  // compiler wait for every row's loads before the next row's issued)
+  auto load_rows = [&](int t0, int rb, int tn, double *xs) {
+    int ri[CU];
+    double ee[CU], cc[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) ri[u] = sI[lr][min(rb + u, tn - 1)];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      ee[u] = src.E[(int64_t)ri[u] * src.ld + i];
+      if (HAS_C) cc[u] = src.C[(int64_t)(t0 + min(rb + u, tn - 1)) * src.ld + i];
+    }
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      double x = ee[u];
+      if (HAS_ETA) x *= sE[lr][min(rb + u, tn - 1)];
+      if (HAS_C) x += cc[u];
+      xs[u] = x;
+    }
   };
   // loadings of variable i (src/chowtest.jl uses dfm.factor_residuals = x - F L')
   // (break models: block b's loadings for rows a[b] .. a[b+1]-1)
@@ -205,9 +223,9 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
   load_l(0);
   int cb = 0, next = BRK ? blk.a[1] : T;
   // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2 (BRK: cx = sum_{t>=bp} f_t e_t)
-  double g1[R], g2[R], cx[R], e2 = 0.0;
+  double g1[R], g2[R], cx[R], cf[R], e2 = 0.0;
 #pragma unroll
-  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; cx[j] = 0.0; }
+  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; cx[j] = 0.0; cf[j] = 0.0; }
   for (int t0 = 0; t0 < T; t0 += TR) {
     __syncthreads();
     stage(t0);
@@ -219,8 +237,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
     // the arithmetic and its order are unchanged
     for (int rb = 0; rb < tn; rb += CU) {
     double xs[CU];
-#pragma unroll
-    for (int u = 0; u < CU; ++u) { const int rq = min(rb + u, tn - 1); xs[u] = xval(rq, t0 + rq); }
+    load_rows(t0, rb, tn, xs);
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       const int rr = rb + u;
@@ -232,6 +249,10 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
 #pragma unroll
       for (int j = 0; j < R; ++j) ev -= sF[lr][rr * R + j] * l[j];
       e2 = fma(ev, ev, e2);
+      if (BRK) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) cf[j] = fma(ev, sF[lr][rr * R + j], cf[j]);
+      }
       if (BRK && t >= bp) {
 #pragma unroll
         for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[lr][rr * R + j], cx[j]);
@@ -247,28 +268,38 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
     }
   }
   // subperiod OLS coefficients gamma_j = A_j^-1 g_j, Wald beta = M^-1 [g1+g2; g2],
-  // LM vector c = g2 - A2 l  (D'E_i = [0; c] for the PCA loadings)
+  // LM vector D'E_i = [F'E_i; F2'E_i] = [cf; c]: c = g2 - A2 l, cf = g1 + g2 -
+  // (A1 + A2) l (break models: both summed explicitly in pass A).  F'E_i
+  // vanishes only to the eigensolver's residual, so it is kept, not assumed 0
   double ga1[R], ga2[R], b1[R], b2[R], cv[R];
 #pragma unroll
   for (int a = 0; a < R; ++a) {
-    double u1 = 0.0, u2 = 0.0, v1 = 0.0, v2 = 0.0, c = g2[a];
+    double u1 = 0.0, u2 = 0.0, v1 = 0.0, v2 = 0.0, c = g2[a], cs = g1[a] + g2[a];
 #pragma unroll
     for (int c2 = 0; c2 < R; ++c2) {
       u1 = fma(P.A1i[a * RR + c2], g1[c2], u1);
       u2 = fma(P.A2i[a * RR + c2], g2[c2], u2);
       v1 = fma(P.Va[c2 * RR + a], g1[c2], fma(P.Vc[c2 * RR + a], g2[c2], v1));
       v2 = fma(P.Wa[c2 * RR + a], g1[c2], fma(P.Wc[c2 * RR + a], g2[c2], v2));
-      if (!BRK) c -= P.A2[a * RR + c2] * l[c2];
+      if (!BRK) { c -= P.A2[a * RR + c2] * l[c2]; cs -= P.ApS[a * RR + c2] * l[c2]; }
     }
     ga1[a] = u1; ga2[a] = u2; b1[a] = v1; b2[a] = v2; cv[a] = BRK ? cx[a] : c;
+    if (!BRK) cf[a] = cs;
+#ifdef DFM_AB_NO_CF
+    cf[a] = 0.0;
+#endif
   }
+  // lmq = [cf; c]' M^-1 [cf; c]; M^-1 = [[Va, Wa], [Wa', Wb]] (r x r blocks)
   double lmq = 0.0;
 #pragma unroll
   for (int a = 0; a < R; ++a) {
-    double s = 0.0;
+    double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-    for (int c2 = 0; c2 < R; ++c2) s = fma(P.Wb[a * RR + c2], cv[c2], s);
-    lmq = fma(cv[a], s, lmq);
+    for (int c2 = 0; c2 < R; ++c2) {
+      s1 = fma(P.Va[a * RR + c2], cf[c2], fma(P.Wa[a * RR + c2], cv[c2], s1));
+      s2 = fma(P.Wa[c2 * RR + a], cf[c2], fma(P.Wb[a * RR + c2], cv[c2], s2));
+    }
+    lmq = fma(cf[a], s1, fma(cv[a], s2, lmq));
   }
   // ---- pass B: subperiod SSRs and the HC0 block sum_t u_t^2 z_t z_t'
   double S[R * (R + 1) / 2], ssr = 0.0;
@@ -282,8 +313,7 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
     const int tn = min(TR, T - t0);
     for (int rb = 0; rb < tn; rb += CU) {
     double xs[CU];
-#pragma unroll
-    for (int uq = 0; uq < CU; ++uq) { const int rq = min(rb + uq, tn - 1); xs[uq] = xval(rq, t0 + rq); }
+    load_rows(t0, rb, tn, xs);
 #pragma unroll
     for (int uq = 0; uq < CU; ++uq) {
       const int rr = rb + uq;
@@ -344,230 +374,11 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
   WD[o] = wv;
 }
 
-// Row-split form (R <= 8, N >= 64): 64 (replicate, variable) pairs per
-// 256-thread block in replicate-major order (a block spans at most two
-// replicates), each pair's rows shared by the block's 4 waves — wave q takes
-// rows t = q (mod 4) of every staged 64-row tile — so a C2-sized job runs 4x
-// the waves of the one-thread-per-pair form (which left ~2 waves per SIMD
-// latency-bound on its 600-row dependent chains).  Each pass's per-wave
-// partial sums are combined in a fixed wave order (0 + 1 + 2 + 3) through LDS;
-// the per-pair arithmetic is the same, only the row sums are associated in
-// four interleaved chains.  Results do not depend on the batch or the block.
-constexpr int CS_PAIRS = 64;
-template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK>
-__global__ __launch_bounds__(256) void chow_split_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
-                                                         int nb, const double *__restrict__ F,
-                                                         const double *__restrict__ Z,
-                                                         const ChowPrep *__restrict__ prep,
-                                                         const double *__restrict__ Lm, double *__restrict__ LR,
-                                                         double *__restrict__ LM, double *__restrict__ WD) {
-  constexpr int TR = 64, RR = CH_RMAX, NR = 2, NS = R * (R + 1) / 2;
-  constexpr int NA = 3 * R + 1, NRED = NA > NS + 1 ? NA : NS + 1;
-  __shared__ double sF[NR][TR * R], sZ[NR][TR * R], sE[NR][TR];
-  __shared__ int sI[NR][TR];
-  __shared__ double red[CS_PAIRS * NRED];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t g0 = (int64_t)blockIdx.x * CS_PAIRS, g = g0 + lane;
-  const int rep = (int)(g / N), i = (int)(g % N), rep0 = (int)(g0 / N);
-  const int nrw = min(nb - 1, (int)((g0 + CS_PAIRS - 1) / N)) - rep0 + 1;
-  const bool ok = rep < nb;
-  const int lr = ok ? rep - rep0 : 0;
-  const ChowPrep &P = prep[ok ? rep : rep0];
-  auto stage = [&](int t0) {
-    for (int e = tid; e < nrw * TR * R; e += 256) {
-      const int q = e / (TR * R), f = e % (TR * R), rr = f / R, j = f % R, t = t0 + rr;
-      const int64_t base = (int64_t)(rep0 + q) * T * r;
-      sF[q][f] = (t < T && j < r) ? F[base + (int64_t)t * r + j] : 0.0;
-      sZ[q][f] = (t < T && j < r) ? Z[base + (int64_t)t * r + j] : 0.0;
-    }
-    for (int e = tid; e < nrw * TR; e += 256) {
-      const int q = e / TR, rr = e % TR, t = t0 + rr;
-      const int64_t ro = (int64_t)(rep0 + q) * src.rs;
-      sE[q][rr] = (HAS_ETA && t < T) ? src.eta[ro + t] : 1.0;
-      sI[q][rr] = t < T ? (HAS_IDX ? src.idx[ro + t] : t) : 0;
-    }
-  };
-  auto xval = [&](int rr, int t) {
-    double x = src.E[(int64_t)sI[lr][rr] * src.ld + i];
-    if (HAS_ETA) x *= sE[lr][rr];
-    if (HAS_C) x += src.C[(int64_t)t * src.ld + i];
-    return x;
-  };
-  // fixed-order combine of the four waves' partials v[0..n) -> red (then read by all)
-  auto combine = [&](const double *v, int n) {
-    for (int wv = 0; wv < 4; ++wv) {
-      if (wave == wv)
-        for (int e = 0; e < n; ++e) red[e * CS_PAIRS + lane] = (wv ? red[e * CS_PAIRS + lane] : 0.0) + v[e];
-      __syncthreads();
-    }
-  };
-  double l[R];
-  auto load_l = [&](int b) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) l[j] = (ok && j < r) ? Lm[b * blk.lbs + ((int64_t)rep * N + i) * r + j] : 0.0;
-  };
-  load_l(0);
-  int cb = 0, next = BRK ? blk.a[1] : T;
-  // ---- pass A (this wave's rows): g_j = F_j' x^(j), e2 = ||x - F l||^2, BRK: cx
-  double pa[NA];
-#pragma unroll
-  for (int e = 0; e < NA; ++e) pa[e] = 0.0;
-  double *g1 = pa, *g2 = pa + R, *cx = pa + 2 * R, &e2 = pa[3 * R];
-  for (int t0 = 0; t0 < T; t0 += TR) {
-    __syncthreads();
-    stage(t0);
-    __syncthreads();
-    const int tn = min(TR, T - t0);
-    double xs[TR / 4];
-#pragma unroll
-    for (int u = 0; u < TR / 4; ++u) { const int rq = min(wave + 4 * u, tn - 1); xs[u] = ok ? xval(rq, t0 + rq) : 0.0; }
-#pragma unroll
-    for (int u = 0; u < TR / 4; ++u) {
-      const int rr = wave + 4 * u;
-      if (rr >= tn || !ok) break;
-      const int t = t0 + rr;
-      if (BRK) while (t >= next) { ++cb; next = blk.a[cb + 1]; load_l(cb); }
-      const double x = xs[u];
-      double ev = x;
-#pragma unroll
-      for (int j = 0; j < R; ++j) ev -= sF[lr][rr * R + j] * l[j];
-      e2 = fma(ev, ev, e2);
-      if (BRK && t >= bp) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[lr][rr * R + j], cx[j]);
-      }
-      if (t < bp) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) g1[j] = fma(x, sF[lr][rr * R + j], g1[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[lr][rr * R + j], g2[j]);
-      }
-    }
-  }
-  combine(pa, NA);
-#pragma unroll
-  for (int e = 0; e < NA; ++e) pa[e] = red[e * CS_PAIRS + lane];
-  __syncthreads();
-  if (!BRK) load_l(0);
-  double ga1[R], ga2[R], b1[R], b2[R], cv[R];
-#pragma unroll
-  for (int a = 0; a < R; ++a) {
-    double u1 = 0.0, u2 = 0.0, v1 = 0.0, v2 = 0.0, c = g2[a];
-#pragma unroll
-    for (int c2 = 0; c2 < R; ++c2) {
-      u1 = fma(P.A1i[a * RR + c2], g1[c2], u1);
-      u2 = fma(P.A2i[a * RR + c2], g2[c2], u2);
-      v1 = fma(P.Va[c2 * RR + a], g1[c2], fma(P.Vc[c2 * RR + a], g2[c2], v1));
-      v2 = fma(P.Wa[c2 * RR + a], g1[c2], fma(P.Wc[c2 * RR + a], g2[c2], v2));
-      if (!BRK) c -= P.A2[a * RR + c2] * l[c2];
-    }
-    ga1[a] = u1; ga2[a] = u2; b1[a] = v1; b2[a] = v2; cv[a] = BRK ? cx[a] : c;
-  }
-  double lmq = 0.0;
-#pragma unroll
-  for (int a = 0; a < R; ++a) {
-    double s = 0.0;
-#pragma unroll
-    for (int c2 = 0; c2 < R; ++c2) s = fma(P.Wb[a * RR + c2], cv[c2], s);
-    lmq = fma(cv[a], s, lmq);
-  }
-  // ---- pass B (this wave's rows): subperiod SSRs, HC0 block sum_t u_t^2 z_t z_t'
-  double pb[NS + 1];
-#pragma unroll
-  for (int e = 0; e <= NS; ++e) pb[e] = 0.0;
-  double *S = pb, &ssr = pb[NS];
-  for (int t0 = 0; t0 < T; t0 += TR) {
-    __syncthreads();
-    stage(t0);
-    __syncthreads();
-    const int tn = min(TR, T - t0);
-    double xs[TR / 4];
-#pragma unroll
-    for (int u = 0; u < TR / 4; ++u) { const int rq = min(wave + 4 * u, tn - 1); xs[u] = ok ? xval(rq, t0 + rq) : 0.0; }
-#pragma unroll
-    for (int u = 0; u < TR / 4; ++u) {
-      const int rr = wave + 4 * u;
-      if (rr >= tn || !ok) break;
-      const int t = t0 + rr;
-      const double x = xs[u];
-      const bool post = t >= bp;
-      double uu = x, rs = x;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const double f = sF[lr][rr * R + j];
-        uu -= f * (post ? b1[j] + b2[j] : b1[j]);
-        rs -= f * (post ? ga2[j] : ga1[j]);
-      }
-      ssr = fma(rs, rs, ssr);
-      const double u2 = uu * uu;
-      double zs[R];
-#pragma unroll
-      for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[lr][rr * R + j];
-      int e = 0;
-#pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
-    }
-  }
-  combine(pb, NS + 1);
-  if (wave != 0 || !ok) return;
-#pragma unroll
-  for (int e = 0; e <= NS; ++e) pb[e] = red[e * CS_PAIRS + lane];
-  // Wald = b2' S^-1 b2 via in-register Cholesky of S (as chow_all_kernel)
-  double wv = 0.0;
-  {
-    double Lc[NS];
-    int e = 0;
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int c2 = 0; c2 <= a; ++c2) {
-        double s = (a < r && c2 < r) ? S[e] : (a == c2 ? 1.0 : 0.0);
-#pragma unroll
-        for (int p = 0; p < c2; ++p) s -= Lc[a * (a + 1) / 2 + p] * Lc[c2 * (c2 + 1) / 2 + p];
-        Lc[e] = (a == c2) ? sqrt(s) : s / Lc[c2 * (c2 + 1) / 2 + c2];
-        ++e;
-      }
-    double yv[R];
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-      double s = (a < r) ? b2[a] : 0.0;
-#pragma unroll
-      for (int p = 0; p < a; ++p) s -= Lc[a * (a + 1) / 2 + p] * yv[p];
-      yv[a] = s / Lc[a * (a + 1) / 2 + a];
-      wv = fma(yv[a], yv[a], wv);
-    }
-  }
-  const int64_t o = (int64_t)rep * N + i;
-  LR[o] = T * (log(e2) - log(ssr));
-  LM[o] = T * lmq / e2;
-  WD[o] = wv;
-}
-
 template <int R>
 static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int N, int r, int bp, int nb,
                           const double *F, const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
                           double *LM, double *WD, hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
-  if (R <= 8 && N >= CS_PAIRS) {   // row-split form (chow_split_kernel)
-    const dim3 sgrid((unsigned)(((int64_t)nb * N + CS_PAIRS - 1) / CS_PAIRS)), sblock(256);
-#define DFM_CS(C_, E_, X_, B_)                                                                                 \
-  hipLaunchKernelGGL((chow_split_kernel<(R <= 8 ? R : 8), C_, E_, X_, B_>), sgrid, sblock, 0, st, src, blk, T, N, r, \
-                     bp, nb, F, Z, prep, Lm, LR, LM, WD)
-    if (blk.n > 1) {
-      if (c && e && x) DFM_CS(true, true, true, true);
-      else if (c && !e && x) DFM_CS(true, false, true, true);
-      else DFM_CS(false, false, false, true);
-    } else {
-      if (c && e && x) DFM_CS(true, true, true, false);
-      else if (c && !e && x) DFM_CS(true, false, true, false);
-      else DFM_CS(false, false, false, false);
-    }
-#undef DFM_CS
-    return;
-  }
   const bool flat = R <= 8 && N >= CH_FLAT_MIN_N;
   // non-flat: narrow panels get a block of round_up(N, 64) threads, not a half-idle 256
   const int nth = flat ? 256 : std::min(256, (N + 63) / 64 * 64);

@@ -848,6 +848,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   bool finished = false;
   std::vector<int> act;
   const int cheb = 1;   // degree-2 Chebyshev filter between Rayleigh-Ritz steps
+  int next_poll = poll;
   for (; it <= maxit; ++it) {
     const int check_only = (it == maxit);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
@@ -862,12 +863,15 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0, cheb);
     if (cheb) hipLaunchKernelGGL(eig_cheb_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, p);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
-    if (it > 0 && (it % poll) == 0) {
+    if (it == next_poll) {
       int a = -1;
       hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
       hipError_t e = hipStreamSynchronize(st);
       if (e != hipSuccess) return 1000 + (int)e;
       if (a == 0) { finished = true; break; }
+      // a straggler tail (< 1/8 of the batch active): poll every step, so the
+      // empty iterations after its last replicate retires are not launched
+      next_poll = it + ((int64_t)a * 8 < nb ? 1 : poll);
     }
   }
   (void)finished;

@@ -331,11 +331,7 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
       if (clist) {
         if (row < M && col < ccount * col_group) C[(int64_t)row * ldc + g2_phys_col(col, clist, ccount, col_group)] = v;
       } else if (row < M && col < Nc) {
-#ifdef DFM_AB_HZ_NT
-        __builtin_nontemporal_store(v, &C[(int64_t)row * ldc + col]);
-#else
         C[(int64_t)row * ldc + col] = v;
-#endif
       }
     }
 }
