@@ -151,7 +151,7 @@ def test_break_chow_all_matches_oracle(dfm, oracle, T, N, r, breaks):
         ref = np.array([[oracle.LR_test(o, bp, i), oracle.LM_test(o, bp, i), oracle.Wald_test(o, bp, i)]
                         for i in range(nv)])
         assert rel(LR[:nv], ref[:, 0]) < STAT_RTOL, bp
-        lm_within(LM[:nv], o, bp, range(nv), oracle)
+        lm_within(LM[:nv], o, bp, range(nv), oracle, gm=g)
         assert rel(W[:nv], ref[:, 2]) < STAT_RTOL, bp
         assert dfm.LM_test(g, bp, 3) == LM[2]
 

