@@ -9,6 +9,9 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -162,6 +165,50 @@ struct dfm_ctx {
   size_t warena_cap = 0, warena_need = 0;
 };
 
+// The host thread of a model's second bootstrap lane (bootstrap_lanes):
+// persistent, so a call costs a hand-off, not a thread start.
+struct LaneWorker {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool has = false, done = false, quit = false;
+  std::thread th;   // last: starts after the members it uses
+  LaneWorker() : th([this] { loop(); }) {}
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return has || quit; });
+      if (quit) return;
+      std::function<void()> j = std::move(job);
+      has = false;
+      lk.unlock();
+      j();
+      lk.lock();
+      done = true;
+      cv.notify_all();
+    }
+  }
+  void run(std::function<void()> j) {
+    std::lock_guard<std::mutex> g(mu);
+    job = std::move(j);
+    has = true;
+    done = false;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+  }
+  ~LaneWorker() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      quit = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+};
+
 struct dfm_model {
   dfm_ctx *ctx = nullptr;
   int T = 0, N = 0, q = 0, r = 0, crit = -1, kmax = 0, m = 0, orient = 0, k_eig = 0;
@@ -197,6 +244,12 @@ struct dfm_model {
   // dfm_chow: the all-variables statistics of the last break period asked for
   int64_t chow_bp = -1;
   std::vector<double> chow_cache;   // LR (N), LM (N), Wald (N)
+  // second lane of small factored bootstrap jobs (dfm_bootstrap_dev): a clone
+  // of this fit on its own context / stream of the same device, made on first use
+  dfm_model *lane = nullptr;
+  LaneWorker *lane_worker = nullptr;
+  bool is_lane = false;
+  dfm_ctx *count_ctx = nullptr;   // a lane counts its GEMM products into its parent's context
 };
 
 static int fail(dfm_ctx *ctx, int code, const char *fmt, ...) {
@@ -485,6 +538,14 @@ extern "C" {
 
 int dfm_model_destroy(dfm_model *m) {
   if (!m) return -1;
+  delete m->lane_worker;
+  m->lane_worker = nullptr;
+  if (m->lane) {   // the lane model, then its context (the model held the last reference but one)
+    dfm_ctx *lc = m->lane->ctx;
+    dfm_model_destroy(m->lane);
+    dfm_ctx_destroy(lc);
+    m->lane = nullptr;
+  }
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
   for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->Lall, m->Ub, m->colssr, m->H, m->EL, m->S,
@@ -966,8 +1027,101 @@ __global__ void or_status_kernel(const int *s1, const int *s2, int nb, int *flag
   }
 }
 
+static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+                         const dfm_stat *stats, int ns, double *out);
+
+// Small jobs (a rank's shard of a multi-GPU bootstrap: C3 at 8 GPUs is 1 250
+// replicates per device; C2's 999) leave the chip part-idle: the
+// per-replicate passes (y2, Rayleigh-Ritz, ap2, Chebyshev, Chow: one
+// workgroup or one wave per replicate) run ~1 round of the resident slots or
+// less, and every launch gap and convergence poll is exposed.  Such jobs run
+// as two lanes — the halves of the replicate range on two streams, each
+// driven by its own host thread — so one lane's latency-bound passes overlap
+// the other's GEMMs (measured at C3 with two Python-driven contexts: 1 250
+// replicates 4.12 -> 3.76 ms, 2 500: 6.96 -> 6.55 ms; 9 999 gains < 2 % and
+// stays one lane, keeping its kernels' timings solo).  Every kernel is
+// batch-invariant (a replicate's result never depends on its batch), so the
+// rows are bit-identical to one lane (tests/test_gpu_multi.py).
+constexpr int64_t kLaneMin = 512, kLaneMax = 6000;
+static bool lane_split(const dfm_model *M, int64_t B, const dfm_stat *stats, int ns) {
+  if (M->is_lane || M->batch != 0 || B < kLaneMin || B > kLaneMax || ns < 0 || (ns > 0 && !stats)) return false;
+  const int p = eig_block_p(M->m, M->r, M->ctx->block);
+  if (p > 32 || p < M->r) return false;
+  for (int i = 0; i < ns; ++i)
+    if (stats[i].kind < 0 || stats[i].kind > DFM_STAT_ITERS) return false;
+  return M->r <= 16;   // the subspace solver's paths (not the dense / GEMM-built wide ones)
+}
+
+static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+                           const dfm_stat *stats, int ns, double *out) {
+  dfm_ctx *ctx = M->ctx;
+  hipSetDevice(ctx->device);
+  if (!M->lane) {
+    dfm_ctx *lc = nullptr;
+    int rc = dfm_ctx_create(ctx->device, &lc);
+    if (rc) return fail(ctx, 1002, "bootstrap lane: no context (%d)", rc);
+    dfm_model *L = nullptr;
+    rc = dfm_model_clone(M, lc, &L);
+    if (rc) {
+      const std::string e = lc->err;
+      dfm_ctx_destroy(lc);
+      return fail(ctx, rc, "bootstrap lane: %s", e.c_str());
+    }
+    L->is_lane = true;
+    L->count_ctx = ctx;
+    M->lane = L;
+    M->lane_worker = new LaneWorker();
+  }
+  dfm_model *L = M->lane;
+  dfm_ctx *lc = L->ctx;
+  lc->tol = ctx->tol; lc->tol_values = ctx->tol_values; lc->maxit = ctx->maxit;
+  lc->block = ctx->block; lc->poll = ctx->poll; lc->timing = ctx->timing;
+  L->mode = M->mode;
+  // the lane's work starts after the caller's work on the main stream (its inputs)
+  hipEvent_t ev;
+  HIPCHK(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCHK(ctx, hipEventRecord(ev, ctx->stream));
+  HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ev, 0));
+  const int64_t width = dfm_stats_width(M, stats, ns), T = M->T, h = (B + 1) / 2;
+  int rc1 = 0;
+  M->lane_worker->run([&]() {
+    hipSetDevice(lc->device);
+    rc1 = bootstrap_one(L, kind, B - h, idx + h * T, eta ? eta + h * T : nullptr, stats, ns,
+                        out ? out + h * width : nullptr);
+  });
+  const int rc0 = bootstrap_one(M, kind, h, idx, eta, stats, ns, out);
+  M->lane_worker->wait();
+  hipEventDestroy(ev);
+  // the lane's host-side counters and kernel timings join the caller's context
+  // (its device-side GEMM-product counts went to ctx->cnt_dev directly)
+  if (lc->timing) {
+    harvest(lc);
+    for (int i = 0; i < DFM_KC_COUNT; ++i) {
+      ctx->ms[i] += lc->ms[i]; ctx->launches[i] += lc->launches[i];
+      lc->ms[i] = 0; lc->launches[i] = 0;
+    }
+  }
+  ctx->eig_batches += lc->eig_batches;
+  ctx->eig_iters += lc->eig_iters;
+  ctx->eig_iters_max = std::max(ctx->eig_iters_max, lc->eig_iters_max);
+  ctx->rep_iters += lc->rep_iters;
+  ctx->gemm_products += lc->gemm_products;
+  lc->eig_batches = lc->eig_iters = lc->eig_iters_max = lc->rep_iters = lc->gemm_products = 0;
+  if (rc0) return rc0;
+  if (rc1) return fail(ctx, rc1, "bootstrap lane: %s", lc->err.c_str());
+  return 0;
+}
+
 int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
                       const dfm_stat *stats, int ns, double *out) {
+  if (!M) return -1;
+  if (idx && (kind != DFM_BOOT_WILD || eta) && lane_split(M, B, stats, ns))
+    return bootstrap_lanes(M, kind, B, idx, eta, stats, ns, out);
+  return bootstrap_one(M, kind, B, idx, eta, stats, ns, out);
+}
+
+static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+                         const dfm_stat *stats, int ns, double *out) {
   if (!M) return -1;
   dfm_ctx *ctx = M->ctx;
   if (B < 0 || !idx || (kind == DFM_BOOT_WILD && !eta) || (ns > 0 && (!stats || !out)) || ns < 0)
@@ -1167,7 +1321,7 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst,
-                                ctx->cnt_dev, esub);
+                                (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);
@@ -2299,14 +2453,12 @@ extern "C" int dfm_model_clone(const dfm_model *S, dfm_ctx *ctx, dfm_model **out
   M->trace = S->trace; M->V = S->V; M->critval = S->critval; M->sigma2 = S->sigma2;
   M->batch = S->batch; M->mode = S->mode;
   M->nblk = S->nblk; M->ba = S->ba; M->bt = S->bt; M->bm = S->bm; M->blam = S->blam;
-  std::vector<double> stage;
+  // device-to-device (peer) copies: no staging through host memory
   auto dup = [&](const double *src, size_t n, double **dst) -> int {
-    stage.resize(std::max<size_t>(n, 1));
-    hipSetDevice(sc->device);
-    if (hipMemcpy(stage.data(), src, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     hipSetDevice(ctx->device);
     if (dalloc(dst, n) != hipSuccess) return 1;
-    return hipMemcpy(*dst, stage.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess ? 0 : 1;
+    if (!src || n == 0) return 0;
+    return hipMemcpyPeer(*dst, ctx->device, src, sc->device, n * 8) == hipSuccess ? 0 : 1;
   };
   const size_t T = S->T, N = S->N, r = S->r, panel = T * S->ld;
   int bad = 0;

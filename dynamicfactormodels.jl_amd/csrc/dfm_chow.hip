@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
 constexpr int CH_FLAT_REPS = 4, CH_FLAT_MIN_N = 86;   // ceil(256 / 86) + 1 <= 4
 
 template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK, bool FLAT = false>
-__global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
+__global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
                                                        int nb, const double *__restrict__ F,
                                                        const double *__restrict__ Z,
                                                        const ChowPrep *__restrict__ prep,
@@ -151,7 +151,14 @@ __global__ __launch_bounds__(256) void chow_all_kernel(PanelSrc src, ChowBlocks 
                                                        double *__restrict__ WD) {
   constexpr int TR = 64;
   constexpr int RR = CH_RMAX;
-  constexpr int CU = 16;   // rows whose gathered values are in flight together
+  // rows whose gathered values are in flight together: 16, or 8 at R = 8,
+  // whose per-variable state (36 HC0 sums, four R-vectors of coefficients)
+  // already fills most of the 2-wave register budget.  The launch bound keeps
+  // R <= 8 at 2 waves per SIMD (256 registers): what the per-variable state
+  // does not fit is spilled once per thread around pass B, not inside the row
+  // loops — unbounded, the compiler took 256 VGPRs + 76 AGPRs at R = 4 and ran
+  // one wave per SIMD
+  constexpr int CU = R <= 4 ? 16 : (R <= 8 ? 8 : 16);
   constexpr int NR = FLAT ? CH_FLAT_REPS : 1;   // replicates staged per block
   __shared__ double sF[NR][TR * R], sZ[NR][TR * R], sE[NR][TR];
   __shared__ int sI[NR][TR];

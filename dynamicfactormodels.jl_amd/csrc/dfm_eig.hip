@@ -810,8 +810,9 @@ __global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm
   long long a = 0, b = 0;
   for (int it = 0; it <= last_gemm; ++it) a += it - 1 < 0 ? nb : active[it - 1];
   for (int it = 0; it <= last_cheb; ++it) b += active[it];
-  cnt[0] += a;       // one thread; launches on the context's stream are ordered
-  cnt[1] += a + b;
+  // device-scope atomics: a model's two bootstrap lanes count into one context
+  atomicAdd(reinterpret_cast<unsigned long long *>(cnt), (unsigned long long)a);
+  atomicAdd(reinterpret_cast<unsigned long long *>(cnt + 1), (unsigned long long)(a + b));
 }
 static int64_t count_rep_iters(const int *active_dev, int last, int shift, int nb, hipStream_t st) {
   if (last < 0) return 0;
@@ -1022,7 +1023,12 @@ size_t fact_workspace_bytes(int T, int nb, int P) {
 // (tools/mfma16_layout.hip).  An accumulator register g holds rows
 // 4g .. 4g+3 in exactly the B-operand layout, so Q'Y etc. need no lane movement.
 // Reductions over waves run in a fixed order: bit-reproducible, batch-invariant.
-constexpr int F2_T_MAX = 4096;   // dynamic LDS of ap2: 16 T + 4 bytes
+constexpr int F2_T_MAX = 4096;
+// waves per replicate workgroup of the factored passes (y2, ap2, Chebyshev)
+#ifndef DFM_BW
+#define DFM_BW 4
+#endif
+constexpr int BW = DFM_BW;   // dynamic LDS of ap2: 16 T + 4 bytes
 
 // Convergence verdict from per-column squared residuals res2[j] (j < k), on
 // one whole wave (same rules as check_converged: strict eigenvector-residual
@@ -1106,7 +1112,7 @@ template <int P>
 // its own iteration, no register prefetch of the next): these per-replicate
 // passes are HBM-latency-bound, and resident waves buy more bandwidth than
 // per-wave prefetch did (2 -> 4 WGs/CU: y2 -24 %, ap2 -13 %)
-__global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
+__global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
                                                       const double *__restrict__ eta,
                                                       const double *__restrict__ HZ, int64_t ldz,
                                                       const double *__restrict__ ab,
@@ -1125,12 +1131,12 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
   {
     const int32_t *ixg = idx + (int64_t)rep * T;
     const double *etg = eta ? eta + (int64_t)rep * T : nullptr;
-    for (int e = tid; e < T; e += 256) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; }
+    for (int e = tid; e < T; e += 64 * BW) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; }
   }
   const double *abr = ab + (int64_t)rep * 32 * P;
-  for (int e = tid; e < 16 * P; e += 256) sa[e] = abr[e];
+  for (int e = tid; e < 16 * P; e += 64 * BW) sa[e] = abr[e];
   __syncthreads();
-  for (int e = tid; e < 16 * P; e += 256) {
+  for (int e = tid; e < 16 * P; e += 64 * BW) {
     const int j = e / P, c = e % P;
     double v = abr[16 * P + e];
     if (j < r)
@@ -1159,7 +1165,7 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
   const int ntile = (T + 15) >> 4;
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Y2Tile<P> cur;
-  for (int tile = wave; tile < ntile; tile += 4) {
+  for (int tile = wave; tile < ntile; tile += BW) {
     y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
@@ -1202,7 +1208,7 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
         }
   }
   // fixed-order sum over the four waves
-  for (int wv = 0; wv < 4; ++wv) {
+  for (int wv = 0; wv < BW; ++wv) {
     if (wave == wv) {
 #pragma unroll
       for (int m3 = 0; m3 < 3; ++m3)
@@ -1219,7 +1225,7 @@ __global__ __launch_bounds__(256, 4) void boot_y2_kernel(FactBase fb, EigWork w,
     __syncthreads();
   }
   double *pp = w.part + (int64_t)rep * 3 * P * P;
-  for (int e = tid; e < 3 * NT * NT * 256; e += 256) {
+  for (int e = tid; e < 3 * NT * NT * 256; e += 64 * BW) {
     const int l = e & 63, g = (e >> 6) & 3, blk = e >> 8;
     const int b = blk % NT, a = (blk / NT) % NT, m3 = blk / (NT * NT);
     pp[m3 * P * P + (16 * a + 4 * g + (l >> 4)) * P + 16 * b + (l & 15)] = red[e];
@@ -1299,7 +1305,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
   dv4 cacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) cacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
-  for (int tile = wave; tile < ntile; tile += 4) {
+  for (int tile = wave; tile < ntile; tile += BW) {
     const int s0 = tile * 16;
     // all four row groups' first GU bucket entries are fetched together
     // (independent loads in flight); longer buckets finish serially
@@ -1355,7 +1361,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
   // a and cc: fixed-order sums over the waves -> ab[rep] = [a (16 x P); cc (16 x P)]
   double *abr = ab + (int64_t)rep * 32 * P;
   for (int pass = 0; pass < 2; ++pass) {
-    for (int wv = 0; wv < 4; ++wv) {
+    for (int wv = 0; wv < BW; ++wv) {
       if (wave == wv)
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct)
@@ -1367,7 +1373,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
           }
       __syncthreads();
     }
-    for (int e = tid; e < NT * 256; e += 256) {
+    for (int e = tid; e < NT * 256; e += 64 * BW) {
       const int l = e & 63, g = (e >> 6) & 3, ct = e >> 8;
       abr[pass * 16 * P + (4 * g + (l >> 4)) * P + 16 * ct + (l & 15)] = sred[e];
     }
@@ -1382,7 +1388,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
 // eta (T doubles), off (T+1 ints), lst (T ints) of this replicate.
 template <int P>
 // 4 workgroups per CU (see boot_y2_kernel)
-__global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
+__global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
                                                        int it, int init, int last, int cheb,
                                                        const double *__restrict__ eta,
                                                        const int *__restrict__ off, const int *__restrict__ lst,
@@ -1396,8 +1402,8 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   double *set = sdyn;                          // eta_t
   int *so = (int *)(sdyn + T), *sl = so + T + 1;
   __shared__ double sred[NT * 256];
-  __shared__ double sres[4][P];
-  __shared__ double stile[4][2][16 * (P + 1)];   // per-wave Q / Y tile transposes (ap2_load_lds)
+  __shared__ double sres[BW][P];
+  __shared__ double stile[BW][2][16 * (P + 1)];   // per-wave Q / Y tile transposes (ap2_load_lds)
   __shared__ int s_conv;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
   const int li = lane & 15, lk = lane >> 4;
@@ -1405,7 +1411,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
     const double *et = eta ? eta + (int64_t)rep * T : nullptr;
     const int *o = off + (int64_t)rep * (T + 1);
     const int *L = lst + (int64_t)rep * T;
-    for (int e = tid; e < T; e += 256) { set[e] = et ? et[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
+    for (int e = tid; e < T; e += 64 * BW) { set[e] = et ? et[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
     if (tid == 0) so[T] = o[T];
   }
   double *small = w.small + (int64_t)rep * small_stride<P>();
@@ -1434,7 +1440,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   const int ntile = (T + 15) >> 4;
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Ap2Tile<P> cur;
-  for (int tile = wave; tile < ntile; tile += 4) {
+  for (int tile = wave; tile < ntile; tile += BW) {
     ap2_load_lds<P>(cur, tile, T, r, lane, init, Qr, Yr, fb, stile[wave][0], stile[wave][1]);
     const int t0 = tile * 16;
     double qv[NT][4];
@@ -1510,7 +1516,12 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   if (wave == 0) {
     int conv = 0;
     if (!init) {
-      if (lane < P) sres[0][lane] = ((sres[0][lane] + sres[1][lane]) + sres[2][lane]) + sres[3][lane];
+      if (lane < P) {
+        double v = sres[0][lane];
+#pragma unroll
+        for (int wv = 1; wv < BW; ++wv) v += sres[wv][lane];
+        sres[0][lane] = v;
+      }
       __builtin_amdgcn_wave_barrier();
       const int itc = it + 1;
       const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
@@ -1527,7 +1538,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
   if (!init && (s_conv || last)) {
     // Ritz vectors U = Q A for the final output (eig_final_kernel)
     double *Ur = w.U + (int64_t)rep * T * P;
-    for (int tile = wave; tile < ntile; tile += 4) {
+    for (int tile = wave; tile < ntile; tile += BW) {
       const int t0 = tile * 16, ta = t0 + li;
       dv4 u[NT];
 #pragma unroll
@@ -1565,7 +1576,7 @@ __global__ __launch_bounds__(256, 4) void boot_ap2_kernel(FactBase fb, EigWork w
 // by the next Rayleigh-Ritz step (CholQR folded into eig_small), and its
 // Z = P'D Qn, a = F'Qn, cc = EL'Z are produced here for the next GEMM.
 template <int P>
-__global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork w, int T, int p,
+__global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigWork w, int T, int p,
                                                         const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta,
                                                         const int *__restrict__ off, const int *__restrict__ lst,
@@ -1588,13 +1599,13 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
     const double *etg = eta ? eta + (int64_t)rep * T : nullptr;
     const int *o = off + (int64_t)rep * (T + 1);
     const int *L = lst + (int64_t)rep * T;
-    for (int e = tid; e < T; e += 256) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
+    for (int e = tid; e < T; e += 64 * BW) { six[e] = ixg[e]; set[e] = etg ? etg[e] : 1.0; so[e] = o[e]; sl[e] = L[e]; }
     if (tid == 0) so[T] = o[T];
   }
   double *abr = ab + (int64_t)rep * 32 * P;
-  for (int e = tid; e < 16 * P; e += 256) sa[e] = abr[e];
+  for (int e = tid; e < 16 * P; e += 64 * BW) sa[e] = abr[e];
   __syncthreads();
-  for (int e = tid; e < 16 * P; e += 256) {
+  for (int e = tid; e < 16 * P; e += 64 * BW) {
     const int j = e / P, c = e % P;
     double v = abr[16 * P + e];
     if (j < r)
@@ -1625,7 +1636,7 @@ __global__ __launch_bounds__(256, 4) void boot_cheb_kernel(FactBase fb, EigWork 
   for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
-  for (int tile = wave; tile < ntile; tile += 4) {
+  for (int tile = wave; tile < ntile; tile += BW) {
     y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Xr);   // cur.q = X rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
@@ -1733,7 +1744,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace);
-    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, eta,
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, eta,
                        off, lst, qin, qs, alt, Zc, ldz, ab, seed);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
@@ -1746,14 +1757,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(256), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, ab,
+    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, ab,
                        qin, qs, alt);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, kJacobiSweeps);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(256), lds, st, fb, w, m, k, p, tol, it, 0,
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
                        it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, qin, qs, alt, Zc, ldz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it == next_poll) {   // convergence poll, right after the step that retires replicates
@@ -1782,7 +1793,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       if (e != hipSuccess) return 1000 + (int)e;
       last_cheb = it;
       if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-      hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(256), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st, fb,
+      hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st, fb,
                          w, m, p, idx, eta, off, lst, HZ, ldz, ab, alt, cur, Zc);
       if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     } else {

@@ -90,6 +90,32 @@ __global__ void soft_stats_kernel(const double *__restrict__ Z, int64_t ld, int 
   c[(int64_t)f * p + j] = cy / nf;
 }
 
+// Problem f's standardised training rows, transposed: Zt_f[j][c] =
+// Zs[tidx[f n + c]][j] for c < n (tidx's pad entries point at the block's zero
+// row) and 0 for n <= c < ldk — a p x ldk row-major panel per problem, the
+// plain operand of the LDS-DMA Gram G_f = Zt_f Zt_f' (gram_dma_kernel).  The
+// training rows keep their order, so every G_f entry sums the same products
+// in the same order as the fused-gather K1 Gram it replaces.  32 x 32 tiles
+// through LDS: gathered rows read along j, panel rows written along c.
+__global__ __launch_bounds__(256) void soft_transpose_kernel(const double *__restrict__ Zs, int64_t ld,
+                                                             const int32_t *__restrict__ tidx, int n, int p,
+                                                             int64_t ldk, double *__restrict__ Zt) {
+  __shared__ double tile[32][33];
+  const int f = blockIdx.z, c0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int32_t *tl = tidx + (int64_t)f * n;
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, j = j0 + tx;
+    tile[k][tx] = (c < n && j < p) ? Zs[(int64_t)tl[c] * ld + j] : 0.0;
+  }
+  __syncthreads();
+  double *Zf = Zt + (int64_t)f * p * ldk;
+  for (int k = ty; k < 32; k += 8) {
+    const int j = j0 + k, c = c0 + tx;
+    if (j < p && c < ldk) Zf[(int64_t)j * ldk + c] = tile[tx][k];
+  }
+}
+
 // G_f /= n_f (the Gram kernel leaves Zs_f' Zs_f)
 __global__ void soft_scale_kernel(double *__restrict__ G, int64_t strideG, int64_t count,
                                   const double *__restrict__ ystat) {
@@ -1254,6 +1280,8 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   double *cc = (double *)alloc((size_t)nprob * p * 8);
   uint8_t *ju = (uint8_t *)alloc((size_t)nprob * p);
   double *G = (double *)alloc((size_t)nprob * strideG * 8);
+  const int64_t ldk = ((int64_t)n + 15) / 16 * 16;
+  double *Zt = (double *)alloc((size_t)nprob * p * ldk * 8);
   double *alm = (double *)alloc((size_t)nprob * nlambda * 8);
   double *bpath = (double *)alloc((size_t)nprob * nlambda * p * 8);
   double *rsq = (double *)alloc((size_t)nprob * nlambda * 8);
@@ -1285,8 +1313,14 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   hipLaunchKernelGGL(soft_stats_kernel, dim3((p + 255) / 256, nprob), dim3(256), 0, st, Zp, ld, n, p, yd, fd,
                      ystat, Zs, mu, sd, ju, cc);
   // ---- standardised Grams of every problem on MFMA: G_f = Zs_f' Zs_f / n_f
-  PanelSrc src{nullptr, Zs, tidx, nullptr, ld, (int64_t)n};
-  e = launch_gram(1, src, p, n, n, G, p, strideG, nprob, st);
+  // each problem's training rows as a transposed plain panel, then one
+  // LDS-DMA Gram per problem (C4: 3 160 lower 64 x 64 tiles each)
+  hipLaunchKernelGGL(soft_transpose_kernel, dim3((unsigned)((ldk + 31) / 32), (p + 31) / 32, nprob), dim3(256), 0,
+                     st, Zs, ld, tidx, n, p, ldk, Zt);
+  for (int f = 0; f < nprob && e == hipSuccess; ++f) {
+    PanelSrc src{nullptr, Zt + (size_t)f * p * ldk, nullptr, nullptr, ldk, 0};
+    e = launch_gram(0, src, p, n, n, G + (size_t)f * strideG, p, strideG, 1, st);
+  }
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: Gram launch failed"); }
   hipLaunchKernelGGL(soft_scale_kernel, dim3(2048, nprob), dim3(256), 0, st, G, strideG, strideG, ystat);
   hipLaunchKernelGGL(soft_unit_diag_kernel, dim3((p + 255) / 256, nprob), dim3(256), 0, st, G, strideG, p, ju);

@@ -47,6 +47,30 @@ def test_bootstrap_multi_is_bit_identical(dfm, oracle, T, N, r, mode, n):
                           dfm.residual_bootstrap(copies, B, S.V(), idx=ridx))
 
 
+@pytest.mark.parametrize("T,N,r,mode,B", [(200, 400, 4, "factored", 700), (96, 150, 3, "direct", 600),
+                                          (150, 60, 3, "auto", 520), (80, 160, 2, "auto", 6000)])
+def test_two_lanes_are_bit_identical(dfm, oracle, T, N, r, mode, B):
+    """Jobs of 512..6000 replicates in automatic batching run as two lanes
+    (the halves of the replicate range on two streams / host threads,
+    dfm_bootstrap_dev); an explicit batch size keeps one lane.  Rows equal to
+    the bit, with the Chow statistics, coefficients and iteration counts."""
+    y, x, w = panel(oracle, T, N, r, 700 + T)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    g.set_bootstrap_mode(mode)
+    idx, eta = dfm.draw_wild_fast(77, B, T)
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.eigenvalue(1), S.coefficient(1), S.t_stat(2), S.LR_all(T // 2),
+             S.LM(T // 2, 1), S.iterations()]
+    lanes = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    g.set_batch(B)
+    one = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
+    assert np.array_equal(lanes, one)
+    ridx = oracle.draw_residual(np.random.default_rng(3), B, T)
+    one_r = dfm.residual_bootstrap(g, B, S.V(), idx=ridx)
+    g.set_batch(0)
+    assert np.array_equal(dfm.residual_bootstrap(g, B, S.V(), idx=ridx), one_r)
+
+
 def test_bootstrap_multi_break_model(dfm, oracle):
     y, x, w = panel(oracle, 120, 200, 2, 91, model="Breitung_Eickmeier_2011", b=0.5)
     g = dfm.DynamicFactorModel(y, w, x, 2, "ICp2", break_indices=[61])

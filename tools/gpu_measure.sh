@@ -26,6 +26,15 @@ step trace_direct 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_dir
 step configs 600 python -u tools/bench_configs.py --configs c1,c2,c4,c5 --reps 3
 cat "$OUT/configs.out"
 step trace_c2 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 2
+step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
+step c5 300 python -u bench.py --workload c5 --steps 10 --warmup 2 --no-cpu-baseline
+tail -1 "$OUT/c5.out"
+step c5_rolling 300 python -u bench.py --workload c5 --rolling 1000 --steps 10 --warmup 2 --no-cpu-baseline
+tail -1 "$OUT/c5_rolling.out"
+for R in 5000 2500 1250; do   # the per-rank share of the 9999 replicates at N = 2 / 4 / 8
+  step shard$R 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --replicates $R
+  tail -1 "$OUT/shard$R.out"
+done
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemm|gram_kernel|gram_dma|boot_|chow" -f csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traffic.json"
@@ -33,5 +42,4 @@ python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" > "$OUT/pmc_traff
 step pmc_fetch_c2 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "chow|gram_wk|gemmh|eig_|factors" -f csv -d "$OUT/pmc_fetch_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 1
 step pmc_write_c2 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "chow|gram_wk|gemmh|eig_|factors" -f csv -d "$OUT/pmc_write_c2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 1
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch_c2" "$OUT/pmc_write_c2" > "$OUT/pmc_traffic_c2.json"
-step trace_c4 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_c4" -o run -- python3 tools/bench_configs.py --configs c4 --reps 1
 echo ALLDONE
