@@ -163,6 +163,7 @@ struct dfm_ctx {
   // grown to the largest call's need — no per-call pool malloc/free on the host
   char *warena = nullptr;
   size_t warena_cap = 0, warena_need = 0;
+  hipEvent_t gate = nullptr;   // bootstrap_lanes: the second lane starts behind the caller's prior work
 };
 
 // The host thread of a model's second bootstrap lane (bootstrap_lanes):
@@ -379,6 +380,7 @@ static void ctx_release(dfm_ctx *ctx) {
   for (auto e : ctx->pool) hipEventDestroy(e);
   hipFree(ctx->cnt_dev);
   hipFree(ctx->warena);
+  if (ctx->gate) hipEventDestroy(ctx->gate);
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -1077,11 +1079,14 @@ static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx
   lc->tol = ctx->tol; lc->tol_values = ctx->tol_values; lc->maxit = ctx->maxit;
   lc->block = ctx->block; lc->poll = ctx->poll; lc->timing = ctx->timing;
   L->mode = M->mode;
-  // the lane's work starts after the caller's work on the main stream (its inputs)
-  hipEvent_t ev;
-  HIPCHK(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  HIPCHK(ctx, hipEventRecord(ev, ctx->stream));
-  HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ev, 0));
+  // the lane's work starts after the caller's work on the main stream (its
+  // inputs).  Measured and rejected: starting it half a step late (an event
+  // after the first lane's first eigen-iteration product), so the lanes'
+  // GEMMs and latency-bound passes alternate instead of running in lock-step:
+  // C3 1 250 replicates 3.81 -> 3.93 ms, C2 283 k -> 265 k replicates/s
+  if (!ctx->gate) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->gate, hipEventDisableTiming));
+  HIPCHK(ctx, hipEventRecord(ctx->gate, ctx->stream));
+  HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ctx->gate, 0));
   const int64_t width = dfm_stats_width(M, stats, ns), T = M->T, h = (B + 1) / 2;
   int rc1 = 0;
   M->lane_worker->run([&]() {
@@ -1091,7 +1096,6 @@ static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx
   });
   const int rc0 = bootstrap_one(M, kind, h, idx, eta, stats, ns, out);
   M->lane_worker->wait();
-  hipEventDestroy(ev);
   // the lane's host-side counters and kernel timings join the caller's context
   // (its device-side GEMM-product counts went to ctx->cnt_dev directly)
   if (lc->timing) {

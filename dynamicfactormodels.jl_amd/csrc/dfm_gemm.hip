@@ -472,7 +472,8 @@ int gram_dma_slots(int m) { return (gemm_ring3(m) ? 3 : 2) * 256; }
 template <int NBUF, int MINB>
 __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__restrict__ X, int64_t ld, int m, int K,
                                                              int nt, int tiles, int items, int span, int ksteps,
-                                                             double *__restrict__ G, int64_t ldg, int64_t strideZ) {
+                                                             double *__restrict__ G, int64_t ldg, int64_t strideZ,
+                                                             double alpha) {
   __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__res
                    a3 = acc[fa][4 * q + 3];
       double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
       double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
-      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const double v = ((b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8)) * alpha;   // alpha = 1: exact
       const int row = abase + wr * 32 + 4 * fa + oi;
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
       if (row < m && col < m) {
@@ -562,17 +563,17 @@ __global__ __launch_bounds__(256, MINB) void gram_dma_kernel(const double *__res
 // One launch of gram_dma_kernel over split-K partial images: S images of
 // strideZ elements at G (S == 1: G is the output itself).
 hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int ksteps, double *G, int64_t ldg,
-                           int64_t strideZ, hipStream_t st) {
+                           int64_t strideZ, hipStream_t st, double alpha) {
   const int nt = (m + GT - 1) / GT, tiles = nt * (nt + 1) / 2, items = tiles * S;
   const int span = (items + 7) / 8;
   // 3-deep ring at 3 workgroups per CU for the large Grams (more resident
   // waves beat a deeper ring there: tools/gemm_bench.hip, M = 2000)
   if (gemm_ring3(m))
     hipLaunchKernelGGL((gram_dma_kernel<3, 3>), dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span,
-                       ksteps, G, ldg, strideZ);
+                       ksteps, G, ldg, strideZ, alpha);
   else
     hipLaunchKernelGGL((gram_dma_kernel<4, 2>), dim3(8 * span), dim3(256), 0, st, X, ld, m, K, nt, tiles, items, span,
-                       ksteps, G, ldg, strideZ);
+                       ksteps, G, ldg, strideZ, alpha);
   return hipGetLastError();
 }
 

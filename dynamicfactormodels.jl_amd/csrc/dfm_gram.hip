@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(PanelSrc src, int m, int K
 
 // Fixed-order sum of the split-K partial images: G[r] = sum_z W[r][z].
 __global__ void gram_splitk_sum_kernel(const double *__restrict__ W, int S, int m, int64_t ldg,
-                                       int64_t elems, double *__restrict__ G, int64_t strideG) {
+                                       int64_t elems, double *__restrict__ G, int64_t strideG, double alpha) {
   const int r = blockIdx.y;
   const double *w = W + (int64_t)r * S * elems;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < elems; e += (int64_t)gridDim.x * blockDim.x) {
@@ -207,7 +207,7 @@ __global__ void gram_splitk_sum_kernel(const double *__restrict__ W, int S, int 
     if (j >= m) continue;
     double a = 0.0;
     for (int z = 0; z < S; ++z) a += w[(int64_t)z * elems + e];
-    G[(int64_t)r * strideG + i * ldg + j] = a;
+    G[(int64_t)r * strideG + i * ldg + j] = a * alpha;
   }
 }
 
@@ -223,7 +223,7 @@ int gram_ksplit(int m, int K) {
 }
 
 hipError_t launch_gram_dma(const double *X, int64_t ld, int m, int K, int S, int ksteps, double *G, int64_t ldg,
-                           int64_t strideZ, hipStream_t st);
+                           int64_t strideZ, hipStream_t st, double alpha);
 int gram_dma_slots(int m);
 // K-split of ONE plain-panel Gram (no replicate batch, so no batch
 // invariance to keep): enough (tile, split) workgroups to fill the chip's
@@ -247,9 +247,25 @@ int gram_ksplit_single(int m, int K) {
   return best;
 }
 
+static hipError_t launch_gram_a(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
+                                int64_t strideG, int nrep, hipStream_t st, double alpha);
 // Dispatch.  Returns hipError of the launch.
 hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G,
                        int64_t ldg, int64_t strideG, int nrep, hipStream_t st) {
+  return launch_gram_a(orient, src, m, K, T, G, ldg, strideG, nrep, st, 1.0);
+}
+// G = alpha X X' of ONE plain row-major panel (m >= 64, ld % 16 == 0, zero
+// columns K..ld-1) on the LDS-DMA SYRK, alpha applied in the epilogue (or in
+// the split-K sum): the soft-threshold Grams' 1/n_f without a pass over G.
+// hipErrorInvalidValue when the panel does not take the LDS-DMA path.
+hipError_t launch_gram_plain_scaled(const double *X, int64_t ld, int m, int K, double *G, int64_t ldg, double alpha,
+                                    hipStream_t st) {
+  if (m < GT || ld % 16 != 0) return hipErrorInvalidValue;
+  PanelSrc src{nullptr, X, nullptr, nullptr, ld, 0};
+  return launch_gram_a(ORIENT_ROWS, src, m, K, K, G, ldg, 0, 1, st, alpha);
+}
+static hipError_t launch_gram_a(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
+                                int64_t strideG, int nrep, hipStream_t st, double alpha) {
   const int nt = (m + GT - 1) / GT;
   const int nsteps = (K + KS - 1) / KS;
   const bool plain = orient == ORIENT_ROWS && !src.C && !src.eta && !src.idx && src.ld % 16 == 0 && nrep == 1 &&
@@ -271,10 +287,10 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
   // The k-split counts 16-deep steps of both kernels alike, so the partial
   // sums (and the result bits) do not depend on which kernel ran.
   if (plain) {
-    hipError_t er = launch_gram_dma(src.E, src.ld, m, K, S, ksteps, Gk, ldg, sZ, st);
+    hipError_t er = launch_gram_dma(src.E, src.ld, m, K, S, ksteps, Gk, ldg, sZ, st, S > 1 ? 1.0 : alpha);
     if (er == hipSuccess && S > 1)
       hipLaunchKernelGGL(gram_splitk_sum_kernel, dim3((unsigned)std::min<int64_t>((elems + 255) / 256, 4096), 1),
-                         dim3(256), 0, st, W, S, m, ldg, elems, G, strideG);
+                         dim3(256), 0, st, W, S, m, ldg, elems, G, strideG, alpha);
     if (W) hipFreeAsync(W, st);
     return er != hipSuccess ? er : hipGetLastError();
   }
@@ -309,7 +325,7 @@ hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, dou
 #undef DFM_GRAM_L
   if (S > 1) {
     hipLaunchKernelGGL(gram_splitk_sum_kernel, dim3((unsigned)std::min<int64_t>((elems + 255) / 256, 4096), nr),
-                       dim3(256), 0, st, W, S, m, ldg, elems, G + (int64_t)r0 * strideG, strideG);
+                       dim3(256), 0, st, W, S, m, ldg, elems, G + (int64_t)r0 * strideG, strideG, 1.0);
   }
   }
   if (W) hipFreeAsync(W, st);

@@ -32,6 +32,8 @@
 namespace dfm {
 hipError_t launch_gram(int orient, const PanelSrc &src, int m, int K, int T, double *G, int64_t ldg,
                        int64_t strideG, int nrep, hipStream_t st);
+hipError_t launch_gram_plain_scaled(const double *X, int64_t ld, int m, int K, double *G, int64_t ldg, double alpha,
+                                    hipStream_t st);
 __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, double *, int64_t);
 
 // y mean / population sd over each problem's training rows (fold != f; f = 0: all).
@@ -1298,10 +1300,12 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   if (e == hipSuccess) e = hipMemcpyAsync(fd, folds, (size_t)n * 4, hipMemcpyHostToDevice, st);
   // training-row lists per problem, padded with the block's zero row n
   std::vector<int32_t> tl((size_t)nprob * n);
+  std::vector<int> ntrain(nprob);
   for (int f = 0; f < nprob; ++f) {
     int c = 0;
     for (int i = 0; i < n; ++i)
       if (folds[i] != f) tl[(size_t)f * n + c++] = f * (n + 1) + i;
+    ntrain[f] = c;
     for (; c < n; ++c) tl[(size_t)f * n + c] = f * (n + 1) + n;
   }
   if (e == hipSuccess) e = hipMemcpyAsync(tidx, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, st);
@@ -1317,12 +1321,20 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   // LDS-DMA Gram per problem (C4: 3 160 lower 64 x 64 tiles each)
   hipLaunchKernelGGL(soft_transpose_kernel, dim3((unsigned)((ldk + 31) / 32), (p + 31) / 32, nprob), dim3(256), 0,
                      st, Zs, ld, tidx, n, p, ldk, Zt);
+  // G_f = Zt_f Zt_f' / n_f: the 1/n_f (the same double soft_ystats_kernel
+  // forms) applied in the Gram's epilogue, no pass over the (K+1) p^2 Grams
+  const bool scaled = p >= 64;
   for (int f = 0; f < nprob && e == hipSuccess; ++f) {
-    PanelSrc src{nullptr, Zt + (size_t)f * p * ldk, nullptr, nullptr, ldk, 0};
-    e = launch_gram(0, src, p, n, n, G + (size_t)f * strideG, p, strideG, 1, st);
+    if (scaled) {
+      e = launch_gram_plain_scaled(Zt + (size_t)f * p * ldk, ldk, p, n, G + (size_t)f * strideG, p,
+                                   1.0 / (double)ntrain[f], st);
+    } else {
+      PanelSrc src{nullptr, Zt + (size_t)f * p * ldk, nullptr, nullptr, ldk, 0};
+      e = launch_gram(0, src, p, n, n, G + (size_t)f * strideG, p, strideG, 1, st);
+    }
   }
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: Gram launch failed"); }
-  hipLaunchKernelGGL(soft_scale_kernel, dim3(2048, nprob), dim3(256), 0, st, G, strideG, strideG, ystat);
+  if (!scaled) hipLaunchKernelGGL(soft_scale_kernel, dim3(2048, nprob), dim3(256), 0, st, G, strideG, strideG, ystat);
   hipLaunchKernelGGL(soft_unit_diag_kernel, dim3((p + 255) / 256, nprob), dim3(256), 0, st, G, strideG, p, ju);
   // ---- lambda grid of the full fit: lambda_max = max_j |c_j| over non-constant columns
   std::vector<double> hc(p), hys(3 * nprob);
