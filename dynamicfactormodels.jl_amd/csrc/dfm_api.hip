@@ -98,6 +98,8 @@ struct FactBase {
   int64_t ldH;
   const double *F, *EL, *S, *H, *cF, *hd;
 };
+__global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int64_t strideG, int m,
+                                 double *__restrict__ trace);
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
@@ -526,12 +528,12 @@ static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const do
   if (p > 32 || p < k) return fail(ctx, -20, "eigensolver block %d unsupported for k=%d m=%d", p, k, m);
   const int P = p <= 16 ? 16 : 32;
   const size_t bytes = eig_workspace_bytes_padded(m, nb, P, ctx->maxit);
-  char *ws = nullptr;
-  HIPCHK(ctx, hipMalloc(&ws, bytes));
+  char *ws = nullptr;   // stream-ordered pool memory: no device-wide sync in the free
+  HIPCHK(ctx, hipMallocAsync((void **)&ws, bytes, ctx->stream));
   int rc = eig_run(G, m, (int64_t)m * m, m, nb, k, p, warm, kw, ctx->tol, ctx->maxit, ctx->poll, ws,
                    lam, Uk, trace, status_dev, nullptr, ctx->stream, timer_cb, ctx, 0);
+  hipFreeAsync(ws, ctx->stream);
   hipStreamSynchronize(ctx->stream);
-  hipFree(ws);
   if (rc != 0) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
   return 0;
 }
@@ -736,9 +738,15 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
         CKB(fail(ctx, -30, "kmax > 24 needs the full spectrum of every block; supported for Gram "
                            "size <= %d (block %d: %d)", spectrum_any_max(), j, M->bm[j]));
       }
-      // top-k pairs: the trace, and the sweep's eigenvalues when no spectrum
-      CKB(top_eig(j, bev[j].empty() ? kmax : 1));
-      if (bev[j].empty()) bev[j] = blam[j];
+      if (bev[j].empty()) {   // top-k pairs: the sweep's eigenvalues and the trace
+        CKB(top_eig(j, kmax));
+        bev[j] = blam[j];
+      } else {                // a spectrum gave the eigenvalues: only the trace (the Gram's diagonal)
+        hipLaunchKernelGGL(eig_trace_kernel, dim3(1), dim3(64), 0, st, Gb[j], (int64_t)M->bm[j],
+                           (int64_t)M->bm[j] * M->bm[j], M->bm[j], tr_d);
+        CK(hipMemcpyAsync(&btr[j], tr_d, 8, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+      }
     } else {
       CKB(top_eig(j, r_req));
       bev[j] = blam[j];
