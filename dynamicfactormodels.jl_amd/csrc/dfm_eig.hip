@@ -805,11 +805,12 @@ thread_local int64_t g_last_gemm_products = 0;   // replicate-products H . Z of 
 // replicate-products (those plus the Chebyshev GEMMs 0..last_cheb, shift 0)
 // to cnt[0], cnt[1] — no host synchronisation after the eigen loop.
 __global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm, int last_cheb, int nb,
-                                   long long *cnt) {
+                                   long long *cnt, int cp0, int cp1) {
   if (threadIdx.x != 0) return;
   long long a = 0, b = 0;
   for (int it = 0; it <= last_gemm; ++it) a += it - 1 < 0 ? nb : active[it - 1];
-  for (int it = 0; it <= last_cheb; ++it) b += active[it];
+  // Chebyshev products: cp0 after the first Rayleigh-Ritz step, cp1 after the others
+  for (int it = 0; it <= last_cheb; ++it) b += (long long)active[it] * (it == 0 ? cp0 : cp1);
   // device-scope atomics: a model's two bootstrap lanes count into one context
   atomicAdd(reinterpret_cast<unsigned long long *>(cnt), (unsigned long long)a);
   atomicAdd(reinterpret_cast<unsigned long long *>(cnt + 1), (unsigned long long)(a + b));
@@ -1072,6 +1073,31 @@ DFM_DEV bool decide_converged(const double *res2, const double *th, const double
   return ok;
 }
 
+#ifdef DFM_DIAG_X
+// diagnostic build only (tools/c3_excess.py): how far each replicate's
+// eigenvalue-bound test is from passing at Rayleigh-Ritz step it + 1
+__device__ double g_diag_x[4][16384];
+DFM_DEV void diag_excess(const double *res2, const double *th, int k, int p, double tol, double trace, int rep,
+                         int it) {
+  const int lane = threadIdx.x & 63;
+  double r1 = 0.0, bsum = 0.0, tsum = 0.0;
+  for (int j = lane; j < k; j += 64) {
+    const double gap = fmin(j > 0 ? fabs(th[j] - th[j - 1]) : INFINITY, j + 1 < p ? fabs(th[j] - th[j + 1]) : INFINITY);
+    const double bnd = res2[j] / (0.5 * gap);
+    bsum += bnd; tsum += th[j];
+    r1 = fmax(r1, bnd / (-tol * fabs(th[j])));
+  }
+  bsum = wave_sum(bsum); tsum = wave_sum(tsum);
+  for (int o = 32; o >= 1; o >>= 1) r1 = fmax(r1, __shfl_xor(r1, o));
+  const double vnum = fmax(fabs(trace - tsum), 1e-6 * fabs(trace));
+  const double x = fmax(r1, bsum / (-tol * vnum));
+  if (lane == 0 && it >= 0 && it < 4 && rep < 16384) g_diag_x[it][rep] = x;
+}
+extern "C" int dfm_diag_read_x(double *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_x), sizeof(g_diag_x)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // One 16-row tile's operands for y2: F / EL[idx] rows in A-operand layout
 // (row t0 + (lane & 15), factor 4kk + (lane >> 4)), HZ[idx] and Q in the
 // accumulator layout (row t0 + 4g + (lane >> 4), column 16ct + (lane & 15)).
@@ -1232,6 +1258,20 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   }
 }
 
+// End b of the Chebyshev filter's damping interval [0, b]: theta_p, the
+// block's smallest Ritz value (above every unwanted eigenvalue once the block
+// has converged a little), or after the first Rayleigh-Ritz step of a warm
+// start at least bbeta * theta_k: there the guard columns' Ritz values are
+// still far below lambda_p (C3: theta_16 ~ 0.8e3 vs lambda_17 ~ 8e3) and
+// [0, theta_p] would leave most of the unwanted spectrum undamped, while the
+// wanted theta_k is already accurate (b < theta_k keeps every wanted
+// eigenvalue amplified; a b short of lambda_{p+1} only slows the filter).
+template <int P>
+DFM_DEV double filter_end(const double *small, int k, int p, double bbeta) {
+  const double tp = small[2 * P * P + p - 1];
+  return bbeta > 0.0 ? fmax(tp, bbeta * small[2 * P * P + k - 1]) : tp;
+}
+
 // One 16-row tile's operands for ap2 (ap2_load_lds): Q and Y rows in A-operand layout
 // (row t0 + (lane & 15), column 4kk + (lane >> 4)), F rows for a = F'Qn in
 // A-operand layout per row group g (row t0 + 4g + (lane >> 4), factor lane & 15),
@@ -1389,8 +1429,8 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
 template <int P>
 // 4 workgroups per CU (see boot_y2_kernel)
 __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWork w, int T, int k, int p, double tol,
-                                                       int it, int init, int last, int cheb,
-                                                       const double *__restrict__ eta,
+                                                       int it, int init, int last, int cheb, double fa1,
+                                                       double fa0, double bbeta, const double *__restrict__ eta,
                                                        const int *__restrict__ off, const int *__restrict__ lst,
                                                        const double *__restrict__ Qc, int64_t qs,
                                                        double *__restrict__ Yq, double *__restrict__ Zc, int64_t ldz,
@@ -1430,9 +1470,10 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   const double *Qr = Qc + (int64_t)rep * qs;   // qs = 0: the shared warm start (init / first step)
   double *Yr = Yq + (int64_t)rep * T * P;
-  // Chebyshev coefficients from b = theta_p (boot_cheb_kernel): X = cf1 V + cf0 Q Bm
-  const double bch = init ? 0.0 : small[2 * P * P + p - 1];
-  const double cf1 = bch > 0.0 ? -8.0 / bch : 1.0, cf0 = bch > 0.0 ? 1.0 : 0.0;
+  // the filter's two low-order terms (boot_cheb_kernel): X = (fa1 / b) V + fa0 Q Bm,
+  // fa1 / fa0 = T*_d's y^1 / y^0 coefficients, b = filter_end
+  const double bch = init ? 0.0 : filter_end<P>(small, k, p, bbeta);
+  const double cf1 = bch > 0.0 ? fa1 / bch : 1.0, cf0 = bch > 0.0 ? fa0 : 0.0;
   double res2[NT];
   dv4 aacc[NT];
 #pragma unroll
@@ -1527,6 +1568,9 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
       const double *prev = small + 2 * P * P + 2 * P + ((itc - 1) & 1) * P;
       double *next = small + 2 * P * P + 2 * P + (itc & 1) * P;
       conv = decide_converged(sres[0], small + 2 * P * P, prev, next, k, p, tol, w.trace[rep], itc, w.subspace) ? 1 : 0;
+#ifdef DFM_DIAG_X
+      diag_excess(sres[0], small + 2 * P * P, k, p, tol, w.trace[rep], rep, it);
+#endif
     }
     if (lane == 0) {
       s_conv = conv;
@@ -1565,24 +1609,27 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, rep, ab, aacc, sred);
 }
 
-// Chebyshev step (degree 2) of the factored solver.  After ap2 has produced
-// V = Y Bm (= G* Q Bm, orthonormal), X = -(8/b) V + Q Bm (in w.U) and Z(V), and the GEMM
-// H . Z(V), this forms W = G* V exactly as y2 forms Y and replaces the power
-// step by the degree-2 Chebyshev filter on [0, b], b = theta_p (the block's
-// smallest Ritz value, above every unwanted eigenvalue):
-//   T2(2G/b - 1) (Q Bm) = (8/b^2) W - (8/b) V + QB
-// which damps the unwanted spectrum ~T2(2 lambda_k/b - 1) times faster than
-// two power steps relative to the wanted one.  The new basis is orthonormalised
-// by the next Rayleigh-Ritz step (CholQR folded into eig_small), and its
-// Z = P'D Qn, a = F'Qn, cc = EL'Z are produced here for the next GEMM.
+// Chebyshev step s (2 <= s <= d) of the degree-d filter of the factored solver.
+// With V0 = Q Bm, K_i = G*^i V0 and y = G*/b (b = filter_end), the filter is
+// the shifted Chebyshev polynomial T*_d(y) = T_d(2y - 1) = sum_i a_i y^i
+// applied in monomial form: ap2 leaves X = (a_1/b) K_1 + a_0 V0 (in w.U) and
+// Z(K_1); step s gets K_s = G* K_{s-1} from the GEMM H . Z(K_{s-1}) (formed
+// exactly as y2 forms Y) and adds (a_s/b^s) K_s to X.  A middle step (s < d)
+// writes X back and hands K_s on (Z, a and cc of K_s) to the next GEMM; the
+// final step writes the filtered basis X into Q with its Z, a, cc for the next
+// Rayleigh-Ritz step.  Degree 2: T2(2G/b - 1)(Q Bm) = (8/b^2) W - (8/b) V + Q Bm.
+// The filter damps the unwanted spectrum ~T_d(2 lambda_k/b - 1) times
+// relative to the wanted one; the basis is orthonormalised by the next
+// Rayleigh-Ritz step (CholQR folded into eig_small).
 template <int P>
 __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigWork w, int T, int p,
                                                         const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta,
                                                         const int *__restrict__ off, const int *__restrict__ lst,
                                                         const double *__restrict__ HZ, int64_t ldz,
-                                                        double *__restrict__ ab, const double *__restrict__ Vc,
-                                                        double *__restrict__ Qo, double *__restrict__ Zc) {
+                                                        double *__restrict__ ab, double fas, int spow, int fin,
+                                                        double bbeta, int k, double *__restrict__ Qo,
+                                                        double *__restrict__ Zc) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -1614,8 +1661,10 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   }
   __syncthreads();
   const double *small = w.small + (int64_t)rep * small_stride<P>();
-  const double b = small[2 * P * P + p - 1];
-  const double c2 = b > 0.0 ? 8.0 / (b * b) : 0.0;
+  const double b = filter_end<P>(small, k, p, bbeta);
+  double bs = b;
+  for (int i = 1; i < spow; ++i) bs *= b;   // b^s (b * b at s = 2)
+  const double c2 = b > 0.0 ? fas / bs : 0.0;
   bool dd[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) dd[ct] = small[2 * P * P + P + 16 * ct + li] != 0.0;
@@ -1628,9 +1677,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
       bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
     }
-  const double *Xr = w.U + (int64_t)rep * T * P;   // X = c1 V + c0 Q Bm (ap2)
+  double *Xr = w.U + (int64_t)rep * T * P;   // X: the filter's terms so far (ap2, earlier steps)
   double *Qr = Qo + (int64_t)rep * T * P;
-  (void)Vc;
   dv4 aacc[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
@@ -1664,8 +1712,15 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         const double wv = fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]);
-        double q = dd[ct] ? cur.q[ct][g] : fma(c2, wv, cur.q[ct][g]);
-        if (c >= p || !v) q = 0.0;
+        double x = dd[ct] ? cur.q[ct][g] : fma(c2, wv, cur.q[ct][g]);
+        if (c >= p || !v) x = 0.0;
+        // final: the filtered basis; middle: X back over the rows this lane
+        // read, and K_s goes on to the next product
+        double q = x;
+        if (!fin) {
+          if (v) Xr[(int64_t)t * P + c] = x;
+          q = (c >= p || !v) ? 0.0 : wv;
+        }
         qv[ct][g] = q;
         if (v) Qr[(int64_t)t * P + c] = q;
       }
@@ -1702,6 +1757,34 @@ __global__ __launch_bounds__(1024) void active_list_kernel(const int *__restrict
     if (!done[i]) list[pos++] = i;
   if (tid == 1023) *count = part[1023];
 }
+
+// Shifted Chebyshev coefficients T*_d(y) = T_d(2y - 1) = sum_i a_i y^i
+// (T*_0 = 1, T*_1 = 2y - 1, T*_{n+1} = 2 (2y - 1) T*_n - T*_{n-1}).
+constexpr int kChebDMax = 8;
+static void shifted_cheb(int d, double *a) {   // a[0..kChebDMax]
+  double t0[kChebDMax + 1] = {1.0}, t1[kChebDMax + 1] = {-1.0, 2.0};
+  if (d == 0) { for (int i = 0; i <= kChebDMax; ++i) a[i] = t0[i]; return; }
+  for (int n = 1; n < d; ++n) {
+    double t2[kChebDMax + 1];
+    for (int i = 0; i <= kChebDMax; ++i) t2[i] = -2.0 * t1[i] - t0[i] + (i > 0 ? 4.0 * t1[i - 1] : 0.0);
+    for (int i = 0; i <= kChebDMax; ++i) { t0[i] = t1[i]; t1[i] = t2[i]; }
+  }
+  for (int i = 0; i <= kChebDMax; ++i) a[i] = t1[i];
+}
+// Filter schedule of the factored solver.  From a warm start (the base fit's
+// eigenvectors): a degree-6 filter on [0, max(theta_p, 0.2 theta_k)] after
+// the first Rayleigh-Ritz step, degree 2 on [0, theta_p] after the later ones.
+// C3 (tools/eig_proto.py, the CPU model of this loop; tools/c3_excess.py, the
+// convergence excess measured on the GPU): with degree 2 throughout the first
+// filter gains only ~3e3 in the eigenvalue bound (theta_16 ~ 0.8e3 far below
+// lambda_17 ~ 8e3) against ~5e4 for the later ones, and replicates retire at
+// the 4th (96 %) or 5th Rayleigh-Ritz step after 7.09 products; with this
+// schedule every replicate of the CPU model retires at the 2nd step after 7
+// products — two Rayleigh-Ritz passes and the straggler tail fewer, two more
+// Chebyshev passes.  Cold starts (no warm vectors: expanding windows) keep
+// degree 2 on [0, theta_p].
+constexpr int kChebWarmD0 = 6, kChebD = 2;
+constexpr double kChebWarmBeta = 0.2;
 
 template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
@@ -1744,12 +1827,23 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace);
-    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, eta,
+    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
+                       0.0, 0.0, eta,
                        off, lst, qin, qs, alt, Zc, ldz, ab, seed);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  int it = 0, last_gemm = -1, last_cheb = -1, next_poll = poll - 1;
+  const bool warm_started = warm && kw >= k;
+  const int d0 = warm_started ? kChebWarmD0 : kChebD;
+  const double beta0 = warm_started ? kChebWarmBeta : 0.0;
+  double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
+  shifted_cheb(d0, ca0);
+  shifted_cheb(kChebD, ca1);
+  // first convergence poll right after the step most replicates retire at
+  int it = 0, last_gemm = -1, last_cheb = -1, next_poll = warm_started ? 1 : poll - 1;
   for (; it < maxit; ++it) {
+    const int dg = it == 0 ? d0 : kChebD;
+    const double *ca = it == 0 ? ca0 : ca1;
+    const double bb = it == 0 ? beta0 : 0.0;
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
     hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
                                cl_on ? alist : nullptr, cl_on ? acount : nullptr);
@@ -1765,7 +1859,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
-                       it == maxit - 1 ? 1 : 0, cheb, eta, off, lst, qin, qs, alt, Zc, ldz, ab, seed);
+                       it == maxit - 1 ? 1 : 0, cheb, ca[1], ca[0], bb, eta, off, lst, qin, qs, alt, Zc, ldz, ab,
+                       seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it == next_poll) {   // convergence poll, right after the step that retires replicates
       int a = -1;
@@ -1784,18 +1879,21 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       }
     }
     if (cheb && it < maxit - 1) {
-      // second product G* V and the degree-2 Chebyshev combination: the new
-      // basis goes back into cur (Q), Y/V stay in alt
-      if (tf) tf(tctx, DFM_KC_GEMM, 1);
-      e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
-                      cl_on ? alist : nullptr, cl_on ? acount : nullptr);
-      if (tf) tf(tctx, DFM_KC_GEMM, 0);
-      if (e != hipSuccess) return 1000 + (int)e;
+      // products G* K_{s-1}, s = 2..d, and the degree-d Chebyshev combination:
+      // the new basis goes back into cur (Q), Y/V stay in alt
+      for (int sp = 2; sp <= dg; ++sp) {
+        if (tf) tf(tctx, DFM_KC_GEMM, 1);
+        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
+                        cl_on ? alist : nullptr, cl_on ? acount : nullptr);
+        if (tf) tf(tctx, DFM_KC_GEMM, 0);
+        if (e != hipSuccess) return 1000 + (int)e;
+        if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
+        hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st,
+                           fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[sp], sp, sp == dg ? 1 : 0, bb, k, cur,
+                           Zc);
+        if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
+      }
       last_cheb = it;
-      if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-      hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st, fb,
-                         w, m, p, idx, eta, off, lst, HZ, ldz, ab, alt, cur, Zc);
-      if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     } else {
       std::swap(cur, alt);
     }
@@ -1805,11 +1903,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   g_last_iters = it;
   // the Chebyshev GEMM of iteration it runs after that iteration's check
   if (cnt) {
-    hipLaunchKernelGGL(count_iters_kernel, dim3(1), dim3(64), 0, st, w.active, last_gemm, last_cheb, nb, cnt);
+    hipLaunchKernelGGL(count_iters_kernel, dim3(1), dim3(64), 0, st, w.active, last_gemm, last_cheb, nb, cnt,
+                       d0 - 1, kChebD - 1);
     g_last_rep_iters = g_last_gemm_products = 0;
   } else {
     g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
-    g_last_gemm_products = g_last_rep_iters + count_rep_iters(w.active, last_cheb, 0, nb, st);
+    const int64_t c0 = count_rep_iters(w.active, std::min(last_cheb, 0), 0, nb, st);
+    const int64_t call = count_rep_iters(w.active, last_cheb, 0, nb, st);
+    g_last_gemm_products = g_last_rep_iters + c0 * (d0 - 1) + (call - c0) * (kChebD - 1);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
