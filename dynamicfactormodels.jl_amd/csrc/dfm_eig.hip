@@ -1470,8 +1470,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   const double *Qr = Qc + (int64_t)rep * qs;   // qs = 0: the shared warm start (init / first step)
   double *Yr = Yq + (int64_t)rep * T * P;
-  // the filter's two low-order terms (boot_cheb_kernel): X = (fa1 / b) V + fa0 Q Bm,
-  // fa1 / fa0 = T*_d's y^1 / y^0 coefficients, b = filter_end
+  // the filter's first Horner term (boot_cheb_kernel): S = (fa1 / b) Y Bm + fa0 Q Bm,
+  // fa1 / fa0 = T*_d's y^d / y^(d-1) coefficients, b = filter_end
   const double bch = init ? 0.0 : filter_end<P>(small, k, p, bbeta);
   const double cf1 = bch > 0.0 ? fa1 / bch : 1.0, cf0 = bch > 0.0 ? fa0 : 0.0;
   double res2[NT];
@@ -1503,7 +1503,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
           qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
           if (cheb) qb[ct] = mfma16(cur.qa[kk], bBm[kk][ct], qb[ct]);
         }
-      if (cheb) {   // X = c1 V + c0 Q Bm, the filter's low-order terms (boot_cheb_kernel), kept in w.U
+      if (cheb) {   // V0 = Q Bm for the filter's later steps (boot_cheb_kernel), kept in w.U
         double *Xr = w.U + (int64_t)rep * T * P;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -1512,8 +1512,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
 #pragma unroll
             for (int ct = 0; ct < NT; ++ct) {
               const int c = 16 * ct + li;
-              double x = fma(cf1, qn[ct][g], cf0 * qb[ct][g]);
-              if (c < p && dd[ct]) x = hash_unit(seed, t, 1000003ull * (it + 1) + c);   // = V
+              double x = qb[ct][g];
+              if (c < p && dd[ct]) x = hash_unit(seed, t, 1000003ull * (it + 1) + c);   // = S
               if (c >= p) x = 0.0;
               Xr[(int64_t)t * P + c] = x;
             }
@@ -1530,7 +1530,9 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
           const int c = 16 * ct + li;
           const double wr = ya[ct][g] - th[ct] * u[ct][g];
           if (v && c < k) res2[ct] = fma(wr, wr, res2[ct]);
-          double q = qn[ct][g];
+          // the filter's first Horner term S_{d-1} = (a_d / b) K_1 + a_{d-1} V0
+          // (K_1 = Y Bm = G* V0), or the plain power step Y Bm
+          double q = cheb ? fma(cf1, qn[ct][g], cf0 * qb[ct][g]) : qn[ct][g];
           if (c < p && dd[ct]) q = hash_unit(seed, t, 1000003ull * (it + 1) + c);
           if (c >= p || !v) q = 0.0;
           qv[ct][g] = q;
@@ -1609,15 +1611,17 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, rep, ab, aacc, sred);
 }
 
-// Chebyshev step s (2 <= s <= d) of the degree-d filter of the factored solver.
-// With V0 = Q Bm, K_i = G*^i V0 and y = G*/b (b = filter_end), the filter is
-// the shifted Chebyshev polynomial T*_d(y) = T_d(2y - 1) = sum_i a_i y^i
-// applied in monomial form: ap2 leaves X = (a_1/b) K_1 + a_0 V0 (in w.U) and
-// Z(K_1); step s gets K_s = G* K_{s-1} from the GEMM H . Z(K_{s-1}) (formed
-// exactly as y2 forms Y) and adds (a_s/b^s) K_s to X.  A middle step (s < d)
-// writes X back and hands K_s on (Z, a and cc of K_s) to the next GEMM; the
-// final step writes the filtered basis X into Q with its Z, a, cc for the next
-// Rayleigh-Ritz step.  Degree 2: T2(2G/b - 1)(Q Bm) = (8/b^2) W - (8/b) V + Q Bm.
+// One Horner step of the degree-d Chebyshev filter of the factored solver.
+// With V0 = Q Bm and y = G*/b (b = filter_end), the filter is the shifted
+// Chebyshev polynomial T*_d(y) = T_d(2y - 1) = sum_i a_i y^i, evaluated as
+// S_d = a_d V0, S_i = G* S_{i+1} / b + a_i V0, T*_d(y) V0 = S_0: ap2 leaves
+// S_{d-1} = (a_d / b) K_1 + a_{d-1} V0 (K_1 = Y Bm = G* V0, no product) with
+// its Z, a, cc, and V0 in w.U; each step gets W = G* S_{i+1} from the GEMM
+// H . Z(S_{i+1}) (formed exactly as y2 forms Y) and writes S_i = W / b + a_i V0
+// with the Z, a, cc of S_i for the next GEMM (or, S_0, the next Rayleigh-Ritz
+// step).  The same step serves the middle and the end of the filter, with
+// one running vector (the monomial form also rewrote a running sum per
+// step).  Degree 2: T2(2G/b - 1)(Q Bm) = (8/b^2) G*^2 V0 - (8/b) G* V0 + V0.
 // The filter damps the unwanted spectrum ~T_d(2 lambda_k/b - 1) times
 // relative to the wanted one; the basis is orthonormalised by the next
 // Rayleigh-Ritz step (CholQR folded into eig_small).
@@ -1627,8 +1631,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
                                                         const double *__restrict__ eta,
                                                         const int *__restrict__ off, const int *__restrict__ lst,
                                                         const double *__restrict__ HZ, int64_t ldz,
-                                                        double *__restrict__ ab, double fas, int spow, int fin,
-                                                        double bbeta, int k, double *__restrict__ Qo,
+                                                        double *__restrict__ ab, double fai, double bbeta, int k,
+                                                        double *__restrict__ Qo,
                                                         double *__restrict__ Zc) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
@@ -1662,9 +1666,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   __syncthreads();
   const double *small = w.small + (int64_t)rep * small_stride<P>();
   const double b = filter_end<P>(small, k, p, bbeta);
-  double bs = b;
-  for (int i = 1; i < spow; ++i) bs *= b;   // b^s (b * b at s = 2)
-  const double c2 = b > 0.0 ? fas / bs : 0.0;
+  // b <= 0 (a degenerate block): plain power steps
+  const double cb = b > 0.0 ? 1.0 / b : 1.0, cv0 = b > 0.0 ? fai : 0.0;
   bool dd[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) dd[ct] = small[2 * P * P + P + 16 * ct + li] != 0.0;
@@ -1677,7 +1680,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
       bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
     }
-  double *Xr = w.U + (int64_t)rep * T * P;   // X: the filter's terms so far (ap2, earlier steps)
+  const double *Xr = w.U + (int64_t)rep * T * P;   // V0 = Q Bm (ap2)
   double *Qr = Qo + (int64_t)rep * T * P;
   dv4 aacc[NT];
 #pragma unroll
@@ -1685,7 +1688,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Xr);   // cur.q = X rows
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Xr);   // cur.q = V0 rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1712,15 +1715,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         const double wv = fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]);
-        double x = dd[ct] ? cur.q[ct][g] : fma(c2, wv, cur.q[ct][g]);
-        if (c >= p || !v) x = 0.0;
-        // final: the filtered basis; middle: X back over the rows this lane
-        // read, and K_s goes on to the next product
-        double q = x;
-        if (!fin) {
-          if (v) Xr[(int64_t)t * P + c] = x;
-          q = (c >= p || !v) ? 0.0 : wv;
-        }
+        double q = dd[ct] ? cur.q[ct][g] : fma(cb, wv, cv0 * cur.q[ct][g]);
+        if (c >= p || !v) q = 0.0;
         qv[ct][g] = q;
         if (v) Qr[(int64_t)t * P + c] = q;
       }
@@ -1859,8 +1855,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
-                       it == maxit - 1 ? 1 : 0, cheb, ca[1], ca[0], bb, eta, off, lst, qin, qs, alt, Zc, ldz, ab,
-                       seed);
+                       it == maxit - 1 ? 1 : 0, cheb, ca[dg], ca[dg - 1], bb, eta, off, lst, qin, qs, alt, Zc, ldz,
+                       ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it == next_poll) {   // convergence poll, right after the step that retires replicates
       int a = -1;
@@ -1879,8 +1875,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       }
     }
     if (cheb && it < maxit - 1) {
-      // products G* K_{s-1}, s = 2..d, and the degree-d Chebyshev combination:
-      // the new basis goes back into cur (Q), Y/V stay in alt
+      // d - 1 products G* S_{i+1} and Horner steps S_i, i = d-2 .. 0: the new
+      // basis S_0 goes back into cur (Q), Y stays in alt
       for (int sp = 2; sp <= dg; ++sp) {
         if (tf) tf(tctx, DFM_KC_GEMM, 1);
         e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
@@ -1889,8 +1885,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
         if (e != hipSuccess) return 1000 + (int)e;
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
         hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st,
-                           fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[sp], sp, sp == dg ? 1 : 0, bb, k, cur,
-                           Zc);
+                           fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[dg - sp], bb, k, cur, Zc);
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
       }
       last_cheb = it;
