@@ -184,23 +184,28 @@ def hbm_rooflines(timing, eig, Bn, steps):
     region; algorithmic bytes per replicate-pass, DESIGN.md section 3, P = 16):
       y2  (class eig_gq):    Y = G*Q rows from the gathered HZ rows, Q'Y / Y'Y / Q'Q:
                              reads Q and HZ[idx], writes Y = 3 T P 8 B per Rayleigh-Ritz step
-      ap2 + Chebyshev step (class eig_apply): 5 T P 8 B per pass (Q, Y in; X, Qn, Z out);
-                             passes = Rayleigh-Ritz steps + one init per replicate + Chebyshev steps
+      ap2 (class eig_apply): 5 T P 8 B per pass (Q, Y in; the filter's first Horner term S,
+                             V0 = Q Bm and Z out); passes = Rayleigh-Ritz steps + one init per replicate
+      Chebyshev (Horner) step (class eig_apply): 4 T P 8 B per pass (HZ[idx], V0 in; S, Z out);
+                             passes = GEMM products - Rayleigh-Ritz steps
     Replicate-passes come from the library's own counters (eig_iterations)."""
     P = 16
     out = []
     rr = eig.get("replicate_iterations", 0)
-    cheb = eig.get("gemm_products", 0) - rr
-    for cls, name, per, units in (
-            ("eig_gq", "boot_y2_kernel", 3 * T * P * 8, rr),
-            ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel", 5 * T * P * 8, rr + Bn * steps + max(cheb, 0))):
+    cheb = max(eig.get("gemm_products", 0) - rr, 0)
+    tp8 = T * P * 8
+    for cls, name, parts in (
+            ("eig_gq", "boot_y2_kernel", ((3 * tp8, rr),)),
+            ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel", ((5 * tp8, rr + Bn * steps), (4 * tp8, cheb)))):
         ms, n = timing.get(cls, (0.0, 0))
+        units = sum(u for _, u in parts)
         if not n or not units:
             continue
-        gbs = per * units / (ms * 1e-3) / 1e9
+        byts = sum(b * u for b, u in parts)
+        gbs = byts / (ms * 1e-3) / 1e9
         out.append({"kernel": name, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_replicate_pass": per,
-                    "replicate_passes": int(units)})
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                    "bytes_per_replicate_pass": [b for b, _ in parts], "replicate_passes": [int(u) for _, u in parts]})
     return out
 
 

@@ -26,6 +26,7 @@
 #include "dfm_common.h"
 #include "../../include/dfm.h"
 #include <algorithm>
+#include <utility>
 #include <cmath>
 #include <vector>
 
@@ -390,10 +391,12 @@ DFM_DEV void lp_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 // spin (every lane of the wave) until *f >= target; LDS reads are in order per wave
 DFM_DEV void lp_wait(const int *f, int target, LpPipe *pp, long long tmo) {
   const volatile int *vf = f;
+  const volatile int *ve = &pp->err;
   if (*vf < target) {
     const long long t0 = wall_clock64();
     while (*vf < target) {
       __builtin_amdgcn_s_sleep(1);
+      if (*ve) break;   // another wave timed out: the launch is failing, do not wait out a timeout per spin
       if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
     }
   }
@@ -414,6 +417,7 @@ DFM_DEV void lp_wait_cons(LpPipe *pp, int w0, int target, long long tmo) {
     const long long t0 = wall_clock64();
     while (lp_min_cons(pp, w0) < target) {
       __builtin_amdgcn_s_sleep(1);
+      if (((const volatile int *)&pp->err)[0]) break;
       if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
     }
   }
@@ -1164,7 +1168,9 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   A.snapL = (double *)alloc((size_t)nprob * LP_NBL * 2 * ldaa * 8);
   A.snapR = (double *)alloc((size_t)nprob * LP_NBL * 4 * 8);
   A.bpath = bpath; A.rsq_out = rsq; A.nlam_out = nl; A.status = sts;
-  A.tmo = 2000000000LL;   // 20 s of the 100 MHz wall clock
+  // 2 s of the 100 MHz wall clock: every legitimate wait is microseconds to
+  // milliseconds (C4's whole path: 49 ms)
+  A.tmo = 200000000LL;
   // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
   static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
   if (prof) A.prof = (long long *)alloc((size_t)nprob * LP_PROF * 8);
@@ -1174,8 +1180,22 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     *why = "out of device memory";
     return hipErrorOutOfMemory;
   }
-  e = hipMemsetAsync(A.ctl, 0, (size_t)nprob * sizeof(LassoCtl), st);
-  if (e == hipSuccess) e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
+  // every scratch buffer starts zeroed, as on a fresh allocation: a second
+  // call in one process gets recycled pool memory, and round 3 saw such calls
+  // stall intermittently (first calls never did)
+  e = hipSuccess;
+  for (auto z : {std::make_pair((void *)A.ctl, (size_t)nprob * sizeof(LassoCtl)),
+                 std::make_pair((void *)A.g2, (size_t)nprob * 2 * p * 8),
+                 std::make_pair((void *)A.isact, (size_t)nprob * p * 4),
+                 std::make_pair((void *)A.klist, (size_t)nprob * LP_LMAX * 4),
+                 std::make_pair((void *)A.dlist, (size_t)nprob * LP_LMAX * 8),
+                 std::make_pair((void *)A.save, (size_t)nprob * 2 * LP_LMAX * 8),
+                 std::make_pair((void *)A.GAA, (size_t)nprob * ldaa * ldaa * 8),
+                 std::make_pair((void *)A.snapC, (size_t)nprob * LP_NCH * p * 8),
+                 std::make_pair((void *)A.snapL, (size_t)nprob * LP_NBL * 2 * ldaa * 8),
+                 std::make_pair((void *)A.snapR, (size_t)nprob * LP_NBL * 4 * 8),
+                 std::make_pair((void *)nl, (size_t)nprob * 4)})
+    if (e == hipSuccess) e = hipMemsetAsync(z.first, 0, z.second, st);
   // A plain launch sized to the co-resident capacity (occupancy API above):
   // the kernel needs every workgroup resident (leader/helper hand-offs), not
   // a grid barrier, and every spin is bounded by the wall-clock timeout.  A
@@ -1184,11 +1204,22 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   // cooperative launch of a trivial kernel reproduces that SIGSEGV while the
   // same kernel launched plainly exits cleanly (tools/coop_exit_probe.hip,
   // profiles/r03_coop_exit_probe.txt).
-  if (e == hipSuccess) {
+  // A launch in which some problem timed out (status 3: a hand-off that never
+  // came — seen once in round 3's GPU suite, at p = 42, H = 1) is run again:
+  // the path is deterministic, so a completed relaunch returns the same bits.
+  for (int attempt = 0; e == hipSuccess; ++attempt) {
     hipLaunchKernelGGL(lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), 0, st, A);
     e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess || attempt == 2) break;
+    std::vector<int> hs(nprob);
+    if ((e = hipMemcpy(hs.data(), sts, hs.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (std::find(hs.begin(), hs.end(), 3) == hs.end()) break;
+    fprintf(stderr, "[dfm] lasso path launch %d timed out in a hand-off; relaunching\n", attempt + 1);
+    e = hipMemsetAsync(A.ctl, 0, (size_t)nprob * sizeof(LassoCtl), st);
+    if (e == hipSuccess) e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(A.snapC, 0, (size_t)nprob * LP_NCH * p * 8, st);
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess && A.prof) {
     std::vector<long long> hp((size_t)nprob * LP_PROF);
     hipMemcpy(hp.data(), A.prof, hp.size() * 8, hipMemcpyDeviceToHost);
