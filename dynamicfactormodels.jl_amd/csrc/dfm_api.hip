@@ -103,7 +103,8 @@ __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int6
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr, int subspace = 0);
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr, int subspace = 0,
+                     double spread = 0.0);
 size_t fact_workspace_bytes(int T, int nb, int P);
 int fact_t_max();
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
@@ -530,7 +531,14 @@ static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const do
   const size_t bytes = eig_workspace_bytes_padded(m, nb, P, ctx->maxit);
   char *ws = nullptr;   // stream-ordered pool memory: no device-wide sync in the free
   HIPCHK(ctx, hipMallocAsync((void **)&ws, bytes, ctx->stream));
-  int rc = eig_run(G, m, (int64_t)m * m, m, nb, k, p, warm, kw, ctx->tol, ctx->maxit, ctx->poll, ws,
+  // a single fit's eigenvectors are polished to the rounding floor (the
+  // residual rule at 1e-14; the floor and stagnation tests end it): statistics
+  // of the fit with a near-zero value (an LR of ~0.4 between two nearly equal
+  // SSRs) move by ~1e-10 relative when its eigenvectors stop at 1e-12 of the
+  // gap (a break fit's LR in tests/test_gpu_breaks.py: 4e-10 off the oracle;
+  // the tridiagonal path's inverse-iteration vectors: 9e-10)
+  const double tol = nb == 1 ? std::min(ctx->tol, 1e-14) : ctx->tol;
+  int rc = eig_run(G, m, (int64_t)m * m, m, nb, k, p, warm, kw, tol, ctx->maxit, ctx->poll, ws,
                    lam, Uk, trace, status_dev, nullptr, ctx->stream, timer_cb, ctx, 0);
   hipFreeAsync(ws, ctx->stream);
   hipStreamSynchronize(ctx->stream);
@@ -1331,9 +1339,13 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
     PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld, T};
     if (fact) {
       const double *et = kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr;
+      // the base fit's wanted-eigenvalue spread lambda_1 / lambda_r bounds the
+      // warm first filter's degree (eig_run_fact2_t)
+      const double spread = (M->lam.size() >= (size_t)r && r > 0 && M->lam[r - 1] > 0.0) ? M->lam[0] / M->lam[r - 1]
+                                                                                        : 0.0;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst,
-                                (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub);
+                                (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       Scope sc(ctx, DFM_KC_FACTORS);

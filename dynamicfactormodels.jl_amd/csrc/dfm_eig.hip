@@ -28,6 +28,7 @@ constexpr int EROWS = 64;  // rows per workgroup in gq/apply
 
 struct EigWork {
   double *Q, *Y, *U;       // nb x m x P
+  double *S;               // nb x m x P: the direct path's second Horner vector (filters of degree > 2)
   double *part;            // nb x nrb x 3 x P x P
   double *rpart;           // nb x nrb x P
   double *small;           // nb x SMALL_STRIDE (A, Bm, theta, dead)
@@ -254,13 +255,17 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   emit_partials<P, SQ>(sQ, sY, w.part + ((int64_t)rep * nrb + rb) * 3 * P * P);
 }
 
-// Chebyshev step of the direct path (the factored path's boot_cheb_kernel on
-// an explicit Gram): with V = Y Bm in w.Y and Q Bm in w.Q (eig_apply, cheb),
-// Qn = (8/b^2) G V - (8/b) V + Q Bm = T2(2G/b - 1) Q Bm, b = theta_p; dead
-// (re-randomised) columns keep V.  Rows of one 64-row block per workgroup.
+// One Horner step of the direct path's Chebyshev filter (the factored path's
+// boot_cheb_kernel on an explicit Gram): eig_apply leaves V0 = Q Bm in w.Q and
+// S_{d-1} = (a_d/b) G V0 + a_{d-1} V0 in w.Y; step i reads S_{i+1} (Sin, every
+// row) and writes S_i = G S_{i+1} / b + a_i V0 (Sout: w.S / w.Y alternately,
+// w.Q for S_0, the next basis; a thread reads its V0 entry before it writes
+// S_0 over it).  b = theta_p; dead (re-randomised) columns keep V0.  Rows of
+// one 64-row block per workgroup.
 template <int P>
 __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict__ G, int64_t ldg,
-                                                       int64_t strideG, EigWork w, int m, int p) {
+                                                       int64_t strideG, EigWork w, int m, int p,
+                                                       const double *Sin, double *Sout, double fai) {
   constexpr int SQ = P + 4;
   __shared__ __attribute__((aligned(16))) double sV[EROWS * SQ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -268,10 +273,12 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
   if (w.done[rep]) return;
   const double *small = w.small + (int64_t)rep * small_stride<P>();
   const double b = small[2 * P * P + p - 1];
-  const double c2 = b > 0.0 ? 8.0 / (b * b) : 0.0;
+  // b <= 0 (a degenerate block): plain power steps
+  const double cb = b > 0.0 ? 1.0 / b : 1.0, cv0 = b > 0.0 ? fai : 0.0;
   const double *Gr = G + (int64_t)rep * strideG;
-  const double *Vr = w.Y + (int64_t)rep * m * P;
-  double *Qr = w.Q + (int64_t)rep * m * P;
+  const double *Vr = Sin + (int64_t)rep * m * P;
+  double *So = Sout + (int64_t)rep * m * P;
+  const double *V0 = w.Q + (int64_t)rep * m * P;
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
   const int row0 = rb * EROWS + wave * 16;
   double acc[4][P / 4];
@@ -321,10 +328,10 @@ __global__ __launch_bounds__(256) void eig_cheb_kernel(const double *__restrict_
       const int row = rb * EROWS + lr;
       if (row < m) {
         const bool dead = small[2 * P * P + P + col] != 0.0;
-        const double x = Qr[(int64_t)row * P + col];   // c1 V + c0 Q Bm (eig_apply)
-        double qn = dead ? x : fma(c2, gv, x);
-        if (col >= p) qn = 0.0;
-        Qr[(int64_t)row * P + col] = qn;
+        const double v0 = V0[(int64_t)row * P + col];
+        double sn = dead ? v0 : fma(cb, gv, cv0 * v0);
+        if (col >= p) sn = 0.0;
+        So[(int64_t)row * P + col] = sn;
       }
     }
 }
@@ -630,7 +637,8 @@ template <int P>
 // cheb = 1: the next basis is formed by eig_cheb_kernel; here V = Y Bm goes
 // to w.Y and Q Bm to w.Q (both over this block's own rows, already staged).
 __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p, int k, int it,
-                                                        uint64_t seed, int64_t rep0, int cheb) {
+                                                        uint64_t seed, int64_t rep0, int cheb, double fa1,
+                                                        double fa0) {
   constexpr int SQ = P + 1;
   __shared__ double sQ[EROWS * SQ], sY[EROWS * SQ], sW[EROWS * P];
   __shared__ double sA[P * P], sB[P * P], sT[2 * P];
@@ -662,11 +670,12 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
     if (c < k) { const double wv = ya - sT[c] * u; sW[r * P + c] = row < m ? wv * wv : 0.0; }
     if (row < m) {
       Ur[(int64_t)row * P + c] = u;
-      if (cheb) {   // V, and X = c1 V + c0 Q Bm (dead columns: V) for eig_cheb_kernel
+      if (cheb) {   // the filter's first Horner term S = (a_d/b) V + a_{d-1} Q Bm, and V0 = Q Bm (dead: V)
         const double bch = sT[p - 1];
-        const double x = (c < p && sT[P + c] != 0.0) ? qn : (bch > 0.0 ? fma(-8.0 / bch, qn, qb) : qn);
-        Yr[(int64_t)row * P + c] = qn;
-        Qr[(int64_t)row * P + c] = c >= p ? 0.0 : x;
+        const bool dead = c < p && sT[P + c] != 0.0;
+        const double sv = dead ? qn : (bch > 0.0 ? fma(fa1 / bch, qn, fa0 * qb) : qn);
+        Yr[(int64_t)row * P + c] = c >= p ? 0.0 : sv;
+        Qr[(int64_t)row * P + c] = c >= p ? 0.0 : (dead ? qn : qb);
       } else {
         Qr[(int64_t)row * P + c] = qn;
       }
@@ -748,7 +757,7 @@ __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k,
 size_t eig_workspace_bytes(int m, int nb, int P, int maxit) {
   const int nrb = (m + EROWS - 1) / EROWS;
   size_t s = 0;
-  s += 3 * (size_t)nb * m * P * 8;               // Q, Y, U
+  s += 4 * (size_t)nb * m * P * 8;               // Q, Y, U, S
   s += (size_t)nb * nrb * 3 * P * P * 8;         // part
   s += (size_t)nb * nrb * P * 8;                 // rpart
   s += (size_t)nb * (2 * P * P + 4 * P) * 8;     // small
@@ -764,6 +773,7 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   w.Q = (double *)take((size_t)nb * m * P * 8);
   w.Y = (double *)take((size_t)nb * m * P * 8);
   w.U = (double *)take((size_t)nb * m * P * 8);
+  w.S = (double *)take((size_t)nb * m * P * 8);
   w.part = (double *)take((size_t)nb * nrb * 3 * P * P * 8);
   w.rpart = (double *)take((size_t)nb * nrb * P * 8);
   w.small = (double *)take((size_t)nb * (2 * P * P + 4 * P) * 8);
@@ -825,6 +835,9 @@ static int64_t count_rep_iters(const int *active_dev, int last, int shift, int n
   return s;
 }
 
+constexpr int kChebDMax = 8, kChebDirectStrict = 4;
+static void shifted_cheb(int d, double *a);
+
 // Solve nb problems.  Returns 0 ok, 1 not converged (status per replicate),
 // negative on bad args, or a hipError_t (>1000).
 template <int P>
@@ -849,9 +862,20 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   int it = 0;
   bool finished = false;
   std::vector<int> act;
-  const int cheb = 1;   // degree-2 Chebyshev filter between Rayleigh-Ritz steps
+  const int cheb = 1;   // Chebyshev filter between Rayleigh-Ritz steps
+  // degree: 4 for the first four filters of a warm-started batch or a single
+  // fit under the strict eigenvector rule (C2's Chow statistics: 8-9
+  // Rayleigh-Ritz steps with degree 2, 5 with degree 4 in tools/eig_proto.py),
+  // 2 for the polishing steps after them and for eigenvalue-only solves
+  // (single fits, nb = 1, too: cold-started, polished to 1e-14 by run_eig)
+  const bool warm_strict = tol >= 0.0 && ((warm && kw >= k) || nb == 1);
+  double ca4[kChebDMax + 1], ca2[kChebDMax + 1];
+  shifted_cheb(kChebDirectStrict, ca4);
+  shifted_cheb(2, ca2);
   int next_poll = poll;
   for (; it <= maxit; ++it) {
+    const int dg = warm_strict && it < 4 ? kChebDirectStrict : 2;
+    const double *ca = dg == 2 ? ca2 : ca4;
     const int check_only = (it == maxit);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
     hipLaunchKernelGGL(eig_gq_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, k,
@@ -862,8 +886,14 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, nrb, kJacobiSweeps);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0, cheb);
-    if (cheb) hipLaunchKernelGGL(eig_cheb_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, p);
+    hipLaunchKernelGGL(eig_apply_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, w, m, p, k, it, seed, rep0, cheb,
+                       ca[dg], ca[dg - 1]);
+    for (int j = 1; cheb && j < dg; ++j) {   // S_{dg-1-j}: in w.Y / w.S alternately, S_0 into w.Q
+      const double *sin = (j & 1) ? w.Y : w.S;
+      double *sout = j == dg - 1 ? w.Q : ((j & 1) ? w.S : w.Y);
+      hipLaunchKernelGGL(eig_cheb_kernel<P>, dim3(nrb, nb), dim3(256), 0, st, G, ldg, strideG, w, m, p, sin, sout,
+                         ca[dg - 1 - j]);
+    }
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it == next_poll) {
       int a = -1;
@@ -1756,7 +1786,6 @@ __global__ __launch_bounds__(1024) void active_list_kernel(const int *__restrict
 
 // Shifted Chebyshev coefficients T*_d(y) = T_d(2y - 1) = sum_i a_i y^i
 // (T*_0 = 1, T*_1 = 2y - 1, T*_{n+1} = 2 (2y - 1) T*_n - T*_{n-1}).
-constexpr int kChebDMax = 8;
 static void shifted_cheb(int d, double *a) {   // a[0..kChebDMax]
   double t0[kChebDMax + 1] = {1.0}, t1[kChebDMax + 1] = {-1.0, 2.0};
   if (d == 0) { for (int i = 0; i <= kChebDMax; ++i) a[i] = t0[i]; return; }
@@ -1781,13 +1810,24 @@ static void shifted_cheb(int d, double *a) {   // a[0..kChebDMax]
 // degree 2 on [0, theta_p].
 constexpr int kChebWarmD0 = 6, kChebD = 2;
 constexpr double kChebWarmBeta = 0.2;
+// The filter amplifies wanted eigenvalue lambda_1 over lambda_k by about
+// T_d(x_1) / T_d(x_k) ~ (x_1 / x_k)^d, x = 2 lambda / b - 1 (x_k = 9 at
+// b = 0.2 lambda_k): the filtered block's condition number.  Its degree is
+// capped so that stays below ~1e6 (CholQR2 keeps every wanted direction in
+// fp64): C3's lambda_1 / lambda_8 = 1.6 allows 6 (the cap); a panel with one
+// dominant factor (C2's base fit: lambda_1 / lambda_4 = 50) gets 3.
+static int first_filter_degree(double spread) {
+  const double ratio = std::max(1.0001, 1.1 * spread);
+  const int d = (int)std::floor(std::log(1e6) / std::log(ratio));
+  return std::max(kChebD, std::min(kChebWarmD0, d));
+}
 
 template <int P>
 static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                            char *fws, double *lam, double *Uk, double *trace_out, int *status,
                            hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst, long long *cnt,
-                           int subspace) {
+                           int subspace, double spread) {
   const int m = fb.T;
   EigWork w = carve(ws, m, nb, P, maxit);
   w.subspace = subspace;
@@ -1828,8 +1868,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
                        off, lst, qin, qs, alt, Zc, ldz, ab, seed);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  const bool warm_started = warm && kw >= k;
-  const int d0 = warm_started ? kChebWarmD0 : kChebD;
+  const bool warm_started = warm && kw >= k && spread >= 1.0;
+  const int d0 = warm_started ? first_filter_degree(spread) : kChebD;
   const double beta0 = warm_started ? kChebWarmBeta : 0.0;
   double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
   shifted_cheb(d0, ca0);
@@ -1919,14 +1959,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt, int subspace) {
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt, int subspace, double spread) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
   if (fb.r > 16 || fb.T > F2_T_MAX) return -1;   // callers take the direct path
   if (p <= 16)
     return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                               trace_out, status, st, tf, tctx, off, lst, cnt, subspace);
+                               trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread);
   return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                             trace_out, status, st, tf, tctx, off, lst, cnt, subspace);
+                             trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread);
 }
 int fact_t_max() { return F2_T_MAX; }
 

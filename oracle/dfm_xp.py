@@ -356,3 +356,26 @@ def lm_referee(F, Ei, bp: int) -> float:
     ee = (E * E).sum()
     vv = (v * v).sum()
     return float((((ee - vv) / ee) * float(T)).f64())
+
+
+def lr_referee(F, xi, Ei, bp: int) -> float:
+    """LR_test (src/chowtest.jl:19-23) of one variable in double-double from
+    fp64 inputs F (T x r, the fit's vcat(F_j)), x_i (the data column) and E_i
+    (the factor residual column): T (log |E_i|^2 - log(SSR_1 + SSR_2)), SSR_j
+    the residual sum of squares of x_i on F over rows < bp / >= bp
+    (residuals_subperiods, :4-13).  A near-zero LR (the two sums nearly equal)
+    is where the fp64 oracle's projections lose relative accuracy."""
+    F = np.asarray(F, dtype=np.float64)
+    xi = np.asarray(xi, dtype=np.float64)
+    T = F.shape[0]
+    ssr = None
+    for a, b in ((0, bp), (bp, T)):
+        X = DD(F[a:b])
+        y = DD(xi[a:b][:, None])
+        beta = dd_inv(X.T @ X) @ (X.T @ y)
+        e = y - X @ beta
+        s2 = (e * e).sum()
+        ssr = s2 if ssr is None else ssr + s2
+    E = DD(np.asarray(Ei, dtype=np.float64)[:, None])
+    ee = (E * E).sum()
+    return float(T * dd_log(ee / ssr))

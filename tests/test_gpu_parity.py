@@ -47,6 +47,29 @@ def lm_within(got, d, bp, vs, oracle, gm=None):
         assert abs(g - ref_g) <= STAT_RTOL * abs(ref_g), (i, g, ref, ref_g, orc)
 
 
+def lr_within(got, d, bp, vs, oracle, gm=None):
+    """LR_test values `got` (variables vs, 0-based) of fit d against the
+    double-double referee (oracle/dfm_xp.py lr_referee): within 1e-10 of it,
+    or no further from it than the oracle's fp64 projections are; else (gm,
+    the engine's own fit of the same panel) within 1e-10 of the exact LR of
+    the engine's F and E_i.  A near-zero LR (two nearly equal SSRs: 0.39 in a
+    break fit of tests/test_gpu_breaks.py) moves ~1e-9 relative between fits
+    whose eigenvectors agree to ~1e-13, and the fp64 oracle itself sits ~1e-9
+    from the exact value there; the factors are held to ANGLE_TOL elsewhere."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import dfm_xp
+    for g, i in zip(np.atleast_1d(got), vs):
+        ref = dfm_xp.lr_referee(d.F, d.x[:, i], d.factor_residuals[:, i], bp)
+        orc = oracle.LR_test(d, bp, i)
+        floor = d.F.shape[0] * 1e-14
+        if abs(g - ref) <= max(STAT_RTOL * abs(ref), abs(orc - ref), floor):
+            continue
+        assert gm is not None, (i, g, ref, orc)
+        ref_g = dfm_xp.lr_referee(gm.F, gm.x[:, i], gm.factor_residuals[:, i], bp)
+        assert abs(g - ref_g) <= max(STAT_RTOL * abs(ref_g), floor), (i, g, ref, ref_g, orc)
+
+
 def max_sin_angle(A, B):
     """sin of the largest principal angle between span(A) and span(B)."""
     Qa, _ = np.linalg.qr(A)

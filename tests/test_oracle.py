@@ -317,6 +317,8 @@ def test_xp_referee_pins_the_oracle(oracle):
         ref = np.array([[oracle.LR_test(o, T // 2, i), oracle.LM_test(o, T // 2, i), oracle.Wald_test(o, T // 2, i)]
                         for i in range(N)])
         assert np.allclose(np.column_stack([LR, LM, W]), ref, rtol=1e-11, atol=0)
+        lr1 = [XP.lr_referee(o.F, o.x[:, i], o.factor_residuals[:, i], T // 2) for i in range(N)]
+        assert np.allclose(lr1, ref[:, 0], rtol=1e-11, atol=0)
 
 
 def test_xp_fixture_agrees_with_golden():

@@ -30,7 +30,7 @@ def shifted_cheb(d):
     return t1
 
 
-def solve(G, Q0, degs, k=R, tol=1e-12, maxit=12, beta=0.0):
+def solve(G, Q0, degs, k=R, tol=1e-12, maxit=30, beta=0.0, strict=False):
     Q = Q0.copy()
     tr = np.trace(G)
     prods = 0
@@ -51,11 +51,16 @@ def solve(G, Q0, degs, k=R, tol=1e-12, maxit=12, beta=0.0):
         gap = np.full(P, np.inf)
         gap[1:] = np.minimum(gap[1:], np.abs(th[1:] - th[:-1]))
         gap[:-1] = np.minimum(gap[:-1], np.abs(th[:-1] - th[1:]))
-        bnd = res2[:k] / (0.5 * gap[:k])
-        ok = np.all((bnd <= tol * np.abs(th[:k])) | (np.sqrt(res2[:k]) <= 2e-14 * th[0]))
-        vnum = max(abs(tr - th[:k].sum()), 1e-6 * abs(tr))
-        if ok and bnd.sum() <= tol * vnum:
-            return it + 1, prods
+        if strict:   # subspace rule: res_j <= tol |theta_j - theta_k|
+            res = np.sqrt(res2[:k])
+            if np.all((res <= tol * np.abs(th[:k] - th[k])) | (res <= 2e-14 * th[0])):
+                return it + 1, prods
+        else:
+            bnd = res2[:k] / (0.5 * gap[:k])
+            ok = np.all((bnd <= tol * np.abs(th[:k])) | (np.sqrt(res2[:k]) <= 2e-14 * th[0]))
+            vnum = max(abs(tr - th[:k].sum()), 1e-6 * abs(tr))
+            if ok and bnd.sum() <= tol * vnum:
+                return it + 1, prods
         ZZ = A.T @ (Y.T @ Y) @ A
         L2 = np.linalg.cholesky(0.5 * (ZZ + ZZ.T))
         Bm = A @ np.linalg.inv(L2).T
@@ -79,9 +84,27 @@ def solve(G, Q0, degs, k=R, tol=1e-12, maxit=12, beta=0.0):
 def main():
     nrep = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     scheds = sys.argv[2:] or ["r8:2", "w16:2", "w16:3,2", "w16:4,2", "w24:2"]
-    rng = np.random.default_rng(20261015 + 3)
-    y, x, *_ = host.factor_model_DGP(T, N, R, rng=rng)
+    global T, N, R
+    c2 = os.environ.get("SHAPE") in ("c2", "c1")
+    c1 = os.environ.get("SHAPE") == "c1"
+    strict = c2 or os.environ.get("STRICT") == "1"
+    if c1:   # tools/bench_configs.py c1: T = 200, N = 100, r = 3 (the fit itself: one Gram)
+        T, N = 200, 100
+        rng = np.random.default_rng(20261015 + 1)
+        y, x, *_ = host.factor_model_DGP(T, N, 3, rng=rng)
+        R = 3
+    elif c2:   # tools/bench_configs.py c2: T = 600, N = 130, Breitung-Eickmeier DGP, r = 4 (ICp2)
+        T, N = 600, 130
+        rng = np.random.default_rng(20261015 + 2)
+        y, x, *_ = host.factor_model_DGP(T, N, 3, model="Breitung_Eickmeier_2011", b=0.5, rng=rng)
+        R = int(os.environ.get("R", "4"))
+    else:
+        rng = np.random.default_rng(20261015 + 3)
+        y, x, *_ = host.factor_model_DGP(T, N, R, rng=rng)
     x = host.normalize(x)
+    if c2:   # T >= N: the N x N Gram, eigenvectors = loadings directions
+        x = x.T
+        T, N = N, T
     G0 = x @ x.T
     lam, Uall = np.linalg.eigh(G0)
     Uall = Uall[:, ::-1]
@@ -89,12 +112,16 @@ def main():
     Lb = x.T @ F / T
     C = F @ Lb.T
     E = x - C
-    idx, eta = host.draw_wild_fast(1_000_003, nrep, T)
+    Tr = x.shape[1] if c2 else T   # rows resampled: the panel's time dimension
+    idx, eta = host.draw_wild_fast(1_000_003, nrep, Tr)
     hrng = np.random.default_rng(5)
     rnd = hrng.uniform(-1, 1, size=(T, P))
     Gs = []
     for b in range(nrep):
-        Xs = C + eta[b][:, None] * E[idx[b]]
+        if c2:   # rows of the T x N panel are columns here
+            Xs = C + eta[b][None, :] * E[:, idx[b]]
+        else:
+            Xs = C + eta[b][:, None] * E[idx[b]]
         Gs.append(Xs @ Xs.T)
     for sc in scheds:
         start, degs = sc.split(":")
@@ -105,7 +132,14 @@ def main():
             beta = float(beta)
         kw = int(start[1:])
         Q0 = np.hstack([Uall[:, :min(kw, P)], rnd[:, min(kw, P):]]) if start[0] in "rw" else None
-        its, prs = zip(*[solve(G, Q0, degs, beta=beta) for G in Gs])
+        res = []
+        for G in Gs:
+            try:
+                res.append(solve(G, Q0, degs, k=R, beta=beta, strict=strict,
+                                 tol=float(os.environ.get("TOL", "1e-12"))))
+            except np.linalg.LinAlgError:
+                res.append((99, 99))
+        its, prs = zip(*res)
         print(f"{sc:12s} RR steps mean {np.mean(its):.2f} max {max(its)}  products mean {np.mean(prs):.2f}"
               f"  hist {dict(zip(*np.unique(its, return_counts=True)))}")
 
