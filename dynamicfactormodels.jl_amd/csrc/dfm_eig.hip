@@ -964,7 +964,8 @@ struct FactBase {
 // sum_t [F_t S F_t' + 2 eta_t F_t.(EL)_idx_t + eta_t^2 H_idx_t,idx_t].
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta, int *__restrict__ off,
-                                                        int *__restrict__ lst, double *__restrict__ trace) {
+                                                        int *__restrict__ lst, double *__restrict__ trace,
+                                                        double *__restrict__ PF, double *__restrict__ E2) {
   extern __shared__ int sh[];   // cnt[T+1], six[T]
   __shared__ double red[256];
   __shared__ int scan[256];
@@ -1009,6 +1010,37 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       L[j + 1] = v;
     }
   }
+  if (PF)   // P'D F (row stride r) and P'D^2 1 of the middle Horner steps (boot_cheb_mid_kernel):
+    for (int s = tid; s < T; s += 256) {   // this thread's own sorted buckets, t ascending
+      const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
+      double a[16], a2 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] = 0.0;
+      for (int q = b0; q < b1; ++q) {
+        const int t = L[q];
+        const double h = et ? et[t] : 1.0;
+        a2 = fma(h, h, a2);
+        if ((r & 1) == 0) {   // 16-B loads of the F row (F rows start 16-B aligned)
+          const double2 *f2 = reinterpret_cast<const double2 *>(fb.F + (int64_t)t * r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (2 * j < r) {
+              const double2 f = f2[j];
+              a[2 * j] = fma(h, f.x, a[2 * j]);
+              a[2 * j + 1] = fma(h, f.y, a[2 * j + 1]);
+            }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (j < r) a[j] = fma(h, fb.F[(int64_t)t * r + j], a[j]);
+        }
+      }
+      double *pf = PF + ((int64_t)rep * T + s) * r;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < r) pf[j] = a[j];
+      E2[(int64_t)rep * T + s] = a2;
+    }
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
     const int i = ix[t];
@@ -1033,10 +1065,17 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
 // Z (the GEMM's B operand) has round_up(T, 16) rows, the pad rows zero, so
 // the H.Z GEMM streams it with running DMA pointers and no k-tail clamp
 static int64_t z_rows(int T) { return ((int64_t)T + 15) / 16 * 16; }
+// the middle Horner steps' per-replicate operands (boot_cheb_mid_kernel):
+// PF = P'D F (T x r, allocated T x 16), e2 = P'D^2 1 (T), FV = F'V0 (16 x P),
+// and F'F (16 x 16, shared)
+static size_t fact_mid_doubles(int T, int nb, int P) {
+  return (size_t)nb * T * 17 + (size_t)nb * 16 * P + 256;
+}
 size_t fact_workspace_bytes(int T, int nb, int P) {
   const int64_t ldz = (int64_t)nb * P;
   const int nrb = (T + EROWS - 1) / EROWS;
-  return (size_t)(z_rows(T) + T) * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096;
+  return (size_t)(z_rows(T) + T) * ldz * 8 + (size_t)nb * nrb * 2 * 32 * P * 8 + 4096 +
+         fact_mid_doubles(T, nb, P) * 8 + 4096;
 }
 
 // ================================================= fused factored iteration
@@ -1760,6 +1799,258 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, rep, ab, aacc, sred);
 }
 
+// The middle Horner steps in row-local form.  With W = G* S_{i+1} = F bB +
+// D P u (bB = S a + cc, u = EL a + HZ, a / cc of S_{i+1}) and S_i = W / b +
+// a_i V0, the next GEMM operand and the step's reductions need no S_i rows:
+//   Z_i = P'D S_i = (PF bB + e2 . u) / b + a_i PV,
+//   a_i = F'S_i   = (F'F bB + PF'u) / b + a_i FV,     cc_i = EL'Z_i,
+// with PF = P'D F, e2 = P'D^2 1 (boot_prep_kernel, once per solve), PV = P'D V0
+// and FV = F'V0 (ap2, once per filter).  Every row s reads HZ[s], PV[s],
+// PF[s], e2[s], EL[s] and writes Z[s]: no CSR gather, no S_i write and
+// re-read, no barrier between the two (the last step, which must hand S_0 to
+// the next Rayleigh-Ritz step, stays boot_cheb_kernel).  Columns that
+// deflated (dd) carry V0: Z = PV, a = FV; columns >= p are zero.
+// F'F (16 x 16, rows / columns >= r zero), one workgroup: four row quarters
+// per entry (t ascending in each), summed in a fixed order
+__global__ __launch_bounds__(1024) void ftf_kernel(FactBase fb, double *__restrict__ FtF) {
+  __shared__ double part[4][256];
+  const int e = threadIdx.x & 255, q = threadIdx.x >> 8, j = e >> 4, i = e & 15, r = fb.r;
+  const int t0 = q * ((fb.T + 3) / 4), t1 = min(fb.T, t0 + (fb.T + 3) / 4);
+  double acc = 0.0;
+  if (j < r && i < r)
+    for (int t = t0; t < t1; ++t) acc = fma(fb.F[(int64_t)t * r + j], fb.F[(int64_t)t * r + i], acc);
+  part[q][e] = acc;
+  __syncthreads();
+  if (q == 0) FtF[e] = (part[0][e] + part[1][e]) + (part[2][e] + part[3][e]);
+}
+
+// fixed-order sum over the waves of a 16 x P accumulator block -> dst (row-major, stride P)
+template <int P>
+DFM_DEV void wave_block_store(const dv4 *acc, double *sred, int wave, int lane, int tid, double *__restrict__ dst) {
+  constexpr int NT = P / 16;
+  for (int wv = 0; wv < BW; ++wv) {
+    if (wave == wv)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int e = (ct * 4 + g) * 64 + lane;
+          sred[e] = (wv ? sred[e] : 0.0) + acc[ct][g];
+        }
+    __syncthreads();
+  }
+  if (dst)
+    for (int e = tid; e < NT * 256; e += 64 * BW) {
+      const int l = e & 63, g = (e >> 6) & 3, ct = e >> 8;
+      dst[(4 * g + (l >> 4)) * P + 16 * ct + (l & 15)] = sred[e];
+    }
+}
+
+// PV = P'D V0 and FV = F'V0 for a filter with middle steps, launched between
+// the Rayleigh-Ritz step's eig_small and ap2: V0 = Q Bm is linear in Q, so
+// PV = Z(Q) Bm and FV = a(Q) Bm from the Z = P'D Q and a = F'Q that the
+// previous step left in Zc / ab (ap2 overwrites both) — row-local, no CSR
+// gather of V0.  Columns that ap2 refills (dead pivots: V0 = hash_unit) take
+// the explicit sums over their buckets / rows.
+template <int P>
+__global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWork w, int T, int p, int it,
+                                                      const double *__restrict__ eta, const int *__restrict__ off,
+                                                      const int *__restrict__ lst, const double *__restrict__ Zc,
+                                                      int64_t ldz, const double *__restrict__ ab, uint64_t seed,
+                                                      double *__restrict__ PV, double *__restrict__ FV) {
+  constexpr int NT = P / 16, KP = P / 4;
+  const int rep = blockIdx.x;
+  if (w.done[rep]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  const double *small = w.small + (int64_t)rep * small_stride<P>();
+  const uint64_t hc = 1000003ull * (it + 1);
+  double bBm[KP][NT];
+  bool dd[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) {
+    const int c = 16 * ct + li;
+    dd[ct] = small[2 * P * P + P + c] != 0.0;
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) bBm[kk][ct] = small[P * P + (4 * kk + lk) * P + c];
+  }
+  const double *et = eta ? eta + (int64_t)rep * T : nullptr;
+  const int *o = off + (int64_t)rep * (T + 1);
+  const int *L = lst + (int64_t)rep * T;
+  double *pvr = PV + (int64_t)rep * T * P;
+  const int ntile = (T + 15) >> 4;
+  for (int tile = wave; tile < ntile; tile += BW) {
+    const int t0 = tile * 16, ta = min(t0 + li, T - 1);
+    double za[KP];
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk) za[kk] = t0 + li < T ? Zc[(int64_t)ta * ldz + (int64_t)rep * P + 4 * kk + lk] : 0.0;
+    dv4 v[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) v[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < KP; ++kk)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) v[ct] = mfma16(za[kk], bBm[kk][ct], v[ct]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = t0 + 4 * g + lk;
+      if (s < T)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const int c = 16 * ct + li;
+          double x = v[ct][g];
+          if (c < p && dd[ct]) {   // refilled column: sum over bucket s (t ascending)
+            x = 0.0;
+            for (int q = o[s]; q < o[s + 1]; ++q) {
+              const int t = L[q];
+              x = fma(et ? et[t] : 1.0, hash_unit(seed, t, hc + c), x);
+            }
+          }
+          if (c >= p) x = 0.0;
+          pvr[(int64_t)s * P + c] = x;
+        }
+    }
+  }
+  const double *aq = ab + (int64_t)rep * 32 * P;
+  double *fvr = FV + (int64_t)rep * 16 * P;
+  for (int e = tid; e < 16 * P; e += 64 * BW) {
+    const int j = e / P, c = e % P;
+    double x = 0.0;
+    if (j < r && c < p) {
+      if (small[2 * P * P + P + c] != 0.0) {
+        for (int t = 0; t < T; ++t) x = fma(fb.F[(int64_t)t * r + j], hash_unit(seed, t, hc + c), x);
+      } else {
+        for (int i = 0; i < P; ++i) x = fma(aq[j * P + i], small[P * P + i * P + c], x);
+      }
+    }
+    fvr[e] = x;
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, EigWork w, int T, int p,
+                                                            const double *__restrict__ HZ, int64_t ldz,
+                                                            double *__restrict__ ab, double fai, double bbeta, int k,
+                                                            const double *__restrict__ PF,
+                                                            const double *__restrict__ E2,
+                                                            const double *__restrict__ PV,
+                                                            const double *__restrict__ FV,
+                                                            const double *__restrict__ FtF,
+                                                            double *__restrict__ Zc) {
+  constexpr int NT = P / 16;
+  const int rep = blockIdx.x;
+  if (w.done[rep]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
+  const int li = lane & 15, lk = lane >> 4;
+  __shared__ double sa[16 * P], sb[16 * P];
+  __shared__ double sred[NT * 256];
+  double *abr = ab + (int64_t)rep * 32 * P;
+  for (int e = tid; e < 16 * P; e += 64 * BW) sa[e] = abr[e];
+  __syncthreads();
+  for (int e = tid; e < 16 * P; e += 64 * BW) {
+    const int j = e / P, c = e % P;
+    double v = abr[16 * P + e];
+    if (j < r)
+      for (int i = 0; i < r; ++i) v = fma(fb.S[j * r + i], sa[i * P + c], v);
+    sb[e] = v;
+  }
+  __syncthreads();
+  const double *small = w.small + (int64_t)rep * small_stride<P>();
+  const double b = filter_end<P>(small, k, p, bbeta);
+  const double cb = b > 0.0 ? 1.0 / b : 1.0, cv0 = b > 0.0 ? fai : 0.0;
+  bool dd[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) dd[ct] = small[2 * P * P + P + 16 * ct + li] != 0.0;
+  const int KR = (r + 3) >> 2;
+  const double *pfr = PF + (int64_t)rep * T * r, *e2r = E2 + (int64_t)rep * T, *pvr = PV + (int64_t)rep * T * P;
+  dv4 aacc[NT], cacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) { aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; cacc[ct] = aacc[ct]; }
+  const int ntile = (T + 15) >> 4;
+  for (int tile = wave; tile < ntile; tile += BW) {
+    const int t0 = tile * 16;
+    const int ta = min(t0 + li, T - 1);
+    double pA[4], eA[4], hz[NT][4], pv[NT][4], e2v[4], pfa[4], ea[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int j = 4 * kk + lk;
+      const bool ok = kk < KR && j < r && t0 + li < T;
+      pA[kk] = ok ? pfr[(int64_t)ta * r + j] : 0.0;
+      eA[kk] = ok ? fb.EL[(int64_t)ta * r + j] : 0.0;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = t0 + 4 * g + lk;
+      const bool v = s < T;
+      const int sc = min(s, T - 1);
+      e2v[g] = v ? e2r[sc] : 0.0;
+      pfa[g] = (v && li < r) ? pfr[(int64_t)sc * r + li] : 0.0;
+      ea[g] = (v && li < r) ? fb.EL[(int64_t)sc * r + li] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const int c = 16 * ct + li;
+        hz[ct][g] = HZ[(int64_t)sc * ldz + (int64_t)rep * P + c];
+        pv[ct][g] = pvr[(int64_t)sc * P + c];
+      }
+    }
+    dv4 yP[NT], yE[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) { yP[ct] = dv4{0.0, 0.0, 0.0, 0.0}; yE[ct] = yP[ct]; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < KR) {   // B operands a / bB from LDS (registers are this kernel's limit)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          yP[ct] = mfma16(pA[kk], sb[(4 * kk + lk) * P + 16 * ct + li], yP[ct]);
+          yE[ct] = mfma16(eA[kk], sa[(4 * kk + lk) * P + 16 * ct + li], yE[ct]);
+        }
+      }
+    }
+    double uv[NT][4], zv[NT][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = t0 + 4 * g + lk;
+      const bool v = s < T;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const int c = 16 * ct + li;
+        const double u = yE[ct][g] + hz[ct][g];
+        double z = dd[ct] ? pv[ct][g] : fma(cb, fma(e2v[g], u, yP[ct][g]), cv0 * pv[ct][g]);
+        if (c >= p || !v) z = 0.0;
+        uv[ct][g] = v ? u : 0.0;
+        zv[ct][g] = z;
+        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + c] = z;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        aacc[ct] = mfma16(pfa[g], uv[ct][g], aacc[ct]);
+        cacc[ct] = mfma16(ea[g], zv[ct][g], cacc[ct]);
+      }
+  }
+  // a_i = (F'F bB + PF'u) / b + a_i FV  (dd columns: FV; columns >= p: 0)
+  wave_block_store<P>(aacc, sred, wave, lane, tid, nullptr);
+  const double *fvr = FV + (int64_t)rep * 16 * P;
+  for (int e = tid; e < 16 * P; e += 64 * BW) {
+    const int j = e / P, c = e % P;
+    const int ct = c >> 4, l = ((j & 3) << 4) | (c & 15), g = j >> 2;
+    double a = 0.0;
+    if (j < r && c < p) {
+      if (small[2 * P * P + P + c] != 0.0) a = fvr[e];
+      else {
+        double f = 0.0;
+        for (int i = 0; i < r; ++i) f = fma(FtF[j * 16 + i], sb[i * P + c], f);
+        a = fma(cb, f + sred[(ct * 4 + g) * 64 + l], cv0 * fvr[e]);
+      }
+    }
+    abr[e] = a;
+  }
+  __syncthreads();
+  wave_block_store<P>(cacc, sred, wave, lane, tid, abr + 16 * P);
+}
+
 // Ascending list of the still-active replicates (done == 0) and their count,
 // one 1024-thread workgroup: per-thread chunk counts, an LDS scan, in-order
 // writes.  Feeds the compacted H.Z GEMM of the straggler phase.
@@ -1835,6 +2126,9 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)z_rows(m) * ldz;
   double *ab = HZ + (size_t)m * ldz;
+  // middle Horner steps' operands (fact_mid_doubles), after ab's region
+  double *PFb = ab + (size_t)nb * ((m + EROWS - 1) / EROWS) * 2 * 32 * P + 512;
+  double *E2b = PFb + (size_t)nb * m * 16, *FVb = E2b + (size_t)nb * m, *FtF = FVb + (size_t)nb * 16 * P;
   if (z_rows(m) > m) hipMemsetAsync(Zc + (size_t)m * ldz, 0, (size_t)(z_rows(m) - m) * ldz * 8, st);
   const size_t lds = (size_t)m * 8 + (size_t)(2 * m + 1) * 4;
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
@@ -1855,6 +2149,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   struct Q0Free { double *q; hipStream_t s; ~Q0Free() { hipFreeAsync(q, s); } } q0free{Q0, st};
   const double *qin = Q0;
   int64_t qs = 0;
+  const bool warm_started = warm && kw >= k && spread >= 1.0;
+  const int d0 = warm_started ? first_filter_degree(spread) : kChebD;
+  // a first filter of degree >= 3 has middle Horner steps (boot_cheb_mid_kernel)
+  const bool mid = d0 >= 3;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   {
     const int64_t n = (int64_t)m * P;
@@ -1862,14 +2160,13 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0);
     hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
-                       off, lst, w.trace);
+                       off, lst, w.trace, mid ? PFb : nullptr, E2b);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
                        0.0, 0.0, eta,
                        off, lst, qin, qs, alt, Zc, ldz, ab, seed);
   }
+  if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  const bool warm_started = warm && kw >= k && spread >= 1.0;
-  const int d0 = warm_started ? first_filter_degree(spread) : kChebD;
   const double beta0 = warm_started ? kChebWarmBeta : 0.0;
   double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
   shifted_cheb(d0, ca0);
@@ -1894,6 +2191,9 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, kJacobiSweeps);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 0);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
+    if (mid && it == 0 && it < maxit - 1)   // before ap2 overwrites Z(Q) and a(Q)
+      hipLaunchKernelGGL(boot_pv_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, it, eta, off, lst, Zc, ldz,
+                         ab, seed, w.S, FVb);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
                        it == maxit - 1 ? 1 : 0, cheb, ca[dg], ca[dg - 1], bb, eta, off, lst, qin, qs, alt, Zc, ldz,
                        ab, seed);
@@ -1924,8 +2224,12 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
         if (tf) tf(tctx, DFM_KC_GEMM, 0);
         if (e != hipSuccess) return 1000 + (int)e;
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
-        hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4, st,
-                           fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[dg - sp], bb, k, cur, Zc);
+        if (mid && it == 0 && sp < dg)
+          hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, ab,
+                             ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, FtF, Zc);
+        else
+          hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
+                             st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[dg - sp], bb, k, cur, Zc);
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
       }
       last_cheb = it;
