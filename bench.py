@@ -186,17 +186,23 @@ def hbm_rooflines(timing, eig, Bn, steps):
                              reads Q and HZ[idx], writes Y = 3 T P 8 B per Rayleigh-Ritz step
       ap2 (class eig_apply): 5 T P 8 B per pass (Q, Y in; the filter's first Horner term S,
                              V0 = Q Bm and Z out); passes = Rayleigh-Ritz steps + one init per replicate
-      Chebyshev (Horner) step (class eig_apply): 4 T P 8 B per pass (HZ[idx], V0 in; S, Z out);
-                             passes = GEMM products - Rayleigh-Ritz steps
+      last Horner step of a filter (boot_cheb_kernel, class eig_apply): 5 T P 8 B per pass
+                             (HZ[idx], V0 in; S written and re-read by the CSR gather, Z out);
+                             passes = one per filter = Rayleigh-Ritz steps - replicates
+      middle Horner steps (boot_cheb_mid_kernel, class eig_apply): (2 P + r + 1) T 8 B in
+                             (HZ, PV, PF, e2 rows) + T P 8 B out (Z); passes = the other
+                             GEMM products after the Rayleigh-Ritz ones
     Replicate-passes come from the library's own counters (eig_iterations)."""
     P = 16
     out = []
     rr = eig.get("replicate_iterations", 0)
     cheb = max(eig.get("gemm_products", 0) - rr, 0)
+    last = max(min(rr - Bn * steps, cheb), 0)
     tp8 = T * P * 8
     for cls, name, parts in (
             ("eig_gq", "boot_y2_kernel", ((3 * tp8, rr),)),
-            ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel", ((5 * tp8, rr + Bn * steps), (4 * tp8, cheb)))):
+            ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel + boot_cheb_mid_kernel",
+             ((5 * tp8, rr + Bn * steps), (5 * tp8, last), ((2 * P + R + 1) * T * 8 + tp8, cheb - last)))):
         ms, n = timing.get(cls, (0.0, 0))
         units = sum(u for _, u in parts)
         if not n or not units:
@@ -403,7 +409,9 @@ def main():
         "stopping_rule": "eigenvector residual (strict)" if args.strict else
                          "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
         "eig_iterations": eig,
-        "eig_filter": "degree-2 Chebyshev filter on [0, theta_p] between Rayleigh-Ritz steps",
+        "eig_filter": ("Chebyshev filters in Horner form: degree 6 on [0, max(theta_p, 0.2 theta_k)] after the "
+                       "first Rayleigh-Ritz step of the warm start (middle steps row-local), degree 2 on "
+                       "[0, theta_p] after later ones"),
         "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps),
     }
     if weak:

@@ -15,7 +15,7 @@ step() {   # name, timeout, command...
   return 0
 }
 if [ -z "$SKIP_TESTS" ]; then
-  step pytest 900 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 180 --timeout-method thread -p no:cacheprovider
+  step pytest 900 python -u -m pytest tests -m gpu -v --maxfail=20 --timeout 100 --timeout-method thread -p no:cacheprovider
   tail -8 "$OUT/pytest.out"
 fi
 step bench 300 python -u bench.py --steps 20 --warmup 5

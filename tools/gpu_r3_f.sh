@@ -11,7 +11,7 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -30 "$OUT/$name.err"; exit $rc; fi
   return 0
 }
-step pytest 600 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 200 --timeout-method thread -p no:cacheprovider
+step pytest 600 python -u -m pytest tests -m gpu -v --maxfail=20 --timeout 100 --timeout-method thread -p no:cacheprovider
 tail -4 "$OUT/pytest.out"
 for R in 1250 2500 9999; do
   step b$R 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --replicates $R
