@@ -208,6 +208,7 @@ struct LassoArgs {
   double *bpath, *rsq_out;
   int *nlam_out, *status;
   long long tmo;    // spin timeout, wall-clock ticks (100 MHz)
+  long long tmo_path;   // whole-path budget of a leader, wall-clock ticks
   long long *prof;  // diagnostics (nullable): [nprob][8] leader wall-clock ticks per phase + counts
 };
 
@@ -406,6 +407,18 @@ DFM_DEV void lp_post(int *f, int v) {   // after this wave's LDS writes
   lp_lds_fence();
   if ((threadIdx.x & 63) == 0) *(volatile int *)f = v;
 }
+// waves 1..7 leave a sweep at the block wave 0 stopped at (pp->stop, set
+// before pub(k + 1)) — at or past it, never only AT it: once a spin has timed
+// out (pp->err) the waits return at once and these waves can run ahead of
+// wave 0, and an equality test they have passed would keep them in the
+// unbounded (!ORD) loop with nothing left to wait on — or as soon as the
+// launch is failing
+template <bool ORD>
+DFM_DEV bool lp_sweep_over(const LpPipe *pp, int k) {
+  if (((const volatile int *)&pp->err)[0]) return true;
+  const int stp = ((const volatile int *)&pp->stop)[0];
+  return !ORD && stp > 0 && stp <= k + 1;
+}
 DFM_DEV int lp_min_cons(const LpPipe *pp, int w0) {
   const volatile int *c = pp->cons;
   int m = INT_MAX;
@@ -453,7 +466,8 @@ template <bool ORD>
 DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, int &gkey, const double *GAA, int ldaa,
                       const int *s_ia, double *s_g, double *s_a, const int *s_rank, double *s_dr, double *s_gmr,
                       double *s_gb, LpPipe *pp, double *s_sc, int *s_nc, int *kl, double *dl, double *snapL,
-                      double *snapR, long long tmo, long long *tk, int maxsw = 1, double thr = 0.0) {
+                      double *snapR, long long tmo, long long *tk, int maxsw = 1, double thr = 0.0,
+                      long long tpath0 = 0, long long tmo_path = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (n <= 0) return;
   if (gkey != key || bstart != 0) {
@@ -537,14 +551,25 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
 #pragma unroll
           for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
           ++sw;
-          last = mx < thr || sw >= maxsw;
-          if (lane == 0) { s_sc[1] = mx; pp->nsw = sw; if (last) pp->stop = k + 1; }
+          // the leader's whole-path budget (tmo_path): fail like a timed-out hand-off
+          const bool over = tmo_path > 0 &&
+                            __builtin_amdgcn_readfirstlane((int)(wall_clock64() - tpath0 > tmo_path)) != 0;
+          last = mx < thr || sw >= maxsw || over;
+          if (lane == 0) {
+            s_sc[1] = mx; pp->nsw = sw;
+            if (last) pp->stop = k + 1;
+            if (over) ((volatile int *)&pp->err)[0] = 1;
+          }
           dlx_s = 0.0;
         }
       }
       lp_post(&pp->pub, k + 1);
       if (tk && tid == 0) { tk[6] += wall_clock64() - t1; tk[2] += 1; }
       if (last) break;
+      if (*(volatile int *)&pp->err) {   // a spin timed out: the launch is failing (status 3)
+        if (lane == 0) *(volatile int *)&pp->stop = k + 1;
+        break;
+      }
     }
   } else if (wave == 1) {
     // ------------------------------------------------ next block first, R^2
@@ -614,9 +639,8 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
         }
       }
       if (ORD && lane == 0) snapR[bn * 4 + 0] = rsq;
-      const bool fin = !ORD && *(volatile int *)&pp->stop == k + 1;   // (set before pub(k + 1))
       lp_post(&pp->cons[1], k + 1);
-      if (fin) break;
+      if (lp_sweep_over<ORD>(pp, k)) break;
     }
     if (ORD) {
 #pragma unroll
@@ -708,9 +732,8 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           snA[(int64_t)bn * 2 * ldaa + q2] = s_a[q2];
         }
       }
-      const bool fin = !ORD && *(volatile int *)&pp->stop == k + 1;   // (set before pub(k + 1))
       lp_post(&pp->cons[wave], k + 1);
-      if (fin) break;
+      if (lp_sweep_over<ORD>(pp, k)) break;
     }
   }
   long long te = tk && tid == 0 ? wall_clock64() : 0;
@@ -835,6 +858,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     return s_i[4] != 0;
   };
   long long pt = wall_clock64();
+  const long long tstart = pt;
   long long pacc[LP_PROF] = {0};
   long long *tk = A.prof ? pacc + 8 : nullptr;
   auto ptick = [&](int i) {   // leader phase timing (A.prof): thread 0 only
@@ -846,6 +870,12 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     const double rsq0 = s_sc[0];
     int jz = 1;
     for (;;) {
+      // a whole-path wall-clock budget (A.tmo_path): a launch that has not
+      // finished by then fails as a timed-out hand-off does (status 3, the
+      // host relaunches) instead of running out elnet1's 1e5 passes
+      if (tid == 0) s_i[7] = wall_clock64() - tstart > A.tmo_path;
+      __syncthreads();
+      if (s_i[7]) { st = 3; fail_m = m; break; }
       if (!(iz && jz)) {
         // ---------------- full pass (speculative: see the header comment)
         for (int t = tid; t < nin; t += blockDim.x) { lp_st(sv + t, s_a[t]); lp_st(sv + LP_LMAX + t, s_g[t]); }
@@ -1008,7 +1038,8 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         ptick(6);
         if (nin > 0) {
           lp_sweep<false>(nullptr, nin, 0, lam, 2 * ver, gkey, GAA, ldaa, s_ia, s_g, s_a, s_rank, s_d, s_log, s_gb,
-                          &s_pp, s_sc, &s_i[1], kl, dl, nullptr, nullptr, A.tmo, tk, A.maxit + 1 - nlp, A.thr);
+                          &s_pp, s_sc, &s_i[1], kl, dl, nullptr, nullptr, A.tmo, tk, A.maxit + 1 - nlp, A.thr,
+                          tstart, A.tmo_path);
         } else {
           if (tid == 0) s_pp.nsw = 1;   // (no active variable: one empty pass, max d^2 = 0)
           __syncthreads();
@@ -1171,6 +1202,7 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   // 2 s of the 100 MHz wall clock: every legitimate wait is microseconds to
   // milliseconds (C4's whole path: 49 ms)
   A.tmo = 200000000LL;
+  A.tmo_path = 1000000000LL;   // 10 s (C4: 49 ms)
   // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
   static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
   if (prof) A.prof = (long long *)alloc((size_t)nprob * LP_PROF * 8);
