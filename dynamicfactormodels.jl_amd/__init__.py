@@ -17,7 +17,7 @@ from .api import (Context, DFMError, Stat, DynamicFactorModel, DynamicFactorMode
                   chow_all, LR_test, LM_test, Wald_test, targeted_predictors, default_context,
                   CRITERIA, pseudo_out_of_sample_refits, pseudo_out_of_sample_refits_dev,
                   pseudo_out_of_sample_forecasts, MSE, normalize, normalize_dev, clone_model,
-                  lasso_path, get_factors, predict, pseudo_out_of_sample_windows)
+                  lasso_path, lasso_stats, get_factors, predict, pseudo_out_of_sample_windows)
 from .api import (criterion_PCp1, criterion_PCp2, criterion_PCp3, criterion_ICp1,  # noqa: F401
                   criterion_ICp2, criterion_ICp3, criterion_BIC)
 from . import _lib
@@ -30,6 +30,6 @@ __all__ = [
     "factor_residual_variance", "criterion_value", "wild_bootstrap", "residual_bootstrap",
     "chow_all", "LR_test", "LM_test", "Wald_test", "targeted_predictors", "default_context",
     "CRITERIA", "pseudo_out_of_sample_refits", "pseudo_out_of_sample_refits_dev",
-    "pseudo_out_of_sample_forecasts", "MSE", "normalize_dev", "clone_model", "lasso_path",
+    "pseudo_out_of_sample_forecasts", "MSE", "normalize_dev", "clone_model", "lasso_path", "lasso_stats",
     "get_factors", "predict", "pseudo_out_of_sample_windows",
 ]

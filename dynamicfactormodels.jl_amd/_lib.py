@@ -108,7 +108,13 @@ SIGNATURES = [
                                     c_double_p, C.c_int64, C.c_int64, C.c_int64, c_int32_p,
                                     C.c_int, C.c_double, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     c_double_p, c_double_p, c_double_p, c_double_p, c_uint8_p]),
+    ("dfm_lasso_stats", C.c_int, [c_int64_p, C.c_int, C.c_int]),
 ]
+
+# dfm_lasso_stats slots (include/dfm.h DFM_LASSO_STAT_*)
+LASSO_STATS = ("launches", "relaunches", "timeouts", "task_timeouts", "done_timeouts", "pipe_timeouts",
+               "budget_overruns", "recovered", "max_skew_us", "late_entries", "max_kernel_us",
+               "max_host_us", "slow_launches")
 
 _lock = threading.Lock()
 _lib = None

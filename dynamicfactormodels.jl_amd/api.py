@@ -715,6 +715,16 @@ def lasso_path(G, c, ju, lambdas, *, early: bool = False, thresh: float = 1e-7, 
     return betas[:L.value], rsq[:L.value]
 
 
+def lasso_stats(reset: bool = False) -> dict:
+    """The lasso path kernel's launch record (``dfm_lasso_stats``,
+    process-wide): launches, relaunches and every timed-out leader/helper
+    spin by kind.  ``reset`` zeroes it after reading."""
+    lib = _lib.load()
+    out = (C.c_int64 * len(_lib.LASSO_STATS))()
+    lib.dfm_lasso_stats(out, len(_lib.LASSO_STATS), int(reset))
+    return dict(zip(_lib.LASSO_STATS, list(out)))
+
+
 # ---------------------------------------------------------- expanding windows
 def _window_kmax(T: int, N: int, kmax) -> int:
     """Row width of the windows' eigenvalue / coefficient outputs: the last

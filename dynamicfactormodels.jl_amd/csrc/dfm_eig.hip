@@ -139,8 +139,8 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
         if (j < k && r == 0) {
           const double res = sqrt(v);
           double gap = INFINITY;
-          if (w.subspace) {
-            if (k < p) gap = fabs(th[j] - th[k]);
+          if (w.subspace && k < p) {   // (k == p: no unwanted Ritz value, the neighbour rule)
+            gap = fabs(th[j] - th[k]);
           } else {
             if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
             if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
@@ -1112,8 +1112,8 @@ DFM_DEV bool decide_converged(const double *res2, const double *th, const double
   for (int j = lane; j < k; j += 64) {
     const double rs = res2[j], res = sqrt(rs);
     double gap = INFINITY;
-    if (subspace && tol >= 0.0) {   // strict rule, subspace form (EigWork::subspace)
-      if (k < p) gap = fabs(th[j] - th[k]);
+    if (subspace && tol >= 0.0 && k < p) {   // strict rule, subspace form (EigWork::subspace; k == p: neighbours)
+      gap = fabs(th[j] - th[k]);
     } else {
       if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
       if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));

@@ -26,6 +26,11 @@
 #include "dfm_common.h"
 #include "../../include/dfm.h"
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <utility>
 #include <cmath>
 #include <vector>
@@ -188,6 +193,25 @@ struct LassoCtl {   // per problem, zeroed before the launch
   LpLine done[64];  // helper h: {tag = task number, value = first entering variable (or INT_MAX)}
 };
 
+// Per-workgroup launch record (always on; 128 B, zeroed before every
+// attempt).  Every bounded spin that runs out reports itself here — which
+// wait, the tag it expected and the granule it last saw — and re-reads the
+// granule after an agent acquire and by an atomic read-modify-write; the
+// host turns the records into the counters of dfm_lasso_stats and an
+// error / stderr line.
+enum { LD_NONE = 0, LD_TASK = 1, LD_DONE = 2, LD_PIPE = 3, LD_BUDGET = 4 };
+struct alignas(128) LassoDiag {
+  long long t_start, t_end;    // wall clock (100 MHz) at the workgroup's entry / exit
+  long long t_pub_exit;        // leader: when it published LP_EXIT
+  long long t_to;              // first timed-out spin: when it gave up
+  long long t_rec;             // ... when a re-read found the granule (0: never)
+  unsigned long long seen;     // ... the granule its relaxed polls last returned
+  unsigned long long seen_inv; // ... re-read after fence(acquire, agent)
+  unsigned long long seen_rmw; // ... read by an agent-scope fetch_or(0)
+  int kind, expect, xcc, hwid; // first timeout's kind (LD_*), the tag it waited for; placement
+  int m, seq, lane, ntmo;      // lambda index / task number / the polled helper; timeouts in all
+};
+
 struct LassoArgs {
   const double *G;
   int64_t strideG;
@@ -210,6 +234,7 @@ struct LassoArgs {
   long long tmo;    // spin timeout, wall-clock ticks (100 MHz)
   long long tmo_path;   // whole-path budget of a leader, wall-clock ticks
   long long *prof;  // diagnostics (nullable): [nprob][8] leader wall-clock ticks per phase + counts
+  LassoDiag *diag;  // [gridDim.x] launch records
 };
 
 DFM_DEV double lp_ld(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -230,6 +255,45 @@ DFM_DEV void lp_release() {
 DFM_DEV void lp_acquire() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+DFM_DEV int lp_xcc() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x;
+}
+DFM_DEV int lp_hwid() {
+  int h;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+  return h;
+}
+// a timed-out spin: count it, and fill the record if it is the workgroup's first
+DFM_DEV bool lp_note(LassoDiag *d, int kind, int want, unsigned long long seen, int m, int seq, int lane) {
+  atomicAdd(&d->ntmo, 1);
+  if (atomicCAS(&d->kind, 0, kind) != 0) return false;
+  d->t_to = wall_clock64();
+  d->expect = want; d->seen = seen; d->m = m; d->seq = seq; d->lane = lane;
+  return true;
+}
+// A relaxed poll of granule g ran out at `seen` (tag < want): record it,
+// re-read g after an agent acquire (seen_inv) and by an agent-scope atomic
+// read-modify-write (seen_rmw), then keep polling by RMW for one more
+// timeout.  Returns the granule once its tag reaches `want`, else the last
+// value read (the hand-off failed).
+DFM_DEV unsigned long long lp_recheck(LassoDiag *d, int kind, int want, unsigned long long *g,
+                                      unsigned long long seen, int m, int seq, int lane, long long tmo) {
+  const bool first = lp_note(d, kind, want, seen, m, seq, lane);
+  const long long t0 = wall_clock64();
+  lp_acquire();
+  const unsigned long long vi = lp_ldu(g);
+  unsigned long long v = __hip_atomic_fetch_or(g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (first) { d->seen_inv = vi; d->seen_rmw = v; }
+  if ((int)(vi >> 32) >= want) v = vi;
+  while ((int)(v >> 32) < want && wall_clock64() - t0 <= tmo) {
+    __builtin_amdgcn_s_sleep(2);
+    v = __hip_atomic_fetch_or(g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (first && (int)(v >> 32) >= want) d->t_rec = wall_clock64();
+  return v;
 }
 DFM_DEV int lp_ldi(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DFM_DEV void lp_st(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -386,9 +450,20 @@ struct LpPipe {
   int nch[2];              // changes in the published block (slot)
   int stop;                // wave 0: 1 + the index of the last block (entry-order passes: dlx < thr or budget)
   int nsw;                 // wave 0: sweeps done
-  int err;                 // a spin timed out
+  int err;                 // a spin timed out (1) or the leader's path budget ran out (2)
+  int errw, errt, errv;    // the first timed-out wait: 16 wave + counter (int offset in LpPipe), target, value seen
 };
 DFM_DEV void lp_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// a pipeline wait timed out: fail the sweep, recording which wait (the first)
+DFM_DEV void lp_pipe_fail(LpPipe *pp, const int *f, int target, int seen) {
+  volatile int *e = &pp->err;
+  if (*e == 0) {
+    ((volatile int *)&pp->errw)[0] = 16 * (threadIdx.x >> 6) + (int)(f - reinterpret_cast<const int *>(pp));
+    ((volatile int *)&pp->errt)[0] = target;
+    ((volatile int *)&pp->errv)[0] = seen;
+  }
+  *e = 1;
+}
 // spin (every lane of the wave) until *f >= target; LDS reads are in order per wave
 DFM_DEV void lp_wait(const int *f, int target, LpPipe *pp, long long tmo) {
   const volatile int *vf = f;
@@ -398,7 +473,7 @@ DFM_DEV void lp_wait(const int *f, int target, LpPipe *pp, long long tmo) {
     while (*vf < target) {
       __builtin_amdgcn_s_sleep(1);
       if (*ve) break;   // another wave timed out: the launch is failing, do not wait out a timeout per spin
-      if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
+      if (wall_clock64() - t0 > tmo) { lp_pipe_fail(pp, f, target, *vf); break; }
     }
   }
   asm volatile("" ::: "memory");
@@ -431,7 +506,7 @@ DFM_DEV void lp_wait_cons(LpPipe *pp, int w0, int target, long long tmo) {
     while (lp_min_cons(pp, w0) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (((const volatile int *)&pp->err)[0]) break;
-      if (wall_clock64() - t0 > tmo) { ((volatile int *)&pp->err)[0] = 1; break; }
+      if (wall_clock64() - t0 > tmo) { lp_pipe_fail(pp, pp->cons + w0, target, lp_min_cons(pp, w0)); break; }
     }
   }
   asm volatile("" ::: "memory");
@@ -558,7 +633,7 @@ DFM_DEV void lp_sweep(const int *ord, int n, int bstart, double lam, int key, in
           if (lane == 0) {
             s_sc[1] = mx; pp->nsw = sw;
             if (last) pp->stop = k + 1;
-            if (over) ((volatile int *)&pp->err)[0] = 1;
+            if (over) ((volatile int *)&pp->err)[0] = 2;
           }
           dlx_s = 0.0;
         }
@@ -750,6 +825,8 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
   LassoCtl *ctl = A.ctl + f;
+  LassoDiag *dg = A.diag + blockIdx.x;
+  if (tid == 0) { dg->t_start = wall_clock64(); dg->xcc = lp_xcc(); dg->hwid = lp_hwid(); }
   int *kl = A.klist + (int64_t)f * LP_LMAX;
   double *dl = A.dlist + (int64_t)f * LP_LMAX;
   if (role > 0) {   // ------------------------------------------------ helper
@@ -765,6 +842,10 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         while ((int)((gv = lp_ldu(&ctl->task.v)) >> 32) < q) {
           if (wall_clock64() - t0 > A.tmo) { ok = 0; break; }
           __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) {   // reported, re-read; the task may still be found
+          gv = lp_recheck(dg, LD_TASK, q, &ctl->task.v, gv, -1, q, h, A.tmo);
+          ok = (int)(gv >> 32) >= q;
         }
         lp_acquire();
         s_i[0] = ok ? (int)(unsigned)gv : -1;
@@ -800,6 +881,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     if (A.prof && h == 0 && tid == 0)
       for (int i = 0; i < 4; ++i) A.prof[(int64_t)f * LP_PROF + 20 + i] = hb[i];
     if (A.prof && h == 0 && tid == 0) { A.prof[(int64_t)f * LP_PROF + 26] = hb[4]; A.prof[(int64_t)f * LP_PROF + 27] = hb[5]; }
+    if (tid == 0) dg->t_end = wall_clock64();
     return;
   }
   // ----------------------------------------------------------------- leader
@@ -818,7 +900,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   double *bp = A.bpath + (int64_t)f * nlam * p;
   for (int j = tid; j < p; j += blockDim.x) { lp_st(g2 + j, c[j]); lp_sti(isact + j, 0); }
   if (tid == 0) { s_sc[0] = 0.0; s_sc[1] = 0.0; s_i[1] = 0; s_i[2] = 0; s_pp.err = 0; }
-  int seq = 0, gcur = 0, nlp = 0, iz = 0, L = nlam, st = 0, fail_m = nlam, nin = 0;
+  int seq = 0, gcur = 0, nlp = 0, iz = 0, L = nlam, st = 0, fail_m = nlam, nin = 0, cur_m = 0;
   int ver = 0, gkey = -1;   // active-set version (entries); the sweep order s_gb's block belongs to
   // publish a task to the helpers and wait for all of them (H == 0: run it here)
   // publish a task to the helpers (payload: kl, dl, isact, g2, lam) and wait
@@ -837,8 +919,9 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       const long long t0 = wall_clock64();
       int ok = 1;
       unsigned int v = INT_MAX;
+      bool mine = true;
       for (;;) {
-        bool mine = true;
+        mine = true;
         if (lane < H) {
           const unsigned long long gv = lp_ldu(&ctl->done[lane].v);
           mine = (int)(gv >> 32) >= seq;
@@ -847,6 +930,15 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         if (__all(mine)) break;
         if (wall_clock64() - t0 > A.tmo) { ok = 0; break; }
         __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) {   // reported, re-read by every lane still waiting
+        if (!mine) {
+          const unsigned long long gv = lp_recheck(dg, LD_DONE, seq, &ctl->done[lane].v,
+                                                   lp_ldu(&ctl->done[lane].v), cur_m, seq, lane, A.tmo);
+          mine = (int)(gv >> 32) >= seq;
+          v = (unsigned)gv;
+        }
+        ok = __all(mine) ? 1 : 0;
       }
       lp_acquire();
       int first = lane < H ? (int)v : INT_MAX;
@@ -864,8 +956,17 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   auto ptick = [&](int i) {   // leader phase timing (A.prof): thread 0 only
     if (A.prof && tid == 0) { const long long t = wall_clock64(); pacc[i] += t - pt; pt = t; }
   };
+  // a pipeline wait of the last sweep timed out (1) or the path budget ran out (2): record it
+  auto sweep_failed = [&]() -> int {
+    const int e = s_pp.err;
+    if (e && tid == 0)
+      lp_note(dg, e == 2 ? LD_BUDGET : LD_PIPE, s_pp.errt, (unsigned long long)(unsigned)s_pp.errv, cur_m, seq,
+              s_pp.errw);
+    return e == 0 ? 0 : e == 2 ? 4 : 3;
+  };
   for (int m = 0; m < nlam && !st; ++m) {
     const double lam = alm[m];
+    cur_m = m;
     __syncthreads();
     const double rsq0 = s_sc[0];
     int jz = 1;
@@ -875,7 +976,10 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       // host relaunches) instead of running out elnet1's 1e5 passes
       if (tid == 0) s_i[7] = wall_clock64() - tstart > A.tmo_path;
       __syncthreads();
-      if (s_i[7]) { st = 3; fail_m = m; break; }
+      if (s_i[7]) {
+        if (tid == 0) lp_note(dg, LD_BUDGET, 0, 0, m, seq, -1);
+        st = 4; fail_m = m; break;
+      }
       if (!(iz && jz)) {
         // ---------------- full pass (speculative: see the header comment)
         for (int t = tid; t < nin; t += blockDim.x) { lp_st(sv + t, s_a[t]); lp_st(sv + LP_LMAX + t, s_g[t]); }
@@ -892,7 +996,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
                          &s_pp, s_sc, &s_i[1], kl, dl, snL, snR, A.tmo, tk);
           ptick(0);
           if (tid == 0) { pacc[16] += 1; pacc[17] += nin - LP_B * rsb; }
-          if (s_pp.err) { st = 3; fail_m = m; break; }
+          if (const int e = sweep_failed()) { st = e; fail_m = m; break; }
           if (!run_task(LP_FULL, s_i[1], lam, c0)) { st = 3; fail_m = m; break; }
           ptick(1);
           const int v = s_i[3];
@@ -1048,7 +1152,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
         const int nsw = s_pp.nsw;
         nlp += nsw;
         if (tid == 0) { pacc[18] += nsw; pacc[19] += (long long)nsw * nin; }
-        if (s_pp.err) { st = 3; fail_m = m; break; }
+        if (const int e = sweep_failed()) { st = e; fail_m = m; break; }
         if (!(s_sc[1] < A.thr) && nlp > A.maxit) { st = 1; fail_m = m; break; }
       }
       // ---------------- refresh: g_j -= dot(da, c_j,A) over the non-active j
@@ -1098,6 +1202,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     }
   }
   run_task(LP_EXIT, 0, 0.0, 0);
+  if (tid == 0) dg->t_pub_exit = wall_clock64();
   ptick(6);
   if (A.prof && tid == 64) {
     A.prof[(int64_t)f * LP_PROF + 24] = pacc[24];
@@ -1114,6 +1219,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     A.status[gridDim.x / (H + 1) + f] = st ? fail_m : nlam;   // lambda index of a failure
     if (f == 0) __hip_atomic_store(A.nlam_out, L, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     else A.nlam_out[f] = L;
+    dg->t_end = wall_clock64();
   }
 }
 
@@ -1161,6 +1267,31 @@ hipStream_t ctx_stream(dfm_ctx *ctx);
 int ctx_device(dfm_ctx *ctx);
 }  // namespace dfm
 
+// Process-wide record of the lasso launches (dfm_lasso_stats): every
+// timed-out spin is counted and reported, so a test can assert there were
+// none.  Slots: DFM_LASSO_STAT_* in include/dfm.h.
+static std::atomic<long long> g_lasso_stats[DFM_LASSO_NSTATS];
+static void lasso_stat_add(int i, long long v) { g_lasso_stats[i].fetch_add(v, std::memory_order_relaxed); }
+static void lasso_stat_max(int i, long long v) {
+  long long o = g_lasso_stats[i].load(std::memory_order_relaxed);
+  while (v > o && !g_lasso_stats[i].compare_exchange_weak(o, v, std::memory_order_relaxed)) {}
+}
+static long long env_ms(const char *name, long long dflt) {
+  const char *v = getenv(name);
+  if (!v || !*v) return dflt;
+  const long long x = atoll(v);
+  return x > 0 ? x : dflt;
+}
+static const char *lasso_diag_kind(int k) {
+  switch (k) {
+    case LD_TASK: return "helper task poll";
+    case LD_DONE: return "leader done poll";
+    case LD_PIPE: return "leader pipeline wait";
+    case LD_BUDGET: return "leader path budget";
+    default: return "none";
+  }
+}
+
 // Every problem's path in one co-resident launch (lasso_coop_kernel): nprob
 // groups of 1 leader + H helper workgroups, H as large as the chip's
 // co-resident workgroups allow (<= one per 256 columns, <= 64).  Scratch is
@@ -1177,6 +1308,8 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   const int maxb = per_cu * ncu;
   int H = std::min(std::min(maxb / nprob - 1, std::max(1, (p + 255) / 256)), 64);
   if (H < 1) { *why = "more lasso problems than co-resident workgroup pairs"; return hipErrorInvalidConfiguration; }
+  const int nblk = nprob * (H + 1);
+  if (nblk > maxb) { *why = "lasso grid above the co-resident capacity"; return hipErrorInvalidConfiguration; }
   const int ldaa = std::min(p, LP_LMAX);
   std::vector<void *> bufs;
   auto alloc = [&](size_t bytes) -> void * {
@@ -1198,59 +1331,115 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   A.snapC = (double *)alloc((size_t)nprob * LP_NCH * p * 8);
   A.snapL = (double *)alloc((size_t)nprob * LP_NBL * 2 * ldaa * 8);
   A.snapR = (double *)alloc((size_t)nprob * LP_NBL * 4 * 8);
+  A.diag = (LassoDiag *)alloc((size_t)nblk * sizeof(LassoDiag));
   A.bpath = bpath; A.rsq_out = rsq; A.nlam_out = nl; A.status = sts;
-  // 2 s of the 100 MHz wall clock: every legitimate wait is microseconds to
-  // milliseconds (C4's whole path: 49 ms)
-  A.tmo = 200000000LL;
-  A.tmo_path = 1000000000LL;   // 10 s (C4: 49 ms)
+  // Spin timeout: 2 s of the 100 MHz wall clock (every legitimate wait is
+  // microseconds to milliseconds).  Whole-path budget of a leader: 10 s plus
+  // 2 us per (variable, lambda) — C4 (p 5002, 100 lambdas) 11 s against the
+  // 49 ms it takes.  DFM_LASSO_TMO_MS / DFM_LASSO_BUDGET_MS override both.
+  A.tmo = env_ms("DFM_LASSO_TMO_MS", 2000) * 100000LL;
+  A.tmo_path = env_ms("DFM_LASSO_BUDGET_MS", 10000 + (long long)p * nlam / 500) * 100000LL;
   // DFM_LASSO_PROF (diagnostic, stderr): the leaders' per-phase wall time
   static const bool prof = getenv("DFM_LASSO_PROF") != nullptr;
   if (prof) A.prof = (long long *)alloc((size_t)nprob * LP_PROF * 8);
   auto cleanup = [&]() { hipStreamSynchronize(st); for (void *b : bufs) hipFree(b); };
-  if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA || !A.snapC || !A.snapL || !A.snapR) {
+  if (!A.ctl || !A.g2 || !A.isact || !A.klist || !A.dlist || !A.save || !A.GAA || !A.snapC || !A.snapL || !A.snapR ||
+      !A.diag) {
     cleanup();
     *why = "out of device memory";
     return hipErrorOutOfMemory;
   }
-  // every scratch buffer starts zeroed, as on a fresh allocation: a second
-  // call in one process gets recycled pool memory, and round 3 saw such calls
-  // stall intermittently (first calls never did)
-  e = hipSuccess;
-  for (auto z : {std::make_pair((void *)A.ctl, (size_t)nprob * sizeof(LassoCtl)),
-                 std::make_pair((void *)A.g2, (size_t)nprob * 2 * p * 8),
-                 std::make_pair((void *)A.isact, (size_t)nprob * p * 4),
-                 std::make_pair((void *)A.klist, (size_t)nprob * LP_LMAX * 4),
-                 std::make_pair((void *)A.dlist, (size_t)nprob * LP_LMAX * 8),
-                 std::make_pair((void *)A.save, (size_t)nprob * 2 * LP_LMAX * 8),
-                 std::make_pair((void *)A.GAA, (size_t)nprob * ldaa * ldaa * 8),
-                 std::make_pair((void *)A.snapC, (size_t)nprob * LP_NCH * p * 8),
-                 std::make_pair((void *)A.snapL, (size_t)nprob * LP_NBL * 2 * ldaa * 8),
-                 std::make_pair((void *)A.snapR, (size_t)nprob * LP_NBL * 4 * 8),
-                 std::make_pair((void *)nl, (size_t)nprob * 4)})
-    if (e == hipSuccess) e = hipMemsetAsync(z.first, 0, z.second, st);
-  // A plain launch sized to the co-resident capacity (occupancy API above):
-  // the kernel needs every workgroup resident (leader/helper hand-offs), not
-  // a grid barrier, and every spin is bounded by the wall-clock timeout.  A
-  // cooperative launch (hipLaunchCooperativeKernel) guarantees the same on an
-  // idle device but makes rocprofv3 (ROCm 7.2) fault in its exit path: a bare
-  // cooperative launch of a trivial kernel reproduces that SIGSEGV while the
-  // same kernel launched plainly exits cleanly (tools/coop_exit_probe.hip,
-  // profiles/r03_coop_exit_probe.txt).
-  // A launch in which some problem timed out (status 3: a hand-off that never
-  // came — seen once in round 3's GPU suite, at p = 42, H = 1) is run again:
-  // the path is deterministic, so a completed relaunch returns the same bits.
+  // Every scratch buffer starts zeroed before EVERY attempt, as on a fresh
+  // allocation (a second call in one process gets recycled pool memory, and
+  // round 3 saw such calls stall; a relaunch must not start from a failed
+  // attempt's state either).
+  auto zero_all = [&]() -> hipError_t {
+    hipError_t z = hipSuccess;
+    for (auto b : {std::make_pair((void *)A.ctl, (size_t)nprob * sizeof(LassoCtl)),
+                   std::make_pair((void *)A.g2, (size_t)nprob * 2 * p * 8),
+                   std::make_pair((void *)A.isact, (size_t)nprob * p * 4),
+                   std::make_pair((void *)A.klist, (size_t)nprob * LP_LMAX * 4),
+                   std::make_pair((void *)A.dlist, (size_t)nprob * LP_LMAX * 8),
+                   std::make_pair((void *)A.save, (size_t)nprob * 2 * LP_LMAX * 8),
+                   std::make_pair((void *)A.GAA, (size_t)nprob * ldaa * ldaa * 8),
+                   std::make_pair((void *)A.snapC, (size_t)nprob * LP_NCH * p * 8),
+                   std::make_pair((void *)A.snapL, (size_t)nprob * LP_NBL * 2 * ldaa * 8),
+                   std::make_pair((void *)A.snapR, (size_t)nprob * LP_NBL * 4 * 8),
+                   std::make_pair((void *)A.diag, (size_t)nblk * sizeof(LassoDiag)),
+                   std::make_pair((void *)nl, (size_t)nprob * 4), std::make_pair((void *)sts, (size_t)nprob * 8)})
+      if (z == hipSuccess) z = hipMemsetAsync(b.first, 0, b.second, st);
+    return z;
+  };
+  // A plain launch sized to the co-resident capacity (occupancy API above,
+  // checked: nblk <= maxb): the kernel needs every workgroup resident
+  // (leader/helper hand-offs), not a grid barrier, and every spin is bounded
+  // by the wall-clock timeout.  A cooperative launch
+  // (hipLaunchCooperativeKernel) adds only the same size check and makes
+  // rocprofv3 (ROCm 7.2) fault in its exit path: a bare cooperative launch
+  // of a trivial kernel reproduces that SIGSEGV while the same kernel
+  // launched plainly exits cleanly (tools/coop_exit_probe.hip,
+  // profiles/r03_coop_exit_probe.txt).  Residency is measured instead: every
+  // workgroup stamps its entry and exit, and a workgroup that entered after
+  // another had exited is reported.
+  // A launch in which a hand-off failed (status 3) is run again (<= 3
+  // launches; the path is deterministic, so a completed relaunch returns
+  // the same bits); a path-budget overrun (status 4) is not.
+  std::vector<LassoDiag> hd(nblk);
+  static char msg[512];
   for (int attempt = 0; e == hipSuccess; ++attempt) {
-    hipLaunchKernelGGL(lasso_coop_kernel, dim3(nprob * (H + 1)), dim3(LP_NT), 0, st, A);
-    e = hipGetLastError();
+    e = zero_all();
+    if (e != hipSuccess) break;
+    e = hipStreamSynchronize(st);   // (the launch's own wall time below: the memsets and earlier work done)
+    const auto h0 = std::chrono::steady_clock::now();
+    if (e == hipSuccess) hipLaunchKernelGGL(lasso_coop_kernel, dim3(nblk), dim3(LP_NT), 0, st, A);
+    if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess || attempt == 2) break;
-    std::vector<int> hs(nprob);
+    const long long host_us =
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - h0).count();
+    if (e != hipSuccess) break;
+    lasso_stat_add(DFM_LASSO_STAT_LAUNCHES, 1);
+    if (attempt > 0) lasso_stat_add(DFM_LASSO_STAT_RELAUNCHES, 1);
+    std::vector<int> hs(2 * nprob);
     if ((e = hipMemcpy(hs.data(), sts, hs.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
-    if (std::find(hs.begin(), hs.end(), 3) == hs.end()) break;
-    fprintf(stderr, "[dfm] lasso path launch %d timed out in a hand-off; relaunching\n", attempt + 1);
-    e = hipMemsetAsync(A.ctl, 0, (size_t)nprob * sizeof(LassoCtl), st);
-    if (e == hipSuccess) e = hipMemsetAsync(nl, 0, (size_t)nprob * 4, st);
-    if (e == hipSuccess) e = hipMemsetAsync(A.snapC, 0, (size_t)nprob * LP_NCH * p * 8, st);
+    if ((e = hipMemcpy(hd.data(), A.diag, hd.size() * sizeof(LassoDiag), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    // residency: the latest entry against the earliest exit
+    long long t0 = LLONG_MAX, t1 = 0, e0 = LLONG_MAX, e1 = 0;
+    for (const LassoDiag &d : hd) {
+      t0 = std::min(t0, d.t_start); t1 = std::max(t1, d.t_start);
+      e0 = std::min(e0, d.t_end); e1 = std::max(e1, d.t_end);
+    }
+    lasso_stat_max(DFM_LASSO_STAT_MAX_SKEW_US, (t1 - t0) / 100);
+    lasso_stat_max(DFM_LASSO_STAT_MAX_KERNEL_US, (e1 - t0) / 100);
+    lasso_stat_max(DFM_LASSO_STAT_MAX_HOST_US, host_us);
+    if (t1 > e0) lasso_stat_add(DFM_LASSO_STAT_LATE_ENTRIES, 1);
+    if (host_us > 2 * (e1 - t0) / 100 + 50000) {   // the launch, not the kernel, took the time
+      lasso_stat_add(DFM_LASSO_STAT_SLOW_LAUNCHES, 1);
+      fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host for a %lld us kernel (%d workgroups)\n",
+              attempt + 1, host_us, (e1 - t0) / 100, nblk);
+    }
+    for (int b = 0; b < nblk; ++b) {
+      const LassoDiag &d = hd[b];
+      if (!d.ntmo) continue;
+      lasso_stat_add(DFM_LASSO_STAT_TIMEOUTS, d.ntmo);
+      lasso_stat_add(d.kind == LD_TASK ? DFM_LASSO_STAT_TASK_TMO
+                     : d.kind == LD_DONE ? DFM_LASSO_STAT_DONE_TMO
+                     : d.kind == LD_PIPE ? DFM_LASSO_STAT_PIPE_TMO : DFM_LASSO_STAT_BUDGET, 1);
+      if (d.t_rec) lasso_stat_add(DFM_LASSO_STAT_RECOVERED, 1);
+      const int f = b / (H + 1), role = b % (H + 1);
+      const LassoDiag &ld = hd[(size_t)f * (H + 1)];
+      snprintf(msg, sizeof msg,
+               "lasso launch %d: problem %d %s %d (xcc %d hwid %#x): %s timed out %d time(s), waiting for tag %d "
+               "(lambda %d, task %d, lane/wave %d); polls saw %#llx, after acquire %#llx, by RMW %#llx; %s; entry +%lld "
+               "us, timeout +%lld us, leader (xcc %d) exit published +%lld us, exited +%lld us",
+               attempt + 1, f, role ? "helper" : "leader", role ? role - 1 : 0, d.xcc, d.hwid, lasso_diag_kind(d.kind),
+               d.ntmo, d.expect, d.m, d.seq, d.lane, d.seen, d.seen_inv, d.seen_rmw,
+               d.t_rec ? "a re-read found it" : "no re-read found it", (d.t_start - t0) / 100, (d.t_to - t0) / 100,
+               ld.xcc, ld.t_pub_exit ? (ld.t_pub_exit - t0) / 100 : -1, (ld.t_end - t0) / 100);
+      fprintf(stderr, "[dfm] %s\n", msg);
+      *why = msg;
+    }
+    if (attempt == 2 || std::find(hs.begin(), hs.begin() + nprob, 3) == hs.begin() + nprob) break;
+    fprintf(stderr, "[dfm] lasso path launch %d failed in a hand-off; relaunching\n", attempt + 1);
   }
   if (e == hipSuccess && A.prof) {
     std::vector<long long> hp((size_t)nprob * LP_PROF);
@@ -1267,21 +1456,6 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
               q[26] * 1e-5, q[23] * 1e-5, q[24] * 1e-5, q[25] * 1e-5, q[28] * 1e-5, q[30], q[29] * 1e-5);
     }
   }
-  if (e == hipSuccess) {   // a timed-out problem: report its control block
-    std::vector<int> hs(2 * nprob);
-    hipMemcpy(hs.data(), sts, hs.size() * 4, hipMemcpyDeviceToHost);
-    for (int f = 0; f < nprob; ++f)
-      if (hs[f] == 3) {
-        LassoCtl c0;
-        hipMemcpy(&c0, A.ctl + f, sizeof c0, hipMemcpyDeviceToHost);
-        static char msg[256];
-        snprintf(msg, sizeof msg, "lasso problem %d timed out: task %d, helper 0 done %d (H %d)", f,
-                 (int)(c0.task.v >> 32), (int)(c0.done[0].v >> 32), H);
-        *why = msg;
-        fprintf(stderr, "[dfm] %s\n", msg);
-        break;
-      }
-  }
   cleanup();
   return e;
 }
@@ -1290,9 +1464,26 @@ static const char *lasso_status_text(int code) {
   switch (code) {
     case 1: return "lasso coordinate descent did not converge";
     case 2: return "lasso active set above 4096 variables";
-    case 3: return "lasso path kernel timed out waiting for its helper workgroups";
+    case 3: return "lasso path kernel: a leader/helper hand-off timed out in every launch";
+    case 4: return "lasso path kernel: a leader ran past its path time budget (DFM_LASSO_BUDGET_MS)";
     default: return "lasso path failed";
   }
+}
+
+// the status text, with the launch record's report of a timed-out spin
+static const char *lasso_fail_text(int code, const char *why) {
+  static char buf[768];
+  if (code < 3) return lasso_status_text(code);
+  snprintf(buf, sizeof buf, "%s [%s]", lasso_status_text(code), why);
+  return buf;
+}
+
+extern "C" int dfm_lasso_stats(int64_t *out, int n, int reset) {
+  if (!out && !reset) return -2;
+  for (int i = 0; i < n && i < DFM_LASSO_NSTATS; ++i) out[i] = g_lasso_stats[i].load(std::memory_order_relaxed);
+  if (reset)
+    for (auto &x : g_lasso_stats) x.store(0, std::memory_order_relaxed);
+  return DFM_LASSO_NSTATS;
 }
 
 extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w, int q, int64_t ldw,
@@ -1441,7 +1632,7 @@ extern "C" int dfm_targeted_soft(dfm_ctx *ctx, const double *y, const double *w,
   if (e != hipSuccess) { cleanup(); return fail(1000 + (int)e, "dfm_targeted_soft: path kernel failed"); }
   const int L = hnl[0];
   for (int f = 0; f < nprob; ++f)   // a fold's failure past L concerns lambdas the CV never reads
-    if (hst[f] && (f == 0 || hst[nprob + f] < L)) { cleanup(); return fail(2, lasso_status_text(hst[f])); }
+    if (hst[f] && (f == 0 || hst[nprob + f] < L)) { cleanup(); return fail(2, lasso_fail_text(hst[f], why)); }
   hipLaunchKernelGGL(soft_loss_kernel, dim3(L, K), dim3(256), 0, st, Zs, ld, n, p, yd, fd, ystat, bpath, nlambda,
                      sse);
   std::vector<double> hsse((size_t)K * nlambda), hb(p), hmu(p), hsd(p);
@@ -1528,7 +1719,7 @@ extern "C" int dfm_lasso_path(dfm_ctx *ctx, const double *G, const double *c, co
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   freeall();
   if (e != hipSuccess) return ctx_fail(ctx, 1000 + (int)e, "dfm_lasso_path: read-back failed");
-  if (hs[0]) return ctx_fail(ctx, 2, lasso_status_text(hs[0]));
+  if (hs[0]) return ctx_fail(ctx, 2, lasso_fail_text(hs[0], why));
   *L_out = hn;
   return 0;
 }

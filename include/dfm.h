@@ -350,6 +350,29 @@ int dfm_lasso_path(dfm_ctx *ctx, const double *G, const double *c, const uint8_t
                    const double *alms, int nlam, int early, double thr, double *betas, double *rsq,
                    int *L_out);
 
+/* Launch record of the lasso path kernel (process-wide, every context).  Its
+ * leader and helper workgroups meet through bounded spins; each spin that
+ * runs out is counted here (and described on stderr and in dfm_last_error)
+ * instead of passing silently.  out[i] for i < n (slots below); reset != 0
+ * zeroes the record after reading.  Returns DFM_LASSO_NSTATS. */
+enum {
+  DFM_LASSO_STAT_LAUNCHES = 0,   /* kernel launches, relaunches included */
+  DFM_LASSO_STAT_RELAUNCHES,     /* launches after a failed hand-off */
+  DFM_LASSO_STAT_TIMEOUTS,       /* timed-out spins, all kinds */
+  DFM_LASSO_STAT_TASK_TMO,       /* workgroups whose first timeout was a helper's task poll */
+  DFM_LASSO_STAT_DONE_TMO,       /* ... a leader's wait for its helpers */
+  DFM_LASSO_STAT_PIPE_TMO,       /* ... a leader's in-workgroup pipeline wait */
+  DFM_LASSO_STAT_BUDGET,         /* ... a leader's whole-path time budget */
+  DFM_LASSO_STAT_RECOVERED,      /* timed-out polls whose re-read then found the granule */
+  DFM_LASSO_STAT_MAX_SKEW_US,    /* max spread of the workgroups' entry times in one launch (us) */
+  DFM_LASSO_STAT_LATE_ENTRIES,   /* launches where a workgroup entered after another had exited */
+  DFM_LASSO_STAT_MAX_KERNEL_US,  /* longest kernel: first entry to last exit (us) */
+  DFM_LASSO_STAT_MAX_HOST_US,    /* longest launch + synchronisation seen by the host (us) */
+  DFM_LASSO_STAT_SLOW_LAUNCHES,  /* launches whose host time exceeded 2x the kernel + 50 ms */
+  DFM_LASSO_NSTATS
+};
+int dfm_lasso_stats(int64_t *out, int n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

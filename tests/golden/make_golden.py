@@ -150,6 +150,39 @@ def c5():
                         **{k: np.array(v) for k, v in rows.items()})
 
 
+def c5_rolling():
+    """C5's rolling form (BASELINE.json configs[4], `bench.py --workload c5
+    --rolling 1000`) at full size: the same panel as c5(); window w is the
+    IC-sweep constructor DynamicFactorModel_ic(kmax=8) on the L = 1000 rows
+    before date_index = T-P+1+w (0-based rows T-P-L+w .. T-P+w-1), windows 0,
+    100, 199, by the reference-faithful oracle."""
+    rng = np.random.default_rng(20261015 + 5)
+    T, N, P, L = 2000, 20000, 200, 1000
+    y, x, *_ = O.factor_model_DGP(T, N, 8, rng)
+    x = O.normalize(x)
+    w = np.ones((T, 1))
+    wins = [0, 100, 199]
+    rows = {"r": [], "V": [], "crit": [], "eigvals": [], "coef": [], "tstat": []}
+    for wi in wins:
+        a = T - P - L + wi
+        d = O.DynamicFactorModel_ic(y[a:a + L], w[a:a + L], x[a:a + L], "ICp2", kmax=8)
+        r = d.number_of_factors
+        rows["r"].append(r)
+        rows["V"].append(O.factor_residual_variance(d))
+        rows["crit"].append(d.number_of_factors_criterion_value)
+        rows["eigvals"].append(d.eigenvalues[0][:8])
+        c = np.full(9, np.nan)
+        t = np.full(9, np.nan)
+        c[:1 + r] = d.coefficients
+        t[:1 + r] = d.t_stats
+        rows["coef"].append(c)
+        rows["tstat"].append(t)
+        print("c5 rolling window", wi, "r", r, flush=True)
+    np.savez_compressed(os.path.join(HERE, "c5_rolling.npz"), windows=np.array(wins), L=np.array(L),
+                        digest=np.array([x.sum(), np.abs(x).sum(), y.sum()]),
+                        **{k: np.array(v) for k, v in rows.items()})
+
+
 def xp():
     """Extended-precision (double-double) referee values for golden C1 and C2
     (oracle/dfm_xp.py): the values the reference's algebra defines, to ~1e-28,
@@ -217,4 +250,5 @@ if __name__ == "__main__":
     tp()
     soft()
     c5()
+    c5_rolling()
     print("golden fixtures written to", HERE)

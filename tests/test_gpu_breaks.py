@@ -150,8 +150,8 @@ def test_break_chow_all_matches_oracle(dfm, oracle, T, N, r, breaks):
         nv = min(N, 30)
         ref = np.array([[oracle.LR_test(o, bp, i), oracle.LM_test(o, bp, i), oracle.Wald_test(o, bp, i)]
                         for i in range(nv)])
-        lr_within(LR[:nv], o, bp, range(nv), oracle, gm=g)
-        lm_within(LM[:nv], o, bp, range(nv), oracle, gm=g)
+        lr_within(LR[:nv], o, bp, range(nv), oracle)
+        lm_within(LM[:nv], o, bp, range(nv), oracle)
         assert rel(W[:nv], ref[:, 2]) < STAT_RTOL, bp
         assert dfm.LM_test(g, bp, 3) == LM[2]
 

@@ -13,6 +13,12 @@ against the reference-faithful oracle (not only against themselves).
   in tests/golden/c5_windows.npz by make_golden.py (an oracle window costs
   ~40 s of CPU there); the panel is regenerated from its seed and its digest
   checked first.
+* C5 rolling (configs[4], `--rolling 1000`): windows 0 / 100 / 199 of the
+  1000-row rolling refits, frozen in tests/golden/c5_rolling.npz.
+* C2 (configs[1]): B = 999 wild-bootstrap replicates of T=600 N=130 with V,
+  ICp2 and LR/LM/Wald of every variable — the bench's job, which runs as two
+  lanes (two streams) — sampled replicates (first, last, the slowest, two
+  random) against the oracle's Chow tests (src/chowtest.jl:19-42).
 * C4 (configs[3]): hard PER_CANDIDATE thresholding on the full T=400
   N=5000 panel against the oracle (src/targeted_predictors.jl:9-30, D8)."""
 import os
@@ -20,7 +26,7 @@ import os
 import numpy as np
 import pytest
 
-from test_gpu_parity import STAT_RTOL, rel
+from test_gpu_parity import STAT_RTOL, lm_within, lr_within, rel
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -135,6 +141,77 @@ def test_c5_full_panel_windows_match_frozen_oracle(dfm, oracle):
     xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major, as the bench
     del x
     out = dfm.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=200, kmax=8)
+    for k, wi in enumerate(g["windows"]):
+        r = int(g["r"][k])
+        assert out["number_of_factors"][wi] == r, wi
+        assert abs(out["V"][wi] - g["V"][k]) <= STAT_RTOL * g["V"][k]
+        assert abs(out["criterion_value"][wi] - g["crit"][k]) <= STAT_RTOL * abs(g["crit"][k])
+        assert rel(out["eigenvalues"][wi][:8], g["eigvals"][k]) < STAT_RTOL
+        assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < STAT_RTOL            # intercept: sign-free
+        assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < STAT_RTOL
+
+
+def test_c2_b999_two_lane_job_sampled_replicates_match_oracle(dfm, oracle):
+    """BASELINE configs[1] exactly as `tools/bench_configs.py c2` runs it:
+    B = 999 in one dfm_bootstrap_dev call (two lanes), stats V + ICp2 +
+    LR/LM/Wald of all 130 variables at bp = 300.  Sampled replicates against
+    the oracle's refit of the same draw (src/bootstrap.jl:41-51,
+    src/chowtest.jl:19-42): V and the criterion at 1e-10, Wald at 1e-10,
+    LR / LM within the double-double referee bar of the oracle's fit."""
+    import torch
+    T, N, B, bp = 600, 130, 999, 300
+    y, x, *_ = dfm.factor_model_DGP(T, N, 3, model="Breitung_Eickmeier_2011", b=0.5,
+                                    rng=np.random.default_rng(20261015 + 2))
+    x = dfm.normalize(x)
+    w = np.ones((T, 1))
+    ctx = dfm.Context(0)
+    g = dfm.DynamicFactorModel(y, w, x, "ICp2", kmax=8, ctx=ctx)
+    r = g.number_of_factors
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.LR_all(bp), S.LM_all(bp), S.Wald_all(bp), S.iterations()]
+    arr = dfm.api._stat_array(stats)
+    width = int(ctx.lib.dfm_stats_width(g.handle, arr, len(stats)))
+    assert width == 3 + 3 * N
+    idx, eta = dfm.draw_wild_fast(7, B, T)
+    dev = torch.device("cuda", 0)
+    di, de = torch.from_numpy(idx).to(dev), torch.from_numpy(eta).to(dev)
+    out = torch.empty((B, width), dtype=torch.float64, device=dev)
+    ctx.check(ctx.lib.dfm_bootstrap_dev(g.handle, 0, B, di.data_ptr(), de.data_ptr(), arr, len(stats),
+                                        out.data_ptr()))
+    ctx.synchronize()
+    res = out.cpu().numpy()
+    assert np.all(np.isfinite(res))
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    common, E = o.common_component, o.factor_residuals
+    slow = int(np.argmax(res[:, -1]))
+    vs = np.array(list(range(8)) + list(range(N - 8, N)))
+    picks = sorted(set([0, B - 1, slow, B // 2 - 1, B // 2] + list(np.random.default_rng(3).integers(1, B - 1, 2))))
+    for b in picks:   # (B // 2 - 1, B // 2: the last of lane 0, the first of lane 1)
+        d = oracle.DynamicFactorModel(y, w, common + eta[b][:, None] * E[idx[b]], r, "ICp2")
+        assert rel(res[b, 0], oracle.factor_residual_variance(d)) < STAT_RTOL, b
+        assert rel(res[b, 1], d.number_of_factors_criterion_value) < STAT_RTOL, b
+        lr_within(res[b, 2 + vs], d, bp, vs, oracle)
+        lm_within(res[b, 2 + N + vs], d, bp, vs, oracle)
+        assert rel(res[b, 2 + 2 * N + vs], [oracle.Wald_test(d, bp, i) for i in vs]) < STAT_RTOL, b
+
+
+def test_c5_full_panel_rolling_windows_match_frozen_oracle(dfm, oracle):
+    """BASELINE configs[4] in its rolling form (`bench.py --workload c5
+    --rolling 1000`): 200 windows of the 1000 rows before each forecast date
+    of the full T=2000, N=20000 panel, resident in HBM; windows 0, 100, 199
+    against the oracle's IC sweeps frozen in tests/golden/c5_rolling.npz."""
+    import torch
+    g = np.load(os.path.join(GOLD, "c5_rolling.npz"))
+    y, x = c5_panel(oracle)
+    assert abs(x.sum() - g["digest"][0]) < 1e-6
+    assert rel([np.abs(x).sum(), y.sum()], g["digest"][1:]) < 1e-12
+    dev = torch.device("cuda", 0)
+    yd = torch.from_numpy(np.ascontiguousarray(y)).to(dev)
+    wd = torch.ones((2000, 1), dtype=torch.float64, device=dev)
+    xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major, as the bench
+    del x
+    out = dfm.pseudo_out_of_sample_windows(yd, wd, xd, "ICp2", num_predictions=200, kmax=8, rolling=int(g["L"]))
+    assert np.array_equal(out["window_first_row"][g["windows"]], 2000 - 200 - int(g["L"]) + g["windows"])
     for k, wi in enumerate(g["windows"]):
         r = int(g["r"][k])
         assert out["number_of_factors"][wi] == r, wi
