@@ -190,6 +190,14 @@ class Stat:
     def iterations():             # diagnostic: the replicate's eigensolver steps
         return Stat(12)
 
+    @staticmethod
+    def factors():                # the replicate's vcat(F_j), T x r row-major (T r values)
+        return Stat(13)
+
+    @staticmethod
+    def loadings(block: int = 1):  # break block `block`'s (1-based) loadings, N x r (N r values)
+        return Stat(14, _one_based(block))
+
 
 def _one_based(j: int) -> int:
     if int(j) < 1:
@@ -475,7 +483,112 @@ for _n in CRITERIA:
 
 
 # ---------------------------------------------------------------- bootstrap
+class ReplicateFit:
+    """One bootstrap replicate's fit rebuilt on the host, for a reference-style
+    ``stat::Function`` closure (``src/bootstrap.jl:21``, ``:41``:
+    ``stats[b] = stat(DynamicFactorModel(y, w, resampled_x, ...))``).  The
+    device returns the replicate's eigenvalues, V, criterion value,
+    coefficients, t-statistics, factors and per-block loadings
+    (``DFM_STAT_FACTORS`` / ``DFM_STAT_LOADINGS``); the record's other fields
+    (``src/DynamicFactorModel.jl:6-25``) follow from them and the draw:
+    ``x`` = the replicate panel X*_b = C + diag(eta_b) E[idx_b] (as
+    ``:43-46``), ``factor_residuals`` = X*_b - vcat(F_j L_j'), ``residuals`` =
+    y - [w F] coefficients — built lazily."""
+
+    def __init__(self, base, xs, ev, V, crit_value, coef, tstat, F, Ls):
+        self._base, self._xs = base, xs
+        self.y, self.w = base.y, base.w
+        self.number_of_factors = base.number_of_factors
+        self.number_of_factors_criterion = base.number_of_factors_criterion
+        self.break_indices = base.break_indices
+        self.factor_type = base.factor_type
+        self.number_of_factor_lags = 0
+        self.eigenvalues = ev
+        self.V = V
+        self.number_of_factors_criterion_value = crit_value
+        self.coefficients, self.t_stats = coef, tstat
+        self._F = F
+        self.loadings = Ls
+        rows = [len(f) for f in base.factors]
+        cut = np.cumsum([0] + rows)
+        self.factors = [F[cut[j]:cut[j + 1]] for j in range(len(rows))]
+        self._x = self._E = None
+
+    @property
+    def F(self) -> np.ndarray:
+        return self._F
+
+    @property
+    def x(self) -> np.ndarray:
+        if self._x is None:
+            self._x = self._xs()
+        return self._x
+
+    @property
+    def factor_residuals(self) -> np.ndarray:
+        if self._E is None:
+            self._E = self.x - np.vstack([f @ L.T for f, L in zip(self.factors, self.loadings)])
+        return self._E
+
+    @property
+    def design_matrix(self) -> np.ndarray:
+        return np.hstack([self.w, self._F])
+
+    @property
+    def residuals(self) -> np.ndarray:
+        return self.y - self.design_matrix @ self.coefficients
+
+
+def _bootstrap_closure(dfm, kind, B, fn, idx, eta, run_rows):
+    """The host-closure escape: every replicate's fields from the device
+    (chunked to ~0.5 GB of host rows), then ``fn(ReplicateFit)`` per
+    replicate, in replicate order — the reference's loop body
+    (``src/bootstrap.jl:36``, ``:48``) with the refit done on the GPU."""
+    T, N = dfm.x.shape
+    r, q = dfm.number_of_factors, dfm.w.shape[1]
+    d = q + r
+    nblk = len(dfm.factors)
+    crit = bool(dfm.number_of_factors_criterion)
+    stats = [Stat.V()] + ([Stat.criterion()] if crit else []) + [Stat.eigenvalue(j) for j in range(1, r + 1)] + \
+        [Stat.coefficient(j) for j in range(1, d + 1)] + [Stat.t_stat(j) for j in range(1, d + 1)] + \
+        [Stat.factors()] + [Stat.loadings(j) for j in range(1, nblk + 1)]
+    width = 1 + int(crit) + r + 2 * d + T * r + nblk * N * r
+    E = dfm.factor_residuals
+    C0 = dfm.x - E                                    # the common component F L' (blockwise, D1)
+    chunk = int(max(1, min(B, 0.5e9 // (8 * width))))
+    out = np.empty(B)
+    for c0 in range(0, B, chunk):
+        c1 = min(B, c0 + chunk)
+        rows = run_rows(stats, c0, c1)
+        for b in range(c0, c1):
+            row = rows[b - c0]
+            o = 0
+            V = float(row[o]); o += 1
+            cv = float(row[o]) if crit else float("nan"); o += int(crit)
+            ev = row[o:o + r].copy(); o += r
+            coef = row[o:o + d].copy(); o += d
+            ts = row[o:o + d].copy(); o += d
+            F = row[o:o + T * r].reshape(T, r).copy(); o += T * r
+            Ls = []
+            for _ in range(nblk):
+                Ls.append(row[o:o + N * r].reshape(N, r).copy()); o += N * r
+            ib, eb = idx[b], (eta[b] if eta is not None else None)
+            xs = (lambda ib=ib, eb=eb: C0 + (E[ib] * eb[:, None] if eb is not None else E[ib]))
+            out[b] = fn(ReplicateFit(dfm, xs, ev, V, cv, coef, ts, F, Ls))
+    return out
+
+
+def _is_closure(stat) -> bool:
+    return callable(stat) and not isinstance(stat, (Stat, list, tuple))
+
+
 def _run_bootstrap(dfm, kind, B, stat, idx, eta):
+    if _is_closure(stat):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        eta = None if eta is None else np.ascontiguousarray(eta, dtype=np.float64)
+        return _bootstrap_closure(dfm, kind, B, stat, idx, eta,
+                                  lambda st, c0, c1: _run_bootstrap(dfm, kind, c1 - c0, st, idx[c0:c1],
+                                                                    None if eta is None else eta[c0:c1]))
     ctx = dfm._ctx
     stats = list(stat) if isinstance(stat, (list, tuple)) else [stat]
     arr = _stat_array(stats)
@@ -501,6 +614,12 @@ def _run_bootstrap(dfm, kind, B, stat, idx, eta):
 def _run_bootstrap_multi(models, kind, B, stat, idx, eta):
     """The replicate loop sharded over several models (``dfm_bootstrap_multi``):
     replicate b on model floor(b n / B), one host thread per context."""
+    if _is_closure(stat):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        eta = None if eta is None else np.ascontiguousarray(eta, dtype=np.float64)
+        return _bootstrap_closure(models[0], kind, B, stat, idx, eta,
+                                  lambda st, c0, c1: _run_bootstrap_multi(models, kind, c1 - c0, st, idx[c0:c1],
+                                                                          None if eta is None else eta[c0:c1]))
     m0 = models[0]
     ctx = m0._ctx
     stats = list(stat) if isinstance(stat, (list, tuple)) else [stat]

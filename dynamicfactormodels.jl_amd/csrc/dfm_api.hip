@@ -319,6 +319,13 @@ int ctx_device(dfm_ctx *ctx) { return ctx->device; }
 static int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 static bool chow_stat(int k) { return k >= DFM_STAT_LR && k <= DFM_STAT_WALD_ALL; }
 static bool all_var_stat(int k) { return k >= DFM_STAT_LR_ALL && k <= DFM_STAT_WALD_ALL; }
+// values a stat adds to a replicate's row
+static int64_t stat_width(const dfm_model *m, int k) {
+  if (all_var_stat(k)) return m->N;
+  if (k == DFM_STAT_FACTORS) return (int64_t)m->T * m->r;
+  if (k == DFM_STAT_LOADINGS) return (int64_t)m->N * m->r;
+  return 1;
+}
 static int ceil_half(int m) { return (m + 1) / 2; }
 // src/criteria.jl:17-53 at k factors: V(k), PCp's sigma^2 (V of the
 // unrestricted fit), c = (N + T) / (N T), m = min(T, N)
@@ -979,7 +986,7 @@ int dfm_model_set_batch(dfm_model *m, int64_t batch) {
 int64_t dfm_stats_width(const dfm_model *m, const dfm_stat *stats, int nstats) {
   if (!m || (!stats && nstats)) return -1;
   int64_t w = 0;
-  for (int i = 0; i < nstats; ++i) w += all_var_stat(stats[i].kind) ? m->N : 1;
+  for (int i = 0; i < nstats; ++i) w += stat_width(m, stats[i].kind);
   return w;
 }
 
@@ -1066,7 +1073,7 @@ static bool lane_split(const dfm_model *M, int64_t B, const dfm_stat *stats, int
   const int p = eig_block_p(M->m, M->r, M->ctx->block);
   if (p > 32 || p < M->r) return false;
   for (int i = 0; i < ns; ++i)
-    if (stats[i].kind < 0 || stats[i].kind > DFM_STAT_ITERS) return false;
+    if (stats[i].kind < 0 || stats[i].kind > DFM_STAT_LOADINGS) return false;
   return M->r <= 16;   // the subspace solver's paths (not the dense / GEMM-built wide ones)
 }
 
@@ -1158,7 +1165,9 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
   int chow_bp = -1;
   for (int i = 0; i < ns; ++i) {
     const dfm_stat s = stats[i];
-    if (s.kind < 0 || s.kind > DFM_STAT_ITERS) return fail(ctx, -6, "unknown stat kind %d", s.kind);
+    if (s.kind < 0 || s.kind > DFM_STAT_LOADINGS) return fail(ctx, -6, "unknown stat kind %d", s.kind);
+    if (s.kind == DFM_STAT_LOADINGS && (s.arg0 < 0 || s.arg0 >= M->nblk))
+      return fail(ctx, -6, "loadings of break block %d outside 0..%d", s.arg0, M->nblk - 1);
     if (s.kind == DFM_STAT_CRIT) {
       const int c = s.arg0 >= 0 ? s.arg0 : M->crit;
       if (c < 0 || c > 6) return fail(ctx, -6, "criterion stat without a criterion");
@@ -1176,7 +1185,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       if (s.kind <= DFM_STAT_WALD && (s.arg1 < 0 || s.arg1 >= N)) return fail(ctx, -7, "variable index");
     }
     sd[i] = {s.kind, s.arg0, s.arg1, (int)width};
-    width += all_var_stat(s.kind) ? N : 1;
+    width += stat_width(M, s.kind);
   }
   // Statistics that read only the eigenvalues and the trace let the
   // eigensolver stop on the (quadratic) eigenvalue bound instead of the
@@ -1426,6 +1435,15 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       }
       hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
                          n, M->flag_dev);
+      // the replicates' factors / a block's loadings, row by row (host closures)
+      for (int i = 0; i < ns; ++i) {
+        if (sd[i].kind != DFM_STAT_FACTORS && sd[i].kind != DFM_STAT_LOADINGS) continue;
+        const bool fk = sd[i].kind == DFM_STAT_FACTORS;
+        const int64_t cnt = fk ? (int64_t)T * r : (int64_t)N * r;
+        const double *srcp = fk ? w.F : w.L + (size_t)sd[i].arg0 * nb * N * r;
+        HIPCHK(ctx, hipMemcpy2DAsync(out + b0 * width + sd[i].off, (size_t)width * 8, srcp, (size_t)cnt * 8,
+                                     (size_t)cnt * 8, n, hipMemcpyDeviceToDevice, st));
+      }
     }
     if (chow) {
       Scope sc(ctx, DFM_KC_CHOW);

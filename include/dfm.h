@@ -43,7 +43,9 @@ enum dfm_criterion {
 /* Replicate statistics.  The reference's `stat::Function` callback
  * (src/bootstrap.jl:21, :41) cannot run on the device, so it is this fixed
  * menu.  Each dfm_stat yields ONE double per replicate, except the *_ALL
- * kinds which yield N doubles (one per variable). */
+ * kinds (N doubles, one per variable), FACTORS (T r) and LOADINGS (N r):
+ * with those (plus COEF/TSTAT/EIGVAL) a host binding rebuilds each
+ * replicate's fit and runs an arbitrary closure on it. */
 enum dfm_stat_kind {
   DFM_STAT_V = 0,          /* factor_residual_variance, src/criteria.jl:5       */
   DFM_STAT_CRIT = 1,       /* criterion value (arg0 = dfm_criterion code)       */
@@ -57,8 +59,12 @@ enum dfm_stat_kind {
   DFM_STAT_LR_ALL = 9,     /* LR for every variable i (N values), bp = arg0     */
   DFM_STAT_LM_ALL = 10,
   DFM_STAT_WALD_ALL = 11,
-  DFM_STAT_ITERS = 12      /* diagnostic: Rayleigh-Ritz steps of the replicate's eigensolve
+  DFM_STAT_ITERS = 12,     /* diagnostic: Rayleigh-Ritz steps of the replicate's eigensolve
                               (NaN on the dense path); an eigenvalue-only stat */
+  DFM_STAT_FACTORS = 13,   /* the replicate's factors vcat(F_j) (T x r row-major: T r values),
+                              src/DynamicFactorModel.jl:18, :131 — the fields a host-side
+                              stat::Function closure reads (src/bootstrap.jl:21, :41) */
+  DFM_STAT_LOADINGS = 14   /* break block arg0's loadings L_j (N x r row-major: N r values), :19 */
 };
 typedef struct dfm_stat { int32_t kind, arg0, arg1, pad; } dfm_stat;
 

@@ -132,6 +132,21 @@ int main(int argc, char **argv) {
   CHECK(ctx, dfm_bootstrap(m, DFM_BOOT_RESIDUAL, B, idx, NULL, st, 1, bm));
   put("residual_V", bm, B);
 
+  /* the host-closure escape: every replicate's factors and loadings (T r and
+   * N r values per row) for a stat::Function run on the host */
+  {
+    dfm_stat fl[2];
+    double *fo;
+    int64_t wf;
+    fl[0].kind = DFM_STAT_FACTORS; fl[0].arg0 = 0; fl[0].arg1 = 0; fl[0].pad = 0;
+    fl[1].kind = DFM_STAT_LOADINGS; fl[1].arg0 = 0; fl[1].arg1 = 0; fl[1].pad = 0;
+    wf = dfm_stats_width(m, fl, 2);
+    fo = xmalloc(8 * B * wf);
+    CHECK(ctx, dfm_bootstrap(m, DFM_BOOT_WILD, B, idx, eta, fl, 2, fo));
+    put("wild_factors_loadings", fo, B * wf);
+    free(fo);
+  }
+
   /* the replicate loop sharded over two contexts (dfm_model_clone + multi) */
   CHECK(ctx, dfm_ctx_create(0, &ctx2));
   CHECK(ctx2, dfm_model_clone(m, ctx2, &m2));
@@ -225,6 +240,15 @@ int main(int argc, char **argv) {
     e[0] = (double)rc;
     put("error_rc", e, 1);
     fprintf(out, "error_msg_nonempty %d\n", (int)(strlen(dfm_last_error(ctx)) > 0));
+  }
+
+  /* the lasso path kernel's launch record (no lasso ran: all zero) */
+  {
+    int64_t ls[DFM_LASSO_NSTATS];
+    double d[DFM_LASSO_NSTATS];
+    int i, n = dfm_lasso_stats(ls, DFM_LASSO_NSTATS, 0);
+    for (i = 0; i < n; ++i) d[i] = (double)ls[i];
+    put("lasso_stats", d, n);
   }
 
   dfm_model_destroy(mb);

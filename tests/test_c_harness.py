@@ -89,6 +89,9 @@ def test_harness_matches_python_binding_and_oracle(dfm, oracle, tmp_path):
     wild = dfm.wild_bootstrap(g, B, stats, idx=idx, eta=eta)
     assert np.array_equal(h["wild"].reshape(B, -1), wild)
     assert np.array_equal(h["wild_multi"], h["wild"])               # 2-context shards, bit-identical
+    fl = dfm.wild_bootstrap(g, B, [S.factors(), S.loadings(1)], idx=idx, eta=eta)
+    assert fl.shape == (B, (T + N) * r) and np.array_equal(h["wild_factors_loadings"].reshape(B, -1), fl)
+    assert np.array_equal(h["lasso_stats"], np.zeros(len(dfm._lib.LASSO_STATS)))
     assert np.array_equal(h["residual_V"], dfm.residual_bootstrap(g, B, S.V(), idx=idx))
     for b in range(2):
         d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]],

@@ -328,6 +328,39 @@ def test_bootstrap_chow_all_matches_oracle(dfm, oracle, T, N):
         assert rel(out[b, 2 * N + vs], ref[:, 2]) < STAT_RTOL
 
 
+@pytest.mark.parametrize("T,N,breaks", [(80, 120, []), (160, 24, []), (120, 60, [61])])
+def test_bootstrap_host_closure_matches_oracle_loop(dfm, oracle, T, N, breaks):
+    """The reference's `stat::Function` (src/bootstrap.jl:21, :41) as a host
+    closure: the device refits every replicate and returns its factors,
+    loadings, eigenvalues, coefficients and t-statistics (DFM_STAT_FACTORS /
+    LOADINGS); the closure then runs on the rebuilt record — here the
+    oracle's own LR_test and factor_residual_variance, exactly as the
+    reference's loop would call them — against the oracle's loop."""
+    r = 2
+    y, x, w = panel(oracle, T, N, r, 41, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2", break_indices=breaks)
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2", breaks)
+    B, bp = 3, T // 2 + 3
+    idx, eta = oracle.draw_wild(np.random.default_rng(8), B, T)
+    lr = dfm.wild_bootstrap(g, B, lambda d: oracle.LR_test(d, bp, 2), idx=idx, eta=eta)
+    V = dfm.wild_bootstrap(g, B, oracle.factor_residual_variance, idx=idx, eta=eta)
+    reps = []
+    dfm.wild_bootstrap(g, B, lambda d: reps.append(d) or 0.0, idx=idx, eta=eta)
+    assert lr.shape == (B,) and V.shape == (B,)
+    for b in range(B):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + eta[b][:, None] * o.factor_residuals[idx[b]],
+                                      r, "ICp2", breaks)
+        lr_within([lr[b]], d, bp, [2], oracle)
+        assert rel(V[b], oracle.factor_residual_variance(d)) < STAT_RTOL
+        rep = reps[b]
+        assert len(rep.factors) == len(d.factors) == len(breaks) + 1
+        assert max_sin_angle(rep.F, d.F) < ANGLE_TOL
+        assert np.max(np.abs(rep.x - d.x)) < 1e-12 * np.max(np.abs(d.x))
+        s = signs(rep.F, d.F)
+        assert rel(rep.coefficients[1:] * s, d.coefficients[1:]) < STAT_RTOL
+        assert rel(rep.t_stats[1:] * s, d.t_stats[1:]) < STAT_RTOL
+
+
 @pytest.mark.parametrize("T,N", [(80, 120), (160, 24)])
 def test_bootstrap_chow_with_block_equal_r(dfm, oracle, T, N):
     """Eigen block p == r (dfm_ctx_set_eig_params block = r): the subspace
