@@ -37,22 +37,21 @@ struct ChowBlocks {
   int64_t lbs;
 };
 
-struct ChowPrep {   // per replicate, written by chow_prep_kernel
-  // Mi: 2r x 2r, A1i, A2i, ApS = A1 + A2: r x r (row stride CH_RMAX*2)
-  double Mi[4 * CH_RMAX * CH_RMAX];
-  double A1i[CH_RMAX * CH_RMAX], A2i[CH_RMAX * CH_RMAX], A2[CH_RMAX * CH_RMAX],
-      ApS[CH_RMAX * CH_RMAX];
-  double Va[CH_RMAX * CH_RMAX], Vc[CH_RMAX * CH_RMAX], Wa[CH_RMAX * CH_RMAX], Wc[CH_RMAX * CH_RMAX],
-      Wb[CH_RMAX * CH_RMAX];
-  int bad;
-};
+// Per replicate, written by chow_prep_kernel: nine RC x RC matrices (RC =
+// the Chow kernel's padded factor count 4 / 8 / 16, zero outside r),
+// back to back — A1^-1, A2^-1, A2, A1 + A2 and the blocks of M^-1 below —
+// so the kernel reads them at small immediate offsets from one base (the
+// 16 x 16-padded layout of round 3 needed a 64-bit address per element and
+// the compiler spilled them).
+enum { CP_A1I = 0, CP_A2I, CP_A2, CP_APS, CP_VA, CP_VC, CP_WA, CP_WC, CP_WB, CP_NMAT };
+constexpr size_t CH_PREP_BYTES = (size_t)CP_NMAT * CH_RMAX * CH_RMAX * 8;
 
 size_t chow_workspace_bytes(int T, int N, int r, int nb) {
-  return (size_t)nb * sizeof(ChowPrep) + (size_t)nb * T * r * 8 + (size_t)3 * nb * N * 8 + 4096;
+  return (size_t)nb * CH_PREP_BYTES + (size_t)nb * T * r * 8 + (size_t)3 * nb * N * 8 + 4096;
 }
 
 __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict__ F, int T, int r,
-                                                        int bp, ChowPrep *__restrict__ prep,
+                                                        int bp, int RC, double *__restrict__ prep,
                                                         double *__restrict__ Z) {
   constexpr int S = 2 * CH_RMAX + 1;
   __shared__ double A1[CH_RMAX * S], A2s[CH_RMAX * S], M[2 * CH_RMAX * S], Mi[2 * CH_RMAX * S],
@@ -93,29 +92,25 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
   block_spd_inverse(M, Mi, Lw, Tw, n2, S, &bad);
   block_spd_inverse(A1, A1i, Lw, Tw, r, S, &bad);
   block_spd_inverse(A2s, A2i, Lw, Tw, r, S, &bad);
-  ChowPrep *P = prep + rep;
-  constexpr int R = CH_RMAX;
-  // every entry is written (zeros outside r): the main kernel reads R x R blocks
-  for (int e = tid; e < 4 * R * R; e += 256) {
-    const int a = e / (2 * R), c = e % (2 * R);
-    P->Mi[e] = (a < n2 && c < n2) ? Mi[a * S + c] : 0.0;
-  }
-  for (int e = tid; e < R * R; e += 256) {
-    const int a = e / R, c = e % R;
+  double *P = prep + (size_t)rep * CP_NMAT * RC * RC;
+  // every entry is written (zeros outside r): the main kernel reads RC x RC blocks
+  for (int e = tid; e < RC * RC; e += 256) {
+    const int a = e / RC, c = e % RC;
     const bool in = a < r && c < r;
-    P->A1i[e] = in ? A1i[a * S + c] : 0.0;
-    P->A2i[e] = in ? A2i[a * S + c] : 0.0;
-    P->A2[e] = in ? A2s[a * S + c] : 0.0;
-    P->ApS[e] = in ? A1[a * S + c] + A2s[a * S + c] : 0.0;
+    const int q = RC * RC;
+    P[CP_A1I * q + e] = in ? A1i[a * S + c] : 0.0;
+    P[CP_A2I * q + e] = in ? A2i[a * S + c] : 0.0;
+    P[CP_A2 * q + e] = in ? A2s[a * S + c] : 0.0;
+    P[CP_APS * q + e] = in ? A1[a * S + c] + A2s[a * S + c] : 0.0;
     // Mi = [[P11, P12], [P21, P22]]:  beta1 = P11 g1 + (P11 + P12) g2,
     // beta2 = P21 g1 + (P21 + P22) g2 (stored transposed-ready, see kernel)
-    P->Va[e] = in ? Mi[a * S + c] : 0.0;
-    P->Vc[e] = in ? Mi[a * S + c] + Mi[(r + a) * S + c] : 0.0;
-    P->Wa[e] = in ? Mi[a * S + r + c] : 0.0;
-    P->Wc[e] = in ? Mi[a * S + r + c] + Mi[(r + a) * S + r + c] : 0.0;
-    P->Wb[e] = in ? Mi[(r + a) * S + r + c] : 0.0;
+    P[CP_VA * q + e] = in ? Mi[a * S + c] : 0.0;
+    P[CP_VC * q + e] = in ? Mi[a * S + c] + Mi[(r + a) * S + c] : 0.0;
+    P[CP_WA * q + e] = in ? Mi[a * S + r + c] : 0.0;
+    P[CP_WC * q + e] = in ? Mi[a * S + r + c] + Mi[(r + a) * S + r + c] : 0.0;
+    P[CP_WB * q + e] = in ? Mi[(r + a) * S + r + c] : 0.0;
   }
-  if (tid == 0) P->bad = bad;
+  (void)bad;   // (a singular M leaves inf / NaN statistics, as the reference's inv)
   // z_t = Wa' f_t (t < bp) or Wc' f_t (t >= bp)
   for (int e = tid; e < T * r; e += 256) {
     const int t = e / r, j = e % r;
@@ -129,28 +124,57 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
 }
 
 // FLAT = false: one thread per variable, grid (variable blocks, replicate);
-// the block is sized to the panel width (64 .. 256) and the replicate's
-// ChowPrep is staged in LDS.  FLAT = true (N >= CH_FLAT_MIN_N, R <= 8): one
+// the block is sized to the panel width (64 .. 256).  FLAT = true (R <= 8, N
+// wide enough that a block spans <= CH_FLAT_REPS replicates): one
 // thread per (replicate, variable) pair in replicate-major order, so the lanes
 // of a 256-thread block run on into the next replicate's variables instead of
 // idling at the panel edge (C2, N = 130: 3 waves per replicate of which 62
 // lanes idle -> 2.03 waves); a block spans at most CH_FLAT_REPS replicates,
-// each with its own staged F, Z, eta and idx rows, and reads the small
-// ChowPrep matrices from global memory (L2).  Per (replicate, variable) the
+// each with its own staged F, Z, eta and idx rows.  Both read the small
+// prep matrices from global memory (L1/L2).  Per (replicate, variable) the
 // arithmetic and its order are the same in both forms.
 constexpr int CH_FLAT_REPS = 4, CH_FLAT_MIN_N = 86;   // ceil(256 / 86) + 1 <= 4
+//
+// KS > 1 (R <= 4): KS lanes per (replicate, variable), lane k taking rows
+// t = t0 + k, t0 + k + KS, ... of every staged tile; the per-lane partial sums
+// (pass A's F'x, ||E_i||^2, pass B's SSR and HC0 block) are combined across
+// the KS lanes by xor shuffles in a fixed order before they are used.  A
+// C2-sized job (500 replicates x 130 variables) is then 4 waves per SIMD
+// instead of one — the kernel is latency-bound (a dependent chain per
+// accumulator over T rows), not VALU-bound.
+constexpr int CH_KS = 4;
+template <int R, int KS>
+constexpr int chow_waves() { return (R <= 4 && KS > 1) ? 3 : (R <= 8 ? 2 : 1); }
+// x[a] / x[a] := v for a runtime a, by compile-time indices (no scratch)
+template <int R>
+DFM_DEV double rsel(const double (&x)[R], int a) {
+  double v = x[0];
+#pragma unroll
+  for (int j = 1; j < R; ++j) v = a == j ? x[j] : v;
+  return v;
+}
+template <int R>
+DFM_DEV void rput(double (&x)[R], int a, double v) {
+#pragma unroll
+  for (int j = 0; j < R; ++j) x[j] = a == j ? v : x[j];
+}
+template <int KS>
+DFM_DEV double ks_sum(double v) {
+  if constexpr (KS >= 2) v += __shfl_xor(v, 1);
+  if constexpr (KS >= 4) v += __shfl_xor(v, 2);
+  return v;
+}
 
-template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK, bool FLAT = false>
-__global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
+template <int R, bool HAS_C, bool HAS_ETA, bool HAS_IDX, bool BRK, bool FLAT = false, int KS = 1>
+__global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(PanelSrc src, ChowBlocks blk, int T, int N, int r, int bp,
                                                        int nb, const double *__restrict__ F,
                                                        const double *__restrict__ Z,
-                                                       const ChowPrep *__restrict__ prep,
+                                                       const double *__restrict__ prep,
                                                        const double *__restrict__ Lm,
                                                        double *__restrict__ LR,
                                                        double *__restrict__ LM,
                                                        double *__restrict__ WD) {
   constexpr int TR = 64;
-  constexpr int RR = CH_RMAX;
   // rows whose gathered values are in flight together: 16, or 8 at R = 8,
   // whose per-variable state (36 HC0 sums, four R-vectors of coefficients)
   // already fills most of the 2-wave register budget.  The launch bound keeps
@@ -158,32 +182,25 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
   // does not fit is spilled once per thread around pass B, not inside the row
   // loops — unbounded, the compiler took 256 VGPRs + 76 AGPRs at R = 4 and ran
   // one wave per SIMD
-  constexpr int CU = R <= 4 ? 16 : (R <= 8 ? 8 : 16);
+  constexpr int CU = KS > 1 ? 8 : (R <= 4 ? 16 : (R <= 8 ? 8 : 16));
   constexpr int NR = FLAT ? CH_FLAT_REPS : 1;   // replicates staged per block
   __shared__ double sF[NR][TR * R], sZ[NR][TR * R], sE[NR][TR];
   __shared__ int sI[NR][TR];
-  const int tid = threadIdx.x, nth = blockDim.x;
+  const int tid = threadIdx.x, nth = blockDim.x, ks = tid % KS;
   int rep, i, rep0, nrw;
-  if constexpr (FLAT) {
-    const int64_t g = (int64_t)blockIdx.x * nth + tid, g0 = (int64_t)blockIdx.x * nth;
+  if constexpr (FLAT) {   // (replicate, variable) pairs, KS threads each
+    const int64_t g = ((int64_t)blockIdx.x * nth + tid) / KS, g0 = (int64_t)blockIdx.x * nth / KS;
     rep = (int)(g / N); i = (int)(g % N);
     rep0 = (int)(g0 / N);
-    nrw = min(nb - 1, (int)((g0 + nth - 1) / N)) - rep0 + 1;
+    nrw = min(nb - 1, (int)((g0 + nth / KS - 1) / N)) - rep0 + 1;
   } else {
-    rep = blockIdx.y; i = blockIdx.x * nth + tid; rep0 = rep; nrw = 1;
+    rep = blockIdx.y; i = (blockIdx.x * nth + tid) / KS; rep0 = rep; nrw = 1;
   }
   const bool ok = FLAT ? rep < nb : i < N;
   const int lr = FLAT ? (ok ? rep - rep0 : 0) : 0;   // this thread's staged replicate
-  const ChowPrep *Pp;
-  if constexpr (FLAT) {
-    Pp = prep + (ok ? rep : rep0);
-  } else {
-    __shared__ ChowPrep sP;
-    for (int e = tid; e < (int)(sizeof(ChowPrep) / 8); e += nth)
-      reinterpret_cast<double *>(&sP)[e] = reinterpret_cast<const double *>(prep + rep)[e];
-    Pp = &sP;
-  }
-  const ChowPrep &P = *Pp;
+  // this pair's replicate's prep block (matrix m at Pc + m R^2, row-major R x R)
+  const double *Pc = prep + (size_t)(ok ? rep : rep0) * CP_NMAT * R * R;
+  auto PM = [&](int m, int a, int c) -> double { return Pc[m * R * R + a * R + c]; };
   auto stage = [&](int t0) {
     for (int e = tid; e < nrw * TR * R; e += nth) {
       const int q = e / (TR * R), f = e % (TR * R), rr = f / R, j = f % R, t = t0 + rr;
@@ -202,20 +219,21 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
   // first, then every row's loads, then the arithmetic — all 2 CU loads in
   // flight together (computing each row's x as its loads arrive made the
   // compiler wait for every row's loads before the next row's issued)
+  // (this lane's rows of the tile: rb, rb + KS, ..., rb + (CU - 1) KS)
   auto load_rows = [&](int t0, int rb, int tn, double *xs) {
     int ri[CU];
     double ee[CU], cc[CU];
 #pragma unroll
-    for (int u = 0; u < CU; ++u) ri[u] = sI[lr][min(rb + u, tn - 1)];
+    for (int u = 0; u < CU; ++u) ri[u] = sI[lr][min(rb + KS * u, tn - 1)];
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       ee[u] = src.E[(int64_t)ri[u] * src.ld + i];
-      if (HAS_C) cc[u] = src.C[(int64_t)(t0 + min(rb + u, tn - 1)) * src.ld + i];
+      if (HAS_C) cc[u] = src.C[(int64_t)(t0 + min(rb + KS * u, tn - 1)) * src.ld + i];
     }
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       double x = ee[u];
-      if (HAS_ETA) x *= sE[lr][min(rb + u, tn - 1)];
+      if (HAS_ETA) x *= sE[lr][min(rb + KS * u, tn - 1)];
       if (HAS_C) x += cc[u];
       xs[u] = x;
     }
@@ -227,6 +245,7 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
 #pragma unroll
     for (int j = 0; j < R; ++j) l[j] = (ok && j < r) ? Lm[b * blk.lbs + ((int64_t)rep * N + i) * r + j] : 0.0;
   };
+  if (!ok) i = 0;   // (idle lanes gather a valid column; they write nothing)
   load_l(0);
   int cb = 0, next = BRK ? blk.a[1] : T;
   // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2 (BRK: cx = sum_{t>=bp} f_t e_t)
@@ -242,15 +261,15 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
     // CU rows per round: every row's gathered x loaded before the sums
     // (CU loads in flight per thread instead of one dependent load per row);
     // the arithmetic and its order are unchanged
-    for (int rb = 0; rb < tn; rb += CU) {
+    for (int rb = ks; rb < tn; rb += KS * CU) {
     double xs[CU];
     load_rows(t0, rb, tn, xs);
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
-      const int rr = rb + u;
-      if (rr >= tn) break;
+      const int rr = rb + KS * u;
+      if (rr < tn) {   // (a guard, not a break: the loop must unroll)
       const int t = t0 + rr;
-      if (BRK && t == next) { ++cb; next = blk.a[cb + 1]; load_l(cb); }
+      if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
       const double x = xs[u];
       double ev = x;
 #pragma unroll
@@ -271,45 +290,59 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
 #pragma unroll
         for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[lr][rr * R + j], g2[j]);
       }
+      }
     }
     }
+  }
+  if constexpr (KS > 1) {   // the KS lanes' partial sums, in a fixed order
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      g1[j] = ks_sum<KS>(g1[j]); g2[j] = ks_sum<KS>(g2[j]);
+      if (BRK) { cx[j] = ks_sum<KS>(cx[j]); cf[j] = ks_sum<KS>(cf[j]); }
+    }
+    e2 = ks_sum<KS>(e2);
   }
   // subperiod OLS coefficients gamma_j = A_j^-1 g_j, Wald beta = M^-1 [g1+g2; g2],
   // LM vector D'E_i = [F'E_i; F2'E_i] = [cf; c]: c = g2 - A2 l, cf = g1 + g2 -
   // (A1 + A2) l (break models: both summed explicitly in pass A).  F'E_i
   // vanishes only to the eigensolver's residual, so it is kept, not assumed 0
   double ga1[R], ga2[R], b1[R], b2[R], cv[R];
-#pragma unroll
+  // rows a in a loop that is NOT unrolled, register arrays read and written
+  // by compile-time index only (rsel / rput): the prep-matrix reads of row a
+  // are then issued per row — unrolled, the compiler hoisted all 7 R^2 of
+  // them above the row loop (the matrices are read-only) and spilled them
+#pragma unroll 1
   for (int a = 0; a < R; ++a) {
-    double u1 = 0.0, u2 = 0.0, v1 = 0.0, v2 = 0.0, c = g2[a], cs = g1[a] + g2[a];
+    const double g1a = rsel<R>(g1, a), g2a = rsel<R>(g2, a);
+    double u1 = 0.0, u2 = 0.0, v1 = 0.0, v2 = 0.0, c = g2a, cs = g1a + g2a;
 #pragma unroll
     for (int c2 = 0; c2 < R; ++c2) {
-      u1 = fma(P.A1i[a * RR + c2], g1[c2], u1);
-      u2 = fma(P.A2i[a * RR + c2], g2[c2], u2);
-      v1 = fma(P.Va[c2 * RR + a], g1[c2], fma(P.Vc[c2 * RR + a], g2[c2], v1));
-      v2 = fma(P.Wa[c2 * RR + a], g1[c2], fma(P.Wc[c2 * RR + a], g2[c2], v2));
-      if (!BRK) { c -= P.A2[a * RR + c2] * l[c2]; cs -= P.ApS[a * RR + c2] * l[c2]; }
+      u1 = fma(PM(CP_A1I, a, c2), g1[c2], u1);
+      u2 = fma(PM(CP_A2I, a, c2), g2[c2], u2);
+      v1 = fma(PM(CP_VA, c2, a), g1[c2], fma(PM(CP_VC, c2, a), g2[c2], v1));
+      v2 = fma(PM(CP_WA, c2, a), g1[c2], fma(PM(CP_WC, c2, a), g2[c2], v2));
+      if (!BRK) { c -= PM(CP_A2, a, c2) * l[c2]; cs -= PM(CP_APS, a, c2) * l[c2]; }
     }
-    ga1[a] = u1; ga2[a] = u2; b1[a] = v1; b2[a] = v2; cv[a] = BRK ? cx[a] : c;
-    if (!BRK) cf[a] = cs;
-#ifdef DFM_AB_NO_CF
-    cf[a] = 0.0;
-#endif
+    rput<R>(ga1, a, u1); rput<R>(ga2, a, u2); rput<R>(b1, a, v1); rput<R>(b2, a, v2);
+    rput<R>(cv, a, BRK ? rsel<R>(cx, a) : c);
+    if (!BRK) rput<R>(cf, a, cs);
   }
   // lmq = [cf; c]' M^-1 [cf; c]; M^-1 = [[Va, Wa], [Wa', Wb]] (r x r blocks)
   double lmq = 0.0;
-#pragma unroll
+#pragma unroll 1
   for (int a = 0; a < R; ++a) {
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int c2 = 0; c2 < R; ++c2) {
-      s1 = fma(P.Va[a * RR + c2], cf[c2], fma(P.Wa[a * RR + c2], cv[c2], s1));
-      s2 = fma(P.Wa[c2 * RR + a], cf[c2], fma(P.Wb[a * RR + c2], cv[c2], s2));
+      s1 = fma(PM(CP_VA, a, c2), cf[c2], fma(PM(CP_WA, a, c2), cv[c2], s1));
+      s2 = fma(PM(CP_WA, c2, a), cf[c2], fma(PM(CP_WB, a, c2), cv[c2], s2));
     }
-    lmq = fma(cf[a], s1, fma(cv[a], s2, lmq));
+    lmq = fma(rsel<R>(cf, a), s1, fma(rsel<R>(cv, a), s2, lmq));
   }
   // ---- pass B: subperiod SSRs and the HC0 block sum_t u_t^2 z_t z_t'
-  double S[R * (R + 1) / 2], ssr = 0.0;
+  double S[R * (R + 1) / 2], ssr = 0.0, bq[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) bq[j] = b1[j] + b2[j];
 #pragma unroll
   for (int e = 0; e < R * (R + 1) / 2; ++e) S[e] = 0.0;
   for (int t0 = 0; t0 < T; t0 += TR) {
@@ -318,13 +351,13 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    for (int rb = 0; rb < tn; rb += CU) {
+    for (int rb = ks; rb < tn; rb += KS * CU) {
     double xs[CU];
     load_rows(t0, rb, tn, xs);
 #pragma unroll
     for (int uq = 0; uq < CU; ++uq) {
-      const int rr = rb + uq;
-      if (rr >= tn) break;
+      const int rr = rb + KS * uq;
+      if (rr < tn) {
       const int t = t0 + rr;
       const double x = xs[uq];
       const bool post = t >= bp;
@@ -332,7 +365,7 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const double f = sF[lr][rr * R + j];
-        u -= f * (post ? b1[j] + b2[j] : b1[j]);
+        u -= f * (post ? bq[j] : b1[j]);
         rs -= f * (post ? ga2[j] : ga1[j]);
       }
       ssr = fma(rs, rs, ssr);
@@ -345,10 +378,16 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
       for (int a = 0; a < R; ++a)
 #pragma unroll
         for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
+      }
     }
     }
   }
-  if (!ok) return;
+  if constexpr (KS > 1) {
+    ssr = ks_sum<KS>(ssr);
+#pragma unroll
+    for (int e = 0; e < R * (R + 1) / 2; ++e) S[e] = ks_sum<KS>(S[e]);
+  }
+  if (!ok || ks != 0) return;
   // Wald = b2' S^-1 b2 via in-register Cholesky of S (packed lower; padded
   // dimensions r..R-1 are an identity block)
   double wv = 0.0;
@@ -383,22 +422,25 @@ __global__ __launch_bounds__(256, R <= 8 ? 2 : 1) void chow_all_kernel(PanelSrc 
 
 template <int R>
 static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int N, int r, int bp, int nb,
-                          const double *F, const double *Z, const ChowPrep *prep, const double *Lm, double *LR,
+                          const double *F, const double *Z, const double *prep, const double *Lm, double *LR,
                           double *LM, double *WD, hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
-  const bool flat = R <= 8 && N >= CH_FLAT_MIN_N;
-  // non-flat: narrow panels get a block of round_up(N, 64) threads, not a half-idle 256
-  const int nth = flat ? 256 : std::min(256, (N + 63) / 64 * 64);
-  dim3 grid(flat ? (unsigned)(((int64_t)nb * N + 255) / 256) : (unsigned)((N + nth - 1) / nth), flat ? 1 : nb),
+  constexpr int KS = R <= 4 ? CH_KS : 1;   // lanes per (replicate, variable)
+  // flat: a 256-thread block (256 / KS pairs) spans at most CH_FLAT_REPS replicates
+  const bool flat = R <= 8 && (256 / KS + N - 1) / N + 1 <= CH_FLAT_REPS;
+  // non-flat: narrow panels get a block of round_up(N KS, 64) threads, not a half-idle 256
+  const int nth = flat ? 256 : std::min(256, (N * KS + 63) / 64 * 64);
+  dim3 grid(flat ? (unsigned)(((int64_t)nb * N * KS + 255) / 256) : (unsigned)((N * KS + nth - 1) / nth),
+            flat ? 1 : nb),
       block(nth);
 #define DFM_CH(C_, E_, X_, B_)                                                                                  \
   do {                                                                                                          \
     if (flat)                                                                                                   \
-      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, (R <= 8)>), grid, block, 0, st, src, blk, T, N, r, \
-                         bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                   \
+      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, (R <= 8), KS>), grid, block, 0, st, src, blk, T, N, \
+                         r, bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                \
     else                                                                                                        \
-      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_>), grid, block, 0, st, src, blk, T, N, r, bp, nb,   \
-                         F, Z, prep, Lm, LR, LM, WD);                                                           \
+      hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, false, KS>), grid, block, 0, st, src, blk, T, N, r, \
+                         bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                   \
   } while (0)
   if (blk.n > 1) {
     if (c && e && x) DFM_CH(true, true, true, true);
@@ -412,7 +454,7 @@ static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int
 #undef DFM_CH
 }
 
-// scratch layout in ws: [ChowPrep x nb][Z: nb x T x r] ... [3][nb][N] at the END.
+// scratch layout in ws: [prep blocks: nb x CH_PREP_BYTES][Z: nb x T x r] ... [3][nb][N] at the END.
 // Break models: nblk > 1 blocks with first rows brow[0..nblk-1] (brow[0] = 0),
 // loadings of block j at Lm + j * lbs.
 hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
@@ -426,10 +468,11 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
   blk.lbs = lbs;
   for (int j = 0; j < nblk; ++j) blk.a[j] = nblk > 1 ? brow[j] : 0;
   blk.a[nblk] = T;
-  ChowPrep *prep = (ChowPrep *)ws;
-  double *Z = (double *)(ws + (size_t)nb * sizeof(ChowPrep));
+  double *prep = (double *)ws;
+  double *Z = (double *)(ws + (size_t)nb * CH_PREP_BYTES);
   double *scr = (double *)(ws + ws_bytes) - (size_t)3 * nb * N;
-  hipLaunchKernelGGL(chow_prep_kernel, dim3(nb), dim3(256), 0, st, F, T, r, bp, prep, Z);
+  const int RC = r <= 4 ? 4 : (r <= 8 ? 8 : 16);   // the main kernel's padded R (below)
+  hipLaunchKernelGGL(chow_prep_kernel, dim3(nb), dim3(256), 0, st, F, T, r, bp, RC, prep, Z);
   double *LR = scr, *LM = scr + (size_t)nb * N, *WD = scr + (size_t)2 * nb * N;
   // R = padded factor count of the per-variable register blocks (zero
   // padding: r <= 4 runs 4-wide, 10 HC0 accumulators instead of 36)

@@ -393,7 +393,12 @@ __global__ void gram_wk_a0_kernel(const double *__restrict__ F, const double *__
 }
 
 // Per replicate: w (row rep of W, zero-padded to Tp) and B = F' D P E (r x N).
-// idx / eta of the replicate staged in LDS; w_s by a scan over t (fixed order).
+// idx / eta of the replicate staged in LDS.  w_s = sum of eta_t^2 over the
+// t with idx_t = s, ascending t: a counting sort of t by idx_t (bucket
+// counts, a block scan, slots handed out by LDS atomics in any order, each
+// bucket then insertion-sorted by t), O(T) per replicate — the same sums in
+// the same order as a scan over every t (round 3's O(T^2) form, which added
+// +0 for the t outside the bucket), so bit-identical to it.
 template <int RM>
 __global__ __launch_bounds__(256) void gram_wk_prep_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N,
                                                            int r, const double *__restrict__ F,
@@ -401,33 +406,52 @@ __global__ __launch_bounds__(256) void gram_wk_prep_kernel(const double *__restr
                                                            const double *__restrict__ eta, int64_t rs, int Tp,
                                                            double *__restrict__ W, double *__restrict__ Bo) {
   extern __shared__ double pdyn[];
+  __shared__ int scan[256];
   double *se = pdyn;                 // eta_t
   double *sF = pdyn + T;             // F (T x r)
   int *sx = (int *)(sF + (int64_t)T * r);   // idx_t
+  int *cnt = sx + ((T + 7) & ~7);           // bucket starts, then ends (T + 1)
+  int *lst = cnt + ((T + 8) & ~7);          // t by bucket (T)
   const int rep = blockIdx.x, tid = threadIdx.x;
   const int32_t *ix = idx + (int64_t)rep * rs;
   const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
   for (int t = tid; t < T; t += 256) { sx[t] = ix[t]; se[t] = et ? et[t] : 1.0; }
   for (int e = tid; e < T * r; e += 256) sF[e] = F[e];
+  for (int s = tid; s <= T; s += 256) cnt[s] = 0;
   __syncthreads();
-  // w_s = sum over t ascending of eta_t^2 [idx_t == s]: branch-free (adding
-  // +0 leaves the sum unchanged), 8 rows per round from LDS (broadcast reads)
-  double *se2 = pdyn + T + (int64_t)T * r + ((T + 7) & ~7) / 2;   // eta_t^2 (after sx: round_up(T, 8) ints)
-  for (int t = tid; t < T; t += 256) se2[t] = se[t] * se[t];
-  for (int t = T + tid; t < ((T + 7) & ~7); t += 256) { sx[t] = -1; se2[t] = 0.0; }
+  for (int t = tid; t < T; t += 256) atomicAdd(&cnt[sx[t] + 1], 1);
   __syncthreads();
+  {   // inclusive scan of cnt[0..T]: per-thread chunks, then a 256-wide scan of the chunk sums
+    const int per = (T + 1 + 255) / 256, c0 = min(T + 1, tid * per), c1 = min(T + 1, c0 + per);
+    int run = 0;
+    for (int q = c0; q < c1; ++q) run += cnt[q];
+    scan[tid] = run;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const int v = tid >= o ? scan[tid - o] : 0;
+      __syncthreads();
+      scan[tid] += v;
+      __syncthreads();
+    }
+    run = scan[tid] - run;
+    for (int q = c0; q < c1; ++q) { run += cnt[q]; cnt[q] = run; }   // cnt[s] = start of bucket s
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += 256) lst[atomicAdd(&cnt[sx[t]], 1)] = t;
+  __syncthreads();   // cnt[s] is now the END of bucket s
   double *Wr = W + (int64_t)rep * Tp;
   for (int s = tid; s < Tp; s += 256) {
     double acc = 0.0;
-    if (s < T)
-      for (int t0 = 0; t0 < T; t0 += 8) {
-        int xv[8];
-        double ev[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) { xv[u] = sx[t0 + u]; ev[u] = se2[t0 + u]; }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = acc + (xv[u] == s ? ev[u] : 0.0);
+    if (s < T) {
+      const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
+      for (int i = b0 + 1; i < b1; ++i) {   // insertion sort of the bucket by t (Poisson(1) sized)
+        const int v = lst[i];
+        int j = i - 1;
+        while (j >= b0 && lst[j] > v) { lst[j + 1] = lst[j]; --j; }
+        lst[j + 1] = v;
       }
+      for (int i = b0; i < b1; ++i) { const double e = se[lst[i]]; acc = __dadd_rn(acc, __dmul_rn(e, e)); }
+    }
     Wr[s] = acc;
   }
   double *Br = Bo + (int64_t)rep * r * N;
@@ -506,10 +530,11 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done, int col_group, bool b_padded, const int *clist, const int *ccount);
 
-// gram_wk_prep_kernel's dynamic LDS: se (T), sF (T x r), sx (round_up(T, 8) ints), se2
+// gram_wk_prep_kernel's dynamic LDS: se (T), sF (T x r), sx (round_up(T, 8) ints), the
+// bucket bounds (round_up(T + 1, 8) ints) and the bucketed t (T ints)
 size_t gram_wk_prep_lds(int T, int r) {
-  const size_t T8 = (size_t)((T + 7) & ~7);
-  return (size_t)T * 8 + (size_t)T * r * 8 + T8 * 4 + T8 * 8;
+  const size_t T8 = (size_t)((T + 7) & ~7), T18 = (size_t)((T + 8) & ~7);
+  return (size_t)T * 8 + (size_t)T * r * 8 + T8 * 4 + T18 * 4 + (size_t)T * 4;
 }
 int64_t gram_wk_ldk(int N) { return ((int64_t)N * (N + 1) / 2 + 1) / 2 * 2; }
 int gram_wk_tp(int T) { return (T + 15) / 16 * 16; }
