@@ -1211,6 +1211,18 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
                                       ((kd == DFM_STAT_COEF || kd == DFM_STAT_TSTAT) && stats[i].arg0 < q));
   }
   const int esub = (subspace_only && !values_only) ? 1 : 0;
+  // Fields the statistics read (demand-driven, as the stopping rule above):
+  // V, the criteria, eigenvalues and the trace need only the eigensolve;
+  // the replicate factors F* and loadings L* (the factored path's loadings
+  // GEMM) are formed for coefficients / t-statistics, the Chow tests and the
+  // host-closure fields, the OLS + HC2 pass for coefficients / t-statistics.
+  bool need_fl = false, need_ols = false;
+  for (int i = 0; i < ns; ++i) {
+    const int kd = stats[i].kind;
+    need_ols = need_ols || kd == DFM_STAT_COEF || kd == DFM_STAT_TSTAT;
+    need_fl = need_fl || kd == DFM_STAT_COEF || kd == DFM_STAT_TSTAT || chow_stat(kd) || kd == DFM_STAT_FACTORS ||
+              kd == DFM_STAT_LOADINGS;
+  }
   const int p = eig_block_p(m, r, ctx->block);
   // r beyond the subspace eigensolver's block: dense batched eigenpairs,
   // materialised replicate panels for the factor GEMMs, GEMM-built OLS
@@ -1357,9 +1369,11 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
                                 (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
-      Scope sc(ctx, DFM_KC_FACTORS);
-      rc = fact_loadings(fb, M->Ep, M->ld, N, M->L, w.Uk, et, w.off, w.lst, n, w.F, w.L, w.fload, st);
-      if (rc) return fail(ctx, rc, "factored loadings failed");
+      if (need_fl) {
+        Scope sc(ctx, DFM_KC_FACTORS);
+        rc = fact_loadings(fb, M->Ep, M->ld, N, M->L, w.Uk, et, w.off, w.lst, n, w.F, w.L, w.fload, st);
+        if (rc) return fail(ctx, rc, "factored loadings failed");
+      }
     } else if (M->nblk > 1) {
       // refit per break block (src/bootstrap.jl:36, :48 pass dfm.break_indices):
       // block j of X*_b is rows a..a+t_j-1 of C + diag(eta_b) E[idx_b, :]
@@ -1374,7 +1388,8 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
         int rc = eig_any(w.G, mj, n, M->Ubs[j], w.blam, w.Uk, w.btr, b0);
         if (rc) return rc;
         hipLaunchKernelGGL(or_flag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, n, M->flag_dev, 1);
-        if ((rc = factors_any(sj, tj, n, w.F + (size_t)a * r, w.Uk, w.L + (size_t)j * nb * N * r))) return rc;
+        if (need_fl && (rc = factors_any(sj, tj, n, w.F + (size_t)a * r, w.Uk, w.L + (size_t)j * nb * N * r)))
+          return rc;
         hipLaunchKernelGGL(block_accum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.blam, w.btr, n, r,
                            w.lam, w.trace, j == 0 ? 1 : 0);
       }
@@ -1392,8 +1407,8 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       }
       int rc = eig_any(w.G, m, n, M->Ub, w.lam, w.Uk, w.trace, b0);
       if (rc) return rc;
-      bool done_f = false;
-      if (gwk) {   // T >= N: F* = (F (L' L*) + D P (E L*)) / N, no pass over the resampled panel
+      bool done_f = !need_fl;
+      if (gwk && need_fl) {   // T >= N: F* = (F (L' L*) + D P (E L*)) / N, no pass over the resampled panel
         Scope sc(ctx, DFM_KC_FACTORS);
         done_f = launch_factors_cols_fact(M->Ep, M->ld, T, N, r, M->F, M->L, r, idx + b0 * T,
                                           kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, w.Uk, w.F, w.L,
@@ -1401,7 +1416,9 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       }
       if (!done_f && (rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
     }
-    if (q + r <= 32) {
+    if (!need_ols) {
+      HIPCHK(ctx, hipMemsetAsync(w.ost, 0, (size_t)n * 4, st));   // (no design to be singular)
+    } else if (q + r <= 32) {
       Scope sc(ctx, DFM_KC_OLS);
       launch_ols(n, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
                          w.tstat, nullptr, nullptr, w.ost);
