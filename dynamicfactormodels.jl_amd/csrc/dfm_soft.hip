@@ -31,6 +31,7 @@
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <utility>
 #include <cmath>
 #include <vector>
@@ -1393,9 +1394,15 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     const auto h0 = std::chrono::steady_clock::now();
     if (e == hipSuccess) hipLaunchKernelGGL(lasso_coop_kernel, dim3(nblk), dim3(LP_NT), 0, st, A);
     if (e == hipSuccess) e = hipGetLastError();
+    const auto h1 = std::chrono::steady_clock::now();
+    static const bool poll = getenv("DFM_LASSO_SYNC_POLL") != nullptr;   // diagnostic: query instead of a blocking wait
+    if (e == hipSuccess && poll) {
+      while ((e = hipStreamQuery(st)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    const long long host_us =
-        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - h0).count();
+    const auto h2 = std::chrono::steady_clock::now();
+    const long long host_us = std::chrono::duration_cast<std::chrono::microseconds>(h2 - h0).count();
+    const long long launch_us = std::chrono::duration_cast<std::chrono::microseconds>(h1 - h0).count();
     if (e != hipSuccess) break;
     lasso_stat_add(DFM_LASSO_STAT_LAUNCHES, 1);
     if (attempt > 0) lasso_stat_add(DFM_LASSO_STAT_RELAUNCHES, 1);
@@ -1414,8 +1421,8 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     if (t1 > e0) lasso_stat_add(DFM_LASSO_STAT_LATE_ENTRIES, 1);
     if (host_us > 2 * (e1 - t0) / 100 + 50000) {   // the launch, not the kernel, took the time
       lasso_stat_add(DFM_LASSO_STAT_SLOW_LAUNCHES, 1);
-      fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host for a %lld us kernel (%d workgroups)\n",
-              attempt + 1, host_us, (e1 - t0) / 100, nblk);
+      fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host (launch call %lld us) for a %lld us kernel (%d "
+              "workgroups)\n", attempt + 1, host_us, launch_us, (e1 - t0) / 100, nblk);
     }
     for (int b = 0; b < nblk; ++b) {
       const LassoDiag &d = hd[b];

@@ -367,8 +367,8 @@ def test_bootstrap_chow_with_block_equal_r(dfm, oracle, T, N):
     convergence rule has no unwanted Ritz value to measure a gap against, so
     it must fall back to the neighbour gaps (a Chow-only call turns the
     subspace rule on).  Replicates against the oracle at the usual bar."""
-    r = 3
-    y, x, w = panel(oracle, T, N, r, 23, model="Breitung_Eickmeier_2011", b=0.5)
+    r = 3   # (Bai-Ng strong factors: without guard vectors the block converges at lambda_4 / lambda_3 per step)
+    y, x, w = panel(oracle, T, N, r, 23)
     ctx = dfm.Context(0)
     ctx.set_eig_params(block=r)
     g = dfm.DynamicFactorModel(y, w, x, r, ctx=ctx)
