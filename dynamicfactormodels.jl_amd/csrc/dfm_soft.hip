@@ -952,7 +952,12 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   };
   long long pt = wall_clock64();
   const long long tstart = pt;
-  long long pacc[LP_PROF] = {0};
+  // diagnostics accumulators (A.prof) in LDS: a private array whose address
+  // is taken (tk) would put the kernel on scratch
+  __shared__ long long s_prof[LP_PROF];
+  long long *pacc = s_prof;
+  if (tid < LP_PROF) pacc[tid] = 0;
+  __syncthreads();
   long long *tk = A.prof ? pacc + 8 : nullptr;
   auto ptick = [&](int i) {   // leader phase timing (A.prof): thread 0 only
     if (A.prof && tid == 0) { const long long t = wall_clock64(); pacc[i] += t - pt; pt = t; }
