@@ -539,6 +539,9 @@ class ReplicateFit:
         return self.y - self.design_matrix @ self.coefficients
 
 
+_CLOSURE_CHUNK_BYTES = 500_000_000   # host rows per device call of the closure path
+
+
 def _bootstrap_closure(dfm, kind, B, fn, idx, eta, run_rows):
     """The host-closure escape: every replicate's fields from the device
     (chunked to ~0.5 GB of host rows), then ``fn(ReplicateFit)`` per
@@ -555,7 +558,7 @@ def _bootstrap_closure(dfm, kind, B, fn, idx, eta, run_rows):
     width = 1 + int(crit) + r + 2 * d + T * r + nblk * N * r
     E = dfm.factor_residuals
     C0 = dfm.x - E                                    # the common component F L' (blockwise, D1)
-    chunk = int(max(1, min(B, 0.5e9 // (8 * width))))
+    chunk = int(max(1, min(B, _CLOSURE_CHUNK_BYTES // (8 * width))))
     out = np.empty(B)
     for c0 in range(0, B, chunk):
         c1 = min(B, c0 + chunk)
