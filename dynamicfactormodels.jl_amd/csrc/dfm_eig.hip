@@ -926,8 +926,12 @@ int eig_block_P(int m, int k) {
   const int p = std::min(m, std::max(k + 8, 16));
   return p <= 16 ? 16 : (p <= 32 ? 32 : -1);
 }
+// A requested block below k + 1 is raised to k + 1: the Chebyshev filter's
+// interval [0, theta_p] must lie below every wanted eigenvalue, so the block
+// needs at least one guard vector (p == k: theta_p is the k-th WANTED value
+// and the filter stops amplifying it — the k-th vector then never converges)
 int eig_block_p(int m, int k, int req) {
-  int p = req > 0 ? req : std::max(k + 8, 16);
+  int p = req > 0 ? std::max(req, k + 1) : std::max(k + 8, 16);
   p = std::min(p, m);
   return p;
 }

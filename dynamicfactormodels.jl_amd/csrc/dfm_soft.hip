@@ -211,6 +211,7 @@ struct alignas(128) LassoDiag {
   unsigned long long seen_rmw; // ... read by an agent-scope fetch_or(0)
   int kind, expect, xcc, hwid; // first timeout's kind (LD_*), the tag it waited for; placement
   int m, seq, lane, ntmo;      // lambda index / task number / the polled helper; timeouts in all
+  int wend[8];                 // per wave: exit - entry, wall-clock ticks
 };
 
 struct LassoArgs {
@@ -827,7 +828,8 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
   const int grp = blockIdx.x / (A.H + 1), role = blockIdx.x % (A.H + 1), f = grp, p = A.p, H = A.H;
   LassoCtl *ctl = A.ctl + f;
   LassoDiag *dg = A.diag + blockIdx.x;
-  if (tid == 0) { dg->t_start = wall_clock64(); dg->xcc = lp_xcc(); dg->hwid = lp_hwid(); }
+  const long long t_wave = wall_clock64();   // this wave's entry (its exit stamp: wend)
+  if (tid == 0) { dg->t_start = t_wave; dg->xcc = lp_xcc(); dg->hwid = lp_hwid(); }
   int *kl = A.klist + (int64_t)f * LP_LMAX;
   double *dl = A.dlist + (int64_t)f * LP_LMAX;
   if (role > 0) {   // ------------------------------------------------ helper
@@ -883,6 +885,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       for (int i = 0; i < 4; ++i) A.prof[(int64_t)f * LP_PROF + 20 + i] = hb[i];
     if (A.prof && h == 0 && tid == 0) { A.prof[(int64_t)f * LP_PROF + 26] = hb[4]; A.prof[(int64_t)f * LP_PROF + 27] = hb[5]; }
     if (tid == 0) dg->t_end = wall_clock64();
+    if (lane == 0) dg->wend[wave] = (int)(wall_clock64() - t_wave);
     return;
   }
   // ----------------------------------------------------------------- leader
@@ -1227,6 +1230,7 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
     else A.nlam_out[f] = L;
     dg->t_end = wall_clock64();
   }
+  if (lane == 0) dg->wend[wave] = (int)(wall_clock64() - t_wave);
 }
 
 // G_f's diagonal := 1 over the non-constant columns (elnet1's c(k,k) = xv(k) = 1)
@@ -1396,8 +1400,13 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     e = zero_all();
     if (e != hipSuccess) break;
     e = hipStreamSynchronize(st);   // (the launch's own wall time below: the memsets and earlier work done)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (e == hipSuccess) e = hipEventCreate(&ev0);
+    if (e == hipSuccess) e = hipEventCreate(&ev1);
     const auto h0 = std::chrono::steady_clock::now();
+    if (e == hipSuccess) e = hipEventRecord(ev0, st);
     if (e == hipSuccess) hipLaunchKernelGGL(lasso_coop_kernel, dim3(nblk), dim3(LP_NT), 0, st, A);
+    if (e == hipSuccess) e = hipEventRecord(ev1, st);
     if (e == hipSuccess) e = hipGetLastError();
     const auto h1 = std::chrono::steady_clock::now();
     static const bool poll = getenv("DFM_LASSO_SYNC_POLL") != nullptr;   // diagnostic: query instead of a blocking wait
@@ -1408,6 +1417,10 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     const auto h2 = std::chrono::steady_clock::now();
     const long long host_us = std::chrono::duration_cast<std::chrono::microseconds>(h2 - h0).count();
     const long long launch_us = std::chrono::duration_cast<std::chrono::microseconds>(h1 - h0).count();
+    float ev_ms = -1.0f;
+    if (e == hipSuccess && ev0 && ev1) hipEventElapsedTime(&ev_ms, ev0, ev1);
+    if (ev0) hipEventDestroy(ev0);
+    if (ev1) hipEventDestroy(ev1);
     if (e != hipSuccess) break;
     lasso_stat_add(DFM_LASSO_STAT_LAUNCHES, 1);
     if (attempt > 0) lasso_stat_add(DFM_LASSO_STAT_RELAUNCHES, 1);
@@ -1415,10 +1428,11 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     if ((e = hipMemcpy(hs.data(), sts, hs.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess) break;
     if ((e = hipMemcpy(hd.data(), A.diag, hd.size() * sizeof(LassoDiag), hipMemcpyDeviceToHost)) != hipSuccess) break;
     // residency: the latest entry against the earliest exit
-    long long t0 = LLONG_MAX, t1 = 0, e0 = LLONG_MAX, e1 = 0;
+    long long t0 = LLONG_MAX, t1 = 0, e0 = LLONG_MAX, e1 = 0, w1 = 0;
     for (const LassoDiag &d : hd) {
       t0 = std::min(t0, d.t_start); t1 = std::max(t1, d.t_start);
       e0 = std::min(e0, d.t_end); e1 = std::max(e1, d.t_end);
+      for (int wv = 0; wv < LP_NT / 64; ++wv) w1 = std::max(w1, d.t_start + d.wend[wv]);   // (waves enter together)
     }
     lasso_stat_max(DFM_LASSO_STAT_MAX_SKEW_US, (t1 - t0) / 100);
     lasso_stat_max(DFM_LASSO_STAT_MAX_KERNEL_US, (e1 - t0) / 100);
@@ -1426,8 +1440,9 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     if (t1 > e0) lasso_stat_add(DFM_LASSO_STAT_LATE_ENTRIES, 1);
     if (host_us > 2 * (e1 - t0) / 100 + 50000) {   // the launch, not the kernel, took the time
       lasso_stat_add(DFM_LASSO_STAT_SLOW_LAUNCHES, 1);
-      fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host (launch call %lld us) for a %lld us kernel (%d "
-              "workgroups)\n", attempt + 1, host_us, launch_us, (e1 - t0) / 100, nblk);
+      fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host (launch call %lld us, events %.0f us) for a %lld us "
+              "kernel (last wave exit +%lld us, %d workgroups)\n", attempt + 1, host_us, launch_us, ev_ms * 1e3,
+              (e1 - t0) / 100, (w1 - t0) / 100, nblk);
     }
     for (int b = 0; b < nblk; ++b) {
       const LassoDiag &d = hd[b];

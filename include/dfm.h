@@ -78,7 +78,9 @@ const char *dfm_last_error(const dfm_ctx *ctx);
 int dfm_ctx_set_stream(dfm_ctx *ctx, void *hip_stream); /* NULL = own stream */
 int dfm_ctx_synchronize(dfm_ctx *ctx);
 /* Eigensolver controls: relative residual tolerance (default 1e-12), maximum
- * subspace iterations (default 400), block width (0 = auto). */
+ * subspace iterations (default 400), block width (0 = auto; a block below
+ * r + 1 is raised to r + 1: the filtered subspace iteration needs a guard
+ * vector beyond the r wanted ones). */
 int dfm_ctx_set_eig_params(dfm_ctx *ctx, double tol, int max_iter, int block);
 /* Per-kernel HIP-event timing on the context stream (bench/roofline use). */
 /* Bootstrap calls whose statistics are all eigenvalue functions (V, CRIT,

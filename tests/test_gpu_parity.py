@@ -363,10 +363,13 @@ def test_bootstrap_host_closure_matches_oracle_loop(dfm, oracle, T, N, breaks):
 
 @pytest.mark.parametrize("T,N", [(80, 120), (160, 24)])
 def test_bootstrap_chow_with_block_equal_r(dfm, oracle, T, N):
-    """Eigen block p == r (dfm_ctx_set_eig_params block = r): the subspace
-    convergence rule has no unwanted Ritz value to measure a gap against, so
-    it must fall back to the neighbour gaps (a Chow-only call turns the
-    subspace rule on).  Replicates against the oracle at the usual bar."""
+    """A requested eigen block of r (dfm_ctx_set_eig_params block = r): the
+    library raises it to r + 1 — with p == r the subspace convergence rule
+    has no unwanted Ritz value to measure a gap against (it now falls back to
+    the neighbour gaps) and the Chebyshev filter's interval reaches the r-th
+    wanted eigenvalue, which then never converges.  A Chow-only call (the
+    subspace rule) with the smallest block: replicates against the oracle at
+    the usual bar."""
     r = 3   # (Bai-Ng strong factors: without guard vectors the block converges at lambda_4 / lambda_3 per step)
     y, x, w = panel(oracle, T, N, r, 23)
     ctx = dfm.Context(0)
