@@ -1429,10 +1429,13 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     if ((e = hipMemcpy(hd.data(), A.diag, hd.size() * sizeof(LassoDiag), hipMemcpyDeviceToHost)) != hipSuccess) break;
     // residency: the latest entry against the earliest exit
     long long t0 = LLONG_MAX, t1 = 0, e0 = LLONG_MAX, e1 = 0, w1 = 0;
-    for (const LassoDiag &d : hd) {
+    int wb = 0, ww = 0;   // the last wave to leave: workgroup, wave
+    for (int b = 0; b < nblk; ++b) {
+      const LassoDiag &d = hd[b];
       t0 = std::min(t0, d.t_start); t1 = std::max(t1, d.t_start);
       e0 = std::min(e0, d.t_end); e1 = std::max(e1, d.t_end);
-      for (int wv = 0; wv < LP_NT / 64; ++wv) w1 = std::max(w1, d.t_start + d.wend[wv]);   // (waves enter together)
+      for (int wv = 0; wv < LP_NT / 64; ++wv)   // (waves enter together)
+        if (d.t_start + d.wend[wv] > w1) { w1 = d.t_start + d.wend[wv]; wb = b; ww = wv; }
     }
     lasso_stat_max(DFM_LASSO_STAT_MAX_SKEW_US, (t1 - t0) / 100);
     lasso_stat_max(DFM_LASSO_STAT_MAX_KERNEL_US, (e1 - t0) / 100);
@@ -1441,8 +1444,11 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     if (host_us > 2 * (e1 - t0) / 100 + 50000) {   // the launch, not the kernel, took the time
       lasso_stat_add(DFM_LASSO_STAT_SLOW_LAUNCHES, 1);
       fprintf(stderr, "[dfm] lasso launch %d: %lld us on the host (launch call %lld us, events %.0f us) for a %lld us "
-              "kernel (last wave exit +%lld us, %d workgroups)\n", attempt + 1, host_us, launch_us, ev_ms * 1e3,
-              (e1 - t0) / 100, (w1 - t0) / 100, nblk);
+              "kernel (last wave exit +%lld us: problem %d %s %d wave %d, its workgroup's tid 0 left at +%lld us; "
+              "waves' exits there:", attempt + 1, host_us, launch_us, ev_ms * 1e3, (e1 - t0) / 100, (w1 - t0) / 100,
+              wb / (H + 1), wb % (H + 1) ? "helper" : "leader", wb % (H + 1), ww, (hd[wb].t_end - t0) / 100);
+      for (int wv = 0; wv < LP_NT / 64; ++wv) fprintf(stderr, " %d", hd[wb].wend[wv] / 100);
+      fprintf(stderr, " us; %d workgroups)\n", nblk);
     }
     for (int b = 0; b < nblk; ++b) {
       const LassoDiag &d = hd[b];
