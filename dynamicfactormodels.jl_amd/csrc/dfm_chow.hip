@@ -60,26 +60,44 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
   const int tid = threadIdx.x, rep = blockIdx.x;
   const double *Fr = F + (int64_t)rep * T * r;
   if (tid == 0) bad = 0;
-  for (int e = tid; e < 2 * r * r; e += 256) {
-    const int which = e / (r * r), a = (e / r) % r, c = e % r;
-    const int t0 = which ? bp : 0, t1 = which ? T : bp;
-    // 16 rows' operands loaded before their (in-order) products: the sum is
-    // the same dependent chain, without one load latency per row
-    constexpr int PU = 16;
-    double s = 0.0;
-    for (int tb = t0; tb < t1; tb += PU) {
-      double fa[PU], fc[PU];
+  // A1 = F1'F1, A2 = F2'F2: the 2 r^2 entries x ns row strips over the
+  // threads (C2, r = 3: 18 entries x 14 strips — one entry per thread made 18
+  // T/2-long dependent chains the whole workgroup waited on); each strip's
+  // partial sum in LDS, then the strips summed in order (fixed order:
+  // per-replicate, batch-invariant)
+  const int ne = 2 * r * r, ns = ne >= 256 ? 1 : 256 / ne, nst = ne < 256 ? ne : 256;
+  for (int e0 = 0; e0 < ne; e0 += 256) {
+    const int e = e0 + tid % ne, sp = tid / ne;
+    if (e0 + tid < ne * ns && (ns > 1 || e < ne)) {
+      const int which = e / (r * r), a = (e / r) % r, c = e % r;
+      const int t0 = which ? bp : 0, t1 = which ? T : bp, len = t1 - t0;
+      const int q0 = t0 + (int)((int64_t)len * sp / ns), q1 = t0 + (int)((int64_t)len * (sp + 1) / ns);
+      // 16 rows' operands loaded before their (in-order) products
+      constexpr int PU = 16;
+      double sacc = 0.0;
+      for (int tb = q0; tb < q1; tb += PU) {
+        double fa[PU], fc[PU];
 #pragma unroll
-      for (int u = 0; u < PU; ++u) {
-        const int t = min(tb + u, t1 - 1);
-        fa[u] = Fr[(int64_t)t * r + a];
-        fc[u] = Fr[(int64_t)t * r + c];
+        for (int u = 0; u < PU; ++u) {
+          const int t = min(tb + u, q1 - 1);
+          fa[u] = Fr[(int64_t)t * r + a];
+          fc[u] = Fr[(int64_t)t * r + c];
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u)
+          if (tb + u < q1) sacc = fma(fa[u], fc[u], sacc);
       }
-#pragma unroll
-      for (int u = 0; u < PU; ++u)
-        if (tb + u < t1) s = fma(fa[u], fc[u], s);
+      Tw[sp * nst + e - e0] = sacc;   // (Tw: scratch until the inverses below; < 256 entries)
     }
-    (which ? A2s : A1)[a * S + c] = s;
+    __syncthreads();
+    if (tid < min(256, ne - e0)) {
+      const int e = e0 + tid;
+      const int which = e / (r * r), a = (e / r) % r, c = e % r;
+      double sacc = 0.0;
+      for (int q = 0; q < ns; ++q) sacc += Tw[q * nst + tid];
+      (which ? A2s : A1)[a * S + c] = sacc;
+    }
+    __syncthreads();
   }
   __syncthreads();
   const int n2 = 2 * r;
