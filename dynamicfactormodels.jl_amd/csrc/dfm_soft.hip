@@ -1204,9 +1204,18 @@ __global__ __launch_bounds__(LP_NT, 1) void lasso_coop_kernel(LassoArgs A) {
       break;
     }
     // folds stop once the full fit (running concurrently) has published a
-    // path length they have reached
+    // path length they have reached.  ONE thread reads the published length
+    // and the workgroup decides on that one value: read by every thread (as
+    // in round 3), waves could see it on different sides of its publication,
+    // wave 0 then left for the exit while waves 1..7 ran into the next lambda
+    // and waited on wave 0's pipeline counters until the spin timeout — the
+    // 2 s stalls of round 3 (the kernel's workgroups done, these waves not;
+    // tools/soft_repeat.py)
     if (A.early && f > 0) {
-      const int Lp = __hip_atomic_load(A.nlam_out, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (tid == 0) s_i[6] = __hip_atomic_load(A.nlam_out, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int Lp = s_i[6];
       if (Lp > 0 && m + 1 >= Lp) { L = m + 1; break; }
     }
   }
