@@ -114,7 +114,7 @@ SIGNATURES = [
 # dfm_lasso_stats slots (include/dfm.h DFM_LASSO_STAT_*)
 LASSO_STATS = ("launches", "relaunches", "timeouts", "task_timeouts", "done_timeouts", "pipe_timeouts",
                "budget_overruns", "recovered", "max_skew_us", "late_entries", "max_kernel_us",
-               "max_host_us", "slow_launches")
+               "max_host_us", "slow_launches", "wave_splits")
 
 _lock = threading.Lock()
 _lib = None

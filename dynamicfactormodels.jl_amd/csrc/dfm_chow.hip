@@ -160,12 +160,15 @@ constexpr int CH_FLAT_REPS = 4, CH_FLAT_MIN_N = 86;   // ceil(256 / 86) + 1 <= 4
 // C2-sized job (500 replicates x 130 variables) is then 4 waves per SIMD
 // instead of one — the kernel is latency-bound (a dependent chain per
 // accumulator over T rows), not VALU-bound.
-#ifndef DFM_CH_KS   // (A/B builds: make EXTRA=-DDFM_CH_KS=1)
-#define DFM_CH_KS 4
+#ifndef DFM_CH_KS   // (A/B builds: make EXTRA="-DDFM_CH_KS=1 -DDFM_CH_WAVES=2")
+#define DFM_CH_KS 2
+#endif
+#ifndef DFM_CH_WAVES
+#define DFM_CH_WAVES 3
 #endif
 constexpr int CH_KS = DFM_CH_KS;
 template <int R, int KS>
-constexpr int chow_waves() { return (R <= 4 && KS > 1) ? 3 : (R <= 8 ? 2 : 1); }
+constexpr int chow_waves() { return (R <= 4 && KS > 1) ? DFM_CH_WAVES : (R <= 8 ? 2 : 1); }
 // x[a] / x[a] := v for a runtime a, by compile-time indices (no scratch)
 template <int R>
 DFM_DEV double rsel(const double (&x)[R], int a) {

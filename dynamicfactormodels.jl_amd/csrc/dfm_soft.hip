@@ -1439,13 +1439,21 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
     // residency: the latest entry against the earliest exit
     long long t0 = LLONG_MAX, t1 = 0, e0 = LLONG_MAX, e1 = 0, w1 = 0;
     int wb = 0, ww = 0;   // the last wave to leave: workgroup, wave
+    long long split = 0;  // widest spread of one workgroup's wave exits
     for (int b = 0; b < nblk; ++b) {
       const LassoDiag &d = hd[b];
       t0 = std::min(t0, d.t_start); t1 = std::max(t1, d.t_start);
       e0 = std::min(e0, d.t_end); e1 = std::max(e1, d.t_end);
-      for (int wv = 0; wv < LP_NT / 64; ++wv)   // (waves enter together)
+      int lo = INT_MAX, hi = 0;
+      for (int wv = 0; wv < LP_NT / 64; ++wv) {   // (waves enter together)
+        lo = std::min(lo, d.wend[wv]); hi = std::max(hi, d.wend[wv]);
         if (d.t_start + d.wend[wv] > w1) { w1 = d.t_start + d.wend[wv]; wb = b; ww = wv; }
+      }
+      split = std::max(split, (long long)(hi - lo));
     }
+    // a workgroup's waves leave together; 1 ms apart means they took
+    // different paths (round 3's lost wake-up was that: see the folds' exit)
+    if (split > 100000) lasso_stat_add(DFM_LASSO_STAT_WAVE_SPLITS, 1);
     lasso_stat_max(DFM_LASSO_STAT_MAX_SKEW_US, (t1 - t0) / 100);
     lasso_stat_max(DFM_LASSO_STAT_MAX_KERNEL_US, (e1 - t0) / 100);
     lasso_stat_max(DFM_LASSO_STAT_MAX_HOST_US, host_us);

@@ -377,6 +377,7 @@ enum {
   DFM_LASSO_STAT_MAX_KERNEL_US,  /* longest kernel: first entry to last exit (us) */
   DFM_LASSO_STAT_MAX_HOST_US,    /* longest launch + synchronisation seen by the host (us) */
   DFM_LASSO_STAT_SLOW_LAUNCHES,  /* launches whose host time exceeded 2x the kernel + 50 ms */
+  DFM_LASSO_STAT_WAVE_SPLITS,    /* launches where one workgroup's waves left > 1 ms apart */
   DFM_LASSO_NSTATS
 };
 int dfm_lasso_stats(int64_t *out, int n, int reset);

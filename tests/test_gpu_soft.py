@@ -24,15 +24,17 @@ LAM_RTOL = 1e-12
 LOSS_RTOL = 1e-9
 BETA_TOL = 1e-8
 CLEAN = ("relaunches", "timeouts", "task_timeouts", "done_timeouts", "pipe_timeouts", "budget_overruns",
-         "late_entries")
+         "late_entries", "slow_launches", "wave_splits")
 
 
 @pytest.fixture(autouse=True)
 def clean_launch_record(dfm):
     """Every lasso launch of every test completes with no timed-out
-    leader/helper spin, no relaunch and every workgroup resident
-    (``lasso_stats``): a hand-off that only completed through
-    its timeout, or a relaunch that hid one, fails the test."""
+    leader/helper spin, no relaunch, every workgroup resident, every
+    workgroup's waves leaving together and the host's wait no longer than the
+    kernel (``lasso_stats``): a hand-off that only completed
+    through its timeout, a relaunch that hid one, or waves left spinning after
+    their workgroup's wave 0 exited (round 3's 2 s stalls) fail the test."""
     dfm.lasso_stats(reset=True)
     yield
     st = dfm.lasso_stats(reset=True)
@@ -137,8 +139,9 @@ def test_soft_rejects_bad_folds(dfm, oracle):
 
 
 def test_soft_repeated_calls_are_clean_and_stable(dfm, oracle):
-    """Round 3's intermittent lost wake-up showed up once in 60 back-to-back
-    calls of the p = 42 case (a 2 s stall).  200 calls in one process: the
+    """Round 3's intermittent 2 s stall (a fold leader's waves 1..7 spinning
+    until the timeout after wave 0 had left) showed up in ~1 of
+    6 back-to-back calls of this p = 42 case.  200 calls in one process: the
     same mask each time, no call slower than 20x the median, and the launch
     record (fixture above) clean."""
     import time
