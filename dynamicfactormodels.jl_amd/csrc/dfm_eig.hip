@@ -41,7 +41,7 @@ struct EigWork {
   // rotations within span(F_r) — Chow tests, V, criteria, eigenvalues)
   int subspace;
 };
-#define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)wall_clock64(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
 
 // ----------------------------------------------------------------- init
@@ -74,19 +74,20 @@ __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int6
 // same data (so they agree); row block 0 records the verdict.  Called by one
 // whole wave: lane (j, r) loads one partial, the sum over r is a fixed-order
 // shuffle tree — no serial chain of dependent global loads.
+// tail: the small record's tail (theta[P], dead[P], residual history 2 x P);
+// rp: the nrb row-block residual partials (P apart); d: the replicate's done flag.
 template <int P>
-DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb, int k, int p,
-                            double tol, int it, int check_only) {
+DFM_DEV int check_converged(EigWork &w, double *tail, const double *rp, double tr, int d, int rep, int rb,
+                            int nrb, int k, int p, double tol, int it, int check_only) {
   const int lane = threadIdx.x & 63;
-  int d = w.done[rep];
   if (!d && it > 0) {
     // Converged when every wanted Ritz pair j < k satisfies
     //   res_j <= tol * gap_j            (eigenvector error ~ res/gap <= tol)
     // or sits at the rounding floor: res_j <= 2e-14 |theta_1|, or
     //   res_j <= 1e-11 |theta_1| and stagnating (no 2x decrease).
-    const double *th = small + 2 * P * P;
-    const double *prev = small + 2 * P * P + 2 * P + ((it - 1) & 1) * P;
-    double *next = small + 2 * P * P + 2 * P + (it & 1) * P;
+    const double *th = tail;
+    const double *prev = tail + 2 * P + ((it - 1) & 1) * P;
+    double *next = tail + 2 * P + (it & 1) * P;
     const double th0 = fabs(th[0]);
     bool ok = true;
     if (tol < 0.0) {
@@ -102,7 +103,7 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
       bool okall = true, floor_ok = true;
       for (int j = lane; j < k; j += 64) {
         double rs = 0.0;
-        for (int r = 0; r < nrb; ++r) rs += w.rpart[((int64_t)rep * nrb + r) * P + j];
+        for (int r = 0; r < nrb; ++r) rs += rp[r * P + j];
         double gap = INFINITY;
         if (j > 0) gap = fmin(gap, fabs(th[j] - th[j - 1]));
         if (j + 1 < p) gap = fmin(gap, fabs(th[j] - th[j + 1]));
@@ -117,7 +118,6 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
       tsum = wave_sum(tsum);
       // residual energy floored at 1e-6 trace: below that the reference's own
       // rounding of ||E||^2 already exceeds -tol relative (exact-rank panels)
-      const double tr = w.trace[rep];
       const double vnum = fmax(fabs(tr - tsum), 1e-6 * fabs(tr));
       ok = !__any(!okall) && (bsum <= tv * vnum || !__any(!floor_ok));
     } else
@@ -132,7 +132,7 @@ DFM_DEV int check_converged(EigWork &w, double *small, int rep, int rb, int nrb,
         const int j = j0 + jj + lane / G, r = lane % G;
         double v = 0.0;
         if (j < k)
-          for (int rr = r; rr < nrb; rr += G) v += w.rpart[((int64_t)rep * nrb + rr) * P + j];
+          for (int rr = r; rr < nrb; rr += G) v += rp[rr * P + j];
         for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
         // lanes with r == 0 hold the column sums
         bool okj = true;
@@ -186,7 +186,11 @@ __global__ __launch_bounds__(256) void eig_gq_kernel(const double *__restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rep = blockIdx.y, rb = blockIdx.x, nrb = gridDim.x;
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  if (tid < 64) { const int d = check_converged<P>(w, small, rep, rb, nrb, k, p, tol, it, check_only); if (tid == 0) s_skip = d; }
+  if (tid < 64) {
+    const int d = check_converged<P>(w, small + 2 * P * P, w.rpart + (int64_t)rep * nrb * P, w.trace[rep], w.done[rep],
+                                     rep, rb, nrb, k, p, tol, it, check_only);
+    if (tid == 0) s_skip = d;
+  }
   __syncthreads();
   if (s_skip) return;
 
@@ -359,6 +363,12 @@ struct SmallLds {
   int dead[P];
 };
 
+// LDS hand-off inside the ONE wave that runs the p x p algebra (eig_small's
+// single-wave workgroups; in eig_fused the other waves wait at a barrier):
+// a wave's LDS accesses complete in issue order, so waiting for its own
+// outstanding ones (and fencing the compiler) is the whole synchronisation.
+DFM_DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compile-time constant in unrolled loops)
   const long long b = __double_as_longlong(x);
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -422,7 +432,7 @@ DFM_DEV void wave_chol_inv(double *M, double *Li, int *dead, int p) {
     const bool di = dead[i] != 0;
     if (lane < P) Li[i * S + lane] = (i < p && dl && !di) ? x[i] : 0.0;
   }
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // C = op(A) op(B) for P x P LDS matrices (TA/TB transpose flags; C distinct
@@ -448,7 +458,7 @@ DFM_DEV void wave_mm(const double *A, const double *B, double *C) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) C[(16 * rt + 4 * g + lk) * S + 16 * ct + li] = acc[g];
     }
-  __syncthreads();
+  wave_lds_sync();
 }
 
 template <int P>
@@ -458,40 +468,23 @@ DFM_DEV void wave_sym(double *M) {
     const int i = e / P, j = e % P;
     if (i < j) { const double v = 0.5 * (M[i * S + j] + M[j * S + i]); M[i * S + j] = v; M[j * S + i] = v; }
   }
-  __syncthreads();
+  wave_lds_sync();
 }
 
+// The Rayleigh-Ritz step on ONE wave (lanes = threadIdx.x 0..63): in, R1 =
+// Q'Y, R3 = Y'Y, R2 = Q'Q (entries >= p zero); out, A in R2 and Bm in R1
+// (also copied to ab[0, P^2) and ab[P^2, 2 P^2) when ab is given) and the
+// small record's tail: theta[P], then the dead flags[P].
 template <int P>
-__global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb, int jsweeps) {
+DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, double *ab, double *tail) {
   constexpr int S = P + 1;
-  __shared__ SmallLds<P> sm;
   double *const Hq = sm.R1, *const Yq = sm.R3;   // region map: SmallLds
-  const int lane = threadIdx.x, rep = blockIdx.x;
-  if (w.done[rep]) return;
-  SMALL_STAMP(0);
-  // 1. sum partials in fixed order (entries >= p are zero: Q columns >= p are zero)
-  const double *pp = w.part + (int64_t)rep * nrb * 3 * P * P;
-  constexpr int PER = 3 * P * P / 64;   // entries per lane (12 for P = 16)
-  {
-    double acc[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) acc[u] = 0.0;
-    for (int r = 0; r < nrb; ++r) {   // all PER loads of a block issue together
-      double v[PER];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) v[u] = pp[(int64_t)r * 3 * P * P + lane + 64 * u];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) acc[u] += v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = lane + 64 * u;
-      const int which = e / (P * P), a = (e / P) % P, c = e % P;
-      double *M = which == 0 ? sm.R1 : (which == 1 ? sm.R3 : sm.R2);
-      M[a * S + c] = acc[u];
-    }
-  }
-  __syncthreads();
+  // opaque lane and p: called inside eig_fused's iteration loop, whose
+  // optimiser would otherwise hoist this step's lane-derived indices out of
+  // the loop and keep them live through every other phase
+  int lane = threadIdx.x;
+  asm volatile("" : "+v"(lane));
+  asm volatile("" : "+s"(p));
   SMALL_STAMP(1);
   wave_sym<P>(Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
@@ -503,7 +496,7 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   wave_sym<P>(Hq);
   SMALL_STAMP(4);
   for (int e = lane; e < P * S; e += 64) sm.R2[e] = ((e / S) == (e % S)) ? 1.0 : 0.0;   // V
-  __syncthreads();
+  wave_lds_sync();
   double *const V = sm.R2;
   // 3. parallel cyclic Jacobi (circle-method pairs; index p is a dummy when p is odd)
   const int n = p + (p & 1), h = n / 2;
@@ -557,7 +550,7 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
       const bool any = __any(rot);
       rotated = rotated || any;
       if (!any) continue;   // wave-uniform: nothing to apply this round
-      __syncthreads();
+      wave_lds_sync();
       // H <- J' H J by 2x2 blocks; V <- V J
 #pragma unroll
       for (int u = 0; u < NHB; ++u) {
@@ -584,7 +577,7 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
         V[k * S + a] = c * va - sn * vb;
         V[k * S + b] = sn * va + c * vb;
       }
-      __syncthreads();
+      wave_lds_sync();
     }
     if (w.dbg && rep == 0 && lane == 0) w.dbg[15] = sweep + 1;
     if (!rotated) break;
@@ -600,17 +593,16 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
     }
     sm.perm[rank] = j;
   }
-  __syncthreads();
-  double *small = w.small + (int64_t)rep * small_stride<P>();
-  for (int j = lane; j < P; j += 64) small[2 * P * P + j] = j < p ? Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
-  __syncthreads();   // the Ritz values are read from R1 before W overwrites it
+  wave_lds_sync();
+  for (int j = lane; j < P; j += 64) tail[j] = j < p ? Hq[sm.perm[j] * S + sm.perm[j]] : 0.0;
+  wave_lds_sync();   // the Ritz values are read from R1 before W overwrites it
   // W = V[:, perm] (zero-padded), into R1
   double *const W = sm.R1;
   for (int e = lane; e < P * P; e += 64) {
     const int i = e / P, c = e % P;
     W[i * S + c] = (i < p && c < p) ? V[i * S + sm.perm[c]] : 0.0;
   }
-  __syncthreads();
+  wave_lds_sync();
   SMALL_STAMP(6);
   // 5. A = L^-T Vs = Li' W ;  Z'Z = A' (Y'Y) A ;  L2 = chol ;  Bm = A L2^-T
   double *const A = sm.R2;
@@ -623,13 +615,49 @@ __global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb
   SMALL_STAMP(8);
   SMALL_STAMP(9);
   wave_mm<P, false, true>(A, sm.R4, sm.R1);   // Bm = A Li'
-  for (int e = lane; e < P * P; e += 64) {
-    const int a = e / P, c = e % P;
-    small[e] = (a < p && c < p) ? A[a * S + c] : 0.0;
-    small[P * P + e] = (a < p && c < p) ? sm.R1[a * S + c] : 0.0;
-  }
-  for (int j = lane; j < P; j += 64) small[2 * P * P + P + j] = (j < p && sm.dead[j]) ? 1.0 : 0.0;
+  if (ab)
+    for (int e = lane; e < P * P; e += 64) {
+      const int a = e / P, c = e % P;
+      ab[e] = (a < p && c < p) ? A[a * S + c] : 0.0;
+      ab[P * P + e] = (a < p && c < p) ? sm.R1[a * S + c] : 0.0;
+    }
+  for (int j = lane; j < P; j += 64) tail[P + j] = (j < p && sm.dead[j]) ? 1.0 : 0.0;
+  wave_lds_sync();
   SMALL_STAMP(10);
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void eig_small_kernel(EigWork w, int p, int nrb, int jsweeps) {
+  constexpr int S = P + 1;
+  __shared__ SmallLds<P> sm;
+  const int lane = threadIdx.x, rep = blockIdx.x;
+  if (w.done[rep]) return;
+  SMALL_STAMP(0);
+  // 1. sum partials in fixed order (entries >= p are zero: Q columns >= p are zero)
+  const double *pp = w.part + (int64_t)rep * nrb * 3 * P * P;
+  constexpr int PER = 3 * P * P / 64;   // entries per lane (12 for P = 16)
+  {
+    double acc[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc[u] = 0.0;
+    for (int r = 0; r < nrb; ++r) {   // all PER loads of a block issue together
+      double v[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) v[u] = pp[(int64_t)r * 3 * P * P + lane + 64 * u];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) acc[u] += v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = lane + 64 * u;
+      const int which = e / (P * P), a = (e / P) % P, c = e % P;
+      double *M = which == 0 ? sm.R1 : (which == 1 ? sm.R3 : sm.R2);
+      M[a * S + c] = acc[u];
+    }
+  }
+  wave_lds_sync();
+  double *small = w.small + (int64_t)rep * small_stride<P>();
+  small_rr<P>(sm, w, rep, p, jsweeps, small, small + 2 * P * P);
 }
 
 // ---------------------------------------------------------------- apply
@@ -691,9 +719,10 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
 
 // ---------------------------------------------------------------- final
 // lam: nb x k, Uk: nb x m x k (row-major), status: nb (0 ok, 1 not converged)
+// Ur: the replicate's Ritz vectors (m x P), theta its Ritz values; 256 threads.
 template <int P>
-__global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
-                                                        double *__restrict__ Uk, int *__restrict__ status) {
+DFM_DEV void eig_final_body(const double *Ur, const double *theta, int done, int rep, int m, int k,
+                            double *__restrict__ lam, double *__restrict__ Uk, int *__restrict__ status) {
   // one pass over U: each thread keeps the running max |U[r][j]| (first row
   // on ties) of its rows for every column j, then a shuffle reduction per
   // wave and a fixed-order combine of the four waves (smaller row index wins
@@ -701,9 +730,7 @@ __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k,
   __shared__ double sv[P][4];
   __shared__ int si[P][4];
   __shared__ double ssign[P];
-  const int tid = threadIdx.x, rep = blockIdx.x, wv = tid >> 6;
-  const double *Ur = w.U + (int64_t)rep * m * P;
-  const double *theta = w.small + (int64_t)rep * small_stride<P>() + 2 * P * P;
+  const int tid = threadIdx.x, wv = tid >> 6;
   double best[P];
   int bi[P];
 #pragma unroll
@@ -746,11 +773,19 @@ __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k,
   if (tid < k) ssign[tid] = Ur[(int64_t)si[tid][0] * P + tid] < 0.0 ? -1.0 : 1.0;
   __syncthreads();
   if (tid < k) lam[(int64_t)rep * k + tid] = theta[tid];
-  if (tid == 0) status[rep] = w.done[rep] ? 0 : 1;
+  if (tid == 0) status[rep] = done ? 0 : 1;
   for (int64_t e = tid; e < (int64_t)m * k; e += 256) {
     const int r = (int)(e / k), j = (int)(e % k);
     Uk[(int64_t)rep * m * k + e] = ssign[j] * Ur[(int64_t)r * P + j];
   }
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
+                                                        double *__restrict__ Uk, int *__restrict__ status) {
+  const int rep = blockIdx.x;
+  eig_final_body<P>(w.U + (int64_t)rep * m * P, w.small + (int64_t)rep * small_stride<P>() + 2 * P * P, w.done[rep],
+                    rep, m, k, lam, Uk, status);
 }
 
 // ------------------------------------------------------------- host driver
@@ -838,6 +873,335 @@ static int64_t count_rep_iters(const int *active_dev, int last, int shift, int n
 constexpr int kChebDMax = 8, kChebDirectStrict = 4;
 static void shifted_cheb(int d, double *a);
 
+// ---------------------------------------------------------------- fused
+// The whole direct solve of ONE replicate in ONE workgroup (4 waves), P = 16
+// and m <= 16 NGW: the basis Q and the product Y stay in LDS for the whole
+// solve (2 x m x 16 doubles: 37 KB at m = 130, three workgroups per CU), G
+// streams from L2 / MALL once per product.  Each iteration runs the same
+// algebra as the kernel sequence gq -> small -> apply -> cheb:
+//   check    wave 0: iteration it-1's residuals (check_converged), retire / count
+//   Y = G Q  v_mfma_f64_4x4x4_4b; 4-row groups dealt round-robin to the waves
+//   Q'Y, Y'Y, Q'Q   waves 0..2, one product each over all m rows
+//   small_rr wave 0 (the other waves wait at the barrier)
+//   apply    U = Q A -> global (eig_final reads it), residual sums, V0 = Q Bm
+//            and the filter's first Horner term S = (a_d/b) Y Bm + a_{d-1} V0
+//   cheb     dg - 1 times S <- G S / b + a_i V0; S_0 (into Q) is the next basis
+// The multi-kernel path's launch chain, its host polls and its per-row-block
+// partial records are gone: a replicate leaves the loop the moment it
+// converges, the others keep iterating.  Sums run in a fixed order.
+struct ChebCo { double c2[kChebDMax + 1], c4[kChebDMax + 1]; };
+
+// LDS image of an m x 16 block, row r, column c: the 4-column block is
+// XOR-swizzled by (r >> 1) & 3, so the MFMA operand reads (rows 4 (lane >> 4)
+// + ((lane >> 2) & 3), columns 4 fb + (lane & 3)) hit 8 distinct 8-bank
+// groups per half-wave.
+// x, opaque to the optimiser: lane-derived offsets recomputed per phase
+// instead of hoisted out of the iteration loop (every phase's hoisted
+// offsets live at once otherwise — hundreds of VGPRs, spilled)
+DFM_DEV int fz_opaque(int x) { asm volatile("" : "+v"(x)); return x; }
+
+DFM_DEV int fz_ix(int r, int c) { return (r << 4) | ((((c >> 2) ^ ((r >> 1) & 3)) << 2) | (c & 3)); }
+
+// Transpose-reduce of the four v_mfma_f64_4x4x4_4b blocks of accumulators
+// a[fb] (column block fb): the lane gets the 4 x 16 result's element
+// (row lane >> 4, column lane & 15).
+DFM_DEV double mm4_fold(const double (&a)[4], int lane) {
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1;
+  const double k01 = (b1 ? a[1] : a[0]) + __shfl_xor(b1 ? a[0] : a[1], 4);
+  const double k23 = (b1 ? a[3] : a[2]) + __shfl_xor(b1 ? a[2] : a[3], 4);
+  return (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+}
+
+// acc[q] = rows of 4-row group g = wave + 4 q of G S (G: m x m in global, S:
+// the LDS image, rows m..mpad-1 zero).  Lane: row 4 g + (lane & 3), k index
+// k0 + 4 (lane >> 4) + ((lane >> 2) & 3) — a G row's 16 k values per chunk are
+// one 128-byte line.  G comes from L2 / MALL (a batch's Grams outgrow the
+// L2): a register ring holds FZ_DEPTH chunks in flight, the loads of chunk
+// c + FZ_DEPTH - 1 issue before chunk c's MFMAs.
+constexpr int FZ_DEPTH = 3;
+template <int NGW>
+DFM_DEV void fz_gemm(const double *__restrict__ Gr, int64_t ldg, int m, int ng, const double *S, int wave, int lane,
+                     double (&acc)[NGW][4]) {
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int ld = (int)ldg;   // m <= 256: element offsets fit 32 bits (SGPR base + VGPR offset loads)
+  const int nch = (m + 15) >> 4;
+#pragma unroll
+  for (int q = 0; q < NGW; ++q)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[q][b] = 0.0;
+  unsigned off[NGW];   // the lane's G row offset + k of chunk 0
+#pragma unroll
+  for (int q = 0; q < NGW; ++q) off[q] = (unsigned)((4 * (wave + 4 * q) + fi) * ld + fkc);
+  double ring[FZ_DEPTH][NGW];
+  auto load = [&](int c, double (&dst)[NGW]) {
+    const int kg = 16 * c + fkc;
+#pragma unroll
+    for (int q = 0; q < NGW; ++q) {
+      const int g = wave + 4 * q, row = 4 * g + fi;
+      dst[q] = (g < ng && row < m && kg < m) ? Gr[off[q] + 16 * c] : 0.0;
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < FZ_DEPTH - 1; ++s) load(s, ring[s]);
+#pragma unroll 1
+  for (int c0 = 0; c0 < nch; c0 += FZ_DEPTH) {
+#pragma unroll
+    for (int s = 0; s < FZ_DEPTH; ++s) {
+      const int c = c0 + s;
+      load(c + FZ_DEPTH - 1, ring[(s + FZ_DEPTH - 1) % FZ_DEPTH]);
+      if (c < nch) {   // wave-uniform
+        double bf[4];
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) bf[fb] = S[fz_ix(16 * c + fkc, 4 * fb + fi)];
+#pragma unroll
+        for (int q = 0; q < NGW; ++q) {
+          if (wave + 4 * q >= ng) continue;   // wave-uniform
+#pragma unroll
+          for (int fb = 0; fb < 4; ++fb) acc[q][fb] = mfma4(ring[s][q], bf[fb], acc[q][fb]);
+        }
+      }
+    }
+  }
+}
+
+template <int NGW>
+__global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
+    const double *__restrict__ G, int64_t ldg, int64_t strideG, EigWork w, int m, int k, int p, double tol,
+    int maxit, const double *__restrict__ warm, int kw, uint64_t seed, int warm_strict, int jsweeps, ChebCo cc,
+    double *__restrict__ lam, double *__restrict__ Uk, int *__restrict__ status, long long *__restrict__ prof) {
+  constexpr int P = 16, S = P + 1;
+  __shared__ SmallLds<P> sm;
+  __shared__ double s_tail[4 * P];   // the small record's tail: theta[P], dead[P], residual history 2 x P
+  __shared__ double s_rw[4][P];      // per-wave residual sums of one apply
+  __shared__ double s_res[P];        // their fixed-order total (check_converged's one "row block")
+  __shared__ int s_done;
+  __shared__ double s_ca[2][kChebDMax + 1];   // filter coefficients, degree 2 | 4 (indexed at run time: LDS, not the kernarg struct)
+  extern __shared__ double s_dyn[];  // Q | Y, mpad x 16 each (fz_ix images)
+  const int rep = blockIdx.x;
+  const int mpad = (m + 15) & ~15, ng = (m + 3) >> 2;
+  double *const sQ = s_dyn, *const sY = s_dyn + mpad * P;
+  const double *Gr = G + (int64_t)rep * strideG;
+  double *Ur = w.U + (int64_t)rep * m * P;
+  // Every phase derives its thread coordinates from an opaque copy of
+  // threadIdx.x: the lane's MFMA operand coordinates (fi, fkc), its element of
+  // a folded 4 x 16 group result (orow, oc).  Coordinates derived once would
+  // be hoisted out of the iteration loop with everything computed from them,
+  // and all phases' offsets would stay live at once (hundreds of VGPRs).
+#define FZ_THREAD                                                    \
+  const int tid = fz_opaque(threadIdx.x), lane = tid & 63;          \
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);         \
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3); \
+  const int orow = lane >> 4, oc = lane & 15;                        \
+  (void)wave; (void)fi; (void)fkc; (void)orow; (void)oc
+
+  double tr = 0.0;   // trace (eig_trace_kernel's order); wave 0 keeps it for the checks
+  {
+    FZ_THREAD;
+    // start basis (eig_init_kernel's)
+    for (int e = tid; e < mpad * P; e += 256) {
+      const int row = e >> 4, c = e & 15;
+      double v = 0.0;
+      if (row < m) {
+        if (c < kw) v = warm[(int64_t)row * kw + c];
+        else if (c < p) v = hash_unit(seed, row, c);
+      }
+      sQ[fz_ix(row, c)] = v;
+      sY[fz_ix(row, c)] = 0.0;
+    }
+    if (tid < 4 * P) s_tail[tid] = 0.0;
+    if (tid < P) s_res[tid] = 0.0;
+    if (tid <= kChebDMax) { s_ca[0][tid] = cc.c2[tid]; s_ca[1][tid] = cc.c4[tid]; }
+    if (wave == 0) {
+      for (int i = lane; i < m; i += 64) tr += Gr[(int64_t)i * ldg + i];
+      tr = wave_sum(tr);
+      if (lane == 0) { w.trace[rep] = tr; w.done[rep] = 0; }
+    }
+  }
+  __syncthreads();
+  // phase profile of replicate 0 (DFM_EIG_PROF): thread 0's wall clock at the
+  // phase-ending barriers, summed per phase over the iterations
+  const bool pf = prof && rep == 0;   // workgroup-uniform: the sums stay in SGPRs
+  long long pt = pf ? wall_clock64() : 0, pacc[6] = {0, 0, 0, 0, 0, 0};
+#define FZ_MARK(i)                                           \
+  do {                                                       \
+    if (pf) { const long long t_ = wall_clock64(); pacc[i] += t_ - pt; pt = t_; } \
+  } while (0)
+
+  int it = 0;
+  for (;; ++it) {
+    {
+      FZ_THREAD;
+      if (wave == 0) {
+        const int d = check_converged<P>(w, s_tail, s_res, tr, 0, rep, 0, 1, k, p, tol, it, 0);
+        if (lane == 0) s_done = d;
+      }
+    }
+    __syncthreads();
+    FZ_MARK(0);
+    if (s_done || it == maxit) break;   // converged, or the check-only pass after maxit steps
+
+    {   // Y = G Q
+      FZ_THREAD;
+      double acc[NGW][4];
+      fz_gemm<NGW>(Gr, ldg, m, ng, sQ, wave, lane, acc);
+#pragma unroll
+      for (int q = 0; q < NGW; ++q) {
+        const int g = wave + 4 * q;
+        if (g >= ng) continue;
+        const double v = mm4_fold(acc[q], lane);
+        const int row = 4 * g + orow;
+        if (row < m) sY[fz_ix(row, oc)] = v;
+      }
+    }
+    __syncthreads();
+    FZ_MARK(1);
+
+    {   // Q'Y -> R1, Y'Y -> R3, Q'Q -> R2 (stride P + 1), over all mpad rows
+      FZ_THREAD;
+      if (wave < 3) {
+        const double *X1 = wave == 1 ? sY : sQ, *X2 = wave == 2 ? sQ : sY;
+        double *Out = wave == 0 ? sm.R1 : (wave == 1 ? sm.R3 : sm.R2);
+        double a4[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) a4[g][b] = 0.0;
+#pragma unroll 1
+        for (int k0 = 0; k0 < mpad; k0 += 16) {
+          const int kr = k0 + fkc;
+          double af[4], bf[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) af[g] = X1[fz_ix(kr, 4 * g + fi)];
+#pragma unroll
+          for (int fb = 0; fb < 4; ++fb) bf[fb] = X2[fz_ix(kr, 4 * fb + fi)];
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int fb = 0; fb < 4; ++fb) a4[g][fb] = mfma4(af[g], bf[fb], a4[g][fb]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const double v = mm4_fold(a4[g], lane);
+          Out[(4 * g + orow) * S + oc] = v;
+        }
+      }
+    }
+    __syncthreads();
+    FZ_MARK(2);
+
+    {
+      FZ_THREAD;
+      if (wave == 0) {
+        if (pf) {   // stamps of the Rayleigh-Ritz stages (the last step's) after the phase sums
+          EigWork wd = w;
+          wd.dbg = prof + 8;
+          small_rr<P>(sm, wd, rep, p, jsweeps, nullptr, s_tail);
+        } else {
+          small_rr<P>(sm, w, rep, p, jsweeps, nullptr, s_tail);
+        }
+      }
+    }
+    __syncthreads();
+    FZ_MARK(3);
+
+    // apply: A = R2, Bm = R1
+    const int dg = (warm_strict && it < 4) ? kChebDirectStrict : 2;
+    const double *ca = s_ca[dg == 2 ? 0 : 1];
+    const double bch = s_tail[p - 1];
+    {
+      FZ_THREAD;
+      const bool dead_c = oc < p && s_tail[P + oc] != 0.0;
+      double bA[4], bB[4];
+#pragma unroll
+      for (int fb = 0; fb < 4; ++fb) {
+        bA[fb] = sm.R2[fkc * S + 4 * fb + fi];
+        bB[fb] = sm.R1[fkc * S + 4 * fb + fi];
+      }
+      const double th_c = s_tail[oc], fa1 = ca[dg], fa0 = ca[dg - 1];
+      double rs = 0.0;
+#pragma unroll 1   // one group's 16 accumulators live at a time
+      for (int g = wave; g < ng; g += 4) {
+        const int ra = 4 * g + fi;
+        const double aq = sQ[fz_ix(ra, fkc)], ay = sY[fz_ix(ra, fkc)];
+        double u4[4], ya4[4], qn4[4], qb4[4];
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) {
+          u4[fb] = mfma4(aq, bA[fb], 0.0);
+          ya4[fb] = mfma4(ay, bA[fb], 0.0);
+          qn4[fb] = mfma4(ay, bB[fb], 0.0);
+          qb4[fb] = mfma4(aq, bB[fb], 0.0);
+        }
+        const double u = mm4_fold(u4, lane), ya = mm4_fold(ya4, lane);
+        double qn = mm4_fold(qn4, lane), qb = mm4_fold(qb4, lane);
+        const int row = 4 * g + orow;
+        if (dead_c) qn = hash_unit(seed, row, 1000003ull * (it + 1) + oc);
+        if (oc >= p) { qn = 0.0; qb = 0.0; }
+        if (row < m) {
+          if (oc < k) { const double wv = ya - th_c * u; rs += wv * wv; }
+          Ur[(int64_t)row * P + oc] = u;
+          const double sv = dead_c ? qn : (bch > 0.0 ? fma(fa1 / bch, qn, fa0 * qb) : qn);
+          sY[fz_ix(row, oc)] = oc >= p ? 0.0 : sv;
+          sQ[fz_ix(row, oc)] = oc >= p ? 0.0 : (dead_c ? qn : qb);
+        }
+      }
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      if (lane < P) s_rw[wave][lane] = rs;
+    }
+    __syncthreads();
+    {
+      FZ_THREAD;
+      if (tid < P) s_res[tid] = ((s_rw[0][tid] + s_rw[1][tid]) + s_rw[2][tid]) + s_rw[3][tid];
+    }
+    FZ_MARK(4);
+
+    // Chebyshev filter: S_{dg-1} in Y; S_i = G S_{i+1} / b + a_i V0; S_0 into Q
+    const double cb = bch > 0.0 ? 1.0 / bch : 1.0;
+    for (int j = 1; j < dg; ++j) {
+      const double cv0 = bch > 0.0 ? ca[dg - 1 - j] : 0.0;
+      const bool last = j == dg - 1;
+      double *So = last ? sQ : sY;
+      FZ_THREAD;
+      double acc[NGW][4];
+      fz_gemm<NGW>(Gr, ldg, m, ng, sY, wave, lane, acc);
+      if (!last) __syncthreads();   // every wave has read S_{i+1} before S_i overwrites it
+      const bool dead_c = oc < p && s_tail[P + oc] != 0.0;
+#pragma unroll
+      for (int q = 0; q < NGW; ++q) {
+        const int g = wave + 4 * q;
+        if (g >= ng) continue;
+        const double gv = mm4_fold(acc[q], lane);
+        const int row = 4 * g + orow;
+        if (row < m) {
+          const int ix = fz_ix(row, oc);
+          const double v0 = sQ[ix];
+          double sn = dead_c ? v0 : fma(cb, gv, cv0 * v0);
+          if (oc >= p) sn = 0.0;
+          So[ix] = sn;
+        }
+      }
+      __syncthreads();
+    }
+    FZ_MARK(5);
+  }
+  // the last apply's Ritz vectors (this workgroup's own global writes: the
+  // barrier that ended the iteration makes them visible) -> signs, outputs
+  eig_final_body<P>(Ur, s_tail, s_done, rep, m, k, lam, Uk, status);
+  if (pf && threadIdx.x == 0) {
+    for (int i = 0; i < 6; ++i) prof[i] = pacc[i];
+    prof[6] = it;
+    prof[7] = wall_clock64() - pt;   // the final step
+  }
+#undef FZ_MARK
+#undef FZ_THREAD
+}
+
+static int fused_ngw(int m) { return m <= 64 ? 4 : (m <= 144 ? 9 : (m <= 256 ? 16 : 0)); }
+static bool fused_enabled() {
+  static const bool on = [] { const char *e = getenv("DFM_EIG_FUSED"); return !(e && atoi(e) == 0); }();
+  return on;
+}
+
 // Solve nb problems.  Returns 0 ok, 1 not converged (status per replicate),
 // negative on bad args, or a hipError_t (>1000).
 template <int P>
@@ -851,6 +1215,68 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
   hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
+  // degree: 4 for the first four filters of a warm-started batch or a single
+  // fit under the strict eigenvector rule (C2's Chow statistics: 8-9
+  // Rayleigh-Ritz steps with degree 2, 5 with degree 4 in tools/eig_proto.py),
+  // 2 for the polishing steps after them and for eigenvalue-only solves
+  // (single fits, nb = 1, too: cold-started, polished to 1e-14 by run_eig)
+  const bool warm_strict = tol >= 0.0 && ((warm && kw >= k) || nb == 1);
+  if constexpr (P == 16) {
+    const int ngw = fused_enabled() ? fused_ngw(m) : 0;
+    if (ngw) {
+      ChebCo cc;
+      shifted_cheb(kChebDirectStrict, cc.c4);
+      shifted_cheb(2, cc.c2);
+      const size_t lds = (size_t)2 * ((m + 15) & ~15) * P * sizeof(double);
+      // DFM_EIG_PROF=1: phase profile of replicate 0 of every fused solve -> stderr
+      static const bool want_prof = [] { const char *e = getenv("DFM_EIG_PROF"); return e && atoi(e) != 0; }();
+      long long *prof = nullptr;
+      if (want_prof) {
+        static thread_local long long *buf = nullptr;
+        if (!buf && hipMalloc((void **)&buf, 24 * sizeof(long long)) != hipSuccess) buf = nullptr;
+        prof = buf;
+      }
+      if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
+#define DFM_FUSED(NG)                                                                                           \
+  hipFuncSetAttribute((const void *)eig_fused_kernel<NG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+  hipLaunchKernelGGL(eig_fused_kernel<NG>, dim3(nb), dim3(256), lds, st, G, ldg, strideG, w, m, k, p, tol, maxit,  \
+                     warm, kw, seed, (int)warm_strict, kJacobiSweeps, cc, lam, Uk, status, prof)
+      if (ngw == 4) { DFM_FUSED(4); }
+      else if (ngw == 9) { DFM_FUSED(9); }
+      else { DFM_FUSED(16); }
+#undef DFM_FUSED
+      if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
+      // iteration statistics from the per-iteration unconverged counts
+      std::vector<int> a((size_t)maxit + 2, 0);
+      hipMemcpyAsync(a.data(), w.active, a.size() * 4, hipMemcpyDeviceToHost, st);
+      hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return 1000 + (int)e;
+      int last = maxit;
+      for (int i = 0; i <= maxit; ++i)
+        if (a[i] == 0) { last = i; break; }
+      g_last_iters = last;
+      int64_t s = 0;
+      for (int i = 0; i <= std::min(last, maxit - 1); ++i) s += a[i];
+      g_last_rep_iters = s;
+      g_last_gemm_products = s;
+      if (prof) {
+        long long h[24];
+        hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost);
+        const long long *d = h + 8;   // small_rr stamps 1..10, sweeps at 15
+        fprintf(stderr, "eig_fused small stages us: chol1=%.2f mm=%.2f jacobi(%lld sweeps)=%.2f sort=%.2f mm3=%.2f "
+                "chol2=%.2f mm=%.2f\n", (d[2] - d[1]) / 100.0, (d[4] - d[3]) / 100.0, d[15], (d[5] - d[4]) / 100.0,
+                (d[6] - d[5]) / 100.0, (d[7] - d[6]) / 100.0, (d[8] - d[7]) / 100.0, (d[10] - d[9]) / 100.0);
+        fprintf(stderr, "eig_fused m=%d nb=%d rep0: iters=%lld us check=%.1f gq=%.1f part=%.1f small=%.1f apply=%.1f "
+                "cheb=%.1f final=%.1f\n", m, nb, h[6], h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0,
+                h[4] / 100.0, h[5] / 100.0, h[7] / 100.0);
+      }
+      if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
+      if (iters_host) hipMemcpyAsync(iters_host, w.iters, (size_t)nb * 4, hipMemcpyDeviceToHost, st);
+      e = hipGetLastError();
+      if (e != hipSuccess) return 1000 + (int)e;
+      return 0;
+    }
+  }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
   {
     const int64_t n = (int64_t)m * P;
@@ -863,12 +1289,6 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   bool finished = false;
   std::vector<int> act;
   const int cheb = 1;   // Chebyshev filter between Rayleigh-Ritz steps
-  // degree: 4 for the first four filters of a warm-started batch or a single
-  // fit under the strict eigenvector rule (C2's Chow statistics: 8-9
-  // Rayleigh-Ritz steps with degree 2, 5 with degree 4 in tools/eig_proto.py),
-  // 2 for the polishing steps after them and for eigenvalue-only solves
-  // (single fits, nb = 1, too: cold-started, polished to 1e-14 by run_eig)
-  const bool warm_strict = tol >= 0.0 && ((warm && kw >= k) || nb == 1);
   double ca4[kChebDMax + 1], ca2[kChebDMax + 1];
   shifted_cheb(kChebDirectStrict, ca4);
   shifted_cheb(2, ca2);

@@ -392,19 +392,21 @@ __global__ void gram_wk_a0_kernel(const double *__restrict__ F, const double *__
   }
 }
 
-// Per replicate: w (row rep of W, zero-padded to Tp) and B = F' D P E (r x N).
+// Per replicate: w (row rep of W, zero-padded to Tp) and the bucket sums
+// Ft[s][j] = sum_{t : idx_t = s} eta_t F[t][j] (At: rows rep*r + j, Tp
+// columns, zero-padded), so that B = F' D P E = Ft' E for the whole batch is
+// ONE MFMA GEMM At (nb r x T) . E (T x N) — the per-replicate gather of T
+// rows of E (a serial 600-step chain per column) is gone.
 // idx / eta of the replicate staged in LDS.  w_s = sum of eta_t^2 over the
 // t with idx_t = s, ascending t: a counting sort of t by idx_t (bucket
 // counts, a block scan, slots handed out by LDS atomics in any order, each
 // bucket then insertion-sorted by t), O(T) per replicate — the same sums in
 // the same order as a scan over every t (round 3's O(T^2) form, which added
 // +0 for the t outside the bucket), so bit-identical to it.
-template <int RM>
-__global__ __launch_bounds__(256) void gram_wk_prep_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N,
-                                                           int r, const double *__restrict__ F,
+__global__ __launch_bounds__(256) void gram_wk_prep_kernel(int T, int r, const double *__restrict__ F,
                                                            const int32_t *__restrict__ idx,
                                                            const double *__restrict__ eta, int64_t rs, int Tp,
-                                                           double *__restrict__ W, double *__restrict__ Bo) {
+                                                           double *__restrict__ W, double *__restrict__ At) {
   extern __shared__ double pdyn[];
   __shared__ int scan[256];
   double *se = pdyn;                 // eta_t
@@ -454,32 +456,16 @@ __global__ __launch_bounds__(256) void gram_wk_prep_kernel(const double *__restr
     }
     Wr[s] = acc;
   }
-  double *Br = Bo + (int64_t)rep * r * N;
-  constexpr int TU = 16;   // rows gathered per round: TU loads in flight per thread
-  for (int n = tid; n < N; n += 256) {
-    double acc[RM];
-#pragma unroll
-    for (int j = 0; j < RM; ++j) acc[j] = 0.0;
-    for (int t0 = 0; t0 < T; t0 += TU) {
-      double xv[TU];
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        const int t = min(t0 + u, T - 1);
-        xv[u] = Ep[(int64_t)sx[t] * ld + n];
-      }
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        const int t = t0 + u;
-        if (t >= T) break;
-        const double x = se[t] * xv[u];
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-          if (j < r) acc[j] = fma(sF[t * r + j], x, acc[j]);
-      }
+  __syncthreads();   // every bucket sorted by t
+  double *Ar = At + (int64_t)rep * r * Tp;
+  for (int e = tid; e < r * Tp; e += 256) {
+    const int j = e / Tp, s = e - j * Tp;
+    double acc = 0.0;
+    if (s < T) {
+      const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
+      for (int i = b0; i < b1; ++i) { const int t = lst[i]; acc = fma(se[t], sF[t * r + j], acc); }
     }
-#pragma unroll
-    for (int j = 0; j < RM; ++j)
-      if (j < r) Br[(int64_t)j * N + n] = acc[j];
+    Ar[e] = acc;
   }
 }
 
@@ -547,9 +533,9 @@ hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r,
   hipLaunchKernelGGL(gram_wk_a0_kernel, dim3(N), dim3(256), 0, st, F, L, T, N, r, A0);
   return hipGetLastError();
 }
-// workspace doubles for nb replicates: W (nb x Tp), B (nb x r x N), Q (nb x ldk)
+// workspace doubles for nb replicates: W (nb x Tp), B (nb x r x N), Q (nb x ldk), At (nb x r x Tp)
 size_t gram_wk_work(int T, int N, int r, int nb) {
-  return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N));
+  return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N) + (size_t)r * gram_wk_tp(T));
 }
 // nb replicate Grams X*'X* (N x N each, stride N*N) of src (C + diag(eta) E[idx]).
 hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
@@ -557,15 +543,13 @@ hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, con
                           int nb, double *work, double *G, hipStream_t st) {
   const int Tp = gram_wk_tp(T);
   const int64_t ldk = gram_wk_ldk(N);
-  double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)nb * r * N;
-  const size_t lds = gram_wk_prep_lds(T, r);
-  if (r <= 8)
-    hipLaunchKernelGGL(gram_wk_prep_kernel<8>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, r, F, idx, eta, rs, Tp, W,
-                       Bo);
-  else
-    hipLaunchKernelGGL(gram_wk_prep_kernel<16>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, r, F, idx, eta, rs, Tp,
-                       W, Bo);
-  hipError_t e = launch_gemm(false, W, Tp, K, ldk, Q, ldk, nb, (int)ldk, T, st, nullptr, 1, true, nullptr, nullptr);
+  double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)nb * r * N, *At = Q + (size_t)nb * ldk;
+  hipLaunchKernelGGL(gram_wk_prep_kernel, dim3(nb), dim3(256), gram_wk_prep_lds(T, r), st, T, r, F, idx, eta, rs, Tp,
+                     W, At);
+  // B (nb r x N) = At . E, then Q (nb x ldk) = W K
+  hipError_t e = launch_gemm(false, At, Tp, Ep, ld, Bo, N, nb * r, N, T, st, nullptr, 1, false, nullptr, nullptr);
+  if (e != hipSuccess) return e;
+  e = launch_gemm(false, W, Tp, K, ldk, Q, ldk, nb, (int)ldk, T, st, nullptr, 1, true, nullptr, nullptr);
   if (e != hipSuccess) return e;
   const int nt = (N + WK_TILE - 1) / WK_TILE;
   hipLaunchKernelGGL(gram_wk_combine_kernel, dim3(nt * (nt + 1) / 2, nb), dim3(256), 0, st, A0, L, Bo, Q, ldk, N, r,
