@@ -43,6 +43,7 @@ struct EigWork {
 };
 #define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)wall_clock64(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
+constexpr int SMALL_CHOL1_DONE = 0x100;   // small_rr: R4 already holds chol(Q'Q)^-1 (eig_fused forms it during Y = G Q)
 
 // ----------------------------------------------------------------- init
 template <int P>
@@ -388,7 +389,7 @@ DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compil
 template <int P>
 DFM_DEV void wave_chol_inv(double *M, double *Li, int *dead, int p) {
   constexpr int S = P + 1;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   double mx = 0.0;
   for (int j = lane; j < p; j += 64) mx = fmax(mx, fabs(M[j * S + j]));
 #pragma unroll
@@ -464,15 +465,16 @@ DFM_DEV void wave_mm(const double *A, const double *B, double *C) {
 template <int P>
 DFM_DEV void wave_sym(double *M) {
   constexpr int S = P + 1;
-  for (int e = threadIdx.x; e < P * P; e += 64) {
+  for (int e = threadIdx.x & 63; e < P * P; e += 64) {
     const int i = e / P, j = e % P;
     if (i < j) { const double v = 0.5 * (M[i * S + j] + M[j * S + i]); M[i * S + j] = v; M[j * S + i] = v; }
   }
   wave_lds_sync();
 }
 
-// The Rayleigh-Ritz step on ONE wave (lanes = threadIdx.x 0..63): in, R1 =
-// Q'Y, R3 = Y'Y, R2 = Q'Q (entries >= p zero); out, A in R2 and Bm in R1
+// The Rayleigh-Ritz step on ONE wave (any wave of the workgroup): in, R1 =
+// Q'Y, R3 = Y'Y, R2 = Q'Q (entries >= p zero; with SMALL_CHOL1_DONE in
+// jsweeps, R4 = chol(Q'Q)^-1 and sm.dead already formed instead); out, A in R2 and Bm in R1
 // (also copied to ab[0, P^2) and ab[P^2, 2 P^2) when ab is given) and the
 // small record's tail: theta[P], then the dead flags[P].
 template <int P>
@@ -482,13 +484,13 @@ DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, 
   // opaque lane and p: called inside eig_fused's iteration loop, whose
   // optimiser would otherwise hoist this step's lane-derived indices out of
   // the loop and keep them live through every other phase
-  int lane = threadIdx.x;
+  int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(p));
   SMALL_STAMP(1);
   wave_sym<P>(Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
-  wave_chol_inv<P>(sm.R2, sm.R4, sm.dead, p);
+  if (!(jsweeps & SMALL_CHOL1_DONE)) wave_chol_inv<P>(sm.R2, sm.R4, sm.dead, p);
   SMALL_STAMP(2);
   SMALL_STAMP(3);
   wave_mm<P, false, false>(sm.R4, Hq, sm.R2);   // Q'Q is dead once Li is formed
@@ -523,7 +525,7 @@ DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, 
     vs[u] = (h > 0 && e < p * h) ? e % h : 0;
   }
   const int n1 = n - 1, pa = lane, pb = n - 1 - lane;
-  for (int sweep = 0; sweep < jsweeps; ++sweep) {
+  for (int sweep = 0; sweep < (jsweeps & 0xff); ++sweep) {
     bool rotated = false;
     int xa = pa - 1, xb = pb - 1;   // position - 1 + r, wrapped into [0, n - 1)
     for (int r = 0; r < n1; ++r, ++xa, ++xb) {
@@ -835,6 +837,16 @@ typedef void (*timer_fn)(void *ctx, int cls, int begin);
 // iterations, and the residual test of check_converged includes any leftover
 // off-diagonal coupling.
 constexpr int kJacobiSweeps = 2;
+// Jacobi sweeps per Rayleigh-Ritz step of the fused solver: ONE (C2: the
+// same 4.99 steps per replicate as two sweeps, 458k vs 423k rep/s — the
+// inner sweeps accumulate across outer steps).  DFM_EIG_JSWEEPS overrides.
+static int fused_sweeps() {
+  static const int v = [] {
+    const char *a = getenv("DFM_EIG_JSWEEPS");
+    return a ? std::max(1, std::min(8, atoi(a))) : 1;
+  }();
+  return v;
+}
 thread_local int g_last_iters = 0;   // iterations run by the last eig_run / eig_run_factored (host stat)
 // replicate-iterations of the last run's dominant product (G.Q in eig_gq, or
 // the H.Z GEMM in the factored solver) that still had an unconverged
@@ -912,14 +924,14 @@ DFM_DEV double mm4_fold(const double (&a)[4], int lane) {
   return (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
 }
 
-// acc[q] = rows of 4-row group g = wave + 4 q of G S (G: m x m in global, S:
+// acc[q] = rows of 4-row group g = wave + NW q (NW waves share the rows) of G S (G: m x m in global, S:
 // the LDS image, rows m..mpad-1 zero).  Lane: row 4 g + (lane & 3), k index
 // k0 + 4 (lane >> 4) + ((lane >> 2) & 3) — a G row's 16 k values per chunk are
 // one 128-byte line.  G comes from L2 / MALL (a batch's Grams outgrow the
-// L2): a register ring holds FZ_DEPTH chunks in flight, the loads of chunk
-// c + FZ_DEPTH - 1 issue before chunk c's MFMAs.
-constexpr int FZ_DEPTH = 3;
-template <int NGW>
+// L2): a register ring holds FZ_DEPTH chunks in flight (3; 2 when a wave
+// owns more than 9 groups — registers), the loads of chunk c + FZ_DEPTH - 1
+// issue before chunk c's MFMAs.
+template <int NGW, int NW, int FZ_DEPTH = (NGW > 9 ? 2 : 3)>
 DFM_DEV void fz_gemm(const double *__restrict__ Gr, int64_t ldg, int m, int ng, const double *S, int wave, int lane,
                      double (&acc)[NGW][4]) {
   const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
@@ -931,13 +943,13 @@ DFM_DEV void fz_gemm(const double *__restrict__ Gr, int64_t ldg, int m, int ng, 
     for (int b = 0; b < 4; ++b) acc[q][b] = 0.0;
   unsigned off[NGW];   // the lane's G row offset + k of chunk 0
 #pragma unroll
-  for (int q = 0; q < NGW; ++q) off[q] = (unsigned)((4 * (wave + 4 * q) + fi) * ld + fkc);
+  for (int q = 0; q < NGW; ++q) off[q] = (unsigned)((4 * (wave + NW * q) + fi) * ld + fkc);
   double ring[FZ_DEPTH][NGW];
   auto load = [&](int c, double (&dst)[NGW]) {
     const int kg = 16 * c + fkc;
 #pragma unroll
     for (int q = 0; q < NGW; ++q) {
-      const int g = wave + 4 * q, row = 4 * g + fi;
+      const int g = wave + NW * q, row = 4 * g + fi;
       dst[q] = (g < ng && row < m && kg < m) ? Gr[off[q] + 16 * c] : 0.0;
     }
   };
@@ -955,7 +967,7 @@ DFM_DEV void fz_gemm(const double *__restrict__ Gr, int64_t ldg, int m, int ng, 
         for (int fb = 0; fb < 4; ++fb) bf[fb] = S[fz_ix(16 * c + fkc, 4 * fb + fi)];
 #pragma unroll
         for (int q = 0; q < NGW; ++q) {
-          if (wave + 4 * q >= ng) continue;   // wave-uniform
+          if (wave + NW * q >= ng) continue;   // wave-uniform
 #pragma unroll
           for (int fb = 0; fb < 4; ++fb) acc[q][fb] = mfma4(ring[s][q], bf[fb], acc[q][fb]);
         }
@@ -964,7 +976,40 @@ DFM_DEV void fz_gemm(const double *__restrict__ Gr, int64_t ldg, int m, int ng, 
   }
 }
 
-template <int NGW>
+// Out (P x P, stride P + 1) = X1' X2 over the mpad rows of two LDS images,
+// on ONE wave: output 4-row groups g = 0..3 of v_mfma_f64_4x4x4_4b.
+DFM_DEV void fz_xtx(const double *X1, const double *X2, double *Out, int mpad, int lane) {
+  constexpr int S = 17;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  double a4[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) a4[g][b] = 0.0;
+#pragma unroll 1
+  for (int k0 = 0; k0 < mpad; k0 += 16) {
+    const int kr = k0 + fkc;
+    double af[4], bf[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) af[g] = X1[fz_ix(kr, 4 * g + fi)];
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) bf[fb] = X2[fz_ix(kr, 4 * fb + fi)];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int fb = 0; fb < 4; ++fb) a4[g][fb] = mfma4(af[g], bf[fb], a4[g][fb]);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const double v = mm4_fold(a4[g], lane);
+    Out[(4 * g + (lane >> 4)) * S + (lane & 15)] = v;
+  }
+}
+
+// OVL: Y = G Q on waves 0..2 (NG3 groups each) while wave 3 forms Q'Q and
+// its inverse Cholesky factor — the Rayleigh-Ritz step's first factorisation
+// leaves the critical path.
+template <int NGW, int NG3, bool OVL>
 __global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
     const double *__restrict__ G, int64_t ldg, int64_t strideG, EigWork w, int m, int k, int p, double tol,
     int maxit, const double *__restrict__ warm, int kw, uint64_t seed, int warm_strict, int jsweeps, ChebCo cc,
@@ -1042,48 +1087,32 @@ __global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
 
     {   // Y = G Q
       FZ_THREAD;
-      double acc[NGW][4];
-      fz_gemm<NGW>(Gr, ldg, m, ng, sQ, wave, lane, acc);
+      constexpr int NG = OVL ? NG3 : NGW, NW = OVL ? 3 : 4;
+      if (!OVL || wave < 3) {
+        double acc[NG][4];
+        fz_gemm<NG, NW>(Gr, ldg, m, ng, sQ, wave, lane, acc);
 #pragma unroll
-      for (int q = 0; q < NGW; ++q) {
-        const int g = wave + 4 * q;
-        if (g >= ng) continue;
-        const double v = mm4_fold(acc[q], lane);
-        const int row = 4 * g + orow;
-        if (row < m) sY[fz_ix(row, oc)] = v;
+        for (int q = 0; q < NG; ++q) {
+          const int g = wave + NW * q;
+          if (g >= ng) continue;
+          const double v = mm4_fold(acc[q], lane);
+          const int row = 4 * g + orow;
+          if (row < m) sY[fz_ix(row, oc)] = v;
+        }
+      } else {
+        fz_xtx(sQ, sQ, sm.R2, mpad, lane);   // Q'Q
+        wave_lds_sync();
+        wave_chol_inv<P>(sm.R2, sm.R4, sm.dead, p);
       }
     }
     __syncthreads();
     FZ_MARK(1);
 
-    {   // Q'Y -> R1, Y'Y -> R3, Q'Q -> R2 (stride P + 1), over all mpad rows
+    {   // Q'Y -> R1, Y'Y -> R3 (and Q'Q -> R2 unless OVL formed it), stride P + 1, over all mpad rows
       FZ_THREAD;
-      if (wave < 3) {
+      if (wave < (OVL ? 2 : 3)) {
         const double *X1 = wave == 1 ? sY : sQ, *X2 = wave == 2 ? sQ : sY;
-        double *Out = wave == 0 ? sm.R1 : (wave == 1 ? sm.R3 : sm.R2);
-        double a4[4][4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) a4[g][b] = 0.0;
-#pragma unroll 1
-        for (int k0 = 0; k0 < mpad; k0 += 16) {
-          const int kr = k0 + fkc;
-          double af[4], bf[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) af[g] = X1[fz_ix(kr, 4 * g + fi)];
-#pragma unroll
-          for (int fb = 0; fb < 4; ++fb) bf[fb] = X2[fz_ix(kr, 4 * fb + fi)];
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int fb = 0; fb < 4; ++fb) a4[g][fb] = mfma4(af[g], bf[fb], a4[g][fb]);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const double v = mm4_fold(a4[g], lane);
-          Out[(4 * g + orow) * S + oc] = v;
-        }
+        fz_xtx(X1, X2, wave == 0 ? sm.R1 : (wave == 1 ? sm.R3 : sm.R2), mpad, lane);
       }
     }
     __syncthreads();
@@ -1095,9 +1124,9 @@ __global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
         if (pf) {   // stamps of the Rayleigh-Ritz stages (the last step's) after the phase sums
           EigWork wd = w;
           wd.dbg = prof + 8;
-          small_rr<P>(sm, wd, rep, p, jsweeps, nullptr, s_tail);
+          small_rr<P>(sm, wd, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0), nullptr, s_tail);
         } else {
-          small_rr<P>(sm, w, rep, p, jsweeps, nullptr, s_tail);
+          small_rr<P>(sm, w, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0), nullptr, s_tail);
         }
       }
     }
@@ -1163,7 +1192,7 @@ __global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
       double *So = last ? sQ : sY;
       FZ_THREAD;
       double acc[NGW][4];
-      fz_gemm<NGW>(Gr, ldg, m, ng, sY, wave, lane, acc);
+      fz_gemm<NGW, 4>(Gr, ldg, m, ng, sY, wave, lane, acc);
       if (!last) __syncthreads();   // every wave has read S_{i+1} before S_i overwrites it
       const bool dead_c = oc < p && s_tail[P + oc] != 0.0;
 #pragma unroll
@@ -1237,13 +1266,14 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
         prof = buf;
       }
       if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-#define DFM_FUSED(NG)                                                                                           \
-  hipFuncSetAttribute((const void *)eig_fused_kernel<NG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-  hipLaunchKernelGGL(eig_fused_kernel<NG>, dim3(nb), dim3(256), lds, st, G, ldg, strideG, w, m, k, p, tol, maxit,  \
-                     warm, kw, seed, (int)warm_strict, kJacobiSweeps, cc, lam, Uk, status, prof)
-      if (ngw == 4) { DFM_FUSED(4); }
-      else if (ngw == 9) { DFM_FUSED(9); }
-      else { DFM_FUSED(16); }
+#define DFM_FUSED(...)                                                                                          \
+  hipFuncSetAttribute((const void *)eig_fused_kernel<__VA_ARGS__>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                      (int)lds);                                                                                  \
+  hipLaunchKernelGGL((eig_fused_kernel<__VA_ARGS__>), dim3(nb), dim3(256), lds, st, G, ldg, strideG, w, m, k, p, tol, \
+                     maxit, warm, kw, seed, (int)warm_strict, fused_sweeps(), cc, lam, Uk, status, prof)
+      if (ngw == 4) { DFM_FUSED(4, 6, true); }
+      else if (ngw == 9) { DFM_FUSED(9, 12, true); }
+      else { DFM_FUSED(16, 22, false); }
 #undef DFM_FUSED
       if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
       // iteration statistics from the per-iteration unconverged counts

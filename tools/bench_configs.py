@@ -101,6 +101,9 @@ def c2(D, ctx, args):
                                        f"LR/LM/Wald all variables at bp={bp} + V + ICp2 (inputs resident)",
            "value": round(B / s, 1), "unit": "replicates/s", "ms_per_job": round(s * 1e3, 3),
            "kernels_ms_per_job": {k: round(v[0] / (args.reps + 1), 4) for k, v in tm.items() if v[1]}}
+    es = ctx.eig_stats()
+    rec["eig_iterations"] = dict(es, rayleigh_ritz_steps_per_replicate=round(
+        es["replicate_iterations"] / (B * (args.reps + 1)), 3))
     # Gram roofline: the replicate Grams X*'X* (130 x 130 over T = 600), SYRK
     # count N (N + 1) T per replicate (the weighted GEMM Q = W K
     # of the gram_wk path does 2 T N (N + 1) / 2, the same count), over the
