@@ -44,6 +44,8 @@ struct EigWork {
 #define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)wall_clock64(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
 constexpr int SMALL_CHOL1_DONE = 0x100;   // small_rr: R4 already holds chol(Q'Q)^-1 (eig_fused forms it during Y = G Q)
+constexpr int SMALL_STAGE_A = 0x200;      // small_rr: stop once A (R2), theta and Z'Z (R3) are formed
+constexpr int SMALL_STAGE_B = 0x400;      // small_rr: only chol(Z'Z) and Bm (eig_fused: beside the U pass)
 
 // ----------------------------------------------------------------- init
 template <int P>
@@ -370,6 +372,21 @@ struct SmallLds {
 // outstanding ones (and fencing the compiler) is the whole synchronisation.
 DFM_DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// reciprocal and reciprocal square root: hardware seed + two Newton steps
+// (full double precision to within an ulp or so; the Jacobi rotations only
+// need c^2 + s^2 = 1 to rounding, which c = rsq(1 + t^2), s = t c keep)
+DFM_DEV double nr_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+DFM_DEV double nr_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * fma(-hx * y, y, 1.5);
+  return y * fma(-hx * y, y, 1.5);
+}
+
 DFM_DEV double rl64(double x, int l) {   // lane l's x (l wave-uniform: a compile-time constant in unrolled loops)
   const long long b = __double_as_longlong(x);
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -488,6 +505,7 @@ DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, 
   asm volatile("" : "+v"(lane));
   asm volatile("" : "+s"(p));
   SMALL_STAMP(1);
+  if (!(jsweeps & SMALL_STAGE_B)) {
   wave_sym<P>(Hq);
   // 2. Q'Q = L L',  Li = L^-1;  H~ = Li (Q'Y) Li'
   if (!(jsweeps & SMALL_CHOL1_DONE)) wave_chol_inv<P>(sm.R2, sm.R4, sm.dead, p);
@@ -539,10 +557,16 @@ DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, 
         double c = 1.0, sn = 0.0;
         if (b < p) {
           const double hab = Hq[a * S + b], haa = Hq[a * S + a], hbb = Hq[b * S + b];
-          if (fabs(hab) > 1e-300 && fabs(hab) > 8.9e-16 * sqrt(fabs(haa) * fabs(hbb))) {
-            const double zeta = (hbb - haa) / (2.0 * hab);
-            const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-            c = 1.0 / sqrt(1.0 + t * t);
+          // |h_ab| > 4 eps sqrt(|h_aa h_bb|), squared; the rotation from the
+          // hardware reciprocal / reciprocal-square-root seeds plus Newton
+          // steps (the round's critical path: three divisions and three
+          // square roots in correctly rounded form)
+          if (fabs(hab) > 1e-300 && hab * hab > 7.921e-31 * fabs(haa * hbb)) {
+            const double zeta = (hbb - haa) * nr_rcp(2.0 * hab), az = fabs(zeta);
+            const double y = fma(zeta, zeta, 1.0);
+            const double rt = az > 1e150 ? az : y * nr_rsq(y);   // sqrt(1 + zeta^2)
+            const double t = (zeta >= 0.0 ? 1.0 : -1.0) * nr_rcp(az + rt);
+            c = nr_rsq(fma(t, t, 1.0));
             sn = t * c;
             rot = true;
           }
@@ -613,6 +637,9 @@ DFM_DEV void small_rr(SmallLds<P> &sm, EigWork &w, int rep, int p, int jsweeps, 
   wave_mm<P, true, false>(A, sm.R1, sm.R3);   // Z'Z (Y'Y is dead)
   wave_sym<P>(sm.R3);
   SMALL_STAMP(7);
+  }
+  if (jsweeps & SMALL_STAGE_A) return;
+  double *const A = sm.R2;
   wave_chol_inv<P>(sm.R3, sm.R4, sm.dead, p);
   SMALL_STAMP(8);
   SMALL_STAMP(9);
@@ -1124,65 +1151,94 @@ __global__ __launch_bounds__(256, NGW <= 9 ? 2 : 1) void eig_fused_kernel(
         if (pf) {   // stamps of the Rayleigh-Ritz stages (the last step's) after the phase sums
           EigWork wd = w;
           wd.dbg = prof + 8;
-          small_rr<P>(sm, wd, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0), nullptr, s_tail);
+          small_rr<P>(sm, wd, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0) | SMALL_STAGE_A, nullptr, s_tail);
         } else {
-          small_rr<P>(sm, w, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0), nullptr, s_tail);
+          small_rr<P>(sm, w, rep, p, jsweeps | (OVL ? SMALL_CHOL1_DONE : 0) | SMALL_STAGE_A, nullptr, s_tail);
         }
       }
     }
     __syncthreads();
     FZ_MARK(3);
 
-    // apply: A = R2, Bm = R1
+    // U pass (waves 1..3; A = R2, theta): U = Q A -> global, residual sums
+    // of W = Y A - U diag(theta) — beside wave 0's chol(Z'Z) and Bm = R1
+    {
+      FZ_THREAD;
+      if (wave == 0) {
+        if (pf) {
+          EigWork wd = w;
+          wd.dbg = prof + 8;
+          small_rr<P>(sm, wd, rep, p, jsweeps | SMALL_STAGE_B, nullptr, s_tail);
+        } else {
+          small_rr<P>(sm, w, rep, p, jsweeps | SMALL_STAGE_B, nullptr, s_tail);
+        }
+        if (lane < P) s_rw[0][lane] = 0.0;
+      } else {
+        double bA[4];
+#pragma unroll
+        for (int fb = 0; fb < 4; ++fb) bA[fb] = sm.R2[fkc * S + 4 * fb + fi];
+        const double th_c = s_tail[oc];
+        double rs = 0.0;
+#pragma unroll 1
+        for (int g = wave - 1; g < ng; g += 3) {
+          const int ra = 4 * g + fi;
+          const double aq = sQ[fz_ix(ra, fkc)], ay = sY[fz_ix(ra, fkc)];
+          double u4[4], ya4[4];
+#pragma unroll
+          for (int fb = 0; fb < 4; ++fb) {
+            u4[fb] = mfma4(aq, bA[fb], 0.0);
+            ya4[fb] = mfma4(ay, bA[fb], 0.0);
+          }
+          const double u = mm4_fold(u4, lane), ya = mm4_fold(ya4, lane);
+          const int row = 4 * g + orow;
+          if (row < m) {
+            if (oc < k) { const double wv = ya - th_c * u; rs += wv * wv; }
+            Ur[(int64_t)row * P + oc] = u;
+          }
+        }
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+        if (lane < P) s_rw[wave][lane] = rs;
+      }
+    }
+    __syncthreads();
+    FZ_MARK(4);
+
+    // next basis: V = Y Bm, V0 = Q Bm -> the filter's first Horner term S =
+    // (a_d / b) V + a_{d-1} V0 into Y, V0 into Q (dead columns re-randomised)
     const int dg = (warm_strict && it < 4) ? kChebDirectStrict : 2;
     const double *ca = s_ca[dg == 2 ? 0 : 1];
     const double bch = s_tail[p - 1];
     {
       FZ_THREAD;
+      if (tid < P) s_res[tid] = ((s_rw[0][tid] + s_rw[1][tid]) + s_rw[2][tid]) + s_rw[3][tid];
       const bool dead_c = oc < p && s_tail[P + oc] != 0.0;
-      double bA[4], bB[4];
+      double bB[4];
 #pragma unroll
-      for (int fb = 0; fb < 4; ++fb) {
-        bA[fb] = sm.R2[fkc * S + 4 * fb + fi];
-        bB[fb] = sm.R1[fkc * S + 4 * fb + fi];
-      }
-      const double th_c = s_tail[oc], fa1 = ca[dg], fa0 = ca[dg - 1];
-      double rs = 0.0;
-#pragma unroll 1   // one group's 16 accumulators live at a time
+      for (int fb = 0; fb < 4; ++fb) bB[fb] = sm.R1[fkc * S + 4 * fb + fi];
+      const double fa1 = ca[dg], fa0 = ca[dg - 1];
+#pragma unroll 1
       for (int g = wave; g < ng; g += 4) {
         const int ra = 4 * g + fi;
         const double aq = sQ[fz_ix(ra, fkc)], ay = sY[fz_ix(ra, fkc)];
-        double u4[4], ya4[4], qn4[4], qb4[4];
+        double qn4[4], qb4[4];
 #pragma unroll
         for (int fb = 0; fb < 4; ++fb) {
-          u4[fb] = mfma4(aq, bA[fb], 0.0);
-          ya4[fb] = mfma4(ay, bA[fb], 0.0);
           qn4[fb] = mfma4(ay, bB[fb], 0.0);
           qb4[fb] = mfma4(aq, bB[fb], 0.0);
         }
-        const double u = mm4_fold(u4, lane), ya = mm4_fold(ya4, lane);
         double qn = mm4_fold(qn4, lane), qb = mm4_fold(qb4, lane);
         const int row = 4 * g + orow;
         if (dead_c) qn = hash_unit(seed, row, 1000003ull * (it + 1) + oc);
         if (oc >= p) { qn = 0.0; qb = 0.0; }
         if (row < m) {
-          if (oc < k) { const double wv = ya - th_c * u; rs += wv * wv; }
-          Ur[(int64_t)row * P + oc] = u;
           const double sv = dead_c ? qn : (bch > 0.0 ? fma(fa1 / bch, qn, fa0 * qb) : qn);
           sY[fz_ix(row, oc)] = oc >= p ? 0.0 : sv;
           sQ[fz_ix(row, oc)] = oc >= p ? 0.0 : (dead_c ? qn : qb);
         }
       }
-      rs += __shfl_xor(rs, 16);
-      rs += __shfl_xor(rs, 32);
-      if (lane < P) s_rw[wave][lane] = rs;
     }
     __syncthreads();
-    {
-      FZ_THREAD;
-      if (tid < P) s_res[tid] = ((s_rw[0][tid] + s_rw[1][tid]) + s_rw[2][tid]) + s_rw[3][tid];
-    }
-    FZ_MARK(4);
 
     // Chebyshev filter: S_{dg-1} in Y; S_i = G S_{i+1} / b + a_i V0; S_0 into Q
     const double cb = bch > 0.0 ? 1.0 / bch : 1.0;
