@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
 // each with its own staged F, Z, eta and idx rows.  Both read the small
 // prep matrices from global memory (L1/L2).  Per (replicate, variable) the
 // arithmetic and its order are the same in both forms.
-constexpr int CH_FLAT_REPS = 4, CH_FLAT_MIN_N = 86;   // ceil(256 / 86) + 1 <= 4
+constexpr int CH_FLAT_REPS = 4;   // flat when ceil(256 / KS / N) + 1 <= 4 (N >= 86 at KS = 1)
 //
 // KS > 1 (R <= 4): KS lanes per (replicate, variable), lane k taking rows
 // t = t0 + k, t0 + k + KS, ... of every staged tile; the per-lane partial sums
@@ -283,11 +283,16 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     if (!ok) continue;
     const int tn = min(TR, T - t0);
     // CU rows per round: every row's gathered x loaded before the sums
-    // (CU loads in flight per thread instead of one dependent load per row);
-    // the arithmetic and its order are unchanged
-    for (int rb = ks; rb < tn; rb += KS * CU) {
+    // (CU loads in flight per thread instead of one dependent load per row),
+    // and the next round's loads issued before this round's arithmetic (the
+    // gathers are L2 / MALL latency-bound); the arithmetic and its order are
+    // unchanged
     double xs[CU];
-    load_rows(t0, rb, tn, xs);
+    if (ks < tn) load_rows(t0, ks, tn, xs);
+    for (int rb = ks; rb < tn; rb += KS * CU) {
+    double xn[CU];
+    const bool more = rb + KS * CU < tn;
+    if (more) load_rows(t0, rb + KS * CU, tn, xn);
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       const int rr = rb + KS * u;
@@ -315,6 +320,10 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
         for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[lr][rr * R + j], g2[j]);
       }
       }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < CU; ++u) xs[u] = xn[u];
     }
     }
   }
@@ -375,9 +384,12 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    for (int rb = ks; rb < tn; rb += KS * CU) {
     double xs[CU];
-    load_rows(t0, rb, tn, xs);
+    if (ks < tn) load_rows(t0, ks, tn, xs);
+    for (int rb = ks; rb < tn; rb += KS * CU) {
+    double xn[CU];
+    const bool more = rb + KS * CU < tn;
+    if (more) load_rows(t0, rb + KS * CU, tn, xn);
 #pragma unroll
     for (int uq = 0; uq < CU; ++uq) {
       const int rr = rb + KS * uq;
@@ -403,6 +415,10 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
 #pragma unroll
         for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
       }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < CU; ++u) xs[u] = xn[u];
     }
     }
   }

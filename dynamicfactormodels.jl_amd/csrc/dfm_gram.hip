@@ -470,17 +470,22 @@ __global__ __launch_bounds__(256) void gram_wk_prep_kernel(int T, int r, const d
 }
 
 // G[rep] (N x N, row-major, stride N*N) = A0 + L B + (L B)' + unpack(Q[rep]),
-// one workgroup per (lower 32 x 32 tile (I, J), replicate): the tile is
-// computed once (rows n of block I read their contiguous packed Q ranges),
-// staged in LDS, and written as tile (I, J) and, transposed, (J, I) — both
-// coalesced, G exactly symmetric.
-constexpr int WK_TILE = 32;
+// one workgroup per (lower 32 x 32 tile (I, J), replicate): the L rows and B
+// columns of blocks I and J staged in LDS first (every entry's two r-term
+// dot products then read LDS broadcasts instead of 4 r global loads), the
+// tile computed once (rows n of block I read their contiguous packed Q
+// ranges), staged in LDS, and written as tile (I, J) and, transposed,
+// (J, I) — both coalesced, G exactly symmetric.  Same operations in the same
+// order as before (x, y as r-term fma chains, then A0 + (x + y) + Q).
+constexpr int WK_TILE = 32, WK_RMAX = 16;
 __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__restrict__ A0,
                                                               const double *__restrict__ L,
                                                               const double *__restrict__ Bo,
                                                               const double *__restrict__ Q, int64_t ldk, int N, int r,
                                                               double *__restrict__ G) {
   __shared__ double tile[WK_TILE][WK_TILE + 1];
+  __shared__ double sLI[WK_TILE][WK_RMAX + 1], sLJ[WK_TILE][WK_RMAX + 1];   // L rows of blocks I, J
+  __shared__ double sBI[WK_RMAX][WK_TILE + 1], sBJ[WK_RMAX][WK_TILE + 1];   // B columns of blocks I, J
   const int rep = blockIdx.y, tid = threadIdx.x;
   int I = (int)((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= (int)blockIdx.x) ++I;
@@ -489,14 +494,25 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
   const double *Br = Bo + (int64_t)rep * r * N;
   const double *Qr = Q + (int64_t)rep * ldk;
   double *Gr = G + (int64_t)rep * N * N;
+  for (int e = tid; e < WK_TILE * r; e += 256) {
+    const int a = e / r, j = e % r, nI = I * WK_TILE + a, nJ = J * WK_TILE + a;
+    sLI[a][j] = nI < N ? L[(int64_t)nI * r + j] : 0.0;
+    sLJ[a][j] = nJ < N ? L[(int64_t)nJ * r + j] : 0.0;
+  }
+  for (int e = tid; e < WK_TILE * r; e += 256) {
+    const int j = e / WK_TILE, a = e % WK_TILE, nI = I * WK_TILE + a, nJ = J * WK_TILE + a;
+    sBI[j][a] = nI < N ? Br[(int64_t)j * N + nI] : 0.0;
+    sBJ[j][a] = nJ < N ? Br[(int64_t)j * N + nJ] : 0.0;
+  }
+  __syncthreads();
   for (int e = tid; e < WK_TILE * WK_TILE; e += 256) {
     const int a = e / WK_TILE, b = e % WK_TILE, n = I * WK_TILE + a, m = J * WK_TILE + b;
     double v = 0.0;
     if (n < N && m <= n) {
       double x = 0.0, y = 0.0;   // x: L[n] . B[:, m],  y: L[m] . B[:, n]
       for (int j = 0; j < r; ++j) {
-        x = fma(L[(int64_t)n * r + j], Br[(int64_t)j * N + m], x);
-        y = fma(L[(int64_t)m * r + j], Br[(int64_t)j * N + n], y);
+        x = fma(sLI[a][j], sBJ[j][b], x);
+        y = fma(sLJ[b][j], sBI[j][a], y);
       }
       v = (A0[(int64_t)n * N + m] + (x + y)) + Qr[(int64_t)n * (n + 1) / 2 + m];
     }
