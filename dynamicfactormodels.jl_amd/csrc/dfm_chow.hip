@@ -206,10 +206,13 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   // does not fit is spilled once per thread around pass B, not inside the row
   // loops — unbounded, the compiler took 256 VGPRs + 76 AGPRs at R = 4 and ran
   // one wave per SIMD
-  constexpr int CU = KS > 1 ? 8 : (R <= 4 ? 16 : (R <= 8 ? 8 : 16));
+#ifndef DFM_CH_CU   // (A/B builds: rows per gather round at KS > 1)
+#define DFM_CH_CU 8
+#endif
+  constexpr int CU = KS > 1 ? DFM_CH_CU : (R <= 4 ? 16 : (R <= 8 ? 8 : 16));
   constexpr int NR = FLAT ? CH_FLAT_REPS : 1;   // replicates staged per block
   __shared__ double sF[NR][TR * R], sZ[NR][TR * R], sE[NR][TR];
-  __shared__ int sI[NR][TR];
+  __shared__ unsigned sI[NR][TR];   // byte offset of the row's E row (idx_t ld 8)
   const int tid = threadIdx.x, nth = blockDim.x, ks = tid % KS;
   int rep, i, rep0, nrw;
   if constexpr (FLAT) {   // (replicate, variable) pairs, KS threads each
@@ -222,6 +225,8 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   }
   const bool ok = FLAT ? rep < nb : i < N;
   const int lr = FLAT ? (ok ? rep - rep0 : 0) : 0;   // this thread's staged replicate
+  if (!ok) i = 0;   // (idle lanes gather a valid column; they write nothing)
+  const unsigned ld8 = (unsigned)src.ld * 8u, i8 = (unsigned)i * 8u;
   // this pair's replicate's prep block (matrix m at Pc + m R^2, row-major R x R)
   const double *Pc = prep + (size_t)(ok ? rep : rep0) * CP_NMAT * R * R;
   auto PM = [&](int m, int a, int c) -> double { return Pc[m * R * R + a * R + c]; };
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
       const int q = e / TR, rr = e % TR, t = t0 + rr;
       const int64_t ro = (int64_t)(rep0 + q) * src.rs;
       sE[q][rr] = (HAS_ETA && t < T) ? src.eta[ro + t] : 1.0;
-      sI[q][rr] = t < T ? (HAS_IDX ? src.idx[ro + t] : t) : 0;
+      sI[q][rr] = t < T ? (unsigned)(HAS_IDX ? src.idx[ro + t] : t) * ld8 : 0u;
     }
   };
   // CU rows' gathered values x = C + eta E[idx]: the staged row indices
@@ -244,15 +249,21 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   // flight together (computing each row's x as its loads arrive made the
   // compiler wait for every row's loads before the next row's issued)
   // (this lane's rows of the tile: rb, rb + KS, ..., rb + (CU - 1) KS)
+  // Addresses: 32-bit byte offsets from the uniform panel bases (the launcher
+  // checks T ld 8 < 2^32) — the staged E-row offsets plus 8 i, the C row
+  // offsets stepping by KS ld 8 — so a row costs two 32-bit adds, not the
+  // 64-bit index products that were a third of the loop's instructions.
   auto load_rows = [&](int t0, int rb, int tn, double *xs) {
-    int ri[CU];
+    unsigned ro[CU];
     double ee[CU], cc[CU];
 #pragma unroll
-    for (int u = 0; u < CU; ++u) ri[u] = sI[lr][min(rb + KS * u, tn - 1)];
+    for (int u = 0; u < CU; ++u) ro[u] = sI[lr][min(rb + KS * u, tn - 1)] + i8;
+    unsigned co = (unsigned)(t0 + rb) * ld8 + i8;
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
-      ee[u] = src.E[(int64_t)ri[u] * src.ld + i];
-      if (HAS_C) cc[u] = src.C[(int64_t)(t0 + min(rb + KS * u, tn - 1)) * src.ld + i];
+      ee[u] = *(const double *)((const char *)src.E + ro[u]);
+      if (HAS_C) cc[u] = *(const double *)((const char *)src.C + (rb + KS * u < tn ? co : (unsigned)(t0 + tn - 1) * ld8 + i8));
+      co += KS * ld8;
     }
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
@@ -262,6 +273,14 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
       xs[u] = x;
     }
   };
+  // 1: every row of this wave's batch (rows rb, rb + KS, .. of the tile) is
+  // before bp, 2: every row at or after bp, 0: mixed (a wave vote)
+  auto batch_side = [&](int t0, int rb, int tn) {
+    const int ta = t0 + rb, tb = t0 + min(rb + KS * (CU - 1), tn - 1);
+    if (!__any(ok && tb >= bp)) return 1;
+    if (!__any(ok && ta < bp)) return 2;
+    return 0;
+  };
   // loadings of variable i (src/chowtest.jl uses dfm.factor_residuals = x - F L')
   // (break models: block b's loadings for rows a[b] .. a[b+1]-1)
   double l[R];
@@ -269,7 +288,6 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
 #pragma unroll
     for (int j = 0; j < R; ++j) l[j] = (ok && j < r) ? Lm[b * blk.lbs + ((int64_t)rep * N + i) * r + j] : 0.0;
   };
-  if (!ok) i = 0;   // (idle lanes gather a valid column; they write nothing)
   load_l(0);
   int cb = 0, next = BRK ? blk.a[1] : T;
   // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2 (BRK: cx = sum_{t>=bp} f_t e_t)
@@ -282,49 +300,48 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    // CU rows per round: every row's gathered x loaded before the sums
-    // (CU loads in flight per thread instead of one dependent load per row),
-    // and the next round's loads issued before this round's arithmetic (the
-    // gathers are L2 / MALL latency-bound); the arithmetic and its order are
-    // unchanged
-    double xs[CU];
-    if (ks < tn) load_rows(t0, ks, tn, xs);
+    // CU rows per round: every row's gathered x loaded before the sums (CU
+    // loads in flight per thread).  (Prefetching the next round's rows into a
+    // second register set was measured: at 3 waves per SIMD it spills, and a
+    // copy between the sets waits for the prefetched loads.)  A batch wholly
+    // before or after bp (every lane: the wave votes) takes a form without
+    // the per-row subperiod branch.  Same operations per row.
     for (int rb = ks; rb < tn; rb += KS * CU) {
-    double xn[CU];
-    const bool more = rb + KS * CU < tn;
-    if (more) load_rows(t0, rb + KS * CU, tn, xn);
+      double xs[CU];
+      load_rows(t0, rb, tn, xs);
+      const int side = batch_side(t0, rb, tn);   // wave-uniform
 #pragma unroll
-    for (int u = 0; u < CU; ++u) {
-      const int rr = rb + KS * u;
-      if (rr < tn) {   // (a guard, not a break: the loop must unroll)
-      const int t = t0 + rr;
-      if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
-      const double x = xs[u];
-      double ev = x;
+      for (int u = 0; u < CU; ++u) {
+        const int rr = rb + KS * u;
+        if (rr < tn) {   // (a guard, not a break: the loop must unroll)
+        const int t = t0 + rr;
+        if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
+        const double x = xs[u];
+        double fr[R];
 #pragma unroll
-      for (int j = 0; j < R; ++j) ev -= sF[lr][rr * R + j] * l[j];
-      e2 = fma(ev, ev, e2);
-      if (BRK) {
+        for (int j = 0; j < R; ++j) fr[j] = sF[lr][rr * R + j];
+        double ev = x;
 #pragma unroll
-        for (int j = 0; j < R; ++j) cf[j] = fma(ev, sF[lr][rr * R + j], cf[j]);
+        for (int j = 0; j < R; ++j) ev -= fr[j] * l[j];
+        e2 = fma(ev, ev, e2);
+        if (BRK) {
+#pragma unroll
+          for (int j = 0; j < R; ++j) cf[j] = fma(ev, fr[j], cf[j]);
+        }
+        if (BRK && t >= bp) {
+#pragma unroll
+          for (int j = 0; j < R; ++j) cx[j] = fma(ev, fr[j], cx[j]);
+        }
+        // (side != 0: a uniform branch; the mixed batch branches per lane)
+        if (side == 1 || (side == 0 && t < bp)) {
+#pragma unroll
+          for (int j = 0; j < R; ++j) g1[j] = fma(x, fr[j], g1[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < R; ++j) g2[j] = fma(x, fr[j], g2[j]);
+        }
+        }
       }
-      if (BRK && t >= bp) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) cx[j] = fma(ev, sF[lr][rr * R + j], cx[j]);
-      }
-      if (t < bp) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) g1[j] = fma(x, sF[lr][rr * R + j], g1[j]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < R; ++j) g2[j] = fma(x, sF[lr][rr * R + j], g2[j]);
-      }
-      }
-    }
-    if (more) {
-#pragma unroll
-      for (int u = 0; u < CU; ++u) xs[u] = xn[u];
-    }
     }
   }
   if constexpr (KS > 1) {   // the KS lanes' partial sums, in a fixed order
@@ -374,6 +391,7 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   }
   // ---- pass B: subperiod SSRs and the HC0 block sum_t u_t^2 z_t z_t'
   double S[R * (R + 1) / 2], ssr = 0.0, bq[R];
+  bool post_set = false;
 #pragma unroll
   for (int j = 0; j < R; ++j) bq[j] = b1[j] + b2[j];
 #pragma unroll
@@ -384,42 +402,72 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     __syncthreads();
     if (!ok) continue;
     const int tn = min(TR, T - t0);
-    double xs[CU];
-    if (ks < tn) load_rows(t0, ks, tn, xs);
     for (int rb = ks; rb < tn; rb += KS * CU) {
-    double xn[CU];
-    const bool more = rb + KS * CU < tn;
-    if (more) load_rows(t0, rb + KS * CU, tn, xn);
+      double xs[CU];
+      load_rows(t0, rb, tn, xs);
+      const int side = batch_side(t0, rb, tn);   // wave-uniform
+      // rows ascend, so once a batch lies wholly at or after bp every later
+      // one does: the post-break coefficients then replace the pre-break ones
+      // (b1 and ga1 are not read after pass B) and the rows run without the
+      // per-row selects, which only the one mixed batch keeps
+      if (side == 2 && !post_set) {
 #pragma unroll
-    for (int uq = 0; uq < CU; ++uq) {
-      const int rr = rb + KS * uq;
-      if (rr < tn) {
-      const int t = t0 + rr;
-      const double x = xs[uq];
-      const bool post = t >= bp;
-      double u = x, rs = x;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const double f = sF[lr][rr * R + j];
-        u -= f * (post ? bq[j] : b1[j]);
-        rs -= f * (post ? ga2[j] : ga1[j]);
+        for (int j = 0; j < R; ++j) { b1[j] = bq[j]; ga1[j] = ga2[j]; }
+        post_set = true;
       }
-      ssr = fma(rs, rs, ssr);
-      const double u2 = u * u;
-      double zs[R];
+      if (side == 0) {   // the mixed batch: per-row subperiod selects
 #pragma unroll
-      for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[lr][rr * R + j];
-      int e = 0;
+        for (int uq = 0; uq < CU; ++uq) {
+          const int rr = rb + KS * uq;
+          if (rr < tn) {
+          const int t = t0 + rr;
+          const double x = xs[uq];
+          const bool post = t >= bp;
+          double u = x, rs = x;
 #pragma unroll
-      for (int a = 0; a < R; ++a)
+          for (int j = 0; j < R; ++j) {
+            const double f = sF[lr][rr * R + j];
+            u -= f * (post ? bq[j] : b1[j]);
+            rs -= f * (post ? ga2[j] : ga1[j]);
+          }
+          ssr = fma(rs, rs, ssr);
+          const double u2 = u * u;
+          double zs[R];
 #pragma unroll
-        for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
+          for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[lr][rr * R + j];
+          int e = 0;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int uq = 0; uq < CU; ++uq) {
+          const int rr = rb + KS * uq;
+          if (rr < tn) {
+          const double x = xs[uq];
+          double u = x, rs = x;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            const double f = sF[lr][rr * R + j];
+            u -= f * b1[j];
+            rs -= f * ga1[j];
+          }
+          ssr = fma(rs, rs, ssr);
+          const double u2 = u * u;
+          double zs[R];
+#pragma unroll
+          for (int j = 0; j < R; ++j) zs[j] = u2 * sZ[lr][rr * R + j];
+          int e = 0;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int c2 = 0; c2 <= a; ++c2) { S[e] = fma(zs[a], sZ[lr][rr * R + c2], S[e]); ++e; }
+          }
+        }
       }
-    }
-    if (more) {
-#pragma unroll
-      for (int u = 0; u < CU; ++u) xs[u] = xn[u];
-    }
     }
   }
   if constexpr (KS > 1) {
@@ -503,6 +551,7 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
                        const int *brow, int64_t lbs) {
   (void)orient;
   if (r < 1 || r > CH_RMAX || nblk < 1 || nblk > CH_BMAX) return hipErrorInvalidValue;
+  if ((int64_t)T * src.ld * 8 >= ((int64_t)1 << 32)) return hipErrorInvalidValue;   // 32-bit gather offsets
   ChowBlocks blk{};
   blk.n = nblk;
   blk.lbs = lbs;
