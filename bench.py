@@ -154,7 +154,8 @@ def pmc_traffic(kernel):
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from
     FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE); None when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    # the headline bench's own pass (rNN_pmc_traffic.json), not the C2 one (rNN_pmc_traffic_c2.json)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -235,6 +236,8 @@ def main():
                     help="c5: rolling windows of this many rows instead of expanding windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling extra field (N > 1)")
+    ap.add_argument("--all-fields", action="store_true",
+                    help="also time the job with the whole regression record per replicate (F*, L*, OLS formed)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -354,8 +357,11 @@ def main():
     # L* and the OLS pass run too.  The headline stats (V + ICp2) read only
     # the eigenvalues and the trace, and the library forms only the fields the
     # requested statistics read (include/dfm.h).
+    # Opt-in (--all-fields): the default command's rocprofv3 trace then holds
+    # only the headline job's launches, so its H.Z GEMM average agrees with
+    # the HIP-event roofline of the same run.
     full = None
-    if world == 1 and nloc:
+    if args.all_fields and world == 1 and nloc:
         fstats = stats + [D.Stat.coefficient(j) for j in range(1, R + 2)] + [D.Stat.t_stat(j) for j in range(1, R + 2)]
         farr = D.api._stat_array(fstats)
         fwidth = int(ctx.lib.dfm_stats_width(model.handle, farr, len(fstats)))
@@ -437,7 +443,8 @@ def main():
                        "[0, theta_p] after later ones"),
         "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps),
         "fields_formed": "eigenvalues + trace: V and ICp2 read nothing else, so the replicate factors, loadings "
-                         "and OLS are not formed (demand-driven; see all_fields for the full record's rate)",
+                         "and OLS are not formed (demand-driven; `bench.py --all-fields` adds the full record's "
+                         "rate: profiles/r04_bench_all_fields.json)",
     }
     if full:
         rec["all_fields"] = full
