@@ -1365,7 +1365,8 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       const double spread = (M->lam.size() >= (size_t)r && r > 0 && M->lam[r - 1] > 0.0) ? M->lam[0] / M->lam[r - 1]
                                                                                         : 0.0;
       int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
-                                w.eig, w.fact, w.lam, w.Uk, w.trace, w.status, st, timer_cb, ctx, w.off, w.lst,
+                                w.eig, w.fact, w.lam, need_fl ? w.Uk : nullptr, w.trace, w.status, st, timer_cb,
+                                ctx, w.off, w.lst,
                                 (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread);
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);

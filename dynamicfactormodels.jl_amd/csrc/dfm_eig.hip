@@ -40,6 +40,7 @@ struct EigWork {
   // value theta_k (the wanted SUBSPACE converged: for statistics invariant to
   // rotations within span(F_r) — Chow tests, V, criteria, eigenvalues)
   int subspace;
+  int no_vectors;          // eigenvalue-only caller (Uk == nullptr): the Ritz vectors are never written
 };
 #define SMALL_STAMP(i) do { if (w.dbg && rep == 0 && lane == 0) w.dbg[i] = (long long)wall_clock64(); } while (0)
 template <int P> constexpr int small_stride() { return 2 * P * P + 4 * P; }
@@ -752,6 +753,11 @@ __global__ __launch_bounds__(256) void eig_apply_kernel(EigWork w, int m, int p,
 template <int P>
 DFM_DEV void eig_final_body(const double *Ur, const double *theta, int done, int rep, int m, int k,
                             double *__restrict__ lam, double *__restrict__ Uk, int *__restrict__ status) {
+  if (!Uk) {   // eigenvalue-only statistics: no vectors wanted, no pass over U
+    if (threadIdx.x < k) lam[(int64_t)rep * k + threadIdx.x] = theta[threadIdx.x];
+    if (threadIdx.x == 0) status[rep] = done ? 0 : 1;
+    return;
+  }
   // one pass over U: each thread keeps the running max |U[r][j]| (first row
   // on ties) of its rows for every column j, then a shuffle reduction per
   // wave and a fixed-order combine of the four waves (smaller row index wins
@@ -847,6 +853,7 @@ static EigWork carve(char *base, int m, int nb, int P, int maxit) {
   w.active = (int *)take((size_t)(maxit + 2) * 4);
   w.dbg = nullptr;
   w.subspace = 0;
+  w.no_vectors = 0;
   return w;
 }
 
@@ -2161,6 +2168,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   __syncthreads();
   if (!init && (s_conv || last)) {
+    if (w.no_vectors) return;   // eigenvalue-only statistics: eig_final reads theta only
     // Ritz vectors U = Q A for the final output (eig_final_kernel)
     double *Ur = w.U + (int64_t)rep * T * P;
     for (int tile = wave; tile < ntile; tile += BW) {
@@ -2632,6 +2640,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   const int m = fb.T;
   EigWork w = carve(ws, m, nb, P, maxit);
   w.subspace = subspace;
+  w.no_vectors = Uk == nullptr;
   const int64_t ldz = (int64_t)nb * P;
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)z_rows(m) * ldz;
