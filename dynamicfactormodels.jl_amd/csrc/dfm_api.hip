@@ -68,7 +68,8 @@ __global__ void panel_from_colmajor_kernel(const double *, int64_t, int, int, do
 __global__ void colmajor_from_rows_kernel(const double *, int64_t, int, int, double *);
 bool launch_factors_cols_fact(const double *Ep, int64_t ld, int T, int N, int k, const double *Fb, const double *Lb,
                               int rb, const int32_t *idx, const double *eta, int64_t rs, int nb, const double *Uk,
-                              double *F, double *L, int64_t fstride, hipStream_t st);
+                              double *F, double *L, int64_t fstride, double *G, hipStream_t st);
+double *gram_wk_scratch(double *work, int T, int N, int r, int nb);
 int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb, const double *Uk,
                    double *F, double *L, double *colssr, hipStream_t st, double Ts = 0, int64_t fstride = 0);
 __global__ void colssr_cols_kernel(const double *, int64_t, int64_t, int, int, const double *,
@@ -1413,7 +1414,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
         Scope sc(ctx, DFM_KC_FACTORS);
         done_f = launch_factors_cols_fact(M->Ep, M->ld, T, N, r, M->F, M->L, r, idx + b0 * T,
                                           kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, T, n, w.Uk, w.F, w.L,
-                                          (int64_t)T * r, st);
+                                          (int64_t)T * r, gram_wk_scratch(w.gwk, T, N, r, n), st);
       }
       if (!done_f && (rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
     }

@@ -553,6 +553,11 @@ hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r,
 size_t gram_wk_work(int T, int N, int r, int nb) {
   return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N) + (size_t)r * gram_wk_tp(T));
 }
+// the At region (nb r Tp >= nb T r doubles): free once the batch's Grams are
+// formed — the factored F* pass (dfm_model.hip fact_el_kernel) writes E L* there
+double *gram_wk_scratch(double *work, int T, int N, int r, int nb) {
+  return work + (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N));
+}
 // nb replicate Grams X*'X* (N x N each, stride N*N) of src (C + diag(eta) E[idx]).
 hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
                           const double *K, const double *A0, const int32_t *idx, const double *eta, int64_t rs,

@@ -657,31 +657,97 @@ int launch_factors(int orient, const PanelSrc &src, int T, int N, int k, int nb,
 // replicate loadings L* = sqrt(N) U*,
 //   F* = X* L* / N = ( F (L' L*) + D P (E L*) ) / N,
 // so a replicate needs E L* (T x N x k, E shared and L2-resident) and the
-// k x k block L' L* instead of a pass over its resampled panel.  One
-// workgroup per replicate: L* and E L* staged in LDS (the gather idx_t is then
-// an LDS read), L = L* written.  Requirements: k <= KM, (T + N) KM doubles of LDS.
+// k x k block L' L* instead of a pass over its resampled panel.
+// Two launches:
+//  fact_el_kernel — E L* for the whole batch as ONE MFMA product
+//    E (T x N) . [L*_1 .. L*_nb] (N x nb k), one wave per 32 x 16 output tile
+//    (8 x 4 v_mfma_f64_4x4x4 fragments, N in chunks of 16), operands read
+//    straight from L2 into the fragments (E rows: 4 x 128 B segments per
+//    load; a replicate's U is n-major, so its k columns are contiguous),
+//    written replicate-major G[rep][s][j].  (Round 4 computed it per
+//    replicate, one thread per row s walking E's row: 64 rows per load
+//    instruction, L1 thrashed — 0.29 ms per C2 lane, now ~0.01 ms.)
+//  fact_gather_kernel — per replicate: L = L*, M = L' L*, and
+//    F*[t] = (F[t] M + eta_t G[rep][idx_t]) / N.
+// Per replicate the sums run in a fixed order (no dependence on the batch).
+__global__ __launch_bounds__(256) void fact_el_kernel(const double *__restrict__ Ep, int64_t ld, int T, int N, int k,
+                                                      int nb, const double *__restrict__ Uk, double *__restrict__ G) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrt = (T + 31) / 32, ncols = nb * k, nct = (ncols + 15) / 16;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= nrt * nct) return;   // wave-uniform; the kernel has no barriers
+  // consecutive waves: the row tiles of one column tile (its U columns re-read from L1)
+  const int rt = tile % nrt, ct = tile / nrt, rbase = rt * 32, cbase = ct * 16;
+  const double sN = sqrt((double)N);
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const double *ea[8], *ub[4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) ea[f] = Ep + (int64_t)min(rbase + 4 * f + fi, T - 1) * ld;   // past T: discarded
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = min(cbase + 4 * q + fi, ncols - 1), rep = c / k;   // past the batch: discarded
+    ub[q] = Uk + (int64_t)rep * N * k + (c - rep * k);
+  }
+  double acc[8][4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[f][q] = 0.0;
+  for (int k0 = 0; k0 < N; k0 += 16) {
+    const int n = k0 + fkc;
+    const bool okn = n < N;
+    const int nc = okn ? n : N - 1;   // k tail: A's zero times finite B
+    double af[8], bf[4];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) af[f] = ea[f][nc];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bf[q] = ub[q][(int64_t)nc * k];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) af[f] = okn ? af[f] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bf[q] = sN * bf[q];   // L* = sqrt(N) U*, rounded as L is
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[f][q] = mfma4(af[f], bf[q], acc[f][q]);
+  }
+  // the four k-blocks summed and transposed into (row, column) lanes (dfm_gemm.hip's epilogue)
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa) {
+    const double a0 = acc[fa][0], a1 = acc[fa][1], a2 = acc[fa][2], a3 = acc[fa][3];
+    const double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+    const double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+    const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+    const int row = rbase + 4 * fa + oi, col = cbase + 4 * blk + oj;
+    if (row < T && col < ncols) {
+      const int rep = col / k;
+      G[((int64_t)rep * T + row) * k + (col - rep * k)] = v;
+    }
+  }
+}
+
 template <int KM>
-__global__ __launch_bounds__(256) void factors_cols_fact_kernel(const double *__restrict__ Ep, int64_t ld, int T,
-                                                                int N, int k, const double *__restrict__ Fb,
-                                                                const double *__restrict__ Lb, int rb,
-                                                                const int32_t *__restrict__ idx,
-                                                                const double *__restrict__ eta, int64_t rs,
-                                                                const double *__restrict__ Uk,
-                                                                double *__restrict__ F, double *__restrict__ L,
-                                                                int64_t fstride) {
+__global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, const double *__restrict__ Fb,
+                                                          const double *__restrict__ Lb, int rb,
+                                                          const int32_t *__restrict__ idx,
+                                                          const double *__restrict__ eta, int64_t rs,
+                                                          const double *__restrict__ Uk,
+                                                          const double *__restrict__ G, double *__restrict__ F,
+                                                          double *__restrict__ L, int64_t fstride) {
   extern __shared__ double fdyn[];
   double *sL = fdyn;                        // N x KM: L* = sqrt(N) U*
-  double *sEL = sL + (size_t)N * KM;        // T x KM: E L*
   __shared__ double sM[32 * KM];            // rb x k: L' L*
   const int rep = blockIdx.x, tid = threadIdx.x;
   const double sN = sqrt((double)N);
   const double *U = Uk + (int64_t)rep * N * k;
   double *Lr = L + (int64_t)rep * N * k;
-  for (int e = tid; e < N * KM; e += 256) {
-    const int n = e / KM, j = e - n * KM;
-    const double v = j < k ? sN * U[(int64_t)n * k + j] : 0.0;
-    sL[e] = v;
-    if (j < k) Lr[(int64_t)n * k + j] = v;
+  for (int e = tid; e < N * k; e += 256) {
+    const int n = e / k, j = e - n * k;
+    const double v = sN * U[e];
+    sL[n * KM + j] = v;
+    Lr[e] = v;
   }
   __syncthreads();
   // M = L' L* (rb x k): one dot product of length N per entry, in n order
@@ -691,42 +757,32 @@ __global__ __launch_bounds__(256) void factors_cols_fact_kernel(const double *__
     for (int n = 0; n < N; ++n) acc = fma(Lb[(int64_t)n * rb + i], sL[n * KM + j], acc);
     sM[i * KM + j] = acc;
   }
-  // E L*: row s per thread, n in order (the row stays in L1 across n)
-  for (int s0 = tid; s0 < T; s0 += 256) {
-    double acc[KM];
-#pragma unroll
-    for (int j = 0; j < KM; ++j) acc[j] = 0.0;
-    const double *er = Ep + (int64_t)s0 * ld;
-    for (int n = 0; n < N; ++n) {
-      const double x = er[n];
-#pragma unroll
-      for (int j = 0; j < KM; ++j) acc[j] = fma(x, sL[n * KM + j], acc[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < KM; ++j) sEL[s0 * KM + j] = acc[j];
-  }
   __syncthreads();
   const int32_t *ix = idx + (int64_t)rep * rs;
   const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
+  const double *Gr = G + (int64_t)rep * T * k;
   double *Fr = F + (int64_t)rep * fstride;
   const double invN = 1.0 / N;
   for (int e = tid; e < T * k; e += 256) {
     const int t = e / k, j = e - t * k;
     double c = 0.0;   // (F (L' L*))[t][j]
     for (int i = 0; i < rb; ++i) c = fma(Fb[(int64_t)t * rb + i], sM[i * KM + j], c);
-    const double x = fma(et ? et[t] : 1.0, sEL[ix[t] * KM + j], c);
+    const double x = fma(et ? et[t] : 1.0, Gr[(int64_t)ix[t] * k + j], c);
     Fr[(int64_t)t * k + j] = x * invN;
   }
 }
-// nb replicates; false when the shape does not fit (caller keeps launch_factors)
+// nb replicates; G: nb T k doubles of scratch.  false when the shape does not
+// fit (caller keeps launch_factors)
 bool launch_factors_cols_fact(const double *Ep, int64_t ld, int T, int N, int k, const double *Fb, const double *Lb,
                               int rb, const int32_t *idx, const double *eta, int64_t rs, int nb, const double *Uk,
-                              double *F, double *L, int64_t fstride, hipStream_t st) {
-  if (k < 1 || k > 8 || rb < 1 || rb > 32) return false;
-  const size_t lds = (size_t)(T + N) * 8 * 8;
+                              double *F, double *L, int64_t fstride, double *G, hipStream_t st) {
+  if (k < 1 || k > 8 || rb < 1 || rb > 32 || T < 1 || N < 1) return false;
+  const size_t lds = (size_t)N * 8 * 8;
   if (lds > 64 * 1024) return false;
-  hipLaunchKernelGGL(factors_cols_fact_kernel<8>, dim3(nb), dim3(256), lds, st, Ep, ld, T, N, k, Fb, Lb, rb, idx, eta,
-                     rs, Uk, F, L, fstride);
+  const int64_t tiles = (int64_t)((T + 31) / 32) * (((int64_t)nb * k + 15) / 16);
+  hipLaunchKernelGGL(fact_el_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, Ep, ld, T, N, k, nb, Uk, G);
+  hipLaunchKernelGGL(fact_gather_kernel<8>, dim3(nb), dim3(256), lds, st, T, N, k, Fb, Lb, rb, idx, eta, rs, Uk, G, F,
+                     L, fstride);
   return hipGetLastError() == hipSuccess;
 }
 
