@@ -1070,6 +1070,9 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
 // rows are bit-identical to one lane (tests/test_gpu_multi.py).
 constexpr int64_t kLaneMin = 512, kLaneMax = 6000;
 static bool lane_split(const dfm_model *M, int64_t B, const dfm_stat *stats, int ns) {
+  // DFM_NO_LANES=1 (diagnostic): one lane, so a kernel trace shows solo durations
+  static const bool no_lanes = [] { const char *e = getenv("DFM_NO_LANES"); return e && atoi(e) != 0; }();
+  if (no_lanes) return false;
   if (M->is_lane || M->batch != 0 || B < kLaneMin || B > kLaneMax || ns < 0 || (ns > 0 && !stats)) return false;
   const int p = eig_block_p(M->m, M->r, M->ctx->block);
   if (p > 32 || p < M->r) return false;

@@ -469,6 +469,74 @@ __global__ __launch_bounds__(256) void gram_wk_prep_kernel(int T, int r, const d
   }
 }
 
+// B = At . E (nb r x N): the 64 x 64 tiles of the batched GEMM left C2's
+// 130 columns in 3 column blocks (one holding 2 columns) and 96 tiles with a
+// 600-deep serial K loop each — latency-bound on a quarter of the chip
+// (61 us per lane).  Here one wave per 32 x 16 output tile (8 x 4
+// v_mfma_f64_4x4x4 fragments, operands read straight from L2 into the
+// fragments, the next 16-deep chunk's loads issued before this chunk's
+// MFMAs) and split-K over WK_BS fixed k-ranges: partial images Bo[z], summed
+// in z order where they are read (gram_wk_combine_kernel).
+constexpr int WK_BS = 4;
+__global__ __launch_bounds__(256) void gram_wk_b_kernel(const double *__restrict__ At, int Tp, const double *__restrict__ Ep,
+                                                        int64_t ld, int T, int N, int rows, int nch,
+                                                        double *__restrict__ Bo) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrt = (rows + 31) / 32, nct = (N + 15) / 16;
+  const int item = blockIdx.x * 4 + wave;
+  if (item >= nrt * nct * WK_BS) return;   // wave-uniform; the kernel has no barriers
+  const int z = item % WK_BS, tile = item / WK_BS;
+  const int ct = tile % nct, rt = tile / nct, rbase = rt * 32, cbase = ct * 16;
+  const int c0 = z * nch, c1 = min(c0 + nch, Tp / 16);   // this split's 16-deep chunks
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const double *pa[8];
+  int col[4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) pa[f] = At + (int64_t)min(rbase + 4 * f + fi, rows - 1) * Tp + fkc;   // past rows: discarded
+#pragma unroll
+  for (int q = 0; q < 4; ++q) col[q] = min(cbase + 4 * q + fi, N - 1);                         // past N: discarded
+  double acc[8][4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[f][q] = 0.0;
+  // At's columns T..Tp-1 are zero: the k tail reads E's last row (finite)
+  auto load = [&](int c, double (&af)[8], double (&bf)[4]) {
+    const int k = 16 * c;
+    const double *eb = Ep + (int64_t)min(k + fkc, T - 1) * ld;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) af[f] = pa[f][k];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bf[q] = eb[col[q]];
+  };
+  double af[8], bf[4];
+  if (c0 < c1) load(c0, af, bf);
+  for (int c = c0; c < c1; ++c) {
+    double an[8], bn[4];
+    if (c + 1 < c1) load(c + 1, an, bn);
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[f][q] = mfma4(af[f], bf[q], acc[f][q]);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) af[f] = an[f];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bf[q] = bn[q];
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+  double *Bz = Bo + (int64_t)z * rows * N;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa) {
+    const double a0 = acc[fa][0], a1 = acc[fa][1], a2 = acc[fa][2], a3 = acc[fa][3];
+    const double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+    const double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+    const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+    const int row = rbase + 4 * fa + oi, cc = cbase + 4 * blk + oj;
+    if (row < rows && cc < N) Bz[(int64_t)row * N + cc] = v;
+  }
+}
+
 // G[rep] (N x N, row-major, stride N*N) = A0 + L B + (L B)' + unpack(Q[rep]),
 // one workgroup per (lower 32 x 32 tile (I, J), replicate): the L rows and B
 // columns of blocks I and J staged in LDS first (every entry's two r-term
@@ -482,7 +550,7 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
                                                               const double *__restrict__ L,
                                                               const double *__restrict__ Bo,
                                                               const double *__restrict__ Q, int64_t ldk, int N, int r,
-                                                              double *__restrict__ G) {
+                                                              int64_t bstride, double *__restrict__ G) {
   __shared__ double tile[WK_TILE][WK_TILE + 1];
   __shared__ double sLI[WK_TILE][WK_RMAX + 1], sLJ[WK_TILE][WK_RMAX + 1];   // L rows of blocks I, J
   __shared__ double sBI[WK_RMAX][WK_TILE + 1], sBJ[WK_RMAX][WK_TILE + 1];   // B columns of blocks I, J
@@ -501,8 +569,14 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
   }
   for (int e = tid; e < WK_TILE * r; e += 256) {
     const int j = e / WK_TILE, a = e % WK_TILE, nI = I * WK_TILE + a, nJ = J * WK_TILE + a;
-    sBI[j][a] = nI < N ? Br[(int64_t)j * N + nI] : 0.0;
-    sBJ[j][a] = nJ < N ? Br[(int64_t)j * N + nJ] : 0.0;
+    double bi = 0.0, bj = 0.0;   // the split-K partial images, in z order
+#pragma unroll
+    for (int z = 0; z < WK_BS; ++z) {
+      if (nI < N) bi += Br[z * bstride + (int64_t)j * N + nI];
+      if (nJ < N) bj += Br[z * bstride + (int64_t)j * N + nJ];
+    }
+    sBI[j][a] = bi;
+    sBJ[j][a] = bj;
   }
   __syncthreads();
   for (int e = tid; e < WK_TILE * WK_TILE; e += 256) {
@@ -549,14 +623,14 @@ hipError_t gram_wk_precompute(const double *Ep, int64_t ld, int T, int N, int r,
   hipLaunchKernelGGL(gram_wk_a0_kernel, dim3(N), dim3(256), 0, st, F, L, T, N, r, A0);
   return hipGetLastError();
 }
-// workspace doubles for nb replicates: W (nb x Tp), B (nb x r x N), Q (nb x ldk), At (nb x r x Tp)
+// workspace doubles for nb replicates: W (nb x Tp), B (WK_BS x nb x r x N), Q (nb x ldk), At (nb x r x Tp)
 size_t gram_wk_work(int T, int N, int r, int nb) {
-  return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N) + (size_t)r * gram_wk_tp(T));
+  return (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)WK_BS * r * N + (size_t)gram_wk_ldk(N) + (size_t)r * gram_wk_tp(T));
 }
 // the At region (nb r Tp >= nb T r doubles): free once the batch's Grams are
 // formed — the factored F* pass (dfm_model.hip fact_el_kernel) writes E L* there
 double *gram_wk_scratch(double *work, int T, int N, int r, int nb) {
-  return work + (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)r * N + (size_t)gram_wk_ldk(N));
+  return work + (size_t)nb * ((size_t)gram_wk_tp(T) + (size_t)WK_BS * r * N + (size_t)gram_wk_ldk(N));
 }
 // nb replicate Grams X*'X* (N x N each, stride N*N) of src (C + diag(eta) E[idx]).
 hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, const double *F, const double *L,
@@ -564,17 +638,21 @@ hipError_t launch_gram_wk(const double *Ep, int64_t ld, int T, int N, int r, con
                           int nb, double *work, double *G, hipStream_t st) {
   const int Tp = gram_wk_tp(T);
   const int64_t ldk = gram_wk_ldk(N);
-  double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)nb * r * N, *At = Q + (size_t)nb * ldk;
+  double *W = work, *Bo = W + (size_t)nb * Tp, *Q = Bo + (size_t)WK_BS * nb * r * N, *At = Q + (size_t)nb * ldk;
   hipLaunchKernelGGL(gram_wk_prep_kernel, dim3(nb), dim3(256), gram_wk_prep_lds(T, r), st, T, r, F, idx, eta, rs, Tp,
                      W, At);
   // B (nb r x N) = At . E, then Q (nb x ldk) = W K
-  hipError_t e = launch_gemm(false, At, Tp, Ep, ld, Bo, N, nb * r, N, T, st, nullptr, 1, false, nullptr, nullptr);
-  if (e != hipSuccess) return e;
-  e = launch_gemm(false, W, Tp, K, ldk, Q, ldk, nb, (int)ldk, T, st, nullptr, 1, true, nullptr, nullptr);
+  {
+    const int rows = nb * r, nch = (Tp / 16 + WK_BS - 1) / WK_BS;
+    const int64_t items = (int64_t)((rows + 31) / 32) * ((N + 15) / 16) * WK_BS;
+    hipLaunchKernelGGL(gram_wk_b_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, st, At, Tp, Ep, ld, T, N,
+                       rows, nch, Bo);
+  }
+  hipError_t e = launch_gemm(false, W, Tp, K, ldk, Q, ldk, nb, (int)ldk, T, st, nullptr, 1, true, nullptr, nullptr);
   if (e != hipSuccess) return e;
   const int nt = (N + WK_TILE - 1) / WK_TILE;
   hipLaunchKernelGGL(gram_wk_combine_kernel, dim3(nt * (nt + 1) / 2, nb), dim3(256), 0, st, A0, L, Bo, Q, ldk, N, r,
-                     G);
+                     (int64_t)nb * r * N, G);
   return hipGetLastError();
 }
 
