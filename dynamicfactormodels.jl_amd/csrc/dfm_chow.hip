@@ -198,7 +198,10 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
                                                        double *__restrict__ LR,
                                                        double *__restrict__ LM,
                                                        double *__restrict__ WD) {
-  constexpr int TR = 64;
+#ifndef DFM_CH_TR   // (A/B builds: rows per staged tile)
+#define DFM_CH_TR 128
+#endif
+  constexpr int TR = DFM_CH_TR;
   // rows whose gathered values are in flight together: 16, or 8 at R = 8,
   // whose per-variable state (36 HC0 sums, four R-vectors of coefficients)
   // already fills most of the 2-wave register budget.  The launch bound keeps
@@ -291,9 +294,16 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   load_l(0);
   int cb = 0, next = BRK ? blk.a[1] : T;
   // ---- pass A: g_j = F_j' x^(j), e2 = ||x - F l||^2 (BRK: cx = sum_{t>=bp} f_t e_t)
-  double g1[R], g2[R], cx[R], cf[R], e2 = 0.0;
+  // gc: the accumulator of the current side — g1's until the first batch
+  // wholly at or after bp, then (g1 saved) g2's — so the all-pre and all-post
+  // batches share one loop body with no branch; only the one mixed batch
+  // selects per row.  (One per-row if / else over the three cases compiled
+  // to a divergent branch whose arms shuttled g1 / g2 through ~15 register
+  // copies per row.)  Same sums in the same order.
+  double g1[R], g2[R], gc[R], cx[R], cf[R], e2 = 0.0;
+  bool post_a = false;
 #pragma unroll
-  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; cx[j] = 0.0; cf[j] = 0.0; }
+  for (int j = 0; j < R; ++j) { g1[j] = 0.0; g2[j] = 0.0; gc[j] = 0.0; cx[j] = 0.0; cf[j] = 0.0; }
   for (int t0 = 0; t0 < T; t0 += TR) {
     __syncthreads();
     stage(t0);
@@ -303,46 +313,84 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     // CU rows per round: every row's gathered x loaded before the sums (CU
     // loads in flight per thread).  (Prefetching the next round's rows into a
     // second register set was measured: at 3 waves per SIMD it spills, and a
-    // copy between the sets waits for the prefetched loads.)  A batch wholly
-    // before or after bp (every lane: the wave votes) takes a form without
-    // the per-row subperiod branch.  Same operations per row.
+    // copy between the sets waits for the prefetched loads.)
     for (int rb = ks; rb < tn; rb += KS * CU) {
       double xs[CU];
       load_rows(t0, rb, tn, xs);
       const int side = batch_side(t0, rb, tn);   // wave-uniform
+      if (side == 2 && !post_a) {
 #pragma unroll
-      for (int u = 0; u < CU; ++u) {
-        const int rr = rb + KS * u;
-        if (rr < tn) {   // (a guard, not a break: the loop must unroll)
-        const int t = t0 + rr;
-        if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
-        const double x = xs[u];
-        double fr[R];
+        for (int j = 0; j < R; ++j) { g1[j] = gc[j]; gc[j] = g2[j]; }
+        post_a = true;
+      }
+      if (side == 0) {   // the mixed batch (gc holds g1's sums)
 #pragma unroll
-        for (int j = 0; j < R; ++j) fr[j] = sF[lr][rr * R + j];
-        double ev = x;
+        for (int u = 0; u < CU; ++u) {
+          const int rr = rb + KS * u;
+          if (rr < tn) {   // (a guard, not a break: the loop must unroll)
+          const int t = t0 + rr;
+          if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
+          const double x = xs[u];
+          double fr[R];
 #pragma unroll
-        for (int j = 0; j < R; ++j) ev -= fr[j] * l[j];
-        e2 = fma(ev, ev, e2);
-        if (BRK) {
+          for (int j = 0; j < R; ++j) fr[j] = sF[lr][rr * R + j];
+          double ev = x;
 #pragma unroll
-          for (int j = 0; j < R; ++j) cf[j] = fma(ev, fr[j], cf[j]);
+          for (int j = 0; j < R; ++j) ev -= fr[j] * l[j];
+          e2 = fma(ev, ev, e2);
+          if (BRK) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) cf[j] = fma(ev, fr[j], cf[j]);
+          }
+          if (BRK && t >= bp) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) cx[j] = fma(ev, fr[j], cx[j]);
+          }
+          const bool pre = t < bp;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            const double a1 = fma(x, fr[j], gc[j]), a2 = fma(x, fr[j], g2[j]);
+            gc[j] = pre ? a1 : gc[j];
+            g2[j] = pre ? g2[j] : a2;
+          }
+          }
         }
-        if (BRK && t >= bp) {
+      } else {
 #pragma unroll
-          for (int j = 0; j < R; ++j) cx[j] = fma(ev, fr[j], cx[j]);
-        }
-        // (side != 0: a uniform branch; the mixed batch branches per lane)
-        if (side == 1 || (side == 0 && t < bp)) {
+        for (int u = 0; u < CU; ++u) {
+          const int rr = rb + KS * u;
+          if (rr < tn) {
+          const int t = t0 + rr;
+          if (BRK && t >= next) { while (t >= next) { ++cb; next = blk.a[cb + 1]; } load_l(cb); }
+          const double x = xs[u];
+          double fr[R];
 #pragma unroll
-          for (int j = 0; j < R; ++j) g1[j] = fma(x, fr[j], g1[j]);
-        } else {
+          for (int j = 0; j < R; ++j) fr[j] = sF[lr][rr * R + j];
+          double ev = x;
 #pragma unroll
-          for (int j = 0; j < R; ++j) g2[j] = fma(x, fr[j], g2[j]);
-        }
+          for (int j = 0; j < R; ++j) ev -= fr[j] * l[j];
+          e2 = fma(ev, ev, e2);
+          if (BRK) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) cf[j] = fma(ev, fr[j], cf[j]);
+          }
+          if (BRK && t >= bp) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) cx[j] = fma(ev, fr[j], cx[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < R; ++j) gc[j] = fma(x, fr[j], gc[j]);
+          }
         }
       }
     }
+  }
+  if (post_a) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) g2[j] = gc[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; ++j) g1[j] = gc[j];
   }
   if constexpr (KS > 1) {   // the KS lanes' partial sums, in a fixed order
 #pragma unroll

@@ -693,15 +693,21 @@ __global__ __launch_bounds__(256) void fact_el_kernel(const double *__restrict__
   for (int f = 0; f < 8; ++f)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[f][q] = 0.0;
-  for (int k0 = 0; k0 < N; k0 += 16) {
-    const int n = k0 + fkc;
-    const bool okn = n < N;
-    const int nc = okn ? n : N - 1;   // k tail: A's zero times finite B
-    double af[8], bf[4];
+  // the next 16-deep chunk's loads issue before this chunk's MFMAs; the k
+  // tail (n >= N) reads row N - 1 (finite), zeroed on the A side
+  auto load = [&](int k0, double (&af)[8], double (&bf)[4]) {
+    const int nc = min(k0 + fkc, N - 1);
 #pragma unroll
     for (int f = 0; f < 8; ++f) af[f] = ea[f][nc];
 #pragma unroll
     for (int q = 0; q < 4; ++q) bf[q] = ub[q][(int64_t)nc * k];
+  };
+  double af[8], bf[4];
+  load(0, af, bf);
+  for (int k0 = 0; k0 < N; k0 += 16) {
+    double an[8], bn[4];
+    if (k0 + 16 < N) load(k0 + 16, an, bn);
+    const bool okn = k0 + fkc < N;
 #pragma unroll
     for (int f = 0; f < 8; ++f) af[f] = okn ? af[f] : 0.0;
 #pragma unroll
@@ -710,6 +716,10 @@ __global__ __launch_bounds__(256) void fact_el_kernel(const double *__restrict__
     for (int f = 0; f < 8; ++f)
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[f][q] = mfma4(af[f], bf[q], acc[f][q]);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) af[f] = an[f];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bf[q] = bn[q];
   }
   // the four k-blocks summed and transposed into (row, column) lanes (dfm_gemm.hip's epilogue)
   const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
@@ -739,6 +749,7 @@ __global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, c
   extern __shared__ double fdyn[];
   double *sL = fdyn;                        // N x KM: L* = sqrt(N) U*
   __shared__ double sM[32 * KM];            // rb x k: L' L*
+  __shared__ double sP[256];                // its partial sums
   const int rep = blockIdx.x, tid = threadIdx.x;
   const double sN = sqrt((double)N);
   const double *U = Uk + (int64_t)rep * N * k;
@@ -750,12 +761,23 @@ __global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, c
     Lr[e] = v;
   }
   __syncthreads();
-  // M = L' L* (rb x k): one dot product of length N per entry, in n order
-  for (int e = tid; e < rb * k; e += 256) {
-    const int i = e / k, j = e - i * k;
-    double acc = 0.0;
-    for (int n = 0; n < N; ++n) acc = fma(Lb[(int64_t)n * rb + i], sL[n * KM + j], acc);
-    sM[i * KM + j] = acc;
+  // M = L' L* (rb x k <= 256 entries): np = 256 / (rb k) partial sums per
+  // entry (partial q over n = q, q + np, ...), then summed in q order — a
+  // single thread's N-long chain per entry was most of this kernel's time
+  {
+    const int ne = rb * k, np = 256 / ne, e = tid / np, q = tid - e * np;
+    if (e < ne) {
+      const int i = e / k, j = e - i * k;
+      double acc = 0.0;
+      for (int n = q; n < N; n += np) acc = fma(Lb[(int64_t)n * rb + i], sL[n * KM + j], acc);
+      sP[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < ne) {
+      double acc = 0.0;
+      for (int u = 0; u < np; ++u) acc += sP[tid * np + u];
+      sM[(tid / k) * KM + tid % k] = acc;
+    }
   }
   __syncthreads();
   const int32_t *ix = idx + (int64_t)rep * rs;
