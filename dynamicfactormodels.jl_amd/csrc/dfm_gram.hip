@@ -545,7 +545,10 @@ __global__ __launch_bounds__(256) void gram_wk_b_kernel(const double *__restrict
 // ranges), staged in LDS, and written as tile (I, J) and, transposed,
 // (J, I) — both coalesced, G exactly symmetric.  Same operations in the same
 // order as before (x, y as r-term fma chains, then A0 + (x + y) + Q).
-constexpr int WK_TILE = 32, WK_RMAX = 16;
+#ifndef DFM_WK_TILE   // (A/B builds: combine tile edge)
+#define DFM_WK_TILE 32
+#endif
+constexpr int WK_TILE = DFM_WK_TILE, WK_RMAX = 16;
 __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__restrict__ A0,
                                                               const double *__restrict__ L,
                                                               const double *__restrict__ Bo,
