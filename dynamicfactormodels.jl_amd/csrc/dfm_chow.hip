@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
                                                         double *__restrict__ Z) {
   constexpr int S = 2 * CH_RMAX + 1;
   __shared__ double A1[CH_RMAX * S], A2s[CH_RMAX * S], M[2 * CH_RMAX * S], Mi[2 * CH_RMAX * S],
-      Lw[2 * CH_RMAX * S], Tw[2 * CH_RMAX * S], A1i[CH_RMAX * S], A2i[CH_RMAX * S];
+      Lw[2 * CH_RMAX * S], Tw[2 * CH_RMAX * S], A1i[CH_RMAX * S], A2i[CH_RMAX * S], Lw1[CH_RMAX * S],
+      Tw1[CH_RMAX * S], Lw2[CH_RMAX * S], Tw2[CH_RMAX * S];
   __shared__ int bad;
   const int tid = threadIdx.x, rep = blockIdx.x;
   const double *Fr = F + (int64_t)rep * T * r;
@@ -107,9 +108,15 @@ __global__ __launch_bounds__(256) void chow_prep_kernel(const double *__restrict
     M[a * S + c] = v;
   }
   __syncthreads();
-  block_spd_inverse(M, Mi, Lw, Tw, n2, S, &bad);
-  block_spd_inverse(A1, A1i, Lw, Tw, r, S, &bad);
-  block_spd_inverse(A2s, A2i, Lw, Tw, r, S, &bad);
+  // the three inverses side by side on waves 0..2 (one after another across
+  // the workgroup they were ~40 barriers)
+  {
+    const int wv = tid >> 6;
+    if (wv == 0) wave_spd_inverse(M, Mi, Lw, Tw, n2, S, &bad);
+    else if (wv == 1) wave_spd_inverse(A1, A1i, Lw1, Tw1, r, S, &bad);
+    else if (wv == 2) wave_spd_inverse(A2s, A2i, Lw2, Tw2, r, S, &bad);
+  }
+  __syncthreads();
   double *P = prep + (size_t)rep * CP_NMAT * RC * RC;
   // every entry is written (zeros outside r): the main kernel reads RC x RC blocks
   for (int e = tid; e < RC * RC; e += 256) {

@@ -748,12 +748,19 @@ __global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, c
                                                           double *__restrict__ L, int64_t fstride) {
   extern __shared__ double fdyn[];
   double *sL = fdyn;                        // N x KM: L* = sqrt(N) U*
+  double *sEt = sL + (size_t)N * KM;        // eta_t (T)
+  int *sIx = (int *)(sEt + T);              // idx_t (T)
   __shared__ double sM[32 * KM];            // rb x k: L' L*
   __shared__ double sP[256];                // its partial sums
   const int rep = blockIdx.x, tid = threadIdx.x;
   const double sN = sqrt((double)N);
   const double *U = Uk + (int64_t)rep * N * k;
   double *Lr = L + (int64_t)rep * N * k;
+  {   // the replicate's draws, staged (the gather below then issues its G loads without waiting for idx)
+    const int32_t *ix = idx + (int64_t)rep * rs;
+    const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
+    for (int t = tid; t < T; t += 256) { sIx[t] = ix[t]; sEt[t] = et ? et[t] : 1.0; }
+  }
   for (int e = tid; e < N * k; e += 256) {
     const int n = e / k, j = e - n * k;
     const double v = sN * U[e];
@@ -780,8 +787,6 @@ __global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, c
     }
   }
   __syncthreads();
-  const int32_t *ix = idx + (int64_t)rep * rs;
-  const double *et = eta ? eta + (int64_t)rep * rs : nullptr;
   const double *Gr = G + (int64_t)rep * T * k;
   double *Fr = F + (int64_t)rep * fstride;
   const double invN = 1.0 / N;
@@ -789,7 +794,7 @@ __global__ __launch_bounds__(256) void fact_gather_kernel(int T, int N, int k, c
     const int t = e / k, j = e - t * k;
     double c = 0.0;   // (F (L' L*))[t][j]
     for (int i = 0; i < rb; ++i) c = fma(Fb[(int64_t)t * rb + i], sM[i * KM + j], c);
-    const double x = fma(et ? et[t] : 1.0, Gr[(int64_t)ix[t] * k + j], c);
+    const double x = fma(sEt[t], Gr[(int64_t)sIx[t] * k + j], c);
     Fr[(int64_t)t * k + j] = x * invN;
   }
 }
@@ -799,7 +804,7 @@ bool launch_factors_cols_fact(const double *Ep, int64_t ld, int T, int N, int k,
                               int rb, const int32_t *idx, const double *eta, int64_t rs, int nb, const double *Uk,
                               double *F, double *L, int64_t fstride, double *G, hipStream_t st) {
   if (k < 1 || k > 8 || rb < 1 || rb > 32 || T < 1 || N < 1) return false;
-  const size_t lds = (size_t)N * 8 * 8;
+  const size_t lds = (size_t)N * 8 * 8 + (size_t)T * 12;
   if (lds > 64 * 1024) return false;
   const int64_t tiles = (int64_t)((T + 31) / 32) * (((int64_t)nb * k + 15) / 16);
   hipLaunchKernelGGL(fact_el_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, Ep, ld, T, N, k, nb, Uk, G);

@@ -44,4 +44,44 @@ DFM_DEV void block_spd_inverse(const double *A, double *Ai, double *Lw, double *
   __syncthreads();
 }
 
+// block_spd_inverse on ONE wave (lanes, no barriers: every LDS write is
+// waited for before the lanes that read it issue their reads) — the same
+// operations in the same order, so several small inverses run side by side
+// on different waves of a workgroup.
+DFM_DEV void wave_spd_inverse(const double *A, double *Ai, double *Lw, double *Tw, int n, int S, int *bad) {
+  const int lane = threadIdx.x & 63;
+  auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  for (int e = lane; e < n * S; e += 64) Lw[e] = 0.0;
+  sync();
+  for (int j = 0; j < n; ++j) {
+    if (lane == 0) {
+      double s = A[j * S + j];
+      for (int p = 0; p < j; ++p) s -= Lw[j * S + p] * Lw[j * S + p];
+      if (!(s > 0.0)) { *bad = 1; s = 1.0; }
+      Lw[j * S + j] = sqrt(s);
+    }
+    sync();
+    for (int i = j + 1 + lane; i < n; i += 64) {
+      double s = A[i * S + j];
+      for (int p = 0; p < j; ++p) s -= Lw[i * S + p] * Lw[j * S + p];
+      Lw[i * S + j] = s / Lw[j * S + j];
+    }
+    sync();
+  }
+  for (int c = lane; c < n; c += 64)
+    for (int i = 0; i < n; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int p = c; p < i; ++p) s -= Lw[i * S + p] * Tw[p * S + c];
+      Tw[i * S + c] = i < c ? 0.0 : s / Lw[i * S + i];
+    }
+  sync();
+  for (int e = lane; e < n * n; e += 64) {
+    const int a = e / n, c = e % n;
+    double s = 0.0;
+    for (int p = (a > c ? a : c); p < n; ++p) s = fma(Tw[p * S + a], Tw[p * S + c], s);
+    Ai[a * S + c] = s;
+  }
+  sync();
+}
+
 }  // namespace dfm
