@@ -565,6 +565,17 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
   const double *Br = Bo + (int64_t)rep * r * N;
   const double *Qr = Q + (int64_t)rep * ldk;
   double *Gr = G + (int64_t)rep * N * N;
+  // this thread's A0 and Q entries, loaded before the staging below (their
+  // latency overlaps it instead of following the barrier)
+  constexpr int EPT = WK_TILE * WK_TILE / 256;
+  double a0v[EPT], qv[EPT];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = tid + 256 * u, a = e / WK_TILE, b = e % WK_TILE, n = I * WK_TILE + a, m = J * WK_TILE + b;
+    const bool in = n < N && m <= n;
+    a0v[u] = in ? A0[(int64_t)n * N + m] : 0.0;
+    qv[u] = in ? Qr[(int64_t)n * (n + 1) / 2 + m] : 0.0;
+  }
   for (int e = tid; e < WK_TILE * r; e += 256) {
     const int a = e / r, j = e % r, nI = I * WK_TILE + a, nJ = J * WK_TILE + a;
     sLI[a][j] = nI < N ? L[(int64_t)nI * r + j] : 0.0;
@@ -582,8 +593,9 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
     sBJ[j][a] = bj;
   }
   __syncthreads();
-  for (int e = tid; e < WK_TILE * WK_TILE; e += 256) {
-    const int a = e / WK_TILE, b = e % WK_TILE, n = I * WK_TILE + a, m = J * WK_TILE + b;
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = tid + 256 * u, a = e / WK_TILE, b = e % WK_TILE, n = I * WK_TILE + a, m = J * WK_TILE + b;
     double v = 0.0;
     if (n < N && m <= n) {
       double x = 0.0, y = 0.0;   // x: L[n] . B[:, m],  y: L[m] . B[:, n]
@@ -591,7 +603,7 @@ __global__ __launch_bounds__(256) void gram_wk_combine_kernel(const double *__re
         x = fma(sLI[a][j], sBJ[j][b], x);
         y = fma(sLJ[b][j], sBI[j][a], y);
       }
-      v = (A0[(int64_t)n * N + m] + (x + y)) + Qr[(int64_t)n * (n + 1) / 2 + m];
+      v = (a0v[u] + (x + y)) + qv[u];
     }
     tile[a][b] = v;
   }
