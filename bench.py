@@ -4,9 +4,16 @@
 
 A step = one complete B=9999-replicate wild-bootstrap job on each GPU
 (src/bootstrap.jl:41-51: per replicate resample X* = F_r L_r' + diag(eta)
-E[idx,:], refit the DFM at r = 8 — Gram, top-8 eigenpairs, factors and
-loadings, OLS + HC2 — and evaluate the stats V(8) and ICp2), followed by the
-RCCL all-gather of the per-replicate statistics (N > 1).  Replicates shard
+E[idx,:], refit the DFM at r = 8 and evaluate the stats V(8) and ICp2),
+followed by the RCCL all-gather of the per-replicate statistics (torchrun).
+What the refit forms is demand-driven: V(8) and ICp2 read only the top-8
+eigenvalues of X*X*' and its trace (src/criteria.jl:5, :35-46), so the timed
+job runs the eigensolve (factored identity: H.Z GEMMs + per-replicate
+Rayleigh-Ritz, Kato-Temple eigenvalue stopping rule) and does NOT form the
+replicate factors F*, loadings L* or the OLS + HC2 regression.  The line's
+`all_fields` extra (timed separately, after the headline region) is the rate
+with the whole regression record per replicate — F*, L*, all OLS
+coefficients and HC2 t-statistics (src/DynamicFactorModel.jl:28-51).  Replicates shard
 across ranks (strong scaling, as BASELINE.json configs[2] states: the 9999
 replicates of a step are sharded contiguously over the ranks, replicate b on
 rank floor(b N / B); a weak-scaling extra field reruns with 9999 per rank).  Inputs (the fitted base model and every replicate's idx/eta) are
@@ -236,8 +243,9 @@ def main():
                     help="c5: rolling windows of this many rows instead of expanding windows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling extra field (N > 1)")
-    ap.add_argument("--all-fields", action="store_true",
-                    help="also time the job with the whole regression record per replicate (F*, L*, OLS formed)")
+    ap.add_argument("--no-all-fields", action="store_true",
+                    help="skip the all_fields extra (the job with the whole regression record per replicate: F*, "
+                         "L*, OLS formed) — for rocprofv3 runs whose trace must hold the headline launches only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -246,7 +254,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # launched by torchrun (any N, N = 1 included): one rank per GPU over RCCL,
+    # the per-replicate rows all-gathered on the device; a plain `python
+    # bench.py` (the driver's N = 1 run) has no process group
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -299,11 +310,11 @@ def main():
         if nloc:
             ctx.check(ctx.lib.dfm_bootstrap_dev(model.handle, 0, nloc, idx_d[s].data_ptr(),
                                                 eta_d[s].data_ptr(), arr, len(stats), out.data_ptr()))
-        holder["rows"] = gather_rows(out[:nloc], Bn) if world > 1 else out
+        holder["rows"] = gather_rows(out[:nloc], Bn) if dist is not None else out
 
     def timed(fn, first, count):
         """Barrier + sync on both sides of `count` steps; max over ranks."""
-        if world > 1:
+        if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -311,10 +322,10 @@ def main():
             fn(s)
         ctx.synchronize()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist is not None:
             dist.barrier()
         el = time.perf_counter() - t0
-        if world > 1:
+        if dist is not None:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -357,11 +368,12 @@ def main():
     # L* and the OLS pass run too.  The headline stats (V + ICp2) read only
     # the eigenvalues and the trace, and the library forms only the fields the
     # requested statistics read (include/dfm.h).
-    # Opt-in (--all-fields): the default command's rocprofv3 trace then holds
-    # only the headline job's launches, so its H.Z GEMM average agrees with
-    # the HIP-event roofline of the same run.
+    # Timed after the headline region (its own barrier-bracketed steps);
+    # `--no-all-fields` leaves it out so a rocprofv3 trace holds only the
+    # headline job's launches (its H.Z GEMM average then agrees with the
+    # HIP-event roofline of the same run).
     full = None
-    if args.all_fields and world == 1 and nloc:
+    if not args.no_all_fields and world == 1 and nloc:
         fstats = stats + [D.Stat.coefficient(j) for j in range(1, R + 2)] + [D.Stat.t_stat(j) for j in range(1, R + 2)]
         farr = D.api._stat_array(fstats)
         fwidth = int(ctx.lib.dfm_stats_width(model.handle, farr, len(fstats)))
@@ -378,7 +390,7 @@ def main():
                 "steps": fk}
         del fout
     res = holder["rows"].cpu().numpy()
-    ok = bool(np.all(np.isfinite(res))) and res.shape[0] >= Bn if world > 1 else bool(np.all(np.isfinite(res)))
+    ok = bool(np.all(np.isfinite(res))) and res.shape[0] >= Bn if dist is not None else bool(np.all(np.isfinite(res)))
 
     total = Bn * args.steps
     value = total / el
@@ -434,6 +446,8 @@ def main():
         "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
         "outputs_finite": ok,
+        "collective": (f"RCCL all-gather of the per-replicate rows over {world} rank(s) "
+                       f"({dist.get_backend()})" if dist is not None else "none (single process, no process group)"),
         "mode": args.mode,
         "stopping_rule": "eigenvector residual (strict)" if args.strict else
                          "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
@@ -443,8 +457,8 @@ def main():
                        "[0, theta_p] after later ones"),
         "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps),
         "fields_formed": "eigenvalues + trace: V and ICp2 read nothing else, so the replicate factors, loadings "
-                         "and OLS are not formed (demand-driven; `bench.py --all-fields` adds the full record's "
-                         "rate: profiles/r04_bench_all_fields.json)",
+                         "and OLS are not formed (demand-driven); the all_fields extra is the rate with the whole "
+                         "regression record (F*, L*, OLS + HC2) formed per replicate",
     }
     if full:
         rec["all_fields"] = full
@@ -454,7 +468,7 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.destroy_process_group()
 
 
@@ -493,14 +507,14 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
             res = D.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=w1 - w0, kmax=km,
                                                     rows=rows, ctx=ctx)
         loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, 1)).to(dev)
-        holder["all"] = gather_rows(loc, P5) if world > 1 else loc
+        holder["all"] = gather_rows(loc, P5) if dist is not None else loc
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     ctx.reset_timing()
     ctx.enable_timing(True)
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -508,12 +522,12 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
         step()
     ctx.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
     ctx.enable_timing(False)
     timing = ctx.read_timing()
-    if world > 1:
+    if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -547,7 +561,7 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     }
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.destroy_process_group()
 
 

@@ -493,7 +493,18 @@ class ReplicateFit:
     (``src/DynamicFactorModel.jl:6-25``) follow from them and the draw:
     ``x`` = the replicate panel X*_b = C + diag(eta_b) E[idx_b] (as
     ``:43-46``), ``factor_residuals`` = X*_b - vcat(F_j L_j'), ``residuals`` =
-    y - [w F] coefficients — built lazily."""
+    y - [w F] coefficients, ``coefficient_covariance`` = the HC2 sandwich of
+    ``:43-46`` from the design matrix and those residuals — built lazily;
+    ``targeted_predictors`` is the base fit's mask (the replicate refit keeps
+    it, ``src/bootstrap.jl:36``, ``:48``).
+
+    ``eigenvalues`` (an extension: the reference record has no eigenvalue
+    field) holds the replicate's top r eigenvalues only — the replicate's
+    subspace solve never forms the rest of the spectrum, unlike the base fit's
+    ``eigenvalues`` — and, for a model with breaks, their sum over the break
+    blocks (what V(r) needs); ``block_eigenvalues`` is ``[eigenvalues]``
+    without breaks and ``None`` with breaks (per-block values are not
+    returned by the replicate path)."""
 
     def __init__(self, base, xs, ev, V, crit_value, coef, tstat, F, Ls):
         self._base, self._xs = base, xs
@@ -503,7 +514,9 @@ class ReplicateFit:
         self.break_indices = base.break_indices
         self.factor_type = base.factor_type
         self.number_of_factor_lags = 0
+        self.targeted_predictors = getattr(base, "targeted_predictors", None)
         self.eigenvalues = ev
+        self.block_eigenvalues = [ev] if len(base.factors) == 1 else None
         self.V = V
         self.number_of_factors_criterion_value = crit_value
         self.coefficients, self.t_stats = coef, tstat
@@ -537,6 +550,15 @@ class ReplicateFit:
     @property
     def residuals(self) -> np.ndarray:
         return self.y - self.design_matrix @ self.coefficients
+
+    @property
+    def coefficient_covariance(self) -> np.ndarray:
+        """``src/DynamicFactorModel.jl:43-46``: inv(D'D) D' diagm(u^2 / (1 - h)) D inv(D'D)."""
+        D = self.design_matrix
+        Ai = np.linalg.inv(D.T @ D)
+        h = np.einsum("ij,jk,ik->i", D, Ai, D)
+        s2 = self.residuals ** 2 / (1.0 - h)
+        return Ai @ ((D.T * s2) @ D) @ Ai
 
 
 _CLOSURE_CHUNK_BYTES = 500_000_000   # host rows per device call of the closure path

@@ -168,7 +168,37 @@ struct dfm_ctx {
   char *warena = nullptr;
   size_t warena_cap = 0, warena_need = 0;
   hipEvent_t gate = nullptr;   // bootstrap_lanes: the second lane starts behind the caller's prior work
+  hipMemPool_t mpool = nullptr;  // this context's stream-ordered scratch (stream_malloc)
 };
+
+// stream -> the owning context's pool (stream_malloc); guarded: contexts are
+// created, re-streamed and destroyed from any host thread
+static std::mutex g_pool_mu;
+static std::vector<std::pair<hipStream_t, hipMemPool_t>> g_pools;
+static void pool_register(hipStream_t st, hipMemPool_t pool) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  for (auto &e : g_pools)
+    if (e.first == st) { e.second = pool; return; }
+  g_pools.emplace_back(st, pool);
+}
+static void pool_unregister(hipMemPool_t pool) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  g_pools.erase(std::remove_if(g_pools.begin(), g_pools.end(), [&](const auto &e) { return e.second == pool; }),
+                g_pools.end());
+}
+namespace dfm {
+hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st) {
+  hipMemPool_t pool = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    for (auto &e : g_pools)
+      if (e.first == st) { pool = e.second; break; }
+  }
+  const hipError_t e = pool ? hipMallocFromPoolAsync(p, bytes, pool, st) : hipMallocAsync(p, bytes, st);
+  if (e == hipSuccess) DFM_POISON_ASYNC(*p, bytes, st);
+  return e;
+}
+}  // namespace dfm
 
 // The host thread of a model's second bootstrap lane (bootstrap_lanes):
 // persistent, so a call costs a hand-off, not a thread start.
@@ -345,7 +375,11 @@ static double crit_formula(int crit, double V, int k, double sigma2, int T, int 
 }
 
 template <class T>
-static hipError_t dalloc(T **p, size_t n) { return hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)); }
+static hipError_t dalloc(T **p, size_t n) {
+  const hipError_t e = hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+  if (e == hipSuccess) DFM_POISON_SYNC(*p, std::max<size_t>(n, 1) * sizeof(T));
+  return e;
+}
 
 extern "C" {
 
@@ -365,12 +399,21 @@ int dfm_ctx_create(int device, dfm_ctx **out) {
     delete c;
     return -4;
   }
-  {   // stream-ordered scratch (split-K Gram partials) stays mapped between calls
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  {   // stream-ordered scratch (split-K Gram partials, eigen workspaces) from
+      // the context's own pool, kept mapped between calls
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    uint64_t keep = UINT64_MAX;
+    if (hipMemPoolCreate(&c->mpool, &props) == hipSuccess) {
+      hipMemPoolSetAttribute(c->mpool, hipMemPoolAttrReleaseThreshold, &keep);
+      pool_register(c->stream, c->mpool);
+    } else {
+      c->mpool = nullptr;   // the default pool then serves this context (stream_malloc's fallback)
     }
+    hipMemPool_t dp;
+    if (hipDeviceGetDefaultMemPool(&dp, device) == hipSuccess) hipMemPoolSetAttribute(dp, hipMemPoolAttrReleaseThreshold, &keep);
   }
   *out = c;
   return 0;
@@ -392,6 +435,10 @@ static void ctx_release(dfm_ctx *ctx) {
   hipFree(ctx->cnt_dev);
   hipFree(ctx->warena);
   if (ctx->gate) hipEventDestroy(ctx->gate);
+  if (ctx->mpool) {
+    pool_unregister(ctx->mpool);
+    hipMemPoolDestroy(ctx->mpool);
+  }
   if (ctx->own) hipStreamDestroy(ctx->own);
   delete ctx;
 }
@@ -400,7 +447,9 @@ const char *dfm_last_error(const dfm_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int dfm_ctx_set_stream(dfm_ctx *ctx, void *s) {
   if (!ctx) return -1;
+  if (ctx->mpool) pool_unregister(ctx->mpool);
   ctx->stream = s ? (hipStream_t)s : ctx->own;
+  if (ctx->mpool) pool_register(ctx->stream, ctx->mpool);
   return 0;
 }
 int dfm_ctx_synchronize(dfm_ctx *ctx) {
@@ -515,6 +564,83 @@ struct DevBuf {
   ~DevBuf() { hipFree(p); }
 };
 
+#ifdef DFM_DEBUG_MEM
+// Debug build: a device buffer inside 64 KB guard bands of 0xA5 bytes, its
+// body poisoned (0xFF).  check() reports guard bytes that changed (offsets
+// relative to the body: negative = the front band) and, given the host copy
+// the body was loaded from, body rows that no longer match it (row = `rowb`
+// bytes: a replicate's draws).
+struct GuardBuf {
+  static constexpr size_t kG = 65536;
+  char *raw = nullptr;
+  void *p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t bytes) {
+    n = std::max<size_t>(bytes, 8);
+    hipError_t e = hipMalloc((void **)&raw, n + 2 * kG);
+    if (e != hipSuccess) return e;
+    (void)hipMemset(raw, 0xA5, kG);
+    (void)hipMemset(raw + kG, 0xFF, n);
+    (void)hipMemset(raw + kG + n, 0xA5, kG);
+    (void)hipDeviceSynchronize();
+    p = raw + kG;
+    return hipSuccess;
+  }
+  int check(const char *name, const void *host, int64_t rowb) {
+    if (!raw) return 0;
+    std::vector<unsigned char> h(n + 2 * kG);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(h.data(), raw, h.size(), hipMemcpyDeviceToHost);
+    int bad = 0;
+    int64_t first = 0, last = 0, cnt = 0;
+    for (size_t i = 0; i < h.size(); ++i) {
+      if (i >= kG && i < kG + n) continue;
+      if (h[i] != 0xA5) {
+        const int64_t o = (int64_t)i - (int64_t)kG;
+        if (!cnt) first = o;
+        last = o;
+        ++cnt;
+      }
+    }
+    if (cnt) {
+      fprintf(stderr, "[dfm debug] %s: %lld guard bytes changed, body offsets %lld .. %lld (body %zu bytes)\n", name,
+              (long long)cnt, (long long)first, (long long)last, n);
+      ++bad;
+    }
+    if (host && rowb > 0) {
+      const unsigned char *b = h.data() + kG, *q = (const unsigned char *)host;
+      int64_t nrow = (int64_t)n / rowb, rbad = 0, r0 = -1, r1 = -1;
+      for (int64_t r = 0; r < nrow; ++r)
+        if (memcmp(b + r * rowb, q + r * rowb, (size_t)rowb) != 0) {
+          if (r0 < 0) r0 = r;
+          r1 = r;
+          ++rbad;
+        }
+      if (rbad) {
+        fprintf(stderr, "[dfm debug] %s: %lld of %lld rows changed on the device during the call (rows %lld .. %lld)\n",
+                name, (long long)rbad, (long long)nrow, (long long)r0, (long long)r1);
+        ++bad;
+      }
+    }
+    hipFree(raw);
+    raw = nullptr;
+    return bad;
+  }
+  ~GuardBuf() { if (raw) hipFree(raw); }
+};
+// DFM_LANE_SKEW_US (debug build): hold one bootstrap lane back this long on the
+// device (> 0: the second lane, < 0: the caller's), so a cross-lane ordering
+// hazard shows up deterministically instead of at the mercy of scheduling
+__global__ void dbg_spin_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+static int dbg_lane_skew_us() {
+  const char *e = getenv("DFM_LANE_SKEW_US");
+  return e ? atoi(e) : 0;
+}
+#endif
+
 // ---------------------------------------------------------------- internals
 // Top-k eigen-decomposition of nb Grams + trace; G workspace provided.
 static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const double *warm, int kw,
@@ -538,7 +664,7 @@ static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const do
   const int P = p <= 16 ? 16 : 32;
   const size_t bytes = eig_workspace_bytes_padded(m, nb, P, ctx->maxit);
   char *ws = nullptr;   // stream-ordered pool memory: no device-wide sync in the free
-  HIPCHK(ctx, hipMallocAsync((void **)&ws, bytes, ctx->stream));
+  HIPCHK(ctx, stream_malloc((void **)&ws, bytes, ctx->stream));
   // a single fit's eigenvectors are polished to the rounding floor (the
   // residual rule at 1e-14; the floor and stagnation tests end it): statistics
   // of the fit with a near-zero value (an LR of ~0.4 between two nearly equal
@@ -1114,6 +1240,13 @@ static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx
   if (!ctx->gate) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->gate, hipEventDisableTiming));
   HIPCHK(ctx, hipEventRecord(ctx->gate, ctx->stream));
   HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ctx->gate, 0));
+#ifdef DFM_DEBUG_MEM
+  if (const int sk = dbg_lane_skew_us()) {   // wall clock: 100 ticks per microsecond
+    hipLaunchKernelGGL(dbg_spin_kernel, dim3(1), dim3(64), 0, sk > 0 ? lc->stream : ctx->stream,
+                       (long long)std::abs(sk) * 100);
+    fprintf(stderr, "[dfm debug] lane skew %d us\n", sk);
+  }
+#endif
   const int64_t width = dfm_stats_width(M, stats, ns), T = M->T, h = (B + 1) / 2;
   int rc1 = 0;
   M->lane_worker->run([&]() {
@@ -1299,7 +1432,15 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
   if (need > M->ws_bytes) {
     hipFree(M->ws);
     M->ws = nullptr; M->ws_bytes = 0;
+#ifdef DFM_DEBUG_MEM
+    // debug build: a 64 KB guard band of 0xA5 after the workspace, checked at the end of the call
+    HIPCHK(ctx, hipMalloc(&M->ws, need + GuardBuf::kG));
+    DFM_POISON_SYNC(M->ws, need);
+    (void)hipMemset(M->ws + need, 0xA5, GuardBuf::kG);
+    (void)hipStreamSynchronize(nullptr);
+#else
     HIPCHK(ctx, hipMalloc(&M->ws, need));
+#endif
     M->ws_bytes = need;
   }
   if (ns > M->sd_cap) {
@@ -1509,6 +1650,21 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
   int flag = 0;
   HIPCHK(ctx, hipMemcpyAsync(&flag, M->flag_dev, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+#ifdef DFM_DEBUG_MEM
+  {
+    std::vector<unsigned char> g(GuardBuf::kG);
+    (void)hipMemcpy(g.data(), M->ws + M->ws_bytes, g.size(), hipMemcpyDeviceToHost);
+    int64_t cnt = 0, first = -1;
+    for (size_t i = 0; i < g.size(); ++i)
+      if (g[i] != 0xA5) { if (first < 0) first = (int64_t)i; ++cnt; }
+    if (cnt) {
+      fprintf(stderr, "[dfm debug] bootstrap workspace (%s, %zu bytes, batch %lld): %lld guard bytes written past "
+              "its end, first at +%lld\n", M->is_lane ? "lane" : "main", M->ws_bytes, (long long)nb, (long long)cnt,
+              (long long)first);
+      return fail(ctx, 9001, "debug build: bootstrap workspace overrun");
+    }
+  }
+#endif
   if (flag & 1) return fail(ctx, 2, "eigensolver did not converge for some replicate");
   if (flag & 2) return fail(ctx, 3, "singular design matrix in some replicate");
   return 0;
@@ -1527,16 +1683,34 @@ int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const d
   const int64_t width = dfm_stats_width(M, stats, ns);
   int32_t *di = nullptr;
   double *de = nullptr, *dout = nullptr;
+#ifdef DFM_DEBUG_MEM
+  // debug build: the draws and the output rows inside guard bands, checked
+  // (with the draws themselves) after the call
+  GuardBuf gi, ge, go;
+  HIPCHK(ctx, gi.alloc((size_t)B * M->T * 4));
+  if (eta) HIPCHK(ctx, ge.alloc((size_t)B * M->T * 8));
+  HIPCHK(ctx, go.alloc((size_t)B * std::max<int64_t>(width, 1) * 8));
+  di = (int32_t *)gi.p; de = (double *)ge.p; dout = (double *)go.p;
+#else
   HIPCHK(ctx, dalloc(&di, (size_t)B * M->T));
   if (eta) HIPCHK(ctx, dalloc(&de, (size_t)B * M->T));
   HIPCHK(ctx, dalloc(&dout, (size_t)B * std::max<int64_t>(width, 1)));
+#endif
   HIPCHK(ctx, hipMemcpyAsync(di, idx, (size_t)B * M->T * 4, hipMemcpyHostToDevice, st));
   if (eta) HIPCHK(ctx, hipMemcpyAsync(de, eta, (size_t)B * M->T * 8, hipMemcpyHostToDevice, st));
   int rc = dfm_bootstrap_dev(M, kind, B, di, kind == DFM_BOOT_WILD ? de : nullptr, stats, ns, dout);
   if (rc == 0 && width > 0)
     rc = hipMemcpyAsync(out, dout, (size_t)B * width * 8, hipMemcpyDeviceToHost, st) == hipSuccess ? 0 : 1001;
   hipStreamSynchronize(st);
+#ifdef DFM_DEBUG_MEM
+  {
+    const int bad = gi.check("idx", idx, M->T * 4) + (eta ? ge.check("eta", eta, M->T * 8) : 0) +
+                    go.check("out", nullptr, width * 8);
+    if (bad && rc == 0) rc = fail(ctx, 9001, "debug build: %d guard / input violations (stderr)", bad);
+  }
+#else
   hipFree(di); hipFree(de); hipFree(dout);
+#endif
   return rc;
 }
 
@@ -1559,11 +1733,11 @@ int upload_panel(dfm_ctx *ctx, const double *X, int T, int N, int64_t ldx, DevPa
   hipStream_t st = ctx->stream;
   dp.ld = round_up(N, 16);
   dp.st = st;
-  HIPCHK(ctx, hipMallocAsync((void **)&dp.P, (size_t)T * dp.ld * 8, st));
+  HIPCHK(ctx, stream_malloc((void **)&dp.P, (size_t)T * dp.ld * 8, st));
   const double *src = X;
   int64_t lds = ldx;
   if (!dev) {
-    HIPCHK(ctx, hipMallocAsync((void **)&dp.raw, (size_t)T * N * 8, st));
+    HIPCHK(ctx, stream_malloc((void **)&dp.raw, (size_t)T * N * 8, st));
     HIPCHK(ctx, hipMemcpy2DAsync(dp.raw, (size_t)T * 8, X, (size_t)ldx * 8, (size_t)T * 8, N,
                                  hipMemcpyHostToDevice, st));
     src = dp.raw;
@@ -2082,7 +2256,7 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
     aneed += b;
     if (aoff + b <= ctx->warena_cap) { void *ptr = ctx->warena + aoff; aoff += b; return ptr; }
     void *ptr = nullptr;
-    if (hipMallocAsync(&ptr, b, st) != hipSuccess) return nullptr;
+    if (stream_malloc(&ptr, b, st) != hipSuccess) return nullptr;
     frees.push_back(ptr);
     return ptr;
   };
@@ -2517,12 +2691,19 @@ extern "C" int dfm_model_clone(const dfm_model *S, dfm_ctx *ctx, dfm_model **out
   M->trace = S->trace; M->V = S->V; M->critval = S->critval; M->sigma2 = S->sigma2;
   M->batch = S->batch; M->mode = S->mode;
   M->nblk = S->nblk; M->ba = S->ba; M->bt = S->bt; M->bm = S->bm; M->blam = S->blam;
-  // device-to-device (peer) copies: no staging through host memory
+  // device-to-device (peer) copies: no staging through host memory.  They are
+  // issued on the NEW context's stream and completed before the clone is
+  // returned: hipMemcpyPeer would run them on the legacy null stream, which
+  // returns before a device-to-device copy lands and which the context's
+  // non-blocking stream does not wait for — round 4's intermittent wrong
+  // two-lane rows were the second lane's first kernels (H = E E', EL = E L,
+  // F S F', the warm start) reading a partly copied fit
+  // (tests/test_gpu_multi.py::test_clone_is_complete_before_its_first_bootstrap)
   auto dup = [&](const double *src, size_t n, double **dst) -> int {
     hipSetDevice(ctx->device);
     if (dalloc(dst, n) != hipSuccess) return 1;
     if (!src || n == 0) return 0;
-    return hipMemcpyPeer(*dst, ctx->device, src, sc->device, n * 8) == hipSuccess ? 0 : 1;
+    return hipMemcpyPeerAsync(*dst, ctx->device, src, sc->device, n * 8, ctx->stream) == hipSuccess ? 0 : 1;
   };
   const size_t T = S->T, N = S->N, r = S->r, panel = T * S->ld;
   int bad = 0;
@@ -2544,6 +2725,7 @@ extern "C" int dfm_model_clone(const dfm_model *S, dfm_ctx *ctx, dfm_model **out
   M->L = M->Lall;
   hipSetDevice(ctx->device);
   if (!bad) bad = dalloc(&M->flag_dev, 4) != hipSuccess;
+  if (!bad) bad = hipStreamSynchronize(ctx->stream) != hipSuccess;   // every copy landed
   if (bad) {
     dfm_model_destroy(M);
     return fail(ctx, 1002, "dfm_model_clone: device copy failed");

@@ -52,6 +52,31 @@ DFM_DEV double hash_unit(uint64_t a, uint64_t b, uint64_t c) {
   return (double)(x >> 11) * (1.0 / 9007199254740992.0) - 0.5;
 }
 
+// Debug build (csrc Makefile EXTRA=-DDFM_DEBUG_MEM, never the production
+// library): every fresh device allocation is filled with 0xFF bytes — NaN
+// doubles, -1 ints — so a read of memory no kernel of the call wrote shows up
+// as NaN / an out-of-range index deterministically instead of as stale data.
+#ifdef DFM_DEBUG_MEM
+inline void dbg_poison_sync(void *p, size_t bytes) {   // null stream only: the contexts' (non-blocking) streams run on
+  if (p && bytes) { (void)hipMemset(p, 0xFF, bytes); (void)hipStreamSynchronize(nullptr); }
+}
+inline void dbg_poison_async(void *p, size_t bytes, hipStream_t st) {
+  if (p && bytes) (void)hipMemsetAsync(p, 0xFF, bytes, st);
+}
+#define DFM_POISON_SYNC(p, b) ::dfm::dbg_poison_sync((void *)(p), (size_t)(b))
+#define DFM_POISON_ASYNC(p, b, st) ::dfm::dbg_poison_async((void *)(p), (size_t)(b), (st))
+#else
+#define DFM_POISON_SYNC(p, b) ((void)0)
+#define DFM_POISON_ASYNC(p, b, st) ((void)0)
+#endif
+
+// Stream-ordered scratch from the pool of the context that owns `st` (each
+// dfm_ctx has its own hipMemPool: a block freed on one context's stream is
+// never handed to another context's stream — the two bootstrap lanes of a
+// model, dfm_bootstrap_multi's shards); streams no context owns fall back to
+// the device's default pool.  Debug builds poison the block.
+hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st);
+
 }  // namespace dfm
 
 // Kernel classes for per-kernel HIP-event timing (dfm_ctx_read_timing).

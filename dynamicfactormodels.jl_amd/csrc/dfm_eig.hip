@@ -2659,7 +2659,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // read with replicate stride 0 by the init pass and the first step's y2 /
   // ap2 (L2-resident) instead of nb materialised copies
   double *Q0 = nullptr;
-  if (hipMallocAsync((void **)&Q0, (size_t)m * P * 8 + (size_t)(nb + 4) * 4, st) != hipSuccess) return 1002;
+  if (stream_malloc((void **)&Q0, (size_t)m * P * 8 + (size_t)(nb + 4) * 4, st) != hipSuccess) return 1002;
   // straggler phase (< 1/8 of the batch active at a poll): the GEMMs tile only
   // the listed replicates' column groups (list built once, a superset of the
   // later active sets; replicates retired since are computed and ignored)

@@ -278,7 +278,7 @@ static hipError_t launch_gram_a(int orient, const PanelSrc &src, int m, int K, i
   int nrc = nrep;   // replicates per launch (bounds the partial images to ~1 GB)
   if (S > 1) {
     nrc = (int)std::max<int64_t>(1, std::min<int64_t>(nrep, ((int64_t)1 << 27) / (elems * S)));
-    hipError_t e = hipMallocAsync((void **)&W, (size_t)nrc * S * elems * 8, st);
+    hipError_t e = stream_malloc((void **)&W, (size_t)nrc * S * elems * 8, st);
     if (e != hipSuccess) return e;
     Gk = W; sZ = elems; sG = elems * S;
   }

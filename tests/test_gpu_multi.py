@@ -71,6 +71,72 @@ def test_two_lanes_are_bit_identical(dfm, oracle, T, N, r, mode, B):
     assert np.array_equal(dfm.residual_bootstrap(g, B, S.V(), idx=ridx), one_r)
 
 
+@pytest.mark.parametrize("mode", ["direct", "factored"])
+def test_clone_is_complete_before_its_first_bootstrap(dfm, oracle, mode):
+    """Root cause of round 4's intermittent two-lane wrong rows:
+    ``dfm_model_clone`` copied the fit with ``hipMemcpyPeer`` — on the legacy
+    null stream, returning before a device-to-device copy lands — while the
+    copy's context stream is non-blocking, so the clone's first kernels
+    (H = E E', EL = E L, F S F', the warm start) could read a partly copied
+    E, L or U.  A large panel (three 96 MB panel copies ahead of L and U)
+    turns that window from microseconds into ~0.1 ms: without the fix the
+    clone's rows — and the second lane's, whose clone is made by the first
+    two-lane call — differ from the original's on every run."""
+    T, N, r = 200, 60000, 3
+    rng = np.random.default_rng(61)
+    y, x, *_ = oracle.factor_model_DGP(T, N, r, rng)
+    x, w = oracle.normalize(x), np.ones((T, 1))
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.eigenvalue(1), S.coefficient(1), S.t_stat(2), S.LM(T // 2, 1),
+             S.iterations()]
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    g.set_bootstrap_mode(mode)
+    c = dfm.clone_model(g, dfm.Context(0))      # and at once a bootstrap on the copy
+    c.set_bootstrap_mode(mode)
+    idx, eta = dfm.draw_wild_fast(3, 8, T)
+    got = dfm.wild_bootstrap(c, 8, stats, idx=idx, eta=eta)
+    assert np.array_equal(got, dfm.wild_bootstrap(g, 8, stats, idx=idx, eta=eta))
+    # the two-lane job on a fresh fit: its first call makes the lane's clone
+    h = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    h.set_bootstrap_mode(mode)
+    B = 600
+    idx, eta = dfm.draw_wild_fast(4, B, T)
+    lanes = dfm.wild_bootstrap(h, B, stats, idx=idx, eta=eta)
+    h.set_batch(B)
+    one = dfm.wild_bootstrap(h, B, stats, idx=idx, eta=eta)
+    bad = np.where(~np.all(lanes == one, axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} two-lane rows differ from one lane (first {bad[:5]}, last {bad[-1:]})"
+
+
+def test_clone_ignores_the_legacy_null_stream(dfm, oracle):
+    """The same hazard made deterministic: the legacy null stream (PyTorch's
+    default stream) is held busy with ~0.1 s of fp64 GEMMs when the fit is
+    cloned.  Round 4's clone queued its copies behind that work (hipMemcpyPeer)
+    and returned at once, and the copy's bootstrap — on the context's
+    non-blocking stream — read buffers not yet copied.  The clone now copies
+    on its own context's stream and waits for those copies only."""
+    import torch
+    T, N, r = 200, 4000, 3
+    rng = np.random.default_rng(62)
+    y, x, *_ = oracle.factor_model_DGP(T, N, r, rng)
+    x, w = oracle.normalize(x), np.ones((T, 1))
+    S = dfm.Stat
+    stats = [S.V(), S.criterion(), S.eigenvalue(1), S.coefficient(1), S.t_stat(2), S.iterations()]
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2")
+    idx, eta = dfm.draw_wild_fast(5, 8, T)
+    ref = dfm.wild_bootstrap(g, 8, stats, idx=idx, eta=eta)
+    a = torch.full((6144, 6144), 1e-4, device="cuda", dtype=torch.float64)
+    torch.cuda.synchronize()
+    assert torch.cuda.current_stream().cuda_stream == 0      # the legacy null stream
+    for _ in range(6):
+        a = a @ a
+    c = dfm.clone_model(g, dfm.Context(0))
+    got = dfm.wild_bootstrap(c, 8, stats, idx=idx, eta=eta)
+    torch.cuda.synchronize()
+    bad = np.where(~np.all(got == ref, axis=1))[0]
+    assert len(bad) == 0, f"clone rows differ: {bad}"
+
+
 def test_bootstrap_multi_break_model(dfm, oracle):
     y, x, w = panel(oracle, 120, 200, 2, 91, model="Breitung_Eickmeier_2011", b=0.5)
     g = dfm.DynamicFactorModel(y, w, x, 2, "ICp2", break_indices=[61])
@@ -182,3 +248,51 @@ def test_gloo_world2_real_engine(dfm, oracle):
     ref = dfm.wild_bootstrap(g, 17, [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.Wald_all(75)], idx=idx, eta=eta)
     for r in (0, 1):
         assert np.array_equal(res[r], ref)
+
+
+def test_rccl_world1_device_gather(dfm, oracle):
+    """The nccl (= RCCL) branch of parallel._comm_device / gather_rows with
+    device tensors, at world size 1 on cuda:0 (an 8-GPU node is the driver's;
+    this runs the same code path on the one-GPU box): the rows of
+    wild_bootstrap_sharded through RCCL equal the unsharded rows
+    (src/bootstrap.jl:43's loop, replicate b on rank floor(b world / B))."""
+    import torch
+    import torch.distributed as dist
+    from dfm_amd.parallel import _comm_device, gather_rows, wild_bootstrap_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        assert _comm_device(None, None) == torch.device("cuda", 0)
+        loc = torch.arange(15, dtype=torch.float64, device="cuda").reshape(5, 3)
+        got = gather_rows(loc, 5)
+        assert got.is_cuda and torch.equal(got, loc)
+        y, x, w = panel(oracle, 150, 300, 3, 45)
+        g = dfm.DynamicFactorModel(y, w, x, 3, "ICp2")
+        idx, eta = dfm.draw_wild_fast(13, 17, 150)
+        stats = [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.Wald_all(75)]
+        rows = wild_bootstrap_sharded(g, 17, stats, idx, eta)
+        assert np.array_equal(rows, dfm.wild_bootstrap(g, 17, stats, idx=idx, eta=eta))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_under_torchrun_world1():
+    """bench.py under torchrun at --nproc-per-node 1 takes the RCCL path (the
+    process group, the device all-gather of the rows, barriers and the
+    max-over-ranks time) — the code the driver's N = 2..8 runs execute."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "1", "--warmup", "1", "--replicates", "600", "--no-cpu-baseline",
+           "--no-all-fields"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 1 and rec["outputs_finite"] and rec["value"] > 0
+    assert rec["collective"].startswith("RCCL all-gather") and "nccl" in rec["collective"]
+

@@ -359,6 +359,37 @@ def test_bootstrap_host_closure_matches_oracle_loop(dfm, oracle, T, N, breaks):
         s = signs(rep.F, d.F)
         assert rel(rep.coefficients[1:] * s, d.coefficients[1:]) < STAT_RTOL
         assert rel(rep.t_stats[1:] * s, d.t_stats[1:]) < STAT_RTOL
+        cs = np.concatenate([[1.0], s])   # the HC2 covariance rebuilt on the host (:43-46), factor signs applied
+        assert rel(rep.coefficient_covariance * np.outer(cs, cs), d.coefficient_covariance) < 1e-9
+
+
+@pytest.mark.parametrize("T,N,breaks", [(120, 60, [61]), (90, 140, [40]), (80, 120, [])])
+def test_residual_bootstrap_host_closure(dfm, oracle, T, N, breaks):
+    """The residual bootstrap's closure path (src/bootstrap.jl:21-39): X*_b =
+    C + E[idx_b] with idx_b drawn WITHIN each break block (:23-28), refit per
+    block; every block's loadings (DFM_STAT_LOADINGS, copied per block out of
+    the replicate's loadings slab) against the oracle's refit, up to sign and
+    principal angle, and a closure statistic against the oracle's loop."""
+    r = 2
+    y, x, w = panel(oracle, T, N, r, 57, model="Breitung_Eickmeier_2011", b=0.5)
+    g = dfm.DynamicFactorModel(y, w, x, r, "ICp2", break_indices=breaks)
+    o = oracle.DynamicFactorModel(y, w, x, r, "ICp2", breaks)
+    B = 3
+    idx = oracle.draw_residual(np.random.default_rng(12), B, T, breaks)
+    reps = []
+    V = dfm.residual_bootstrap(g, B, lambda d: reps.append(d) or oracle.factor_residual_variance(d), idx=idx)
+    for b in range(B):
+        d = oracle.DynamicFactorModel(y, w, o.common_component + o.factor_residuals[idx[b]], r, "ICp2", breaks)
+        rep = reps[b]
+        assert rel(V[b], oracle.factor_residual_variance(d)) < STAT_RTOL
+        assert np.max(np.abs(rep.x - d.x)) < 1e-12 * np.max(np.abs(d.x))
+        assert len(rep.loadings) == len(d.loadings) == len(breaks) + 1
+        for Lg, Lo in zip(rep.loadings, d.loadings):
+            assert max_sin_angle(Lg, Lo[:, :r]) < ANGLE_TOL
+            sj = signs(Lg, Lo[:, :r])
+            assert rel(Lg * sj, Lo[:, :r]) < 1e-9
+        for Fg, Fo in zip(rep.factors, d.factors):
+            assert max_sin_angle(Fg, Fo[:, :r]) < ANGLE_TOL
 
 
 @pytest.mark.parametrize("T,N", [(80, 120), (160, 24)])

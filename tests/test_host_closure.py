@@ -26,6 +26,7 @@ class _Base:
         self.factor_type = "principal components"
         self.factors = [F[:, :r] for F in o.factors]
         self.factor_residuals = o.factor_residuals
+        self.targeted_predictors = np.ones(o.x.shape[1], dtype=bool)
 
 
 def _rows(oracle, o, fits, stats_order=True):
@@ -84,6 +85,12 @@ def test_closure_records_match_oracle_loop(dfm, oracle, T, N, breaks, kind):
         assert np.array_equal(rec.coefficients, d.coefficients) and np.array_equal(rec.t_stats, d.t_stats)
         assert np.max(np.abs(rec.residuals - d.residuals)) <= 1e-12 * np.max(np.abs(d.residuals))
         assert rec.V == oracle.factor_residual_variance(d)
+        # the HC2 sandwich of src/DynamicFactorModel.jl:43-46 rebuilt on the host
+        cov = d.coefficient_covariance
+        assert np.max(np.abs(rec.coefficient_covariance - cov)) <= 1e-10 * np.max(np.abs(cov))
+        assert np.array_equal(rec.targeted_predictors, base.targeted_predictors)
+        assert np.array_equal(rec.eigenvalues, d.eigenvalues[0][:2]) if len(breaks) == 0 else True
+        assert (rec.block_eigenvalues is None) == (len(breaks) > 0)
         assert abs(lr[b] - oracle.LR_test(d, bp, 3)) <= 1e-9 * abs(oracle.LR_test(d, bp, 3))
         assert abs(V[b] - oracle.factor_residual_variance(d)) <= 1e-12 * oracle.factor_residual_variance(d)
 
