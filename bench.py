@@ -186,19 +186,21 @@ def rocprof_avg_ms(kernel_prefix):
     return None, None
 
 
-def hbm_rooflines(timing, eig, Bn, steps):
+def hbm_rooflines(timing, eig, Bn, steps, pz=16):
     """Achieved HBM bandwidth of the per-replicate gather/residual passes of
     the factored solver (HIP-event time of their kernel class over the timed
-    region; algorithmic bytes per replicate-pass, DESIGN.md section 3, P = 16):
+    region; algorithmic bytes per replicate-pass; P = 16
+    columns per row of the per-replicate buffers Q, Y, S, V0, PV; pz = the
+    solver's block, rounded up to even = the columns of Z and HZ):
       y2  (class eig_gq):    Y = G*Q rows from the gathered HZ rows, Q'Y / Y'Y / Q'Q:
-                             reads Q and HZ[idx], writes Y = 3 T P 8 B per Rayleigh-Ritz step
-      ap2 (class eig_apply): 5 T P 8 B per pass (Q, Y in; the filter's first Horner term S,
+                             reads Q and HZ[idx], writes Y = (2 P + pz) T 8 B per Rayleigh-Ritz step
+      ap2 (class eig_apply): (4 P + pz) T 8 B per pass (Q, Y in; the filter's first Horner term S,
                              V0 = Q Bm and Z out); passes = Rayleigh-Ritz steps + one init per replicate
-      last Horner step of a filter (boot_cheb_kernel, class eig_apply): 5 T P 8 B per pass
+      last Horner step of a filter (boot_cheb_kernel, class eig_apply): (3 P + 2 pz) T 8 B per pass
                              (HZ[idx], V0 in; S written and re-read by the CSR gather, Z out);
                              passes = one per filter = Rayleigh-Ritz steps - replicates
-      middle Horner steps (boot_cheb_mid_kernel, class eig_apply): (2 P + r + 1) T 8 B in
-                             (HZ, PV, PF, e2 rows) + T P 8 B out (Z); passes = the other
+      middle Horner steps (boot_cheb_mid_kernel, class eig_apply): (pz + P + r + 1) T 8 B in
+                             (HZ, PV, PF, e2 rows) + T pz 8 B out (Z); passes = the other
                              GEMM products after the Rayleigh-Ritz ones
     Replicate-passes come from the library's own counters (eig_iterations)."""
     P = 16
@@ -206,11 +208,12 @@ def hbm_rooflines(timing, eig, Bn, steps):
     rr = eig.get("replicate_iterations", 0)
     cheb = max(eig.get("gemm_products", 0) - rr, 0)
     last = max(min(rr - Bn * steps, cheb), 0)
-    tp8 = T * P * 8
+    t8 = T * 8
     for cls, name, parts in (
-            ("eig_gq", "boot_y2_kernel", ((3 * tp8, rr),)),
+            ("eig_gq", "boot_y2_kernel", (((2 * P + pz) * t8, rr),)),
             ("eig_apply", "boot_ap2_kernel + boot_cheb_kernel + boot_cheb_mid_kernel",
-             ((5 * tp8, rr + Bn * steps), (5 * tp8, last), ((2 * P + R + 1) * T * 8 + tp8, cheb - last)))):
+             (((4 * P + pz) * t8, rr + Bn * steps), ((3 * P + 2 * pz) * t8, last),
+              ((2 * pz + P + R + 1) * t8, cheb - last)))):
         ms, n = timing.get(cls, (0.0, 0))
         units = sum(u for _, u in parts)
         if not n or not units:
@@ -403,8 +406,8 @@ def main():
         # H (T x T) . Z (T x nb*P).  Algorithmic flop = 2 T^2 P per replicate
         # still unconverged when the GEMM runs (converged replicates' column
         # blocks are skipped), summed by the library over the timed region.
-        P = 16
-        flop_total = 2.0 * T * T * P * eig["gemm_products"]
+        _, PZ = model.fact_block()   # columns per replicate in the GEMM (the solver's block, even)
+        flop_total = 2.0 * T * T * PZ * eig["gemm_products"]
         per_launch_ms = gemm_ms / gemm_n
         achieved = flop_total / (gemm_ms * 1e-3) / 1e12
         roof = {"kernel": "gemmh_kernel_t<3,3,RUN> (batched eigen-iteration H.Z: LDS-DMA 3-deep ring, running "
@@ -414,7 +417,7 @@ def main():
                 "traffic": pmc_traffic("gemmh_kernel_t<3, 3, true>"),
                 "avg_launch_ms": round(per_launch_ms, 4),
                 "flop_per_launch": round(flop_total / gemm_n), "launches": gemm_n,
-                "flop_per_replicate_product": 2 * T * T * P}
+                "flop_per_replicate_product": 2 * T * T * PZ, "block_columns": PZ}
         rp_ms, rp_src = rocprof_avg_ms("dfm::gemmh_kernel_t<3, 3, true>")
         if rp_ms:   # the same algorithmic flop per launch over rocprof's average duration
             roof["rocprof"] = {"avg_launch_ms": round(rp_ms, 4), "source": f"profiles/{rp_src}",
@@ -455,7 +458,7 @@ def main():
         "eig_filter": ("Chebyshev filters in Horner form: degree 6 on [0, max(theta_p, 0.2 theta_k)] after the "
                        "first Rayleigh-Ritz step of the warm start (middle steps row-local), degree 2 on "
                        "[0, theta_p] after later ones"),
-        "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps),
+        "roofline_hbm": hbm_rooflines(timing, eig, nloc, args.steps, model.fact_block()[1] or 16),
         "fields_formed": "eigenvalues + trace: V and ICp2 read nothing else, so the replicate factors, loadings "
                          "and OLS are not formed (demand-driven); the all_fields extra is the rate with the whole "
                          "regression record (F*, L*, OLS + HC2) formed per replicate",

@@ -81,6 +81,7 @@ SIGNATURES = [
     ("dfm_stats_width", C.c_int64, [C.c_void_p, C.POINTER(dfm_stat), C.c_int]),
     ("dfm_model_set_batch", C.c_int, [C.c_void_p, C.c_int64]),
     ("dfm_model_set_mode", C.c_int, [C.c_void_p, C.c_int]),
+    ("dfm_model_fact_block", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dfm_chow_all", C.c_int, [C.c_void_p, C.c_int64, c_double_p, c_double_p, c_double_p]),
     ("dfm_chow", C.c_int, [C.c_void_p, C.c_int64, C.c_int64, c_double_p, c_double_p, c_double_p]),
     ("dfm_model_criterion", C.c_int, [C.c_void_p, C.c_int, c_double_p]),

@@ -304,6 +304,14 @@ class DynamicFactorModelResult:
         """'auto' | 'direct' | 'factored' (N > T panels; see include/dfm.h)."""
         self._ctx.check(self._ctx.lib.dfm_model_set_mode(self._h, {"auto": 0, "direct": 1, "factored": 2}[mode]))
 
+    def fact_block(self):
+        """(p, pz): the factored bootstrap solver's block for this model and the
+        columns per replicate of its batched H.Z GEMM (``dfm_model_fact_block``);
+        (0, 0) when the bootstrap does not take the factored path."""
+        p, pz = C.c_int(), C.c_int()
+        self._ctx.lib.dfm_model_fact_block(self._h, C.byref(p), C.byref(pz))
+        return int(p.value), int(pz.value)
+
     def __del__(self):
         try:
             if self._h and not _lib.shutting_down():

@@ -26,6 +26,7 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
 size_t eig_workspace_bytes_padded(int m, int nb, int P, int maxit);
 const int *eig_iters_ptr(char *ws, int m, int nb, int P, int maxit);
 int eig_block_p(int m, int k, int req);
+int fact_block_p(int m, int k, int req);
 extern thread_local int g_last_iters;   // per host thread: dfm_bootstrap_multi's shards run concurrently
 extern thread_local int64_t g_last_rep_iters;
 extern thread_local int64_t g_last_gemm_products;
@@ -1104,6 +1105,15 @@ int dfm_model_set_mode(dfm_model *m, int mode) {
   return 0;
 }
 
+int dfm_model_fact_block(const dfm_model *m, int *p, int *pz) {
+  if (!m) return -1;
+  const int b = (m->orient == 0 && m->mode != 1 && m->r >= 1 && m->r <= 16 && m->T <= fact_t_max() && m->nblk == 1)
+                    ? fact_block_p(m->m, m->r, m->ctx->block) : 0;
+  if (p) *p = b;
+  if (pz) *pz = (b + 1) & ~1;
+  return b > 0 ? 0 : 1;
+}
+
 int dfm_model_set_batch(dfm_model *m, int64_t batch) {
   if (!m || batch < 0) return -1;
   m->batch = batch;
@@ -1509,7 +1519,8 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       // warm first filter's degree (eig_run_fact2_t)
       const double spread = (M->lam.size() >= (size_t)r && r > 0 && M->lam[r - 1] > 0.0) ? M->lam[0] / M->lam[r - 1]
                                                                                         : 0.0;
-      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, p, M->Ub, r, etol, ctx->maxit, ctx->poll,
+      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, fact_block_p(m, r, ctx->block), M->Ub, r, etol,
+                                ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, need_fl ? w.Uk : nullptr, w.trace, w.status, st, timer_cb,
                                 ctx, w.off, w.lst,
                                 (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread);

@@ -1449,6 +1449,22 @@ int eig_block_p(int m, int k, int req) {
   return p;
 }
 
+// Block of the factored bootstrap solver (N > T, eig_run_fact2_t): k + 4
+// columns, at least 8 (C3: 12 instead of the explicit-Gram solvers' 16).  The
+// H.Z GEMM's work and the Z / HZ traffic scale with the block (Z, HZ hold it
+// compactly, rounded up to even), and the Chebyshev filter does the damping
+// that extra guard vectors would otherwise buy: tools/eig_proto.py at C3
+// (warm start + the degree-6 first filter) retires 94 % of replicates at the
+// 2nd Rayleigh-Ritz step with 12 columns (7.12 products) as with 16 (7.00).
+// A requested block (dfm_ctx_set_eig_params) is taken as for the other
+// solvers; DFM_FACT_GUARD (A/B) overrides the 4.
+int fact_block_p(int m, int k, int req) {
+  if (req > 0) return eig_block_p(m, k, req);
+  static const int guard = [] { const char *e = getenv("DFM_FACT_GUARD"); return e ? atoi(e) : 4; }();
+  if (guard <= 0) return eig_block_p(m, k, 0);
+  return std::min(m, std::max(k + guard, 8));
+}
+
 int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k, int p,
             const double *warm, int kw, double tol, int maxit, int poll, char *ws, double *lam,
             double *Uk, double *trace_out, int *status, int *iters_host, hipStream_t st,
@@ -1694,7 +1710,7 @@ struct Y2Tile {
 };
 template <int P>
 DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, const int *six, const FactBase &fb,
-                     const double *__restrict__ HZ, int64_t ldz, int rep, const double *__restrict__ Qr) {
+                     const double *__restrict__ HZ, int64_t ldz, int pz, int rep, const double *__restrict__ Qr) {
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
   const int ta = min(t0 + li, T - 1);
@@ -1712,7 +1728,7 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) {
       const int c = 16 * ct + li;
-      L.hz[ct][g] = HZ[(int64_t)i * ldz + (int64_t)rep * P + c];
+      L.hz[ct][g] = c < pz ? HZ[(int64_t)i * ldz + (int64_t)rep * pz + c] : 0.0;   // compact Z / HZ: pz columns
       L.q[ct][g] = Qr[(int64_t)t * P + c];
     }
   }
@@ -1726,7 +1742,7 @@ template <int P>
 // per-wave prefetch did (2 -> 4 WGs/CU: y2 -24 %, ap2 -13 %)
 __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWork w, int T, const int32_t *__restrict__ idx,
                                                       const double *__restrict__ eta,
-                                                      const double *__restrict__ HZ, int64_t ldz,
+                                                      const double *__restrict__ HZ, int64_t ldz, int pz,
                                                       const double *__restrict__ ab,
                                                       const double *__restrict__ Qc, int64_t qs,
                                                       double *__restrict__ Yo) {
@@ -1778,7 +1794,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Qr);
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Qr);
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1924,7 +1940,7 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
 template <int P>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
-                           double *__restrict__ Zc, int64_t ldz, int rep, double *__restrict__ ab,
+                           double *__restrict__ Zc, int64_t ldz, int pz, int rep, double *__restrict__ ab,
                            const dv4 *aacc, double *sred) {
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
@@ -1979,7 +1995,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
       const double ea = (v && li < r) ? fb.EL[(int64_t)s * r + li] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + 16 * ct + li] = z[g][ct];
+        if (v && 16 * ct + li < pz) Zc[(int64_t)s * ldz + (int64_t)rep * pz + 16 * ct + li] = z[g][ct];
         cacc[ct] = mfma16(ea, z[g][ct], cacc[ct]);
       }
     }
@@ -2020,7 +2036,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
                                                        const int *__restrict__ off, const int *__restrict__ lst,
                                                        const double *__restrict__ Qc, int64_t qs,
                                                        double *__restrict__ Yq, double *__restrict__ Zc, int64_t ldz,
-                                                       double *__restrict__ ab, uint64_t seed) {
+                                                       int pz, double *__restrict__ ab, uint64_t seed) {
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
   if (!init && w.done[rep]) return;
@@ -2195,7 +2211,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
   const double *Qn = init ? Qr : Yr;
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, rep, ab, aacc, sred);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, pz, rep, ab, aacc, sred);
 }
 
 // One Horner step of the degree-d Chebyshev filter of the factored solver.
@@ -2217,7 +2233,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
                                                         const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta,
                                                         const int *__restrict__ off, const int *__restrict__ lst,
-                                                        const double *__restrict__ HZ, int64_t ldz,
+                                                        const double *__restrict__ HZ, int64_t ldz, int pz,
                                                         double *__restrict__ ab, double fai, double bbeta, int k,
                                                         double *__restrict__ Qo,
                                                         double *__restrict__ Zc) {
@@ -2275,7 +2291,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, rep, Xr);   // cur.q = V0 rows
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Xr);   // cur.q = V0 rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -2314,7 +2330,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
   }
   __syncthreads();   // every wave's Qn rows visible to the CSR gather
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, rep, ab, aacc, sred);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, pz, rep, ab, aacc, sred);
 }
 
 // The middle Horner steps in row-local form.  With W = G* S_{i+1} = F bB +
@@ -2374,7 +2390,7 @@ template <int P>
 __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWork w, int T, int p, int it,
                                                       const double *__restrict__ eta, const int *__restrict__ off,
                                                       const int *__restrict__ lst, const double *__restrict__ Zc,
-                                                      int64_t ldz, const double *__restrict__ ab, uint64_t seed,
+                                                      int64_t ldz, int pz, const double *__restrict__ ab, uint64_t seed,
                                                       double *__restrict__ PV, double *__restrict__ FV) {
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
@@ -2401,7 +2417,8 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
     const int t0 = tile * 16, ta = min(t0 + li, T - 1);
     double za[KP];
 #pragma unroll
-    for (int kk = 0; kk < KP; ++kk) za[kk] = t0 + li < T ? Zc[(int64_t)ta * ldz + (int64_t)rep * P + 4 * kk + lk] : 0.0;
+    for (int kk = 0; kk < KP; ++kk)
+      za[kk] = (t0 + li < T && 4 * kk + lk < pz) ? Zc[(int64_t)ta * ldz + (int64_t)rep * pz + 4 * kk + lk] : 0.0;
     dv4 v[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) v[ct] = dv4{0.0, 0.0, 0.0, 0.0};
@@ -2447,7 +2464,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
 
 template <int P>
 __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, EigWork w, int T, int p,
-                                                            const double *__restrict__ HZ, int64_t ldz,
+                                                            const double *__restrict__ HZ, int64_t ldz, int pz,
                                                             double *__restrict__ ab, double fai, double bbeta, int k,
                                                             const double *__restrict__ PF,
                                                             const double *__restrict__ E2,
@@ -2507,7 +2524,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
-        hz[ct][g] = HZ[(int64_t)sc * ldz + (int64_t)rep * P + c];
+        hz[ct][g] = c < pz ? HZ[(int64_t)sc * ldz + (int64_t)rep * pz + c] : 0.0;
         pv[ct][g] = pvr[(int64_t)sc * P + c];
       }
     }
@@ -2537,7 +2554,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
         if (c >= p || !v) z = 0.0;
         uv[ct][g] = v ? u : 0.0;
         zv[ct][g] = z;
-        if (v) Zc[(int64_t)s * ldz + (int64_t)rep * P + c] = z;
+        if (v && c < pz) Zc[(int64_t)s * ldz + (int64_t)rep * pz + c] = z;
       }
     }
 #pragma unroll
@@ -2625,10 +2642,20 @@ constexpr double kChebWarmBeta = 0.2;
 // capped so that stays below ~1e6 (CholQR2 keeps every wanted direction in
 // fp64): C3's lambda_1 / lambda_8 = 1.6 allows 6 (the cap); a panel with one
 // dominant factor (C2's base fit: lambda_1 / lambda_4 = 50) gets 3.
+// DFM_FACT_D0 / DFM_FACT_BETA (A/B only) override the first filter's degree
+// cap and interval factor.
+static int warm_d0_cap() {
+  static const int v = [] { const char *e = getenv("DFM_FACT_D0"); return e ? std::max(kChebD, std::min(kChebDMax, atoi(e))) : kChebWarmD0; }();
+  return v;
+}
+static double warm_beta() {
+  static const double v = [] { const char *e = getenv("DFM_FACT_BETA"); return e ? atof(e) : kChebWarmBeta; }();
+  return v;
+}
 static int first_filter_degree(double spread) {
   const double ratio = std::max(1.0001, 1.1 * spread);
   const int d = (int)std::floor(std::log(1e6) / std::log(ratio));
-  return std::max(kChebD, std::min(kChebWarmD0, d));
+  return std::max(kChebD, std::min(warm_d0_cap(), d));
 }
 
 template <int P>
@@ -2641,7 +2668,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   EigWork w = carve(ws, m, nb, P, maxit);
   w.subspace = subspace;
   w.no_vectors = Uk == nullptr;
-  const int64_t ldz = (int64_t)nb * P;
+  // Z / HZ hold pz = p rounded up to even columns per replicate (the GEMM's
+  // 16-byte DMA pairs): the H.Z GEMM's work scales with the block p, not P
+  const int pz = (p + 1) & ~1;
+  const int64_t ldz = (int64_t)nb * pz;
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)z_rows(m) * ldz;
   double *ab = HZ + (size_t)m * ldz;
@@ -2682,11 +2712,11 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
                        off, lst, w.trace, mid ? PFb : nullptr, E2b);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
                        0.0, 0.0, eta,
-                       off, lst, qin, qs, alt, Zc, ldz, ab, seed);
+                       off, lst, qin, qs, alt, Zc, ldz, pz, ab, seed);
   }
   if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
-  const double beta0 = warm_started ? kChebWarmBeta : 0.0;
+  const double beta0 = warm_started ? warm_beta() : 0.0;
   double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
   shifted_cheb(d0, ca0);
   shifted_cheb(kChebD, ca1);
@@ -2697,14 +2727,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const double *ca = it == 0 ? ca0 : ca1;
     const double bb = it == 0 ? beta0 : 0.0;
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
-    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
+    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, pz, true,
                                cl_on ? alist : nullptr, cl_on ? acount : nullptr);
     if (tf) tf(tctx, DFM_KC_GEMM, 0);
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, ab,
-                       qin, qs, alt);
+    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, pz,
+                       ab, qin, qs, alt);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, kJacobiSweeps);
@@ -2712,10 +2742,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     if (mid && it == 0 && it < maxit - 1)   // before ap2 overwrites Z(Q) and a(Q)
       hipLaunchKernelGGL(boot_pv_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, it, eta, off, lst, Zc, ldz,
-                         ab, seed, w.S, FVb);
+                         pz, ab, seed, w.S, FVb);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
                        it == maxit - 1 ? 1 : 0, cheb, ca[dg], ca[dg - 1], bb, eta, off, lst, qin, qs, alt, Zc, ldz,
-                       ab, seed);
+                       pz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it == next_poll) {   // convergence poll, right after the step that retires replicates
       int a = -1;
@@ -2738,17 +2768,17 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       // basis S_0 goes back into cur (Q), Y stays in alt
       for (int sp = 2; sp <= dg; ++sp) {
         if (tf) tf(tctx, DFM_KC_GEMM, 1);
-        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, P, true,
+        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, pz, true,
                         cl_on ? alist : nullptr, cl_on ? acount : nullptr);
         if (tf) tf(tctx, DFM_KC_GEMM, 0);
         if (e != hipSuccess) return 1000 + (int)e;
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
         if (mid && it == 0 && sp < dg)
-          hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, ab,
+          hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
                              ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, FtF, Zc);
         else
           hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
-                             st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, ab, ca[dg - sp], bb, k, cur, Zc);
+                             st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, pz, ab, ca[dg - sp], bb, k, cur, Zc);
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
       }
       last_cheb = it;

@@ -235,6 +235,12 @@ int dfm_model_set_batch(dfm_model *m, int64_t batch);
  * Gram is never formed: every eigen-iteration is one MFMA GEMM of the shared
  * H = E E' against the batch's iterates).  Results agree to rounding. */
 int dfm_model_set_mode(dfm_model *m, int mode);
+/* Block of the factored bootstrap solver for this model: p eigen-iterate
+ * columns per replicate, pz = p rounded up to even = the columns each
+ * replicate contributes to the batched H.Z GEMM (its flop per
+ * replicate-product is 2 T^2 pz).  Returns 0, or 1 (p = pz = 0) when the
+ * model's bootstrap never takes the factored path (T >= N, breaks, r > 16). */
+int dfm_model_fact_block(const dfm_model *m, int *p, int *pz);
 
 /* ------------------------------------------------------------ Chow tests
  * LR_test / LM_test / Wald_test (src/chowtest.jl:19-42) for EVERY variable

@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dynamicfactormodels.jl_amd"))
 import host  # noqa: E402
 
-T, N, R, P = 500, 2000, 8, 16
+T, N, R = 500, 2000, 8
+P = int(os.environ.get("P", "16"))
 
 
 def shifted_cheb(d):
