@@ -47,8 +47,15 @@ DFM_DEV void block_spd_inverse(const double *A, double *Ai, double *Lw, double *
 // block_spd_inverse on ONE wave (lanes, no barriers: every LDS write is
 // waited for before the lanes that read it issue their reads) — the same
 // operations in the same order, so several small inverses run side by side
-// on different waves of a workgroup.
-DFM_DEV void wave_spd_inverse(const double *A, double *Ai, double *Lw, double *Tw, int n, int S, int *bad) {
+// on different waves of a workgroup.  A, Ai, Lw, Tw MUST be LDS (__shared__)
+// memory: they are cast to the LDS address space here, so every access is a
+// ds_* instruction and `s_waitcnt lgkmcnt(0)` is the complete wait (a flat or
+// global pointer would need vmcnt too — and is undefined after the cast).
+// `bad` (LDS) is raised with an atomic OR: several waves may report at once.
+typedef __attribute__((address_space(3))) double lds_double;
+DFM_DEV void wave_spd_inverse(const double *A_, double *Ai_, double *Lw_, double *Tw_, int n, int S, int *bad) {
+  const lds_double *A = (const lds_double *)A_;
+  lds_double *Ai = (lds_double *)Ai_, *Lw = (lds_double *)Lw_, *Tw = (lds_double *)Tw_;
   const int lane = threadIdx.x & 63;
   auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   for (int e = lane; e < n * S; e += 64) Lw[e] = 0.0;
@@ -57,7 +64,7 @@ DFM_DEV void wave_spd_inverse(const double *A, double *Ai, double *Lw, double *T
     if (lane == 0) {
       double s = A[j * S + j];
       for (int p = 0; p < j; ++p) s -= Lw[j * S + p] * Lw[j * S + p];
-      if (!(s > 0.0)) { *bad = 1; s = 1.0; }
+      if (!(s > 0.0)) { atomicOr(bad, 1); s = 1.0; }
       Lw[j * S + j] = sqrt(s);
     }
     sync();

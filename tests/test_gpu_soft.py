@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-from test_gpu_parity import GOLD, panel
+from test_gpu_parity import ANGLE_TOL, GOLD, STAT_RTOL, max_sin_angle, panel, rel
 
 pytestmark = pytest.mark.gpu
 LAM_RTOL = 1e-12
@@ -86,6 +86,32 @@ def test_c4_soft_full_size(dfm, oracle):
     assert np.allclose([x.sum(), np.abs(x).sum(), y.sum(), folds.sum()], g["c4_digest"], rtol=1e-12, atol=1e-9)
     mask, path = dfm.targeted_predictors(y, w, x, "soft", folds=folds, return_path=True)
     check(mask, path, g["c4_mask"], g["c4_lam"], g["c4_meanloss"], int(g["c4_best"]), g["c4_beta"])
+
+
+def test_c4_chain_soft_then_pca(dfm, oracle):
+    """BASELINE configs[3] as ONE chain, as tools/bench_configs.py c4 times it:
+    the device's soft glmnetcv mask (src/targeted_predictors.jl:31-36; equal to
+    the frozen fixture bit for bit) selects the columns, then the device PCA
+    of the selected columns (src/DynamicFactorModel.jl:75-95, r = 5) against
+    the oracle's principal_components of the same columns: eigenvalues and
+    trace at the statistic bar, factors and loadings up to sign / principal
+    angle.  (The reference's principal-components branch itself ignores the
+    targeted_predictors argument, :96-100 — the selection is applied to x.)"""
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_golden
+    g = np.load(os.path.join(GOLD, "tp_soft.npz"))
+    y, w, x, folds = make_golden.c4_inputs()
+    mask = dfm.targeted_predictors(y, w, x, "soft", folds=folds)
+    assert np.array_equal(mask, g["c4_mask"]) and mask.sum() > 5
+    xs = x[:, mask]
+    T, Ns = xs.shape
+    k = 5
+    ev, F, L, tr = dfm.principal_components(xs, k)
+    Fo, Lo, wo = oracle.principal_components(xs, T, Ns)
+    assert rel(ev, wo[:k]) < STAT_RTOL
+    assert abs(tr - float(np.sum(xs * xs))) <= 1e-12 * abs(tr)
+    assert max_sin_angle(F, Fo[:, :k]) < ANGLE_TOL and max_sin_angle(L, Lo[:, :k]) < ANGLE_TOL
 
 
 def _lasso_inputs(oracle, T, N, seed, lmr=None, nlam=100):
