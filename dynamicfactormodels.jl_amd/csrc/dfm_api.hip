@@ -199,6 +199,56 @@ hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st) {
   if (e == hipSuccess) DFM_POISON_ASYNC(*p, bytes, st);
   return e;
 }
+
+// The device gate (dfm_common.h): per device, a count of library calls in
+// progress and a solo flag.  Shares wait only while a solo section runs
+// (reader-preferring, so a call holding a share can always start more shared
+// calls on other threads — dfm_bootstrap_multi's shards — without deadlocking
+// behind a waiting solo); a solo section waits for the count to reach zero.
+namespace {
+struct DevGate {
+  std::mutex mu;
+  std::condition_variable cv;
+  int shares = 0;
+  bool solo = false;
+};
+constexpr int kGateDevs = 64;
+DevGate g_gate[kGateDevs];
+thread_local int t_shares[kGateDevs];   // this thread's nesting depth per device
+}  // namespace
+DeviceShare::DeviceShare(int device) : dev(device >= 0 && device < kGateDevs ? device : -1) {
+  if (dev < 0 || t_shares[dev]++ > 0) return;
+  DevGate &g = g_gate[dev];
+  std::unique_lock<std::mutex> lk(g.mu);
+  g.cv.wait(lk, [&] { return !g.solo; });
+  ++g.shares;
+}
+DeviceShare::~DeviceShare() {
+  if (dev < 0 || --t_shares[dev] > 0) return;
+  DevGate &g = g_gate[dev];
+  {
+    std::lock_guard<std::mutex> lk(g.mu);
+    --g.shares;
+  }
+  g.cv.notify_all();
+}
+DeviceSolo::DeviceSolo(int device) : dev(device >= 0 && device < kGateDevs ? device : -1) {
+  if (dev < 0 || t_shares[dev] > 0) { dev = -1; return; }   // (nested in a shared call: would never drain)
+  DevGate &g = g_gate[dev];
+  std::unique_lock<std::mutex> lk(g.mu);
+  g.cv.wait(lk, [&] { return !g.solo && g.shares == 0; });
+  g.solo = true;
+  held = true;
+}
+DeviceSolo::~DeviceSolo() {
+  if (!held) return;
+  DevGate &g = g_gate[dev];
+  {
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.solo = false;
+  }
+  g.cv.notify_all();
+}
 }  // namespace dfm
 
 // The host thread of a model's second bootstrap lane (bootstrap_lanes):
@@ -718,6 +768,7 @@ int dfm_model_fit_breaks(dfm_ctx *ctx, const double *y, const double *w, int q, 
                          const double *X, int64_t T64, int64_t N64, int64_t ldx, int r, int crit,
                          int kmax, const int64_t *breaks, int nbreaks, dfm_model **out) {
   if (!ctx || !out) return -1;
+  DeviceShare gate(ctx->device);
   *out = nullptr;
   if (!y || !X || T64 < 2 || N64 < 1 || ldx < T64 || q < 0 || (q > 0 && (!w || ldw < T64)))
     return fail(ctx, -2, "dfm_model_fit: bad arguments");
@@ -1289,6 +1340,7 @@ static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx
 int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
                       const dfm_stat *stats, int ns, double *out) {
   if (!M) return -1;
+  DeviceShare gate(M->ctx->device);
   if (idx && (kind != DFM_BOOT_WILD || eta) && lane_split(M, B, stats, ns))
     return bootstrap_lanes(M, kind, B, idx, eta, stats, ns, out);
   return bootstrap_one(M, kind, B, idx, eta, stats, ns, out);
@@ -1773,6 +1825,7 @@ int dfm_pca(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, int64_t ldx
   if (!X || T64 < 1 || N64 < 1 || ldx < T64 || k < 1) return fail(ctx, -2, "dfm_pca: bad arguments");
   const int T = (int)T64, N = (int)N64, m = std::min(T, N);
   if (k > m) return fail(ctx, -2, "dfm_pca: k=%d > min(T,N)=%d", k, m);
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   DevPanel dp;
@@ -1821,6 +1874,7 @@ int dfm_gram_spectrum(dfm_ctx *ctx, const double *X, int64_t T64, int64_t N64, i
   if (!X || !eigvals_m || T64 < 1 || N64 < 1 || ldx < T64) return fail(ctx, -2, "bad arguments");
   const int T = (int)T64, N = (int)N64, m = std::min(T, N);
   if (m > spectrum_any_max()) return fail(ctx, -30, "full spectrum supported for min(T,N) <= %d", spectrum_any_max());
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   DevPanel dp;
@@ -1862,6 +1916,7 @@ int dfm_model_criterion(dfm_model *M, int crit, double *value) {
   if (!M || !value) return -1;
   dfm_ctx *ctx = M->ctx;
   if (crit < 0 || crit > 6) return fail(ctx, -31, "unknown criterion %d", crit);
+  DeviceShare gate(ctx->device);
   if (crit <= 2 && std::isnan(M->sigma2)) {
     const int m = M->m;
     if (m > spectrum_any_max())
@@ -1917,6 +1972,7 @@ int dfm_chow_all(dfm_model *M, int64_t bp, double *LR, double *LM, double *Wald)
   dfm_ctx *ctx = M->ctx;
   if (bp < M->r || bp > M->T - M->r) return fail(ctx, -7, "break period %lld out of range", (long long)bp);
   if (M->nblk > 64) return fail(ctx, -7, "Chow statistics support at most 64 break blocks");
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   if (M->r > 16) {   // any r: the GEMM-built tests (dfm_wide.hip)
@@ -1964,6 +2020,7 @@ int dfm_targeted_hard(dfm_ctx *ctx, const double *y, const double *w, int q, int
     return fail(ctx, 3, "joint hard thresholding is singular for q + N >= T (defect D8); use PER_CANDIDATE");
 
   if (mode == DFM_TP_PER_CANDIDATE && (q < 1 || q > 16)) return fail(ctx, -32, "PER_CANDIDATE needs 1 <= q <= 16");
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   DevPanel dp;
@@ -2198,6 +2255,7 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
                         double *V_out, double *crit_out, double *eig_out, double *coef_out, double *tstat_out,
                         double *pred_out, double *true_out, bool dev) {
   if (!ctx) return -1;
+  DeviceShare gate(ctx->device);
   const int T = (int)T64, N = (int)N64;
   if (!y || !X || T < 4 || N < 1 || ldx < T || P < 1 || T - P < 2 || q < 0 || (q > 0 && (!w || ldw < T)) ||
       !r_out)
@@ -2596,6 +2654,7 @@ static int predict_impl(dfm_model *M, int64_t nn, const double *w_new, int64_t l
   const int q = M->q, r = M->r, N = M->N, T = M->T;
   if (nn < 1 || !x_new || ldx < nn || (yhat && q > 0 && (!w_new || ldw < nn)) || (!F_out && !yhat))
     return fail(ctx, -2, "dfm_predict: bad arguments");
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   double *xd = nullptr, *wd = nullptr, *bd = nullptr, *wk = nullptr, *Fd = nullptr, *yd = nullptr;
@@ -2659,6 +2718,7 @@ extern "C" int dfm_normalize_dev(dfm_ctx *ctx, const double *X, int64_t T, int64
   if (!ctx) return -1;
   if (!X || !out || T < 2 || N < 1 || ldx < T || ldo < T || T > INT32_MAX || N > INT32_MAX)
     return fail(ctx, -2, "dfm_normalize: bad arguments");
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   Scope sc(ctx, DFM_KC_MISC);
   hipLaunchKernelGGL(normalize_cols_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, ctx->stream, X, ldx, (int)T,
@@ -2671,6 +2731,7 @@ extern "C" int dfm_normalize(dfm_ctx *ctx, const double *X, int64_t T, int64_t N
                              int64_t ldo) {
   if (!ctx) return -1;
   if (!X || !out || T < 2 || N < 1 || ldx < T || ldo < T) return fail(ctx, -2, "dfm_normalize: bad arguments");
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   DevBuf d;
@@ -2691,6 +2752,7 @@ extern "C" int dfm_model_clone(const dfm_model *S, dfm_ctx *ctx, dfm_model **out
   if (!S || !ctx || !out) return -1;
   *out = nullptr;
   dfm_ctx *sc = S->ctx;
+  DeviceShare gate_src(sc->device), gate_dst(ctx->device);
   hipSetDevice(sc->device);
   HIPCHK(ctx, hipStreamSynchronize(sc->stream));
   dfm_model *M = new dfm_model();

@@ -241,6 +241,9 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
   const double *Pc = prep + (size_t)(ok ? rep : rep0) * CP_NMAT * R * R;
   auto PM = [&](int m, int a, int c) -> double { return Pc[m * R * R + a * R + c]; };
   auto stage = [&](int t0) {
+#ifdef DFM_CH_DIAG_NOSTAGE   // (timing diagnostic, WRONG results: tile 0 staged once and reused)
+    if (t0 > 0) return;
+#endif
     for (int e = tid; e < nrw * TR * R; e += nth) {
       const int q = e / (TR * R), f = e % (TR * R), rr = f / R, j = f % R, t = t0 + rr;
       const int64_t base = (int64_t)(rep0 + q) * T * r;
@@ -277,6 +280,9 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
     }
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
+#ifdef DFM_CH_DIAG_NOLOAD   // (timing diagnostic, WRONG results: no gathered loads)
+      ee[u] = (double)(ro[u] & 7); if (HAS_C) cc[u] = 0.5 * u;
+#endif
       double x = ee[u];
       if (HAS_ETA) x *= sE[lr][min(rb + KS * u, tn - 1)];
       if (HAS_C) x += cc[u];

@@ -77,6 +77,32 @@ inline void dbg_poison_async(void *p, size_t bytes, hipStream_t st) {
 // the device's default pool.  Debug builds poison the block.
 hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st);
 
+// The device gate.  The lasso path kernel needs every workgroup of a grid
+// sized to the whole chip co-resident (leader/helper hand-offs); a kernel of
+// another libdfm context on the same device would hold CUs and make its
+// hand-offs wait out their timeouts.  Every public call that launches work
+// holds a DeviceShare of its device for its duration (nested calls on one
+// thread count once); the lasso launch takes a DeviceSolo — it waits until no
+// libdfm call is in progress on the device, starts none while it runs, and
+// drains the device's queued work (hipDeviceSynchronize) before launching.
+// held == false: the calling thread is itself inside a shared call on the
+// device (the solo could never drain), and the caller fails.
+struct DeviceShare {
+  explicit DeviceShare(int device);
+  ~DeviceShare();
+  DeviceShare(const DeviceShare &) = delete;
+  DeviceShare &operator=(const DeviceShare &) = delete;
+  int dev;
+};
+struct DeviceSolo {
+  explicit DeviceSolo(int device);
+  ~DeviceSolo();
+  DeviceSolo(const DeviceSolo &) = delete;
+  DeviceSolo &operator=(const DeviceSolo &) = delete;
+  int dev;
+  bool held = false;
+};
+
 }  // namespace dfm
 
 // Kernel classes for per-kernel HIP-event timing (dfm_ctx_read_timing).

@@ -1329,6 +1329,15 @@ static hipError_t launch_lasso(const double *G, int64_t strideG, int p, const do
   if (H < 1) { *why = "more lasso problems than co-resident workgroup pairs"; return hipErrorInvalidConfiguration; }
   const int nblk = nprob * (H + 1);
   if (nblk > maxb) { *why = "lasso grid above the co-resident capacity"; return hipErrorInvalidConfiguration; }
+  // The grid fills the chip: no other libdfm work may hold CUs while it
+  // runs.  The device gate (dfm_common.h) waits for every library call on the
+  // device to return and holds new ones off until this launch is done; the
+  // device's queued work is then drained.  (Another process on the same GPU
+  // is outside the gate: its kernels can still delay workgroups, which the
+  // hand-off timeouts and the relaunch below then report.)
+  DeviceSolo solo(dev);
+  if (!solo.held) { *why = "lasso path launched from inside another libdfm call on the device"; return hipErrorInvalidConfiguration; }
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
   const int ldaa = std::min(p, LP_LMAX);
   std::vector<void *> bufs;
   auto alloc = [&](size_t bytes) -> void * {

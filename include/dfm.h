@@ -19,7 +19,13 @@
  *     own, e.g. PyTorch's current stream).  They never synchronise the host
  *     except where a convergence poll needs a 4-byte read-back.
  *   - Indices are 0-based int32 (the Julia shim subtracts 1).
- *   - One context per GPU, used by one host thread at a time.
+ *   - One context per GPU, used by one host thread at a time.  Different
+ *     contexts (of one device or several) may be used from different threads
+ *     at once, except that the lasso path (dfm_targeted_soft, dfm_lasso_path)
+ *     runs alone on its device: it waits for every other libdfm call on that
+ *     device to return, drains the device, and holds new calls off until it
+ *     is done (its grid must own every CU).  Called from inside another
+ *     libdfm call on the same device it fails instead of waiting.
  */
 #ifndef DFM_H
 #define DFM_H

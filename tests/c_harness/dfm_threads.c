@@ -14,7 +14,10 @@
  *      bootstrapping at the same time (the C ABI's threading contract:
  *      different contexts may run concurrently);
  *   4. teardown of a model with a live lane (LaneWorker join, lane context
- *      release).
+ *      release);
+ *   5. the device gate: the lasso path (a grid that must own the whole chip)
+ *      on one thread while another thread's context bootstraps — every path
+ *      bit-identical to the first.
  * Exit 0: all results consistent; 1: a call failed or results differ;
  * 3: no GPU.  The sanitizer reports go to stderr.
  */
@@ -139,6 +142,77 @@ static int multi(uint64_t seed) {
   return 0;
 }
 
+/* a standardised lasso problem: G = Z'Z / n with unit diagonal, c = Z'y / n */
+#define LP_ 40
+#define LN_ 80
+#define LL_ 30
+static void lasso_problem(double *G, double *c, uint8_t *ju, double *alm) {
+  uint64_t s = 99;
+  double Z[LN_ * LP_], y[LN_], lmax = 0.0;
+  int i, j, k;
+  for (i = 0; i < LN_ * LP_; ++i) Z[i] = gauss(&s);
+  for (i = 0; i < LN_; ++i) y[i] = Z[i * LP_] - 0.5 * Z[i * LP_ + 3] + gauss(&s);
+  for (j = 0; j < LP_; ++j) {   /* standardise column j (population sd, as glmnet) */
+    double mu = 0.0, v = 0.0;
+    for (i = 0; i < LN_; ++i) mu += Z[i * LP_ + j];
+    mu /= LN_;
+    for (i = 0; i < LN_; ++i) { Z[i * LP_ + j] -= mu; v += Z[i * LP_ + j] * Z[i * LP_ + j]; }
+    v = 1.0 / __builtin_sqrt(v / LN_);
+    for (i = 0; i < LN_; ++i) Z[i * LP_ + j] *= v;
+  }
+  for (j = 0; j < LP_; ++j) {
+    double a = 0.0;
+    for (i = 0; i < LN_; ++i) a += Z[i * LP_ + j] * y[i];
+    c[j] = a / LN_;
+    ju[j] = 1;
+    if (__builtin_fabs(c[j]) > lmax) lmax = __builtin_fabs(c[j]);
+    for (k = 0; k < LP_; ++k) {
+      double g = 0.0;
+      for (i = 0; i < LN_; ++i) g += Z[i * LP_ + j] * Z[i * LP_ + k];
+      G[j * LP_ + k] = j == k ? 1.0 : g / LN_;
+    }
+  }
+  alm[0] = lmax;
+  for (k = 1; k < LL_; ++k) alm[k] = alm[k - 1] * 0.85;
+}
+
+struct gate_job { volatile int stop; int rc, runs; };
+static void *boot_loop(void *p) {
+  struct gate_job *g = (struct gate_job *)p;
+  while (!g->stop && !g->rc) {
+    g->rc = lanes_vs_one(21 + g->runs, g->runs & 1);
+    ++g->runs;
+  }
+  return NULL;
+}
+
+static int gate(void) {
+  static double G[LP_ * LP_], c[LP_], alm[LL_], b0[LL_ * LP_], r0[LL_], b1[LL_ * LP_], r1[LL_];
+  static uint8_t ju[LP_];
+  dfm_ctx *ctx = NULL;
+  struct gate_job g = {0, 0, 0};
+  pthread_t th;
+  int L0 = 0, L1 = 0, k;
+  lasso_problem(G, c, ju, alm);
+  if (dfm_ctx_create(0, &ctx)) return 3;
+  CK(ctx, dfm_lasso_path(ctx, G, c, ju, LP_, alm, LL_, 0, 1e-7, b0, r0, &L0));
+  pthread_create(&th, NULL, boot_loop, &g);
+  for (k = 0; k < 8; ++k) {
+    int rc = dfm_lasso_path(ctx, G, c, ju, LP_, alm, LL_, 0, 1e-7, b1, r1, &L1);
+    if (rc) { fprintf(stderr, "gate: lasso call %d -> %d: %s\n", k, rc, dfm_last_error(ctx)); g.stop = 1; pthread_join(th, NULL); return 1; }
+    if (L1 != L0 || memcmp(b0, b1, (size_t)L0 * LP_ * 8) || memcmp(r0, r1, (size_t)L0 * 8)) {
+      fprintf(stderr, "gate: lasso call %d differs from the solo path\n", k);
+      g.stop = 1; pthread_join(th, NULL); return 1;
+    }
+  }
+  g.stop = 1;
+  pthread_join(th, NULL);
+  dfm_ctx_destroy(ctx);
+  if (g.rc) return g.rc;
+  fprintf(stderr, "gate: 8 lasso paths alongside %d bootstrap jobs\n", g.runs);
+  return 0;
+}
+
 struct job { uint64_t seed; int mode, rc; };
 static void *worker(void *p) {
   struct job *j = (struct job *)p;
@@ -165,6 +239,8 @@ int main(void) {
   for (i = 0; i < 2; ++i) pthread_join(th[i], NULL);
   for (i = 0; i < 2; ++i)
     if (jobs[i].rc) return jobs[i].rc;
+  /* 5. the lasso's device gate against a bootstrapping context */
+  if ((rc = gate())) return rc;
   printf("dfm_threads OK\n");
   fflush(stdout);
   /* leave without the ROCm runtimes' exit-time teardown: under ASan its

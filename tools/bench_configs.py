@@ -69,6 +69,21 @@ def c1(D, ctx, args):
     return rec
 
 
+def chow_pmc_bytes():
+    """DRAM bytes per chow_all_kernel launch from the latest committed C2 PMC
+    passes (profiles/rNN_pmc_traffic_c2.json, tools/pmc_traffic.py), with the
+    launch's replicate count; None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_c2.json")))
+    if not files:
+        return None
+    rec = json.load(open(files[-1]))
+    for k, v in rec.items():
+        if k.startswith("chow_all_kernel"):
+            return {"hbm_bytes_per_launch": v.get("hbm_bytes_per_launch"), "source": os.path.basename(files[-1])}
+    return None
+
+
 def c2(D, ctx, args):
     import torch
     rng = np.random.default_rng(20261015 + 2)
@@ -116,14 +131,23 @@ def c2(D, ctx, args):
                                 "bound": "mfma", "achieved": round(flop / (gms * 1e-3) / 1e12, 3), "peak": 78.6,
                                 "unit": "TFLOP/s", "frac": round(flop / (gms * 1e-3) / 1e12 / 78.6, 4),
                                 "avg_launch_ms": round(gms / gn, 4), "flop_per_replicate": N * (N + 1) * T}
-    # Chow pass: two reads of X* (gathered rows of C + eta E) per replicate
+    # Chow pass, labelled by its measured bound: fp64 VALU.  Per
+    # (replicate, variable) and row t, pass A forms e = x - F_t l (r FMA), ||e||^2
+    # (1) and F_t'x (r); pass B the subperiod residuals u, rs (2 r), ssr (1),
+    # u^2 z_t (r) and the HC0 block's r (r + 1) / 2 sums: 5 r + 2 + r (r + 1) / 2
+    # FMA = 2 x that in flop.  Its DRAM traffic (PMC FETCH_SIZE / WRITE_SIZE,
+    # profiles/*_pmc_traffic_c2.json) is far below HBM peak: the gathered x rows
+    # come from the L2-resident C and E panels.
     cms, cn = tm.get("chow", (0.0, 0))
     if cn:
-        by = B * (args.reps + 1) * 2 * T * N * 8
-        rec["roofline_chow"] = {"kernel": "chow_prep + chow_all_kernel", "bound": "hbm",
-                                "achieved": round(by / (cms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
-                                "frac": round(by / (cms * 1e-3) / 1e9 / 8000.0, 4),
-                                "bytes_per_replicate": 2 * T * N * 8}
+        r = model.number_of_factors
+        fl = B * (args.reps + 1) * N * T * 2 * (5 * r + 2 + r * (r + 1) // 2)
+        tf = fl / (cms * 1e-3) / 1e12
+        rec["roofline_chow"] = {"kernel": "chow_prep + chow_all_kernel", "bound": "valu (fp64)",
+                                "achieved": round(tf, 3), "peak": 78.6, "unit": "TFLOP/s",
+                                "frac": round(tf / 78.6, 4),
+                                "flop_per_replicate": N * T * 2 * (5 * r + 2 + r * (r + 1) // 2),
+                                "traffic": chow_pmc_bytes()}
     if args.cpu:
         O = oracle()
         o = O.DynamicFactorModel_ic(y, w, x, "ICp2", kmax=8)
