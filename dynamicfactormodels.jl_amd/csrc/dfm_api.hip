@@ -330,10 +330,12 @@ struct dfm_model {
   // dfm_chow: the all-variables statistics of the last break period asked for
   int64_t chow_bp = -1;
   std::vector<double> chow_cache;   // LR (N), LM (N), Wald (N)
-  // second lane of small factored bootstrap jobs (dfm_bootstrap_dev): a clone
-  // of this fit on its own context / stream of the same device, made on first use
-  dfm_model *lane = nullptr;
-  LaneWorker *lane_worker = nullptr;
+  // the extra lanes of small factored bootstrap jobs (dfm_bootstrap_dev):
+  // clones of this fit, each on its own context / stream of the same device
+  // and driven by its own host thread, made on first use
+  static constexpr int kMaxLanes = 4;
+  dfm_model *lane[kMaxLanes - 1] = {};
+  LaneWorker *lane_worker[kMaxLanes - 1] = {};
   bool is_lane = false;
   dfm_ctx *count_ctx = nullptr;   // a lane counts its GEMM products into its parent's context
 };
@@ -735,13 +737,15 @@ extern "C" {
 
 int dfm_model_destroy(dfm_model *m) {
   if (!m) return -1;
-  delete m->lane_worker;
-  m->lane_worker = nullptr;
-  if (m->lane) {   // the lane model, then its context (the model held the last reference but one)
-    dfm_ctx *lc = m->lane->ctx;
-    dfm_model_destroy(m->lane);
-    dfm_ctx_destroy(lc);
-    m->lane = nullptr;
+  for (int j = 0; j < dfm_model::kMaxLanes - 1; ++j) {
+    delete m->lane_worker[j];
+    m->lane_worker[j] = nullptr;
+    if (m->lane[j]) {   // the lane model, then its context (the model held the last reference but one)
+      dfm_ctx *lc = m->lane[j]->ctx;
+      dfm_model_destroy(m->lane[j]);
+      dfm_ctx_destroy(lc);
+      m->lane[j] = nullptr;
+    }
   }
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
@@ -1248,31 +1252,36 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
 // per-replicate passes (y2, Rayleigh-Ritz, ap2, Chebyshev, Chow: one
 // workgroup or one wave per replicate) run ~1 round of the resident slots or
 // less, and every launch gap and convergence poll is exposed.  Such jobs run
-// as two lanes — the halves of the replicate range on two streams, each
-// driven by its own host thread — so one lane's latency-bound passes overlap
-// the other's GEMMs (measured at C3 with two Python-driven contexts: 1 250
-// replicates 4.12 -> 3.76 ms, 2 500: 6.96 -> 6.55 ms; 9 999 gains < 2 % and
-// stays one lane, keeping its kernels' timings solo).  Every kernel is
+// as lanes — contiguous parts of the replicate range on their own streams,
+// each driven by its own host thread — so one lane's latency-bound passes
+// overlap another's GEMMs (measured at C3 with two Python-driven contexts:
+// 1 250 replicates 4.12 -> 3.76 ms, 2 500: 6.96 -> 6.55 ms; 9 999 gains < 2 %
+// and stays one lane, keeping its kernels' timings solo).  Every kernel is
 // batch-invariant (a replicate's result never depends on its batch), so the
 // rows are bit-identical to one lane (tests/test_gpu_multi.py).
 constexpr int64_t kLaneMin = 512, kLaneMax = 6000;
-static bool lane_split(const dfm_model *M, int64_t B, const dfm_stat *stats, int ns) {
-  // DFM_NO_LANES=1 (diagnostic): one lane, so a kernel trace shows solo durations
+static int lane_count(const dfm_model *M, int64_t B, const dfm_stat *stats, int ns) {
+  // DFM_NO_LANES=1 (diagnostic): one lane, so a kernel trace shows solo durations;
+  // DFM_LANES=n (A/B): n lanes (1..4) wherever lanes apply
   static const bool no_lanes = [] { const char *e = getenv("DFM_NO_LANES"); return e && atoi(e) != 0; }();
-  if (no_lanes) return false;
-  if (M->is_lane || M->batch != 0 || B < kLaneMin || B > kLaneMax || ns < 0 || (ns > 0 && !stats)) return false;
+  static const int forced = [] { const char *e = getenv("DFM_LANES"); return e ? atoi(e) : 0; }();
+  if (no_lanes) return 1;
+  if (M->is_lane || M->batch != 0 || B < kLaneMin || B > kLaneMax || ns < 0 || (ns > 0 && !stats)) return 1;
   const int p = eig_block_p(M->m, M->r, M->ctx->block);
-  if (p > 32 || p < M->r) return false;
+  if (p > 32 || p < M->r) return 1;
   for (int i = 0; i < ns; ++i)
-    if (stats[i].kind < 0 || stats[i].kind > DFM_STAT_LOADINGS) return false;
-  return M->r <= 16;   // the subspace solver's paths (not the dense / GEMM-built wide ones)
+    if (stats[i].kind < 0 || stats[i].kind > DFM_STAT_LOADINGS) return 1;
+  if (M->r > 16) return 1;   // the subspace solver's paths (not the dense / GEMM-built wide ones)
+  if (forced > 0) return std::min(forced, dfm_model::kMaxLanes);
+  return 2;
 }
 
-static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx, const double *eta,
+static int bootstrap_lanes(dfm_model *M, int nl, int kind, int64_t B, const int32_t *idx, const double *eta,
                            const dfm_stat *stats, int ns, double *out) {
   dfm_ctx *ctx = M->ctx;
   hipSetDevice(ctx->device);
-  if (!M->lane) {
+  for (int j = 0; j < nl - 1; ++j) {
+    if (M->lane[j]) continue;
     dfm_ctx *lc = nullptr;
     int rc = dfm_ctx_create(ctx->device, &lc);
     if (rc) return fail(ctx, 1002, "bootstrap lane: no context (%d)", rc);
@@ -1285,55 +1294,67 @@ static int bootstrap_lanes(dfm_model *M, int kind, int64_t B, const int32_t *idx
     }
     L->is_lane = true;
     L->count_ctx = ctx;
-    M->lane = L;
-    M->lane_worker = new LaneWorker();
+    M->lane[j] = L;
+    M->lane_worker[j] = new LaneWorker();
   }
-  dfm_model *L = M->lane;
-  dfm_ctx *lc = L->ctx;
-  lc->tol = ctx->tol; lc->tol_values = ctx->tol_values; lc->maxit = ctx->maxit;
-  lc->block = ctx->block; lc->poll = ctx->poll; lc->timing = ctx->timing;
-  L->mode = M->mode;
-  // the lane's work starts after the caller's work on the main stream (its
-  // inputs).  Measured and rejected: starting it half a step late (an event
-  // after the first lane's first eigen-iteration product), so the lanes'
-  // GEMMs and latency-bound passes alternate instead of running in lock-step:
-  // C3 1 250 replicates 3.81 -> 3.93 ms, C2 283 k -> 265 k replicates/s
+  // the lanes' work starts after the caller's work on the main stream (its
+  // inputs).  Measured and rejected: starting the second lane half a step
+  // late (an event after the first lane's first eigen-iteration product), so
+  // the lanes' GEMMs and latency-bound passes alternate instead of running in
+  // lock-step: C3 1 250 replicates 3.81 -> 3.93 ms, C2 283 k -> 265 k
   if (!ctx->gate) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->gate, hipEventDisableTiming));
   HIPCHK(ctx, hipEventRecord(ctx->gate, ctx->stream));
-  HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ctx->gate, 0));
+  for (int j = 0; j < nl - 1; ++j) {
+    dfm_ctx *lc = M->lane[j]->ctx;
+    lc->tol = ctx->tol; lc->tol_values = ctx->tol_values; lc->maxit = ctx->maxit;
+    lc->block = ctx->block; lc->poll = ctx->poll; lc->timing = ctx->timing;
+    M->lane[j]->mode = M->mode;
+    HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ctx->gate, 0));
+  }
 #ifdef DFM_DEBUG_MEM
   if (const int sk = dbg_lane_skew_us()) {   // wall clock: 100 ticks per microsecond
-    hipLaunchKernelGGL(dbg_spin_kernel, dim3(1), dim3(64), 0, sk > 0 ? lc->stream : ctx->stream,
+    hipLaunchKernelGGL(dbg_spin_kernel, dim3(1), dim3(64), 0, sk > 0 ? M->lane[0]->ctx->stream : ctx->stream,
                        (long long)std::abs(sk) * 100);
     fprintf(stderr, "[dfm debug] lane skew %d us\n", sk);
   }
 #endif
-  const int64_t width = dfm_stats_width(M, stats, ns), T = M->T, h = (B + 1) / 2;
-  int rc1 = 0;
-  M->lane_worker->run([&]() {
-    hipSetDevice(lc->device);
-    rc1 = bootstrap_one(L, kind, B - h, idx + h * T, eta ? eta + h * T : nullptr, stats, ns,
-                        out ? out + h * width : nullptr);
-  });
-  const int rc0 = bootstrap_one(M, kind, h, idx, eta, stats, ns, out);
-  M->lane_worker->wait();
-  // the lane's host-side counters and kernel timings join the caller's context
-  // (its device-side GEMM-product counts went to ctx->cnt_dev directly)
-  if (lc->timing) {
-    harvest(lc);
-    for (int i = 0; i < DFM_KC_COUNT; ++i) {
-      ctx->ms[i] += lc->ms[i]; ctx->launches[i] += lc->launches[i];
-      lc->ms[i] = 0; lc->launches[i] = 0;
-    }
+  // lane j takes replicates [b_j, b_{j+1}), b_j = ceil(j B / nl) (lane 0 = this thread)
+  const int64_t width = dfm_stats_width(M, stats, ns), T = M->T;
+  auto b_at = [&](int j) { return (j * B + nl - 1) / nl; };
+  int rcl[dfm_model::kMaxLanes] = {};
+  for (int j = 1; j < nl; ++j) {
+    dfm_model *L = M->lane[j - 1];
+    const int64_t b0 = b_at(j), b1 = b_at(j + 1);
+    int *rc = &rcl[j];
+    M->lane_worker[j - 1]->run([=]() {
+      hipSetDevice(L->ctx->device);
+      *rc = bootstrap_one(L, kind, b1 - b0, idx + b0 * T, eta ? eta + b0 * T : nullptr, stats, ns,
+                          out ? out + b0 * width : nullptr);
+    });
   }
-  ctx->eig_batches += lc->eig_batches;
-  ctx->eig_iters += lc->eig_iters;
-  ctx->eig_iters_max = std::max(ctx->eig_iters_max, lc->eig_iters_max);
-  ctx->rep_iters += lc->rep_iters;
-  ctx->gemm_products += lc->gemm_products;
-  lc->eig_batches = lc->eig_iters = lc->eig_iters_max = lc->rep_iters = lc->gemm_products = 0;
-  if (rc0) return rc0;
-  if (rc1) return fail(ctx, rc1, "bootstrap lane: %s", lc->err.c_str());
+  rcl[0] = bootstrap_one(M, kind, b_at(1), idx, eta, stats, ns, out);
+  for (int j = 1; j < nl; ++j) M->lane_worker[j - 1]->wait();
+  // the lanes' host-side counters and kernel timings join the caller's context
+  // (their device-side GEMM-product counts went to ctx->cnt_dev directly)
+  for (int j = 0; j < nl - 1; ++j) {
+    dfm_ctx *lc = M->lane[j]->ctx;
+    if (lc->timing) {
+      harvest(lc);
+      for (int i = 0; i < DFM_KC_COUNT; ++i) {
+        ctx->ms[i] += lc->ms[i]; ctx->launches[i] += lc->launches[i];
+        lc->ms[i] = 0; lc->launches[i] = 0;
+      }
+    }
+    ctx->eig_batches += lc->eig_batches;
+    ctx->eig_iters += lc->eig_iters;
+    ctx->eig_iters_max = std::max(ctx->eig_iters_max, lc->eig_iters_max);
+    ctx->rep_iters += lc->rep_iters;
+    ctx->gemm_products += lc->gemm_products;
+    lc->eig_batches = lc->eig_iters = lc->eig_iters_max = lc->rep_iters = lc->gemm_products = 0;
+  }
+  if (rcl[0]) return rcl[0];
+  for (int j = 1; j < nl; ++j)
+    if (rcl[j]) return fail(ctx, rcl[j], "bootstrap lane %d: %s", j, M->lane[j - 1]->ctx->err.c_str());
   return 0;
 }
 
@@ -1341,8 +1362,8 @@ int dfm_bootstrap_dev(dfm_model *M, int kind, int64_t B, const int32_t *idx, con
                       const dfm_stat *stats, int ns, double *out) {
   if (!M) return -1;
   DeviceShare gate(M->ctx->device);
-  if (idx && (kind != DFM_BOOT_WILD || eta) && lane_split(M, B, stats, ns))
-    return bootstrap_lanes(M, kind, B, idx, eta, stats, ns, out);
+  const int nl = idx && (kind != DFM_BOOT_WILD || eta) ? lane_count(M, B, stats, ns) : 1;
+  if (nl > 1) return bootstrap_lanes(M, nl, kind, B, idx, eta, stats, ns, out);
   return bootstrap_one(M, kind, B, idx, eta, stats, ns, out);
 }
 

@@ -886,7 +886,7 @@ thread_local int g_last_iters = 0;   // iterations run by the last eig_run / eig
 // the H.Z GEMM in the factored solver) that still had an unconverged
 // replicate: the algorithmic work the roofline figure is priced on.
 thread_local int64_t g_last_rep_iters = 0;
-thread_local int64_t g_last_gemm_products = 0;   // replicate-products H . Z of the last factored run (both Chebyshev GEMMs)
+thread_local int64_t g_last_gemm_products = 0;   // replicate-products of the last run: H . Z (factored, both Chebyshev GEMMs) or G S (fused direct solver)
 
 // Sum of the unconverged-replicate counts seen by the products of iterations
 // 0..last (shift = 1: the product of iteration it runs before that
@@ -1348,10 +1348,15 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
       for (int i = 0; i <= maxit; ++i)
         if (a[i] == 0) { last = i; break; }
       g_last_iters = last;
-      int64_t s = 0;
-      for (int i = 0; i <= std::min(last, maxit - 1); ++i) s += a[i];
+      // a[i] replicates took Rayleigh-Ritz step i, each with dg(i) products
+      // G S (Y = G Q and the filter's dg - 1 Horner steps)
+      int64_t s = 0, prods = 0;
+      for (int i = 0; i <= std::min(last, maxit - 1); ++i) {
+        s += a[i];
+        prods += (int64_t)a[i] * ((warm_strict && i < 4) ? kChebDirectStrict : 2);
+      }
       g_last_rep_iters = s;
-      g_last_gemm_products = s;
+      g_last_gemm_products = prods;
       if (prof) {
         long long h[24];
         hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost);

@@ -69,17 +69,17 @@ def c1(D, ctx, args):
     return rec
 
 
-def chow_pmc_bytes():
-    """DRAM bytes per chow_all_kernel launch from the latest committed C2 PMC
-    passes (profiles/rNN_pmc_traffic_c2.json, tools/pmc_traffic.py), with the
-    launch's replicate count; None when absent."""
+def c2_pmc_bytes(prefix):
+    """DRAM bytes per launch of the C2 kernel named `prefix` from the latest
+    committed C2 PMC passes (profiles/rNN_pmc_traffic_c2.json,
+    tools/pmc_traffic.py; one launch = one 500-replicate lane); None when absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_c2.json")))
     if not files:
         return None
     rec = json.load(open(files[-1]))
     for k, v in rec.items():
-        if k.startswith("chow_all_kernel"):
+        if k.startswith(prefix):
             return {"hbm_bytes_per_launch": v.get("hbm_bytes_per_launch"), "source": os.path.basename(files[-1])}
     return None
 
@@ -138,6 +138,24 @@ def c2(D, ctx, args):
     # FMA = 2 x that in flop.  Its DRAM traffic (PMC FETCH_SIZE / WRITE_SIZE,
     # profiles/*_pmc_traffic_c2.json) is far below HBM peak: the gathered x rows
     # come from the L2-resident C and E panels.
+    # Fused direct eigensolver (eig_fused_kernel, class eig_gq): MFMA products
+    # G S of the replicate's m x m Gram with the 16-column block, 2 m^2 16 flop
+    # each; dfm_ctx_gemm_products counts them exactly (a[i] replicates at
+    # Rayleigh-Ritz step i, dg(i) products each).  A per-replicate latency
+    # chain (one workgroup per replicate): the frac says how far from the MFMA
+    # peak that chain runs, the PMC bytes that it is not HBM-bound either.
+    ems, en = tm.get("eig_gq", (0.0, 0))
+    if en and es.get("gemm_products"):
+        m = min(T, N)
+        fl = 2.0 * m * m * 16 * es["gemm_products"]
+        tf = fl / (ems * 1e-3) / 1e12
+        rec["roofline_eig_fused"] = {"kernel": "eig_fused_kernel (one workgroup per replicate, Q and Y in LDS, "
+                                               "G streamed from L2/MALL, v_mfma_f64_4x4x4_4b)",
+                                     "bound": "mfma (latency chain)", "achieved": round(tf, 3), "peak": 78.6,
+                                     "unit": "TFLOP/s", "frac": round(tf / 78.6, 4),
+                                     "products_per_replicate": round(es["gemm_products"] / (B * (args.reps + 1)), 2),
+                                     "flop_per_product": 2 * m * m * 16,
+                                     "traffic": c2_pmc_bytes("eig_fused_kernel")}
     cms, cn = tm.get("chow", (0.0, 0))
     if cn:
         r = model.number_of_factors
@@ -147,7 +165,7 @@ def c2(D, ctx, args):
                                 "achieved": round(tf, 3), "peak": 78.6, "unit": "TFLOP/s",
                                 "frac": round(tf / 78.6, 4),
                                 "flop_per_replicate": N * T * 2 * (5 * r + 2 + r * (r + 1) // 2),
-                                "traffic": chow_pmc_bytes()}
+                                "traffic": c2_pmc_bytes("chow_all_kernel")}
     if args.cpu:
         O = oracle()
         o = O.DynamicFactorModel_ic(y, w, x, "ICp2", kmax=8)
