@@ -176,10 +176,10 @@ static void lasso_problem(double *G, double *c, uint8_t *ju, double *alm) {
   for (k = 1; k < LL_; ++k) alm[k] = alm[k - 1] * 0.85;
 }
 
-struct gate_job { volatile int stop; int rc, runs; };
+struct gate_job { int stop, rc, runs; };   /* stop: __atomic loads / stores */
 static void *boot_loop(void *p) {
   struct gate_job *g = (struct gate_job *)p;
-  while (!g->stop && !g->rc) {
+  while (!__atomic_load_n(&g->stop, __ATOMIC_ACQUIRE) && !g->rc) {
     g->rc = lanes_vs_one(21 + g->runs, g->runs & 1);
     ++g->runs;
   }
@@ -199,13 +199,13 @@ static int gate(void) {
   pthread_create(&th, NULL, boot_loop, &g);
   for (k = 0; k < 8; ++k) {
     int rc = dfm_lasso_path(ctx, G, c, ju, LP_, alm, LL_, 0, 1e-7, b1, r1, &L1);
-    if (rc) { fprintf(stderr, "gate: lasso call %d -> %d: %s\n", k, rc, dfm_last_error(ctx)); g.stop = 1; pthread_join(th, NULL); return 1; }
+    if (rc) { fprintf(stderr, "gate: lasso call %d -> %d: %s\n", k, rc, dfm_last_error(ctx)); __atomic_store_n(&g.stop, 1, __ATOMIC_RELEASE); pthread_join(th, NULL); return 1; }
     if (L1 != L0 || memcmp(b0, b1, (size_t)L0 * LP_ * 8) || memcmp(r0, r1, (size_t)L0 * 8)) {
       fprintf(stderr, "gate: lasso call %d differs from the solo path\n", k);
-      g.stop = 1; pthread_join(th, NULL); return 1;
+      __atomic_store_n(&g.stop, 1, __ATOMIC_RELEASE); pthread_join(th, NULL); return 1;
     }
   }
-  g.stop = 1;
+  __atomic_store_n(&g.stop, 1, __ATOMIC_RELEASE);
   pthread_join(th, NULL);
   dfm_ctx_destroy(ctx);
   if (g.rc) return g.rc;
