@@ -1504,7 +1504,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
                                                         const double *__restrict__ eta, int *__restrict__ off,
                                                         int *__restrict__ lst, double *__restrict__ trace,
                                                         double *__restrict__ PF, double *__restrict__ E2) {
-  extern __shared__ int sh[];   // cnt[T+1], six[T]
+  extern __shared__ int sh[];   // cnt[T+1], six[T], sorted list L[T]
   __shared__ double red[256];
   __shared__ int scan[256];
   const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
@@ -1536,7 +1536,9 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   // placement: LDS atomics hand out slots inside each bucket (any order),
   // then each bucket is insertion-sorted by t — ascending t per bucket, the
   // serial counting sort's order, in O(T) work (buckets are short)
-  int *L = lst + (int64_t)rep * T;
+  // (in LDS, then one coalesced copy out: the shifts of a sort in global
+  // memory were chains of dependent global round trips)
+  int *L = sh + 2 * T + 1;
   for (int t = tid; t < T; t += 256) L[atomicAdd(&cnt[six[t]], 1)] = t;
   __syncthreads();   // cnt[s] is now the END of bucket s; L visible workgroup-wide
   for (int s = tid; s < T; s += 256) {
@@ -1548,6 +1550,8 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       L[j + 1] = v;
     }
   }
+  __syncthreads();
+  for (int t = tid; t < T; t += 256) lst[(int64_t)rep * T + t] = L[t];
   if (PF)   // P'D F (row stride r) and P'D^2 1 of the middle Horner steps (boot_cheb_mid_kernel):
     for (int s = tid; s < T; s += 256) {   // this thread's own sorted buckets, t ascending
       const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
@@ -2713,7 +2717,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     dim3 grid((unsigned)((n + 255) / 256), 1);
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0);
     hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
-    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(2 * m + 1) * 4, st, fb, idx, eta,
+    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(3 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace, mid ? PFb : nullptr, E2b);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
                        0.0, 0.0, eta,
