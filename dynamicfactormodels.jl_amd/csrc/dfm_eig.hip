@@ -1910,8 +1910,12 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
     double2 qv[PER / 2], yv[PER / 2];
 #pragma unroll
     for (int j = 0; j < PER / 2; ++j) {
+#ifdef DFM_AP2_DIAG_NOLOAD   // (timing diagnostic, WRONG results: no Q / Y tile loads)
+      qv[j] = double2{1e-3 * (tc + j), 1e-3 * c0}; yv[j] = double2{1e-3 * c0, 1e-3 * (tc - j)};
+#else
       qv[j] = *reinterpret_cast<const double2 *>(Qr + (int64_t)tc * P + c0 + 2 * j);
       yv[j] = *reinterpret_cast<const double2 *>(Yr + (int64_t)tc * P + c0 + 2 * j);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < PER / 2; ++j) {
