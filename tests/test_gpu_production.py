@@ -149,6 +149,9 @@ def test_c5_full_panel_windows_match_frozen_oracle(dfm, oracle):
         assert rel(out["eigenvalues"][wi][:8], g["eigvals"][k]) < STAT_RTOL
         assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < STAT_RTOL            # intercept: sign-free
         assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < STAT_RTOL
+        # factor columns in absolute value (eigenvector signs are arbitrary)
+        assert rel(np.abs(out["coefficients"][wi][1:1 + r]), np.abs(g["coef"][k][1:1 + r])) < STAT_RTOL, wi
+        assert rel(np.abs(out["t_stats"][wi][1:1 + r]), np.abs(g["tstat"][k][1:1 + r])) < STAT_RTOL, wi
 
 
 def test_c2_b999_two_lane_job_sampled_replicates_match_oracle(dfm, oracle):
@@ -220,6 +223,9 @@ def test_c5_full_panel_rolling_windows_match_frozen_oracle(dfm, oracle):
         assert rel(out["eigenvalues"][wi][:8], g["eigvals"][k]) < STAT_RTOL
         assert rel(out["t_stats"][wi][:1], g["tstat"][k][:1]) < STAT_RTOL            # intercept: sign-free
         assert rel(out["coefficients"][wi][:1], g["coef"][k][:1]) < STAT_RTOL
+        # factor columns in absolute value (eigenvector signs are arbitrary)
+        assert rel(np.abs(out["coefficients"][wi][1:1 + r]), np.abs(g["coef"][k][1:1 + r])) < STAT_RTOL, wi
+        assert rel(np.abs(out["t_stats"][wi][1:1 + r]), np.abs(g["tstat"][k][1:1 + r])) < STAT_RTOL, wi
 
 
 def test_c4_full_panel_per_candidate_matches_oracle(dfm, oracle):
