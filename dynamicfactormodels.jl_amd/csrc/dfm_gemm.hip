@@ -285,10 +285,20 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
     if (RUN) {
       double *la = stage, *lb = stage + GT * G2_KS;
       const int c0 = (2 * wave) * 128, c1 = c0 + 128;
-      __builtin_amdgcn_global_load_lds((gbl_void_t *)pa0, (lds_void_t *)(la + c0), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t *)pb0, (lds_void_t *)(lb + c0), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t *)pa1, (lds_void_t *)(la + c1), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void_t *)pb1, (lds_void_t *)(lb + c1), 16, 0, 0);
+#if defined(DFM_GEMM_DIAG_AONLY)   // (timing diagnostic, WRONG results: B tiles not re-staged after the first stages)
+      const bool fb = s < NBUF;
+#else
+      const bool fb = true;
+#endif
+#if defined(DFM_GEMM_DIAG_BONLY)   // (timing diagnostic, WRONG results: A tiles not re-staged after the first stages)
+      const bool fa = s < NBUF;
+#else
+      const bool fa = true;
+#endif
+      if (fa) __builtin_amdgcn_global_load_lds((gbl_void_t *)pa0, (lds_void_t *)(la + c0), 16, 0, 0);
+      if (fb) __builtin_amdgcn_global_load_lds((gbl_void_t *)pb0, (lds_void_t *)(lb + c0), 16, 0, 0);
+      if (fa) __builtin_amdgcn_global_load_lds((gbl_void_t *)pa1, (lds_void_t *)(la + c1), 16, 0, 0);
+      if (fb) __builtin_amdgcn_global_load_lds((gbl_void_t *)pb1, (lds_void_t *)(lb + c1), 16, 0, 0);
       pa0 += G2_KS; pa1 += G2_KS; pb0 += bstep; pb1 += bstep;
     } else {
       g2_issue(stage, A, B, ldb, src, s * G2_KS, K);
