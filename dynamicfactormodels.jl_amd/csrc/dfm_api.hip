@@ -106,7 +106,7 @@ int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, 
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
                      timer_fn tf, void *tctx, int *off, int *lst, long long *cnt = nullptr, int subspace = 0,
-                     double spread = 0.0);
+                     double spread = 0.0, const PollBuf *pb = nullptr);
 size_t fact_workspace_bytes(int T, int nb, int P);
 int fact_t_max();
 int fact_loadings(const FactBase &fb, const double *Ep, int64_t ld, int N, const double *Lb,
@@ -170,7 +170,9 @@ struct dfm_ctx {
   size_t warena_cap = 0, warena_need = 0;
   hipEvent_t gate = nullptr;   // bootstrap_lanes: the second lane starts behind the caller's prior work
   hipMemPool_t mpool = nullptr;  // this context's stream-ordered scratch (stream_malloc)
+  PollBuf pollbuf;               // pinned convergence read-backs of the factored solver (host == nullptr: none)
 };
+static const PollBuf *ctx_poll(const dfm_ctx *c) { return c->pollbuf.host ? &c->pollbuf : nullptr; }
 
 // stream -> the owning context's pool (stream_malloc); guarded: contexts are
 // created, re-streamed and destroyed from any host thread
@@ -309,6 +311,7 @@ struct dfm_model {
   size_t ws_bytes = 0;
   StatDesc *sd_dev = nullptr;
   int sd_cap = 0;
+  std::vector<StatDesc> sd_host;   // what sd_dev holds (uploaded only when a call's descriptors differ)
   int *flag_dev = nullptr;
   // factored bootstrap (N > T): H = E E', EL = E L, S = L'L, cF, hd
   int mode = 0;   // 0 auto, 1 direct Gram, 2 factored
@@ -468,6 +471,19 @@ int dfm_ctx_create(int device, dfm_ctx **out) {
     hipMemPool_t dp;
     if (hipDeviceGetDefaultMemPool(&dp, device) == hipSuccess) hipMemPoolSetAttribute(dp, hipMemPoolAttrReleaseThreshold, &keep);
   }
+  {   // the factored solver's look-ahead polls (without them it polls blocking)
+    PollBuf &pb = c->pollbuf;
+    constexpr int kCap = 4096;
+    if (hipHostMalloc((void **)&pb.host, kCap * sizeof(int), hipHostMallocDefault) == hipSuccess &&
+        hipEventCreateWithFlags(&pb.ev[0], hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&pb.ev[1], hipEventDisableTiming) == hipSuccess) {
+      pb.cap = kCap;
+    } else {
+      if (pb.ev[0]) hipEventDestroy(pb.ev[0]);
+      if (pb.host) hipHostFree(pb.host);
+      pb = PollBuf{};
+    }
+  }
   *out = c;
   return 0;
 }
@@ -488,6 +504,11 @@ static void ctx_release(dfm_ctx *ctx) {
   hipFree(ctx->cnt_dev);
   hipFree(ctx->warena);
   if (ctx->gate) hipEventDestroy(ctx->gate);
+  if (ctx->pollbuf.host) {
+    hipEventDestroy(ctx->pollbuf.ev[0]);
+    hipEventDestroy(ctx->pollbuf.ev[1]);
+    hipHostFree(ctx->pollbuf.host);
+  }
   if (ctx->mpool) {
     pool_unregister(ctx->mpool);
     hipMemPoolDestroy(ctx->mpool);
@@ -1530,11 +1551,23 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
     hipFree(M->sd_dev);
     HIPCHK(ctx, dalloc(&M->sd_dev, ns));
     M->sd_cap = ns;
+    M->sd_host.clear();
   }
-  if (ns) HIPCHK(ctx, hipMemcpyAsync(M->sd_dev, sd.data(), ns * sizeof(StatDesc), hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipMemsetAsync(M->flag_dev, 0, 4, st));
+  // the descriptors go up only when they change: a pageable upload per call
+  // was a host round trip in front of every small job's first kernel
+  if (ns && (M->sd_host.size() != (size_t)ns || memcmp(M->sd_host.data(), sd.data(), ns * sizeof(StatDesc)) != 0)) {
+    M->sd_host.clear();
+    HIPCHK(ctx, hipMemcpyAsync(M->sd_dev, sd.data(), ns * sizeof(StatDesc), hipMemcpyHostToDevice, st));
+    M->sd_host = sd;
+  }
   BootWs w;
   boot_ws_bytes(M, (int)nb, P, ctx->maxit, chow && !chow_wide, fact, &w, M->ws);
+  {   // the status flag, and the OLS status rows no OLS pass writes: one launch
+    ZeroSpans zs{};
+    zs.p[0] = M->flag_dev; zs.n[0] = 1;
+    if (!need_ols) { zs.p[1] = w.ost; zs.n[1] = nb; }
+    HIPCHK(ctx, launch_zero_spans(zs, st));
+  }
   // PCp: the unrestricted full-sample Gram of every replicate (no breaks,
   // src/criteria.jl:18), its spectrum, sigma^2 per replicate
   DevBuf pG, pEv, pWk, pSig, wDe, wX, wOls, wCh, wSc;
@@ -1596,7 +1629,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
                                 ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, need_fl ? w.Uk : nullptr, w.trace, w.status, st, timer_cb,
                                 ctx, w.off, w.lst,
-                                (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread);
+                                (M->count_ctx ? M->count_ctx : ctx)->cnt_dev, esub, spread, ctx_poll(ctx));
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
       note_iters(ctx);
       if (need_fl) {
@@ -1647,7 +1680,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       if (!done_f && (rc = factors_any(src, T, n, w.F, w.Uk, w.L))) return rc;
     }
     if (!need_ols) {
-      HIPCHK(ctx, hipMemsetAsync(w.ost, 0, (size_t)n * 4, st));   // (no design to be singular)
+      // (no design to be singular: w.ost zeroed at the top of the call)
     } else if (q + r <= 32) {
       Scope sc(ctx, DFM_KC_OLS);
       launch_ols(n, st, M->y, M->w, q, w.F, T, r, nullptr, nullptr, w.coef,
@@ -2428,7 +2461,7 @@ static int windows_impl(dfm_ctx *ctx, const double *y, const double *w, int q, i
       HIPCHK(ctx, hipMemsetAsync(zero, 0, (size_t)T * 8, st));
       FactBase fb{T, 0, ldH, zero, zero, zero, H, zero, hd};
       rc = eig_run_factored(fb, didx, deta, P, kmax, p, nullptr, 0, ctx->tol, ctx->maxit, ctx->poll, ews, fws,
-                            lam, Uk, tr, stt, st, timer_cb, ctx, off, lst);
+                            lam, Uk, tr, stt, st, timer_cb, ctx, off, lst, nullptr, 0, 0.0, ctx_poll(ctx));
       if (rc) return fail(ctx, rc > 0 ? rc : -21, "eigensolver failed (%d)", rc);
     } else if (orient == 0) {
       // T > the factored solver's range: the windows' masked T x T Grams in

@@ -77,6 +77,25 @@ inline void dbg_poison_async(void *p, size_t bytes, hipStream_t st) {
 // the device's default pool.  Debug builds poison the block.
 hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st);
 
+// Zero up to four spans of 32-bit words in ONE launch (a call's counters,
+// flags and padding rows: each separate memset was a host API round of a few
+// microseconds in the lanes' prologues, with the GPU idle behind it).
+struct ZeroSpans {
+  int *p[4];
+  int64_t n[4];   // words; 0 = unused
+};
+hipError_t launch_zero_spans(const ZeroSpans &z, hipStream_t st);
+
+// A context's pinned read-back slots for the factored solver's convergence
+// polls (eig_run_factored): the active count of iteration it is copied into
+// host[it] behind event ev[it & 1] while the next iteration is already
+// queued, so the GPU never waits on the host's decision.
+struct PollBuf {
+  int *host = nullptr;   // hipHostMalloc'd, cap ints
+  int cap = 0;
+  hipEvent_t ev[2] = {};
+};
+
 // The device gate.  The lasso path kernel needs every workgroup of a grid
 // sized to the whole chip co-resident (leader/helper hand-offs); a kernel of
 // another libdfm context on the same device would hold CUs and make its

@@ -817,8 +817,10 @@ DFM_DEV void eig_final_body(const double *Ur, const double *theta, int done, int
 
 template <int P>
 __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
-                                                        double *__restrict__ Uk, int *__restrict__ status) {
+                                                        double *__restrict__ Uk, int *__restrict__ status,
+                                                        double *__restrict__ trace_out) {
   const int rep = blockIdx.x;
+  if (trace_out && threadIdx.x == 0) trace_out[rep] = w.trace[rep];   // (the caller's copy of trace(G))
   eig_final_body<P>(w.U + (int64_t)rep * m * P, w.small + (int64_t)rep * small_stride<P>() + 2 * P * P, w.done[rep],
                     rep, m, k, lam, Uk, status);
 }
@@ -1429,8 +1431,7 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
   g_last_rep_iters = count_rep_iters(w.active, std::min(it, maxit - 1), 0, nb, st);
   g_last_gemm_products = g_last_rep_iters;
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
-  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
-  if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status, trace_out);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
   if (iters_host) {
     hipMemcpyAsync(iters_host, w.iters, (size_t)nb * 4, hipMemcpyDeviceToHost, st);
@@ -2602,6 +2603,23 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
 // Ascending list of the still-active replicates (done == 0) and their count,
 // one 1024-thread workgroup: per-thread chunk counts, an LDS scan, in-order
 // writes.  Feeds the compacted H.Z GEMM of the straggler phase.
+__global__ __launch_bounds__(256) void zero_spans_kernel(ZeroSpans z) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    for (int64_t i = i0; i < z.n[s]; i += stride) z.p[s][i] = 0;
+}
+hipError_t launch_zero_spans(const ZeroSpans &z, hipStream_t st) {
+  int64_t mx = 0;
+  for (int s = 0; s < 4; ++s) mx = std::max<int64_t>(mx, z.p[s] ? z.n[s] : 0);
+  if (mx == 0) return hipSuccess;
+  ZeroSpans c = z;
+  for (int s = 0; s < 4; ++s)
+    if (!c.p[s]) c.n[s] = 0;
+  hipLaunchKernelGGL(zero_spans_kernel, dim3((unsigned)std::min<int64_t>(512, (mx + 255) / 256)), dim3(256), 0, st, c);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(1024) void active_list_kernel(const int *__restrict__ done, int nb,
                                                            int *__restrict__ list, int *__restrict__ count) {
   __shared__ int part[1024];
@@ -2676,7 +2694,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
                            const double *warm, int kw, double tol, int maxit, int poll, char *ws,
                            char *fws, double *lam, double *Uk, double *trace_out, int *status,
                            hipStream_t st, timer_fn tf, void *tctx, int *off, int *lst, long long *cnt,
-                           int subspace, double spread) {
+                           int subspace, double spread, const PollBuf *pb) {
   const int m = fb.T;
   EigWork w = carve(ws, m, nb, P, maxit);
   w.subspace = subspace;
@@ -2691,10 +2709,15 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // middle Horner steps' operands (fact_mid_doubles), after ab's region
   double *PFb = ab + (size_t)nb * ((m + EROWS - 1) / EROWS) * 2 * 32 * P + 512;
   double *E2b = PFb + (size_t)nb * m * 16, *FVb = E2b + (size_t)nb * m, *FtF = FVb + (size_t)nb * 16 * P;
-  if (z_rows(m) > m) hipMemsetAsync(Zc + (size_t)m * ldz, 0, (size_t)(z_rows(m) - m) * ldz * 8, st);
   const size_t lds = (size_t)m * 8 + (size_t)(2 * m + 1) * 4;
-  hipMemsetAsync(w.active, 0, (size_t)(maxit + 2) * 4, st);
-  hipMemsetAsync(w.iters, 0, (size_t)nb * 4, st);
+  {   // counters, flags and Z's zero k-padding rows: one launch
+    ZeroSpans zs{};
+    zs.p[0] = w.active; zs.n[0] = maxit + 2;
+    zs.p[1] = w.iters; zs.n[1] = nb;
+    zs.p[2] = w.done; zs.n[2] = nb;
+    if (z_rows(m) > m) { zs.p[3] = (int *)(Zc + (size_t)m * ldz); zs.n[3] = (int64_t)(z_rows(m) - m) * ldz * 2; }
+    if (launch_zero_spans(zs, st) != hipSuccess) return 1001;
+  }
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
   double *cur = w.Q, *alt = w.Y;
   const int cheb = 1;   // degree-2 Chebyshev filter between Rayleigh-Ritz steps
@@ -2720,7 +2743,6 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const int64_t n = (int64_t)m * P;
     dim3 grid((unsigned)((n + 255) / 256), 1);
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0);
-    hipMemsetAsync(w.done, 0, (size_t)nb * 4, st);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(3 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace, mid ? PFb : nullptr, E2b);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
@@ -2733,8 +2755,25 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
   shifted_cheb(d0, ca0);
   shifted_cheb(kChebD, ca1);
-  // first convergence poll right after the step most replicates retire at
-  int it = 0, last_gemm = -1, last_cheb = -1, next_poll = warm_started ? 1 : poll - 1;
+  // Convergence polls from the step most replicates retire at (first_poll)
+  // on.  After each such step the device rebuilds the list of active
+  // replicates (the GEMMs compact to it once it holds < 1/8 of the batch,
+  // decided on the device, so no host round trip sits in front of the
+  // straggler phase) and, with a pinned read-back buffer, the active count is
+  // copied to host[it] behind an event.  Outside the tail the host does not
+  // wait for it: it queues the next step first and reads the previous step's
+  // count then (one step of look-ahead — the GPU always has a step queued
+  // while the host decides; a step queued after the last replicate retired
+  // runs as a no-op and counts for nothing, its active count being 0).  In the
+  // straggler tail each step is short and most likely the last, so the count
+  // is awaited before the step's Chebyshev products, as a blocking poll
+  // (queued no-op steps cost more than the wait: 2.50 -> 2.58 ms per
+  // 1 250-replicate shard with look-ahead throughout).  Without the buffer: a
+  // blocking poll every `poll` steps, every step in the tail.
+  const int first_poll = warm_started ? 1 : poll - 1;
+  const bool ahead = pb && pb->host && pb->cap >= maxit + 2;
+  int it = 0, last_gemm = -1, last_cheb = -1, next_poll = first_poll, pend = -1, steps = -1;
+  bool tail = false;
   for (; it < maxit; ++it) {
     const int dg = it == 0 ? d0 : kChebD;
     const double *ca = it == 0 ? ca0 : ca1;
@@ -2760,20 +2799,35 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
                        it == maxit - 1 ? 1 : 0, cheb, ca[dg], ca[dg - 1], bb, eta, off, lst, qin, qs, alt, Zc, ldz,
                        pz, ab, seed);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
-    if (it == next_poll) {   // convergence poll, right after the step that retires replicates
-      int a = -1;
-      hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
-      e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return 1000 + (int)e;
-      if (a == 0) { ++it; break; }
-      // a straggler tail (< 1/8 of the batch active): poll every step, so the
-      // empty iterations after its last replicate retires are not launched,
-      // and compact the GEMMs to the stragglers' columns
-      const bool tail = (int64_t)a * 8 < nb;
-      next_poll = it + (tail ? 1 : poll);
-      if (tail && !cl_on) {
-        hipLaunchKernelGGL(active_list_kernel, dim3(1), dim3(1024), 0, st, w.done, nb, alist, acount);
-        cl_on = true;
+    if (it >= first_poll) {
+      if (ahead) {
+        if ((e = hipMemcpyAsync(pb->host + it, w.active + it, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipEventRecord(pb->ev[it & 1], st)) != hipSuccess)
+          return 1000 + (int)e;
+      }
+      hipLaunchKernelGGL(active_list_kernel, dim3(1), dim3(1024), 0, st, w.done, nb, alist, acount);
+      cl_on = true;
+      if (ahead) {
+        if (pend >= 0) {   // the previous step's count: this step is already queued behind it
+          if ((e = hipEventSynchronize(pb->ev[pend & 1])) != hipSuccess) return 1000 + (int)e;
+          const int a = pb->host[pend];
+          if (a == 0) { steps = pend + 1; ++it; break; }   // (this step ran as a no-op)
+          tail = (int64_t)a * 8 < nb;
+          pend = -1;
+        }
+        if (tail) {   // in the straggler tail: this step's count now, before its Chebyshev products
+          if ((e = hipEventSynchronize(pb->ev[it & 1])) != hipSuccess) return 1000 + (int)e;
+          const int a = pb->host[it];
+          if (a == 0) { ++it; break; }
+        } else {
+          pend = it;
+        }
+      } else if (it == next_poll) {
+        int a = -1;
+        hipMemcpyAsync(&a, w.active + it, 4, hipMemcpyDeviceToHost, st);
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return 1000 + (int)e;
+        if (a == 0) { ++it; break; }
+        next_poll = it + ((int64_t)a * 8 < nb ? 1 : poll);
       }
     }
     if (cheb && it < maxit - 1) {
@@ -2801,7 +2855,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     qin = cur;
     qs = (int64_t)m * P;
   }
-  g_last_iters = it;
+  if (steps < 0) steps = it;
+  g_last_iters = steps;
   // the Chebyshev GEMM of iteration it runs after that iteration's check
   if (cnt) {
     hipLaunchKernelGGL(count_iters_kernel, dim3(1), dim3(64), 0, st, w.active, last_gemm, last_cheb, nb, cnt,
@@ -2814,8 +2869,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     g_last_gemm_products = g_last_rep_iters + c0 * (d0 - 1) + (call - c0) * (kChebD - 1);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
-  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status);
-  if (trace_out) hipMemcpyAsync(trace_out, w.trace, (size_t)nb * 8, hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status, trace_out);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return 1000 + (int)e;
@@ -2825,14 +2879,15 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
 int eig_run_factored(const FactBase &fb, const int32_t *idx, const double *eta, int nb, int k, int p,
                      const double *warm, int kw, double tol, int maxit, int poll, char *ws, char *fws,
                      double *lam, double *Uk, double *trace_out, int *status, hipStream_t st,
-                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt, int subspace, double spread) {
+                     timer_fn tf, void *tctx, int *off, int *lst, long long *cnt, int subspace, double spread,
+                     const PollBuf *pb) {
   if (p < k || p > 32 || p > fb.T || fb.r > 32) return -1;
   if (fb.r > 16 || fb.T > F2_T_MAX) return -1;   // callers take the direct path
   if (p <= 16)
     return eig_run_fact2_t<16>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                               trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread);
+                               trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread, pb);
   return eig_run_fact2_t<32>(fb, idx, eta, nb, k, p, warm, kw, tol, maxit, poll, ws, fws, lam, Uk,
-                             trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread);
+                             trace_out, status, st, tf, tctx, off, lst, cnt, subspace, spread, pb);
 }
 int fact_t_max() { return F2_T_MAX; }
 

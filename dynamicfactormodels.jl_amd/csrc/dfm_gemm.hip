@@ -258,10 +258,23 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
   if (cb >= ncb) return;
   const int abase = rb * GT, bbase = cb * GT;
   // compacted launch (straggler phase): column block cb of the listed
-  // replicates' column groups only
+  // replicates' column groups only.  The list is rebuilt on the device after
+  // every convergence check; compaction applies once it holds < 1/8 of the
+  // batch (Nc / col_group replicates), decided here from its device-side
+  // count, so the host never waits for it.  Either way a column's sum runs in
+  // the same order: the bits do not depend on the mode.
   const int ccount = clist ? *ccount_p : 0;
-  if (clist && bbase >= ccount * col_group) return;
-  if (col_done && !clist) {
+  const bool compact = clist && (int64_t)ccount * 8 < Nc / col_group;
+  clist = compact ? clist : nullptr;
+  if (compact) {
+    if (bbase >= ccount * col_group) return;
+    if (col_done) {   // every listed replicate of the block retired since the list was built
+      bool all = true;
+      const int s0 = bbase / col_group, s1 = min(ccount - 1, (bbase + GT - 1) / col_group);
+      for (int q = s0; q <= s1; ++q) all = all && col_done[clist[q]];
+      if (all) return;
+    }
+  } else if (col_done) {
     bool all = true;
     const int r0 = bbase / col_group, r1 = min(Nc - 1, bbase + GT - 1) / col_group;
     for (int q = r0; q <= r1; ++q) all = all && col_done[q];
