@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -171,6 +173,10 @@ struct dfm_ctx {
   hipEvent_t gate = nullptr;   // bootstrap_lanes: the second lane starts behind the caller's prior work
   hipMemPool_t mpool = nullptr;  // this context's stream-ordered scratch (stream_malloc)
   PollBuf pollbuf;               // pinned convergence read-backs of the factored solver (host == nullptr: none)
+  // the bootstrap lanes' contexts whose kernel timings this context reports:
+  // merged when the timings are read (harvesting a lane's events after every
+  // call put ~30 hipEventElapsedTime calls between a timed job's steps)
+  std::vector<dfm_ctx *> kids;
 };
 static const PollBuf *ctx_poll(const dfm_ctx *c) { return c->pollbuf.host ? &c->pollbuf : nullptr; }
 
@@ -254,43 +260,61 @@ DeviceSolo::~DeviceSolo() {
 }  // namespace dfm
 
 // The host thread of a model's second bootstrap lane (bootstrap_lanes):
-// persistent, so a call costs a hand-off, not a thread start.
+// persistent, so a call costs a hand-off, not a thread start.  Both sides of
+// the hand-off spin briefly (kSpin) before blocking: in a run of jobs the next
+// job, and the lane's finish, come within microseconds, and a condition
+// variable wake-up (~10-20 us) sat in front of the lane's first kernel and
+// behind its last one on every call.
 struct LaneWorker {
+  static constexpr std::chrono::microseconds kSpin{200};
   std::mutex mu;
   std::condition_variable cv;
-  std::function<void()> job;
-  bool has = false, done = false, quit = false;
+  std::function<void()> job;   // guarded by mu
+  std::atomic<bool> has{false}, done{false}, quit{false};
   std::thread th;   // last: starts after the members it uses
   LaneWorker() : th([this] { loop(); }) {}
+  template <class F>
+  static void spin(F ready) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!ready() && std::chrono::steady_clock::now() - t0 < kSpin) __builtin_ia32_pause();
+  }
   void loop() {
-    std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv.wait(lk, [&] { return has || quit; });
-      if (quit) return;
-      std::function<void()> j = std::move(job);
-      has = false;
-      lk.unlock();
+      spin([&] { return has.load(std::memory_order_acquire) || quit.load(std::memory_order_acquire); });
+      std::function<void()> j;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return has.load() || quit.load(); });
+        if (quit.load()) return;
+        j = std::move(job);
+        has.store(false);
+      }
       j();
-      lk.lock();
-      done = true;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        done.store(true, std::memory_order_release);
+      }
       cv.notify_all();
     }
   }
   void run(std::function<void()> j) {
-    std::lock_guard<std::mutex> g(mu);
-    job = std::move(j);
-    has = true;
-    done = false;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      job = std::move(j);
+      done.store(false);
+      has.store(true, std::memory_order_release);
+    }
     cv.notify_all();
   }
   void wait() {
+    spin([&] { return done.load(std::memory_order_acquire); });
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done; });
+    cv.wait(lk, [&] { return done.load(); });
   }
   ~LaneWorker() {
     {
       std::lock_guard<std::mutex> g(mu);
-      quit = true;
+      quit.store(true);
     }
     cv.notify_all();
     th.join();
@@ -390,6 +414,17 @@ static void harvest(dfm_ctx *ctx) {
     ctx->pool.push_back(p.b);
   }
   ctx->pend.clear();
+}
+// a lane context's timings into its parent's (read / reset time, lane teardown)
+static void merge_kid(dfm_ctx *ctx, dfm_ctx *kid) {
+  harvest(kid);
+  for (int i = 0; i < DFM_KC_COUNT; ++i) {
+    ctx->ms[i] += kid->ms[i]; ctx->launches[i] += kid->launches[i];
+    kid->ms[i] = 0; kid->launches[i] = 0;
+  }
+}
+static void merge_kids(dfm_ctx *ctx) {
+  for (dfm_ctx *k : ctx->kids) merge_kid(ctx, k);
 }
 struct Scope {
   dfm_ctx *c; int cls;
@@ -546,11 +581,24 @@ int dfm_ctx_set_value_tol(dfm_ctx *ctx, double tol) {
 int dfm_ctx_enable_timing(dfm_ctx *ctx, int enable) {
   if (!ctx) return -1;
   ctx->timing = enable != 0;
+  if (ctx->timing) {   // events made up front, not one hipEventCreate per timed launch inside the jobs
+    hipSetDevice(ctx->device);
+    auto fill = [](dfm_ctx *c) {
+      while (c->pool.size() < 1024) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) break;
+        c->pool.push_back(e);
+      }
+    };
+    fill(ctx);
+    for (dfm_ctx *c : ctx->kids) fill(c);
+  }
   return 0;
 }
 int dfm_ctx_read_timing(dfm_ctx *ctx, double *ms_out, int64_t *launches_out, int cap) {
   if (!ctx) return -1;
   harvest(ctx);
+  merge_kids(ctx);
   const int n = std::min(cap, (int)DFM_KC_COUNT);
   for (int i = 0; i < n; ++i) {
     if (ms_out) ms_out[i] = ctx->ms[i];
@@ -561,6 +609,7 @@ int dfm_ctx_read_timing(dfm_ctx *ctx, double *ms_out, int64_t *launches_out, int
 int dfm_ctx_reset_timing(dfm_ctx *ctx) {
   if (!ctx) return -1;
   harvest(ctx);
+  merge_kids(ctx);
   for (int i = 0; i < DFM_KC_COUNT; ++i) { ctx->ms[i] = 0; ctx->launches[i] = 0; }
   ctx->eig_batches = ctx->eig_iters = ctx->eig_iters_max = ctx->rep_iters = ctx->gemm_products = 0;
   hipMemsetAsync(ctx->cnt_dev, 0, 2 * sizeof(long long), ctx->stream);
@@ -763,6 +812,11 @@ int dfm_model_destroy(dfm_model *m) {
     m->lane_worker[j] = nullptr;
     if (m->lane[j]) {   // the lane model, then its context (the model held the last reference but one)
       dfm_ctx *lc = m->lane[j]->ctx;
+      hipSetDevice(lc->device);
+      hipStreamSynchronize(lc->stream);
+      merge_kid(m->ctx, lc);   // its unread kernel timings
+      auto &kd = m->ctx->kids;
+      kd.erase(std::remove(kd.begin(), kd.end(), lc), kd.end());
       dfm_model_destroy(m->lane[j]);
       dfm_ctx_destroy(lc);
       m->lane[j] = nullptr;
@@ -1315,6 +1369,7 @@ static int bootstrap_lanes(dfm_model *M, int nl, int kind, int64_t B, const int3
     }
     L->is_lane = true;
     L->count_ctx = ctx;
+    ctx->kids.push_back(lc);
     M->lane[j] = L;
     M->lane_worker[j] = new LaneWorker();
   }
@@ -1355,17 +1410,12 @@ static int bootstrap_lanes(dfm_model *M, int nl, int kind, int64_t B, const int3
   }
   rcl[0] = bootstrap_one(M, kind, b_at(1), idx, eta, stats, ns, out);
   for (int j = 1; j < nl; ++j) M->lane_worker[j - 1]->wait();
-  // the lanes' host-side counters and kernel timings join the caller's context
-  // (their device-side GEMM-product counts went to ctx->cnt_dev directly)
+  // the lanes' host-side counters join the caller's context (their kernel
+  // timings when the caller's are read: merge_kids; their device-side
+  // GEMM-product counts went to ctx->cnt_dev directly)
   for (int j = 0; j < nl - 1; ++j) {
     dfm_ctx *lc = M->lane[j]->ctx;
-    if (lc->timing) {
-      harvest(lc);
-      for (int i = 0; i < DFM_KC_COUNT; ++i) {
-        ctx->ms[i] += lc->ms[i]; ctx->launches[i] += lc->launches[i];
-        lc->ms[i] = 0; lc->launches[i] = 0;
-      }
-    }
+    if (lc->pend.size() > 4096) merge_kid(ctx, lc);   // (bounded: a long timed run)
     ctx->eig_batches += lc->eig_batches;
     ctx->eig_iters += lc->eig_iters;
     ctx->eig_iters_max = std::max(ctx->eig_iters_max, lc->eig_iters_max);
