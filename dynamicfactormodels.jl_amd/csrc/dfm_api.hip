@@ -1814,9 +1814,13 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       }
     }
   }
+  // the status flag through the context's pinned slot (a pageable read-back
+  // is a staging copy kernel and ~25 us of host time at the end of every job)
   int flag = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&flag, M->flag_dev, 4, hipMemcpyDeviceToHost, st));
+  int *fl = ctx->pollbuf.host ? ctx->pollbuf.host + ctx->pollbuf.cap - 1 : &flag;
+  HIPCHK(ctx, hipMemcpyAsync(fl, M->flag_dev, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  flag = *fl;
 #ifdef DFM_DEBUG_MEM
   {
     std::vector<unsigned char> g(GuardBuf::kG);
