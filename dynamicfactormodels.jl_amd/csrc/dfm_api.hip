@@ -89,7 +89,8 @@ hipError_t launch_ols(int nb, hipStream_t st, const double *y, const double *w, 
                       const int *R0 = nullptr);
 struct StatDesc { int kind, arg0, arg1, off; };
 __global__ void stats_kernel(int, int, int, int, int, int, double, const double *, const double *, const double *,
-                             const double *, const double *, const int *, const StatDesc *, int, double *, int64_t);
+                             const double *, const double *, const int *, const StatDesc *, int, double *, int64_t,
+                             const int *, const int *, int *);
 __global__ void tail_sigma2_kernel(const double *, int, int, int, double, double *);
 // dfm_chow.hip
 hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int bp, int nb,
@@ -1761,10 +1762,11 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
         const int *iters = wide ? nullptr : eig_iters_ptr(w.eig, M->nblk > 1 ? M->bm.back() : m, n, P, ctx->maxit);
         hipLaunchKernelGGL(stats_kernel, dim3((n + 127) / 128), dim3(128), 0, st, n, T, N, r, q,
                            M->crit, M->sigma2, pcp ? pSig.p : nullptr, w.lam, w.trace, w.coef, w.tstat, iters,
-                           M->sd_dev, ns, out + b0 * width, width);
+                           M->sd_dev, ns, out + b0 * width, width, w.status, w.ost, M->flag_dev);
+      } else {
+        hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
+                           n, M->flag_dev);
       }
-      hipLaunchKernelGGL(or_status_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.status, w.ost,
-                         n, M->flag_dev);
       // the replicates' factors / a block's loadings, row by row (host closures)
       for (int i = 0; i < ns; ++i) {
         if (sd[i].kind != DFM_STAT_FACTORS && sd[i].kind != DFM_STAT_LOADINGS) continue;

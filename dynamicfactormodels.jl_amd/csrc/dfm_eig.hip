@@ -815,12 +815,18 @@ DFM_DEV void eig_final_body(const double *Ur, const double *theta, int done, int
   }
 }
 
+DFM_DEV void count_iters_body(const int *__restrict__ active, int last_gemm, int last_cheb, int nb, long long *cnt,
+                              int cp0, int cp1);
 template <int P>
 __global__ __launch_bounds__(256) void eig_final_kernel(EigWork w, int m, int k, double *__restrict__ lam,
                                                         double *__restrict__ Uk, int *__restrict__ status,
-                                                        double *__restrict__ trace_out) {
+                                                        double *__restrict__ trace_out, long long *cnt = nullptr,
+                                                        int last_gemm = -1, int last_cheb = -1, int cp0 = 0,
+                                                        int cp1 = 0) {
   const int rep = blockIdx.x;
   if (trace_out && threadIdx.x == 0) trace_out[rep] = w.trace[rep];   // (the caller's copy of trace(G))
+  // the factored run's iteration / product counts (count_iters_kernel's work, one launch fewer)
+  if (cnt && rep == 0 && threadIdx.x == 0) count_iters_body(w.active, last_gemm, last_cheb, gridDim.x, cnt, cp0, cp1);
   eig_final_body<P>(w.U + (int64_t)rep * m * P, w.small + (int64_t)rep * small_stride<P>() + 2 * P * P, w.done[rep],
                     rep, m, k, lam, Uk, status);
 }
@@ -897,9 +903,8 @@ thread_local int64_t g_last_gemm_products = 0;   // replicate-products of the la
 // replicate-iterations (GEMM launches 0..last_gemm, shift 1) and the GEMM
 // replicate-products (those plus the Chebyshev GEMMs 0..last_cheb, shift 0)
 // to cnt[0], cnt[1] — no host synchronisation after the eigen loop.
-__global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm, int last_cheb, int nb,
-                                   long long *cnt, int cp0, int cp1) {
-  if (threadIdx.x != 0) return;
+DFM_DEV void count_iters_body(const int *__restrict__ active, int last_gemm, int last_cheb, int nb, long long *cnt,
+                              int cp0, int cp1) {
   long long a = 0, b = 0;
   for (int it = 0; it <= last_gemm; ++it) a += it - 1 < 0 ? nb : active[it - 1];
   // Chebyshev products: cp0 after the first Rayleigh-Ritz step, cp1 after the others
@@ -907,6 +912,10 @@ __global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm
   // device-scope atomics: a model's two bootstrap lanes count into one context
   atomicAdd(reinterpret_cast<unsigned long long *>(cnt), (unsigned long long)a);
   atomicAdd(reinterpret_cast<unsigned long long *>(cnt + 1), (unsigned long long)(a + b));
+}
+__global__ void count_iters_kernel(const int *__restrict__ active, int last_gemm, int last_cheb, int nb,
+                                   long long *cnt, int cp0, int cp1) {
+  if (threadIdx.x == 0) count_iters_body(active, last_gemm, last_cheb, nb, cnt, cp0, cp1);
 }
 static int64_t count_rep_iters(const int *active_dev, int last, int shift, int nb, hipStream_t st) {
   if (last < 0) return 0;
@@ -2869,9 +2878,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   if (steps < 0) steps = it;
   g_last_iters = steps;
   // the Chebyshev GEMM of iteration it runs after that iteration's check
-  if (cnt) {
-    hipLaunchKernelGGL(count_iters_kernel, dim3(1), dim3(64), 0, st, w.active, last_gemm, last_cheb, nb, cnt,
-                       d0 - 1, kChebD - 1);
+  if (cnt) {   // (counted by eig_final_kernel below)
     g_last_rep_iters = g_last_gemm_products = 0;
   } else {
     g_last_rep_iters = count_rep_iters(w.active, last_gemm, 1, nb, st);
@@ -2880,7 +2887,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     g_last_gemm_products = g_last_rep_iters + c0 * (d0 - 1) + (call - c0) * (kChebD - 1);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 1);
-  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status, trace_out);
+  hipLaunchKernelGGL(eig_final_kernel<P>, dim3(nb), dim3(256), 0, st, w, m, k, lam, Uk, status, trace_out, cnt,
+                     last_gemm, last_cheb, d0 - 1, kChebD - 1);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return 1000 + (int)e;

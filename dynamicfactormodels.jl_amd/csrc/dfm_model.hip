@@ -590,9 +590,14 @@ __global__ void stats_kernel(int nb, int T, int N, int r, int q, int crit, doubl
                              const double *__restrict__ lam, const double *__restrict__ trace,
                              const double *__restrict__ coef, const double *__restrict__ tstat,
                              const int *__restrict__ iters, const StatDesc *__restrict__ sd, int ns,
-                             double *__restrict__ out, int64_t width) {
+                             double *__restrict__ out, int64_t width, const int *__restrict__ st1,
+                             const int *__restrict__ st2, int *__restrict__ flag) {
   const int rep = blockIdx.x * blockDim.x + threadIdx.x;
   if (rep >= nb) return;
+  if (flag) {   // the replicates' solver / OLS status into the job's flag (or_status_kernel's work, one launch fewer)
+    if (st1[rep]) atomicOr(flag, 1);
+    if (st2[rep]) atomicOr(flag, 2);
+  }
   double s = trace[rep];
   for (int j = 0; j < r; ++j) s -= lam[(int64_t)rep * r + j];
   const double V = s / ((double)N * (double)T);
