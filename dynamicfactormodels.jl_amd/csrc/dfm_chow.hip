@@ -621,11 +621,19 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
   double *prep = (double *)ws;
   double *Z = (double *)(ws + (size_t)nb * CH_PREP_BYTES);
   double *scr = (double *)(ws + ws_bytes) - (size_t)3 * nb * N;
+#ifdef DFM_CH_R3   // (A/B builds: r = 3 runs exactly 3-wide; bit-identical, profiles/r05_rejected_chow_r3.txt)
+  const int RC = r == 3 ? 3 : (r <= 4 ? 4 : (r <= 8 ? 8 : 16));
+#else
   const int RC = r <= 4 ? 4 : (r <= 8 ? 8 : 16);   // the main kernel's padded R (below)
+#endif
   hipLaunchKernelGGL(chow_prep_kernel, dim3(nb), dim3(256), 0, st, F, T, r, bp, RC, prep, Z);
   double *LR = scr, *LM = scr + (size_t)nb * N, *WD = scr + (size_t)2 * nb * N;
   // R = padded factor count of the per-variable register blocks (zero
   // padding: r <= 4 runs 4-wide, 10 HC0 accumulators instead of 36)
+#ifdef DFM_CH_R3
+  if (r == 3) launch_chow_r<3>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  else
+#endif
   if (r <= 4) launch_chow_r<4>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
   else if (r <= 8) launch_chow_r<8>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
   else launch_chow_r<16>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
