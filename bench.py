@@ -229,8 +229,10 @@ def hbm_rooflines(timing, eig, Bn, steps, pz=16):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 20 timed steps after 3 warm-up steps: a C3 step is ~15 ms, so the default
+    # timed region is ~0.3 s (5 steps read 641-652 k on the same build)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="replicates per device batch (0 = auto)")
     ap.add_argument("--replicates", type=int, default=B)
     ap.add_argument("--mode", default="auto", choices=["auto", "direct", "factored"])
