@@ -765,6 +765,18 @@ static int dbg_lane_skew_us() {
 }
 #endif
 
+#if defined(DFM_LANE_SKEW_AB) && !defined(DFM_DEBUG_MEM)
+// (A/B builds only: the debug build's lane skew as a timing experiment, no poisoning)
+__global__ void dbg_spin_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+static int dbg_lane_skew_us() {
+  static const int v = [] { const char *e = getenv("DFM_LANE_SKEW_US"); return e ? atoi(e) : 0; }();
+  return v;
+}
+#endif
+
 // ---------------------------------------------------------------- internals
 // Top-k eigen-decomposition of nb Grams + trace; G workspace provided.
 static int run_eig(dfm_ctx *ctx, const double *G, int m, int nb, int k, const double *warm, int kw,
@@ -1388,11 +1400,13 @@ static int bootstrap_lanes(dfm_model *M, int nl, int kind, int64_t B, const int3
     M->lane[j]->mode = M->mode;
     HIPCHK(ctx, hipStreamWaitEvent(lc->stream, ctx->gate, 0));
   }
-#ifdef DFM_DEBUG_MEM
+#if defined(DFM_DEBUG_MEM) || defined(DFM_LANE_SKEW_AB)
   if (const int sk = dbg_lane_skew_us()) {   // wall clock: 100 ticks per microsecond
     hipLaunchKernelGGL(dbg_spin_kernel, dim3(1), dim3(64), 0, sk > 0 ? M->lane[0]->ctx->stream : ctx->stream,
                        (long long)std::abs(sk) * 100);
+#ifdef DFM_DEBUG_MEM
     fprintf(stderr, "[dfm debug] lane skew %d us\n", sk);
+#endif
   }
 #endif
   // lane j takes replicates [b_j, b_{j+1}), b_j = ceil(j B / nl) (lane 0 = this thread)
