@@ -204,7 +204,9 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
                                                        const double *__restrict__ Lm,
                                                        double *__restrict__ LR,
                                                        double *__restrict__ LM,
-                                                       double *__restrict__ WD) {
+                                                       double *__restrict__ WD, double *__restrict__ LRo,
+                                                       double *__restrict__ LMo, double *__restrict__ WDo,
+                                                       int64_t os) {
 #ifndef DFM_CH_TR   // (A/B builds: rows per staged tile)
 #define DFM_CH_TR 128
 #endif
@@ -563,16 +565,22 @@ __global__ __launch_bounds__(256, (chow_waves<R, KS>())) void chow_all_kernel(Pa
       wv = fma(yv[a], yv[a], wv);
     }
   }
-  const int64_t o = (int64_t)rep * N + i;
-  LR[o] = T * (log(e2) - log(ssr));
-  LM[o] = T * lmq / e2;
+  const int64_t o = (int64_t)rep * N + i, oo = (int64_t)rep * os + i;
+  const double vlr = T * (log(e2) - log(ssr)), vlm = T * lmq / e2;
+  LR[o] = vlr;
+  LM[o] = vlm;
   WD[o] = wv;
+  // the caller's strided rows directly (three 2-D copy launches per job before)
+  if (LRo) LRo[oo] = vlr;
+  if (LMo) LMo[oo] = vlm;
+  if (WDo) WDo[oo] = wv;
 }
 
 template <int R>
 static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int N, int r, int bp, int nb,
                           const double *F, const double *Z, const double *prep, const double *Lm, double *LR,
-                          double *LM, double *WD, hipStream_t st) {
+                          double *LM, double *WD, double *LRo, double *LMo, double *WDo, int64_t os,
+                          hipStream_t st) {
   const bool c = src.C, e = src.eta, x = src.idx;
   constexpr int KS = R <= 4 ? CH_KS : 1;   // lanes per (replicate, variable)
   // flat: a 256-thread block (256 / KS pairs) spans at most CH_FLAT_REPS replicates
@@ -586,10 +594,10 @@ static void launch_chow_r(const PanelSrc &src, const ChowBlocks &blk, int T, int
   do {                                                                                                          \
     if (flat)                                                                                                   \
       hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, (R <= 8), KS>), grid, block, 0, st, src, blk, T, N, \
-                         r, bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                \
+                         r, bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, os);                             \
     else                                                                                                        \
       hipLaunchKernelGGL((chow_all_kernel<R, C_, E_, X_, B_, false, KS>), grid, block, 0, st, src, blk, T, N, r, \
-                         bp, nb, F, Z, prep, Lm, LR, LM, WD);                                                   \
+                         bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, os);                                \
   } while (0)
   if (blk.n > 1) {
     if (c && e && x) DFM_CH(true, true, true, true);
@@ -631,16 +639,13 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
   // R = padded factor count of the per-variable register blocks (zero
   // padding: r <= 4 runs 4-wide, 10 HC0 accumulators instead of 36)
 #ifdef DFM_CH_R3
-  if (r == 3) launch_chow_r<3>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
+  if (r == 3) launch_chow_r<3>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, out_stride, st);
   else
 #endif
-  if (r <= 4) launch_chow_r<4>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
-  else if (r <= 8) launch_chow_r<8>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
-  else launch_chow_r<16>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, st);
-  // scatter into the caller's strided output rows
-  if (LRo) hipMemcpy2DAsync(LRo, (size_t)out_stride * 8, LR, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);
-  if (LMo) hipMemcpy2DAsync(LMo, (size_t)out_stride * 8, LM, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);
-  if (WDo) hipMemcpy2DAsync(WDo, (size_t)out_stride * 8, WD, (size_t)N * 8, (size_t)N * 8, nb, hipMemcpyDeviceToDevice, st);
+  if (r <= 4) launch_chow_r<4>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, out_stride, st);
+  else if (r <= 8) launch_chow_r<8>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, out_stride, st);
+  else launch_chow_r<16>(src, blk, T, N, r, bp, nb, F, Z, prep, Lm, LR, LM, WD, LRo, LMo, WDo, out_stride, st);
+  // (the kernel wrote the caller's strided output rows itself)
   return hipGetLastError();
 }
 
