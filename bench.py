@@ -21,6 +21,11 @@ resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+A plain `python bench.py --gpus N` with N > 1 (no torchrun environment) is a
+launcher: before anything touches a GPU it starts `torch.distributed.run` with
+N ranks as a CHILD process (never an exec), forwards its output and exits with
+its status.  Under torchrun, --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -226,6 +231,39 @@ def hbm_rooflines(timing, eig, Bn, steps, pz=16):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` (N > 1, no torchrun environment): run the
+    same command as N ranks under torch.distributed.run in a child process.
+    This process imports no torch and makes no HIP call, so it never holds
+    the GPU; rank 0's JSON line comes through its stdout.  Returns the
+    child's exit status (non-zero if any rank failed)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    rc = p.wait()
+    if rc != 0:
+        print(f"bench.py: torch.distributed.run exited with status {rc}", file=sys.stderr, flush=True)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -252,27 +290,47 @@ def main():
                     help="skip the all_fields extra (the job with the whole regression record per replicate: F*, "
                          "L*, OLS formed) — for rocprofv3 runs whose trace must hold the headline launches only")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dump-rows", default="",
+                    help="rank 0 saves the last timed step's gathered per-replicate rows (.npy) here")
+    ap.add_argument("--share-device", action="store_true",
+                    help="TEST ONLY: every rank on cuda:0 with the gloo backend (a one-GPU box rehearses "
+                         "N ranks; RCCL refuses two ranks on one GPU)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                 f"(launch with --nproc-per-node equal to --gpus)")
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = None
     # launched by torchrun (any N, N = 1 included): one rank per GPU over RCCL,
     # the per-replicate rows all-gathered on the device; a plain `python
     # bench.py` (the driver's N = 1 run) has no process group
     if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.share_device:
+            backend = "gloo"
+            dist.init_process_group("gloo")
+        else:
+            backend = "nccl"
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    # where the exchanged rows and the max-over-ranks time live: the GPU for
+    # RCCL, the host for gloo
+    comm_dev = dev if backend == "nccl" else torch.device("cpu")
 
     import dfm_pkg
     D = dfm_pkg.load()
     ctx = D.Context(local)
     if args.workload == "c5":
-        return bench_windows(args, D, ctx, torch, dist, world, rank, dev)
+        return bench_windows(args, D, ctx, torch, dist, world, rank, dev, comm_dev)
     if args.eig_tol > 0:
         ctx.set_eig_params(tol=args.eig_tol)
     if args.value_tol > 0:
@@ -315,7 +373,7 @@ def main():
         if nloc:
             ctx.check(ctx.lib.dfm_bootstrap_dev(model.handle, 0, nloc, idx_d[s].data_ptr(),
                                                 eta_d[s].data_ptr(), arr, len(stats), out.data_ptr()))
-        holder["rows"] = gather_rows(out[:nloc], Bn) if dist is not None else out
+        holder["rows"] = gather_rows(out[:nloc].to(comm_dev), Bn) if dist is not None else out
 
     def timed(fn, first, count):
         """Barrier + sync on both sides of `count` steps; max over ranks."""
@@ -331,7 +389,7 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         if dist is not None:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=comm_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el
@@ -396,6 +454,8 @@ def main():
         del fout
     res = holder["rows"].cpu().numpy()
     ok = bool(np.all(np.isfinite(res))) and res.shape[0] >= Bn if dist is not None else bool(np.all(np.isfinite(res)))
+    if args.dump_rows and rank == 0:
+        np.save(args.dump_rows, res[:Bn])
 
     total = Bn * args.steps
     value = total / el
@@ -451,8 +511,10 @@ def main():
         "kernels_ms": {k: round(v[0], 3) for k, v in timing.items() if v[1]},
         "kernel_launches": {k: int(v[1]) for k, v in timing.items() if v[1]},
         "outputs_finite": ok,
-        "collective": (f"RCCL all-gather of the per-replicate rows over {world} rank(s) "
-                       f"({dist.get_backend()})" if dist is not None else "none (single process, no process group)"),
+        "collective": ((f"RCCL all-gather of the per-replicate rows over {world} rank(s) ({backend})"
+                        if backend == "nccl" else
+                        f"gloo all-gather of the per-replicate rows over {world} rank(s) sharing cuda:0 (test mode)")
+                       if dist is not None else "none (single process, no process group)"),
         "mode": args.mode,
         "stopping_rule": "eigenvector residual (strict)" if args.strict else
                          "eigenvalue Kato-Temple bound, 1e-12 relative (stats are eigenvalue-only)",
@@ -480,7 +542,7 @@ def main():
 C5_T, C5_N, C5_P, C5_KMAX = 2000, 20000, 200, 8
 
 
-def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
+def bench_windows(args, D, ctx, torch, dist, world, rank, dev, comm_dev):
     """BASELINE.json configs[4]: the refits of pseudo_out_of_sample_forecasts
     (src/utils.jl:54-72), P = 200 expanding windows x ICp2 sweep k <= 8 on a
     T=2000 N=20000 panel.  The panel is resident in HBM (column-major, as Julia
@@ -511,7 +573,7 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
         else:
             res = D.pseudo_out_of_sample_refits_dev(yd, wd, xd, "ICp2", num_predictions=w1 - w0, kmax=km,
                                                     rows=rows, ctx=ctx)
-        loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, 1)).to(dev)
+        loc = torch.from_numpy(_pack_windows(res, w1 - w0, K, 1)).to(comm_dev)
         holder["all"] = gather_rows(loc, P5) if dist is not None else loc
 
     for _ in range(args.warmup):
@@ -533,7 +595,7 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev):
     ctx.enable_timing(False)
     timing = ctx.read_timing()
     if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     allrows = holder["all"].cpu().numpy()

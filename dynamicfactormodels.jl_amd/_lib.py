@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DFM_LIB_PATH: load another build of the same library (A/B timing of a
-# variant built by the csrc Makefile's BUILD/LIB/EXTRA; tools/ab_bench.sh)
+# variant built by the csrc Makefile's BUILD/LIB/EXTRA; tools/gpu_session.sh ab)
 LIB_PATH = os.environ.get("DFM_LIB_PATH") or os.path.join(_HERE, "libdfm.so")
 
 c_double_p = C.POINTER(C.c_double)

@@ -1543,6 +1543,11 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
   // direct path, N > T, no breaks: the replicate Grams by the factored
   // identity (gram_fact_kernel, 2 T^2 r flop each) instead of the SYRK
   const bool gid = !fact && (M->orient == 0) && M->nblk == 1 && r >= 1 && r <= 16 && T <= 4096;
+  // the factored solver's own block (k + 4 columns, fact_block_p) and the
+  // register template it selects: its workspace layout (eig_iters_ptr) follows
+  // pf, not the direct solvers' p
+  const int pf = fact ? fact_block_p(m, r, ctx->block) : p;
+  const int Pf = pf <= 16 ? 16 : 32;
   // T >= N, no breaks, small N: the batch's Grams by one weighted GEMM (gram_wk)
   const bool gwk = use_gram_wk(M);
   if (pcp && m > spectrum_any_max())
@@ -1690,7 +1695,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       // warm first filter's degree (eig_run_fact2_t)
       const double spread = (M->lam.size() >= (size_t)r && r > 0 && M->lam[r - 1] > 0.0) ? M->lam[0] / M->lam[r - 1]
                                                                                         : 0.0;
-      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, fact_block_p(m, r, ctx->block), M->Ub, r, etol,
+      int rc = eig_run_factored(fb, idx + b0 * T, et, n, r, pf, M->Ub, r, etol,
                                 ctx->maxit, ctx->poll,
                                 w.eig, w.fact, w.lam, need_fl ? w.Uk : nullptr, w.trace, w.status, st, timer_cb,
                                 ctx, w.off, w.lst,
@@ -1773,7 +1778,10 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
       {
         // the eigensolver's per-replicate step counts (DFM_STAT_ITERS): the
         // workspace of this batch's (last block's) subspace solve
-        const int *iters = wide ? nullptr : eig_iters_ptr(w.eig, M->nblk > 1 ? M->bm.back() : m, n, P, ctx->maxit);
+        // (the factored solver carves its workspace for ITS block pf, which
+        // can select a narrower template than the direct solvers' P)
+        const int *iters = wide ? nullptr
+                                : eig_iters_ptr(w.eig, M->nblk > 1 ? M->bm.back() : m, n, fact ? Pf : P, ctx->maxit);
         hipLaunchKernelGGL(stats_kernel, dim3((n + 127) / 128), dim3(128), 0, st, n, T, N, r, q,
                            M->crit, M->sigma2, pcp ? pSig.p : nullptr, w.lam, w.trace, w.coef, w.tstat, iters,
                            M->sd_dev, ns, out + b0 * width, width, w.status, w.ost, M->flag_dev);

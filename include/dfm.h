@@ -245,7 +245,10 @@ int dfm_model_set_mode(dfm_model *m, int mode);
  * columns per replicate, pz = p rounded up to even = the columns each
  * replicate contributes to the batched H.Z GEMM (its flop per
  * replicate-product is 2 T^2 pz).  Returns 0, or 1 (p = pz = 0) when the
- * model's bootstrap never takes the factored path (T >= N, breaks, r > 16). */
+ * model's bootstrap never takes the factored path (T >= N, breaks, r > 16).
+ * The answer ignores the statistics of a particular call: a stat list with a
+ * PCp criterion (which reads each replicate's full spectrum) or mode 1 sends
+ * that call down the direct path even when this returns 0. */
 int dfm_model_fact_block(const dfm_model *m, int *p, int *pz);
 
 /* ------------------------------------------------------------ Chow tests

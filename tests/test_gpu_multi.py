@@ -296,3 +296,37 @@ def test_bench_under_torchrun_world1():
     assert rec["n_gpus"] == 1 and rec["outputs_finite"] and rec["value"] > 0
     assert rec["collective"].startswith("RCCL all-gather") and "nccl" in rec["collective"]
 
+
+
+def _bench(root, tmp_path, gpus, tag, extra=()):
+    import json
+    import subprocess
+    import sys
+    dump = str(tmp_path / f"rows_{tag}.npy")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--steps", "1", "--warmup", "1",
+           "--no-cpu-baseline", "--no-all-fields", "--no-weak", "--dump-rows", dump] + list(extra)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    return rec, np.load(dump)
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus2_launches_two_ranks(tmp_path):
+    """`python3 bench.py --gpus 2` — the driver's command form — starts two
+    ranks itself (a torch.distributed.run child; the parent never touches the
+    GPU).  On the one-GPU box both ranks share cuda:0 over gloo
+    (`--share-device`, test only: RCCL refuses two ranks on one GPU).  The
+    C3 job's 9999 replicates split 5000 / 4999 (replicate b on rank
+    floor(2 b / B), src/bootstrap.jl:43) and the gathered rows are
+    bit-identical to the one-process run's."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    one, rows1 = _bench(root, tmp_path, 1, "n1")
+    two, rows2 = _bench(root, tmp_path, 2, "n2", ["--share-device"])
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["config"]["replicates_per_gpu"] == 5000 and two["config"]["replicates"] == 9999
+    assert "over 2 rank(s)" in two["collective"] and two["outputs_finite"]
+    assert rows1.shape == rows2.shape == (9999, rows1.shape[1])
+    assert np.array_equal(rows1, rows2)

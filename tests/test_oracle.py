@@ -333,3 +333,33 @@ def test_xp_fixture_agrees_with_golden():
     assert np.all(xp["c2_boot_bar"] >= 1e-10 * np.abs(xp["c2_boot"]))
     g1 = np.load(os.path.join(GOLD, "c1_bai_ng_T200_N100_r3.npz"))
     assert np.all(np.abs(xp["c1_ic"] - g1["ic_values"]) < 1e-10 * np.abs(xp["c1_ic"]))
+
+
+def test_oracle_pool_matches_serial_oracle(oracle):
+    """tests/oracle_pool.py (the whole-batch checker of the -m gpu production
+    tests) returns, in replicate order, exactly what the serial oracle loop
+    gives for the same draws (src/bootstrap.jl:41-51, src/chowtest.jl:19-42)."""
+    import oracle_pool
+    T, N, r, B, bp = 60, 40, 2, 7, 30
+    y, x, *_ = oracle.factor_model_DGP(T, N, r, np.random.default_rng(5))
+    x = oracle.normalize(x)
+    w = np.ones((T, 1))
+    rng = np.random.default_rng(6)
+    idx = rng.integers(0, T, (B, T)).astype(np.int32)
+    eta = rng.standard_normal((B, T))
+    c3 = oracle_pool.run("c3", y, w, x, r, "ICp2", idx, eta, chunk=3, nproc=2)
+    vs = [0, 5, 39]
+    c2 = oracle_pool.run("c2", y, w, x, r, "ICp2", idx, eta, extra=(bp, vs), chunk=2, nproc=2)
+    ex = oracle_pool.run("c2ref", y, w, x, r, "ICp2", None, None, jobs=[(idx[3:4], eta[3:4], bp, vs)], nproc=2)
+    base = oracle.DynamicFactorModel(y, w, x, r, "ICp2")
+    for b in range(B):
+        d = oracle.DynamicFactorModel(y, w, base.common_component + eta[b][:, None] * base.factor_residuals[idx[b]],
+                                      r, "ICp2")
+        want = [oracle.factor_residual_variance(d), d.number_of_factors_criterion_value, np.sum(d.x ** 2)]
+        assert np.allclose(c3[b], want + list(d.eigenvalues[0][:r]), rtol=1e-13, atol=0)
+        want2 = want[:2] + [oracle.Wald_test(d, bp, i) for i in vs] + [oracle.LR_test(d, bp, i) for i in vs] + \
+            [oracle.LM_test(d, bp, i) for i in vs]
+        assert np.allclose(c2[b], want2, rtol=1e-13, atol=0)
+        if b == 3:
+            assert np.allclose(ex[0][:, 0], want2[2 + 3:2 + 6], rtol=1e-9)
+            assert np.allclose(ex[0][:, 1], want2[2 + 6:], rtol=1e-9)

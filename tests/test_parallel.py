@@ -173,3 +173,33 @@ def test_rolling_window_rows_cover_each_window():
                 seen.append(w0 + j)
         assert seen == list(range(P))
     assert window_rows(T, P, 4, 1, None)[2] == 0                          # expanding: from row 0
+
+
+def test_bench_gpus_must_match_world_size():
+    """Under torchrun, bench.py --gpus N with WORLD_SIZE != N fails loudly
+    before importing torch (no silent one-GPU line for an N-GPU request)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=60, cwd=root, env=env)
+    assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_bench_launcher_propagates_rank_failure():
+    """`python bench.py --gpus 2` without torchrun launches two ranks in a
+    child torch.distributed.run; here (no GPU) the ranks fail, and the
+    launcher must exit non-zero instead of printing a line."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--no-cpu-baseline"], capture_output=True, text=True, timeout=180,
+                       cwd=root, env=env)
+    assert p.returncode != 0
+    assert "launching 2 ranks" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
