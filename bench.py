@@ -194,9 +194,10 @@ def rocprof_avg_ms(kernel_prefix):
 def hbm_rooflines(timing, eig, Bn, steps, pz=16):
     """Achieved HBM bandwidth of the per-replicate gather/residual passes of
     the factored solver (HIP-event time of their kernel class over the timed
-    region; algorithmic bytes per replicate-pass; P = 16
-    columns per row of the per-replicate buffers Q, Y, S, V0, PV; pz = the
-    solver's block, rounded up to even = the columns of Z and HZ):
+    region; algorithmic bytes per replicate-pass; P = pz
+    columns per row of the per-replicate buffers Q, Y, S, V0, PV (compact rows
+    since round 6; 16 before); pz = the solver's block, rounded up to even =
+    the columns of Z and HZ):
       y2  (class eig_gq):    Y = G*Q rows from the gathered HZ rows, Q'Y / Y'Y / Q'Q:
                              reads Q and HZ[idx], writes Y = (2 P + pz) T 8 B per Rayleigh-Ritz step
       ap2 (class eig_apply): (4 P + pz) T 8 B per pass (Q, Y in; the filter's first Horner term S,
@@ -208,7 +209,7 @@ def hbm_rooflines(timing, eig, Bn, steps, pz=16):
                              (HZ, PV, PF, e2 rows) + T pz 8 B out (Z); passes = the other
                              GEMM products after the Rayleigh-Ritz ones
     Replicate-passes come from the library's own counters (eig_iterations)."""
-    P = 16
+    P = pz
     out = []
     rr = eig.get("replicate_iterations", 0)
     cheb = max(eig.get("gemm_products", 0) - rr, 0)
@@ -342,7 +343,7 @@ def main():
     # ---- base model (identical on every rank), resident in HBM
     rng = np.random.default_rng(20261015 + 3)
     y, x, *_ = D.factor_model_DGP(T, N, R, rng=rng)
-    x = D.normalize(x)
+    x = D.normalize(x, ctx=ctx)
     w = np.ones((T, 1))
     model = D.DynamicFactorModel(y, w, x, R, "ICp2", ctx=ctx)
     if args.batch:
@@ -555,7 +556,7 @@ def bench_windows(args, D, ctx, torch, dist, world, rank, dev, comm_dev):
     L = int(args.rolling) or None
     rng = np.random.default_rng(20261015 + 5)
     y, x, *_ = D.factor_model_DGP(T5, N5, 8, rng=rng)
-    x = D.normalize(x)
+    x = D.normalize(x, ctx=ctx)
     yd = torch.from_numpy(np.ascontiguousarray(y)).to(dev)
     wd = torch.ones((T5, 1), dtype=torch.float64, device=dev)
     xd = torch.from_numpy(np.ascontiguousarray(x.T)).to(dev).t()     # column-major T x N in HBM

@@ -51,15 +51,16 @@ constexpr int SMALL_STAGE_B = 0x400;      // small_rr: only chol(Z'Z) and Bm (ei
 // ----------------------------------------------------------------- init
 template <int P>
 __global__ void eig_init_kernel(double *__restrict__ Q, int m, int p, const double *__restrict__ warm,
-                                int kw, int *__restrict__ done, uint64_t seed, int64_t rep0) {
+                                int kw, int *__restrict__ done, uint64_t seed, int64_t rep0, int ps = P) {
+  // ps: row stride (the factored solver's compact rows hold ps = pz <= P columns)
   const int rep = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)m * P) return;
-  const int row = (int)(e / P), c = (int)(e % P);
+  if (e >= (int64_t)m * ps) return;
+  const int row = (int)(e / ps), c = (int)(e % ps);
   double v = 0.0;
   if (c < kw) v = warm[(int64_t)row * kw + c];
   else if (c < p) v = hash_unit(seed, row, c);   // same start for every replicate: call/batch/shard-invariant
-  Q[(int64_t)rep * m * P + e] = v;
+  Q[(int64_t)rep * m * ps + e] = v;
   if (e == 0) done[rep] = 0;
 }
 
@@ -1729,7 +1730,8 @@ struct Y2Tile {
 };
 template <int P>
 DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, const int *six, const FactBase &fb,
-                     const double *__restrict__ HZ, int64_t ldz, int pz, int rep, const double *__restrict__ Qr) {
+                     const double *__restrict__ HZ, int64_t ldz, int pz, int rep, const double *__restrict__ Qr,
+                     int ps) {
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
   const int ta = min(t0 + li, T - 1);
@@ -1748,7 +1750,7 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
     for (int ct = 0; ct < NT; ++ct) {
       const int c = 16 * ct + li;
       L.hz[ct][g] = c < pz ? HZ[(int64_t)i * ldz + (int64_t)rep * pz + c] : 0.0;   // compact Z / HZ: pz columns
-      L.q[ct][g] = Qr[(int64_t)t * P + c];
+      L.q[ct][g] = c < ps ? Qr[(int64_t)t * ps + c] : 0.0;   // compact rows: ps columns
     }
   }
 }
@@ -1764,7 +1766,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
                                                       const double *__restrict__ HZ, int64_t ldz, int pz,
                                                       const double *__restrict__ ab,
                                                       const double *__restrict__ Qc, int64_t qs,
-                                                      double *__restrict__ Yo) {
+                                                      double *__restrict__ Yo, int ps) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -1813,7 +1815,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Qr);
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Qr, ps);
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1838,7 +1840,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         const double y = v ? fma(e, yE[ct][g] + cur.hz[ct][g], yF[ct][g]) : 0.0;
-        if (v) Yr[(int64_t)t * P + c] = y;
+        if (v && c < ps) Yr[(int64_t)t * ps + c] = y;
         Yv[ct][g] = y;
         if (!v) cur.q[ct][g] = 0.0;   // clamped row: no contribution to Q'Y, Q'Q
       }
@@ -1910,7 +1912,7 @@ struct Ap2Tile {
 // layout as ap2_load.
 template <int P>
 DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int init, const double *__restrict__ Qr,
-                          const double *Yr, const FactBase &fb, double *tq, double *ty) {
+                          const double *Yr, const FactBase &fb, double *tq, double *ty, int ps) {
   constexpr int NT = P / 16, KP = P / 4, PER = P / 4;   // doubles per lane per matrix
   const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
   if (!init) {
@@ -1923,8 +1925,10 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
 #ifdef DFM_AP2_DIAG_NOLOAD   // (timing diagnostic, WRONG results: no Q / Y tile loads)
       qv[j] = double2{1e-3 * (tc + j), 1e-3 * c0}; yv[j] = double2{1e-3 * c0, 1e-3 * (tc - j)};
 #else
-      qv[j] = *reinterpret_cast<const double2 *>(Qr + (int64_t)tc * P + c0 + 2 * j);
-      yv[j] = *reinterpret_cast<const double2 *>(Yr + (int64_t)tc * P + c0 + 2 * j);
+      // compact rows (ps columns, ps even): pairs past ps are the zero columns
+      const bool in = c0 + 2 * j < ps;
+      qv[j] = in ? *reinterpret_cast<const double2 *>(Qr + (int64_t)tc * ps + c0 + 2 * j) : double2{0.0, 0.0};
+      yv[j] = in ? *reinterpret_cast<const double2 *>(Yr + (int64_t)tc * ps + c0 + 2 * j) : double2{0.0, 0.0};
 #endif
     }
 #pragma unroll
@@ -1953,7 +1957,7 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
     const double f = r > 0 ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
     L.fa[g] = (t < T && li < r) ? f : 0.0;
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = init ? Qr[(int64_t)tc * P + 16 * ct + li] : 0.0;
+    for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = (init && 16 * ct + li < ps) ? Qr[(int64_t)tc * ps + 16 * ct + li] : 0.0;
   }
 }
 
@@ -1964,7 +1968,7 @@ template <int P>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
                            double *__restrict__ Zc, int64_t ldz, int pz, int rep, double *__restrict__ ab,
-                           const dv4 *aacc, double *sred) {
+                           const dv4 *aacc, double *sred, int ps) {
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
   dv4 cacc[NT];
@@ -1993,7 +1997,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
         const int t = sl[ok ? q : 0];
         ev[g][u] = ok ? set[t] : 0.0;
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) val[g][u][ct] = Qn[(int64_t)t * P + 16 * ct + li];
+        for (int ct = 0; ct < NT; ++ct) val[g][u][ct] = 16 * ct + li < ps ? Qn[(int64_t)t * ps + 16 * ct + li] : 0.0;
       }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -2008,7 +2012,8 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
         const int t = sl[q];
         const double e = set[t];
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) z[g][ct] = fma(e, Qn[(int64_t)t * P + 16 * ct + li], z[g][ct]);
+        for (int ct = 0; ct < NT; ++ct)
+          z[g][ct] = fma(e, 16 * ct + li < ps ? Qn[(int64_t)t * ps + 16 * ct + li] : 0.0, z[g][ct]);
       }
     }
 #pragma unroll
@@ -2059,7 +2064,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
                                                        const int *__restrict__ off, const int *__restrict__ lst,
                                                        const double *__restrict__ Qc, int64_t qs,
                                                        double *__restrict__ Yq, double *__restrict__ Zc, int64_t ldz,
-                                                       int pz, double *__restrict__ ab, uint64_t seed) {
+                                                       int pz, double *__restrict__ ab, uint64_t seed, int ps) {
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
   if (!init && w.done[rep]) return;
@@ -2107,7 +2112,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Ap2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    ap2_load_lds<P>(cur, tile, T, r, lane, init, Qr, Yr, fb, stile[wave][0], stile[wave][1]);
+    ap2_load_lds<P>(cur, tile, T, r, lane, init, Qr, Yr, fb, stile[wave][0], stile[wave][1], ps);
     const int t0 = tile * 16;
     double qv[NT][4];
     if (init) {
@@ -2140,7 +2145,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
               double x = qb[ct][g];
               if (c < p && dd[ct]) x = hash_unit(seed, t, 1000003ull * (it + 1) + c);   // = S
               if (c >= p) x = 0.0;
-              Xr[(int64_t)t * P + c] = x;
+              if (c < ps) Xr[(int64_t)t * ps + c] = x;
             }
         }
       }
@@ -2161,7 +2166,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
           if (c < p && dd[ct]) q = hash_unit(seed, t, 1000003ull * (it + 1) + c);
           if (c >= p || !v) q = 0.0;
           qv[ct][g] = q;
-          if (v) Yr[(int64_t)t * P + c] = q;
+          if (v && c < ps) Yr[(int64_t)t * ps + c] = q;
         }
       }
     }
@@ -2217,7 +2222,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
       for (int ct = 0; ct < NT; ++ct) u[ct] = dv4{0.0, 0.0, 0.0, 0.0};
       double qa[KP];
 #pragma unroll
-      for (int kk = 0; kk < KP; ++kk) qa[kk] = ta < T ? Qr[(int64_t)ta * P + 4 * kk + lk] : 0.0;
+      for (int kk = 0; kk < KP; ++kk) qa[kk] = (ta < T && 4 * kk + lk < ps) ? Qr[(int64_t)ta * ps + 4 * kk + lk] : 0.0;
 #pragma unroll
       for (int kk = 0; kk < KP; ++kk)
 #pragma unroll
@@ -2234,7 +2239,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
   const double *Qn = init ? Qr : Yr;
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, pz, rep, ab, aacc, sred);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, pz, rep, ab, aacc, sred, ps);
 }
 
 // One Horner step of the degree-d Chebyshev filter of the factored solver.
@@ -2259,7 +2264,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
                                                         const double *__restrict__ HZ, int64_t ldz, int pz,
                                                         double *__restrict__ ab, double fai, double bbeta, int k,
                                                         double *__restrict__ Qo,
-                                                        double *__restrict__ Zc) {
+                                                        double *__restrict__ Zc, int ps) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -2314,7 +2319,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Xr);   // cur.q = V0 rows
+    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Xr, ps);   // cur.q = V0 rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -2344,7 +2349,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
         double q = dd[ct] ? cur.q[ct][g] : fma(cb, wv, cv0 * cur.q[ct][g]);
         if (c >= p || !v) q = 0.0;
         qv[ct][g] = q;
-        if (v) Qr[(int64_t)t * P + c] = q;
+        if (v && c < ps) Qr[(int64_t)t * ps + c] = q;
       }
     }
 #pragma unroll
@@ -2353,7 +2358,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
   }
   __syncthreads();   // every wave's Qn rows visible to the CSR gather
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, pz, rep, ab, aacc, sred);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, pz, rep, ab, aacc, sred, ps);
 }
 
 // The middle Horner steps in row-local form.  With W = G* S_{i+1} = F bB +
@@ -2425,7 +2430,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
                                                       const double *__restrict__ eta, const int *__restrict__ off,
                                                       const int *__restrict__ lst, const double *__restrict__ Zc,
                                                       int64_t ldz, int pz, const double *__restrict__ ab, uint64_t seed,
-                                                      double *__restrict__ PV, double *__restrict__ FV) {
+                                                      double *__restrict__ PV, double *__restrict__ FV, int ps) {
   constexpr int NT = P / 16, KP = P / 4;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -2476,7 +2481,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
             }
           }
           if (c >= p) x = 0.0;
-          pvr[(int64_t)s * P + c] = x;
+          if (c < ps) pvr[(int64_t)s * ps + c] = x;
         }
     }
   }
@@ -2505,7 +2510,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
                                                             const double *__restrict__ PV,
                                                             const double *__restrict__ FV,
                                                             const double *__restrict__ FtF,
-                                                            double *__restrict__ Zc) {
+                                                            double *__restrict__ Zc, int ps) {
   constexpr int NT = P / 16;
   const int rep = blockIdx.x;
   if (w.done[rep]) return;
@@ -2559,7 +2564,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         hz[ct][g] = c < pz ? HZ[(int64_t)sc * ldz + (int64_t)rep * pz + c] : 0.0;
-        pv[ct][g] = pvr[(int64_t)sc * P + c];
+        pv[ct][g] = c < ps ? pvr[(int64_t)sc * ps + c] : 0.0;
       }
     }
     dv4 yP[NT], yE[NT];
@@ -2723,6 +2728,14 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // 16-byte DMA pairs): the H.Z GEMM's work scales with the block p, not P
   const int pz = (p + 1) & ~1;
   const int64_t ldz = (int64_t)nb * pz;
+  // the per-replicate T-row buffers (Q, Y, V0 in U, PV in S, the warm start
+  // Q0) hold compact rows of ps = pz columns (columns >= p are zero, so the
+  // register layouts' columns ps..P-1 load as zero and are never stored):
+  // ~20 % fewer bytes in the per-replicate passes at C3 (P = 16, pz = 12).
+  // Replicate slots keep the P-column stride (T P doubles), so a retired
+  // replicate's final Ritz vectors (U, row stride P, eig_final_kernel) never
+  // overlap another replicate's compact rows.
+  const int ps = pz;
   double *Zc = (double *)fws;
   double *HZ = Zc + (size_t)z_rows(m) * ldz;
   double *ab = HZ + (size_t)m * ldz;
@@ -2762,12 +2775,12 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   {
     const int64_t n = (int64_t)m * P;
     dim3 grid((unsigned)((n + 255) / 256), 1);
-    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0);
+    hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0, ps);
     hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(3 * m + 1) * 4, st, fb, idx, eta,
                        off, lst, w.trace, mid ? PFb : nullptr, E2b);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
                        0.0, 0.0, eta,
-                       off, lst, qin, qs, alt, Zc, ldz, pz, ab, seed);
+                       off, lst, qin, qs, alt, Zc, ldz, pz, ab, seed, ps);
   }
   if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
@@ -2806,7 +2819,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
     hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, pz,
-                       ab, qin, qs, alt);
+                       ab, qin, qs, alt, ps);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
     hipLaunchKernelGGL(eig_small_kernel<P>, dim3(nb), dim3(64), 0, st, w, p, 1, kJacobiSweeps);
@@ -2814,10 +2827,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
     if (mid && it == 0 && it < maxit - 1)   // before ap2 overwrites Z(Q) and a(Q)
       hipLaunchKernelGGL(boot_pv_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, it, eta, off, lst, Zc, ldz,
-                         pz, ab, seed, w.S, FVb);
+                         pz, ab, seed, w.S, FVb, ps);
     hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, it, 0,
                        it == maxit - 1 ? 1 : 0, cheb, ca[dg], ca[dg - 1], bb, eta, off, lst, qin, qs, alt, Zc, ldz,
-                       pz, ab, seed);
+                       pz, ab, seed, ps);
     if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
     if (it >= first_poll) {
       if (ahead) {
@@ -2862,10 +2875,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
         if (mid && it == 0 && sp < dg)
           hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
-                             ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, FtF, Zc);
+                             ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, FtF, Zc, ps);
         else
           hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
-                             st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, pz, ab, ca[dg - sp], bb, k, cur, Zc);
+                             st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, pz, ab, ca[dg - sp], bb, k, cur, Zc, ps);
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
       }
       last_cheb = it;

@@ -15,6 +15,7 @@
 #   c2         C2 only, 5 reps (c2.jsonl)
 #   c2prof     rocprofv3 kernel summary of the C2 job, one lane (c2prof/)
 #   c5         bench.py --workload c5, expanding and rolling 1000 (c5.jsonl)
+#   abrows     production vs $VAR: C3 rows bit-identical + alternating timings (3 rounds)
 #   ab         production vs $VAR (a variant libdfm.so) alternating, C3 + 1250 (+ C2 if C2=1)
 #   sanitize   the host sanitizer harnesses (tools/gpu_sanitize.sh)
 TAG=$1; shift
@@ -109,6 +110,14 @@ for step in "$@"; do
         bench_ab "new_$r" - && bench_ab "var_$r" "$VAR"
         bench_ab "new1250_$r" - --replicates 1250 && bench_ab "var1250_$r" "$VAR" --replicates 1250
         if [ "$C2" = 1 ]; then c2_ab "newc2_$r" - && c2_ab "varc2_$r" "$VAR"; fi
+      done ;;
+    abrows)   # production vs $VAR: C3 rows bit-identical, then alternating timings (C3 + 1250)
+      bench_ab var_rows "$VAR" --steps 2 --warmup 1 --dump-rows "$OUT/rows_var.npy"
+      bench_ab new_rows - --steps 2 --warmup 1 --dump-rows "$OUT/rows_new.npy"
+      python3 -c "import numpy as np,sys; a=np.load(sys.argv[1]); b=np.load(sys.argv[2]); print('rows bit-identical:', a.shape, np.array_equal(a, b), float(np.nanmax(np.abs(a-b))))" "$OUT/rows_var.npy" "$OUT/rows_new.npy"
+      for r in 1 2 3; do
+        bench_ab "var_$r" "$VAR" && bench_ab "new_$r" -
+        bench_ab "var1250_$r" "$VAR" --replicates 1250 && bench_ab "new1250_$r" - --replicates 1250
       done ;;
     sanitize)
       bash tools/gpu_sanitize.sh ;;
