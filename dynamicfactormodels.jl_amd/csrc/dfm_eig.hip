@@ -2727,7 +2727,13 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // Z / HZ hold pz = p rounded up to even columns per replicate (the GEMM's
   // 16-byte DMA pairs): the H.Z GEMM's work scales with the block p, not P
   const int pz = (p + 1) & ~1;
-  const int64_t ldz = (int64_t)nb * pz;
+  // (round 6, measured and rejected: Z / HZ rows padded to 128-B lines cut the
+  // H.Z GEMM's FETCH_SIZE 0.40 -> 0.32 GB per launch — unpadded, a 512-B tile
+  // row straddles five lines, one shared with another XCD's column block — but
+  // left the GEMM's time unchanged and slowed the gathering passes 2-4 % with
+  // an even or an odd number of lines per row: C3 15.09 -> 15.27-15.38 ms)
+  const int ncz = nb * pz;
+  const int64_t ldz = ncz;
   // the per-replicate T-row buffers (Q, Y, V0 in U, PV in S, the warm start
   // Q0) hold compact rows of ps = pz columns (columns >= p are zero, so the
   // register layouts' columns ps..P-1 load as zero and are never stored):
@@ -2812,7 +2818,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const double *ca = it == 0 ? ca0 : ca1;
     const double bb = it == 0 ? beta0 : 0.0;
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
-    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, pz, true,
+    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, ncz, m, st, w.done, pz, true,
                                cl_on ? alist : nullptr, cl_on ? acount : nullptr);
     if (tf) tf(tctx, DFM_KC_GEMM, 0);
     if (e != hipSuccess) return 1000 + (int)e;
@@ -2868,7 +2874,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       // basis S_0 goes back into cur (Q), Y stays in alt
       for (int sp = 2; sp <= dg; ++sp) {
         if (tf) tf(tctx, DFM_KC_GEMM, 1);
-        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, (int)ldz, m, st, w.done, pz, true,
+        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, ncz, m, st, w.done, pz, true,
                         cl_on ? alist : nullptr, cl_on ? acount : nullptr);
         if (tf) tf(tctx, DFM_KC_GEMM, 0);
         if (e != hipSuccess) return 1000 + (int)e;

@@ -340,6 +340,14 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
   }
   const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
   const int oi = lane >> 4, oj = lane & 3;
+#if defined(DFM_GEMM_SC1)
+  // A/B: HZ leaves through write-through (sc1) 16-B stores, which drop the
+  // line from this XCD's L2 (MI355X_MICROARCH.md, store flavours) — the
+  // 360 MB output stream then no longer evicts the L2-resident H (2 MB) that
+  // every workgroup re-reads.  Lane pairs (oj, oj ^ 1) combine two adjacent
+  // columns; the even lane stores both.
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(C, 0, (int)((int64_t)M * ldc * 8), 0x00020000);
+#endif
 #pragma unroll
   for (int fa = 0; fa < 8; ++fa)
 #pragma unroll
@@ -351,6 +359,19 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
       const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
       const int row = abase + wr * 32 + 4 * fa + oi;
       const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+#if defined(DFM_GEMM_SC1)
+      if (RUN) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const double vn = __shfl_xor(v, 1);
+        const bool ok = row < M && (clist ? col < ccount * col_group : col < Nc);
+        if (!(oj & 1) && ok) {
+          const int64_t pc = clist ? g2_phys_col(col, clist, ccount, col_group) : (int64_t)col;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, double2{v, vn}), crs,
+                                                 (int)(((int64_t)row * ldc + pc) * 8), 0, 16);
+        }
+        continue;
+      }
+#endif
       if (clist) {
         if (row < M && col < ccount * col_group) C[(int64_t)row * ldc + g2_phys_col(col, clist, ccount, col_group)] = v;
       } else if (row < M && col < Nc) {

@@ -7,6 +7,7 @@
 #   tests      the -m gpu suite (pytest.txt)
 #   bench      the default bench line (bench.json)
 #   prof       rocprofv3 --kernel-trace --stats of the headline workload (prof/)
+#   trace      per-dispatch kernel trace of a 3-step C3 run (TRACE_ARGS: extra bench.py flags)
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the C3 GEMM + passes -> pmc_traffic.json
 #   pmc_c2     FETCH_SIZE / WRITE_SIZE of the C2 job's fused solver + Chow -> pmc_traffic_c2.json
 #   sq_c2      SQ counter passes of the C2 kernels (one lane: DFM_NO_LANES=1)
@@ -54,6 +55,10 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 bench.py \
         --no-cpu-baseline --no-all-fields > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || fail prof $? "$OUT/bench_prof.err"
       line "$OUT/bench_prof.json" bench_under_rocprof ;;
+    trace)   # per-dispatch kernel trace of a short C3 run (trace/: kernel_trace.csv)
+      timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d "$OUT/trace" -o run -- python3 bench.py --steps 3 --warmup 2 \
+        --no-cpu-baseline --no-all-fields ${TRACE_ARGS} > "$OUT/trace.json" 2> "$OUT/trace.err" || fail trace $? "$OUT/trace.err"
+      line "$OUT/trace.json" bench_under_trace ;;
     pmc)
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemmh_kernel|boot_" -f csv -d "$OUT/pmc_f" \
         -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/pmc_f.out" 2> "$OUT/pmc_f.err" \
