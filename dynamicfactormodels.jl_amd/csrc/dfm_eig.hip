@@ -1502,6 +1502,12 @@ int eig_run(const double *G, int64_t ldg, int64_t strideG, int m, int nb, int k,
 //   S = L'L, EL = E L (T x r), H = E E' (T x T)  — S, EL, H shared by all
 // replicates.  H Z for a whole batch is ONE MFMA GEMM (dfm_gemm.hip) with H
 // resident in L2; everything else is O(T r p) per replicate.
+// waves per replicate workgroup of the factored passes (prep, y2, ap2, Chebyshev)
+#ifndef DFM_BW
+#define DFM_BW 4
+#endif
+constexpr int BW = DFM_BW;   // dynamic LDS of ap2: 16 T + 4 bytes
+
 struct FactBase {
   int T, r;
   int64_t ldH;
@@ -1511,11 +1517,29 @@ struct FactBase {
 // Per replicate: CSR of idx (bucket s lists t ascending — fixed summation
 // order, bit-reproducible), and trace(G*) = sum_t ||x*_t||^2 =
 // sum_t [F_t S F_t' + 2 eta_t F_t.(EL)_idx_t + eta_t^2 H_idx_t,idx_t].
+//
+// Round 6: the same kernel then forms the first H.Z product's operand
+// Z0 = P'D Q0 and the first step's ab = [a; cc] (a = F'Q0, cc = EL'Z0) —
+// the init pass of boot_ap2_kernel before, the same arithmetic in the same
+// order (its tile loop and zscatter_tail), without that pass's launch and
+// its reload of the CSR this kernel already holds in LDS.
+template <int P>
+DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
+                           const double *set, const int *so, const int *sl, const double *Qn,
+                           double *__restrict__ Zc, int64_t ldz, int pz, int rep, double *__restrict__ ab,
+                           const dv4 *aacc, double *sred, int ps);
+template <int P>
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta, int *__restrict__ off,
                                                         int *__restrict__ lst, double *__restrict__ trace,
-                                                        double *__restrict__ PF, double *__restrict__ E2) {
-  extern __shared__ int sh[];   // cnt[T+1], six[T], sorted list L[T]
+                                                        double *__restrict__ PF, double *__restrict__ E2,
+                                                        const double *__restrict__ Q0, int ps,
+                                                        double *__restrict__ Zc, int64_t ldz, int pz,
+                                                        double *__restrict__ ab) {
+  static_assert(BW * 64 == 256, "prep runs the factored passes' wave layout");
+  constexpr int NT = P / 16;
+  __shared__ double sred[NT * 256];
+  extern __shared__ int sh[];   // cnt[T+1], six[T], sorted list L[T] (+ so[T+1], eta[T]: Zc)
   __shared__ double red[256];
   __shared__ int scan[256];
   const int tid = threadIdx.x, rep = blockIdx.x, T = fb.T, r = fb.r;
@@ -1594,6 +1618,41 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
         if (j < r) pf[j] = a[j];
       E2[(int64_t)rep * T + s] = a2;
     }
+  if (Zc) {
+    // LDS for zscatter_tail after the sorted list: bucket starts so[0..T], eta_t
+    int *so = sh + 3 * T + 1;
+    double *set = reinterpret_cast<double *>(sh + ((4 * T + 2 + 1) & ~1));
+    for (int q = tid; q <= T; q += 256) so[q] = q ? cnt[q - 1] : 0;
+    for (int t = tid; t < T; t += 256) set[t] = et ? et[t] : 1.0;
+    // a = F'Q0 in boot_ap2_kernel's init order (its tiles, its accumulator layout)
+    const int lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+    const int ntile = (T + 15) >> 4;
+    dv4 aacc[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+    for (int tile = wave; tile < ntile; tile += BW) {
+      const int t0 = tile * 16;
+      double fa[4], qv[NT][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int t = t0 + 4 * g + lk;
+        const int tc = min(t, T - 1);
+        const double f = r > 0 ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
+        fa[g] = (t < T && li < r) ? f : 0.0;
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) {
+          const double q = 16 * ct + li < ps ? Q0[(int64_t)tc * ps + 16 * ct + li] : 0.0;
+          qv[ct][g] = t < T ? q : 0.0;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
+    }
+    __syncthreads();   // so / set visible
+    zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, ldz, pz, rep, ab, aacc, sred, ps);
+  }
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
     const int i = ix[t];
@@ -1647,11 +1706,6 @@ size_t fact_workspace_bytes(int T, int nb, int P) {
 // 4g .. 4g+3 in exactly the B-operand layout, so Q'Y etc. need no lane movement.
 // Reductions over waves run in a fixed order: bit-reproducible, batch-invariant.
 constexpr int F2_T_MAX = 4096;
-// waves per replicate workgroup of the factored passes (y2, ap2, Chebyshev)
-#ifndef DFM_BW
-#define DFM_BW 4
-#endif
-constexpr int BW = DFM_BW;   // dynamic LDS of ap2: 16 T + 4 bytes
 
 // Convergence verdict from per-column squared residuals res2[j] (j < k), on
 // one whole wave (same rules as check_converged: strict eigenvector-residual
@@ -2782,11 +2836,10 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const int64_t n = (int64_t)m * P;
     dim3 grid((unsigned)((n + 255) / 256), 1);
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0, ps);
-    hipLaunchKernelGGL(boot_prep_kernel, dim3(nb), dim3(256), (size_t)(3 * m + 1) * 4, st, fb, idx, eta,
-                       off, lst, w.trace, mid ? PFb : nullptr, E2b);
-    hipLaunchKernelGGL(boot_ap2_kernel<P>, dim3(nb), dim3(64 * BW), lds, st, fb, w, m, k, p, tol, -1, 1, 0, 0, 1.0,
-                       0.0, 0.0, eta,
-                       off, lst, qin, qs, alt, Zc, ldz, pz, ab, seed, ps);
+    // the CSR, trace, PF / e2 and the first product's Z0 and ab (the init
+    // pass boot_ap2_kernel<init = 1> ran separately before round 6)
+    hipLaunchKernelGGL(boot_prep_kernel<P>, dim3(nb), dim3(256), (size_t)((4 * m + 3) & ~1) * 4 + (size_t)m * 8, st,
+                       fb, idx, eta, off, lst, w.trace, mid ? PFb : nullptr, E2b, Q0, ps, Zc, ldz, pz, ab);
   }
   if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
