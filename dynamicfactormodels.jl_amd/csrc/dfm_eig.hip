@@ -1514,6 +1514,15 @@ struct FactBase {
   const double *F, *EL, *S, *H, *cF, *hd;   // T x r, T x r, r x r, T x ldH, T, T
 };
 
+// Z, the H.Z GEMM's B operand, replicate-major in 16-row chunks (round 6,
+// gemmh_zrm_kernel): replicate rep's element (s, c) at
+// rep zrs + (s >> 4) 16 pz + 16 c + (s & 15), zrs = round_up(T, 16) pz; the
+// chunk rows s >= T are zero (boot_prep_kernel writes them each call)
+DFM_DEV int64_t zrm_stride(int T, int pz) { return (int64_t)((T + 15) & ~15) * pz; }
+DFM_DEV int64_t zrm_ix(int rep, int s, int c, int pz, int64_t zrs) {
+  return (int64_t)rep * zrs + (int64_t)(s >> 4) * (16 * pz) + 16 * c + (s & 15);
+}
+
 // Per replicate: CSR of idx (bucket s lists t ascending — fixed summation
 // order, bit-reproducible), and trace(G*) = sum_t ||x*_t||^2 =
 // sum_t [F_t S F_t' + 2 eta_t F_t.(EL)_idx_t + eta_t^2 H_idx_t,idx_t].
@@ -1526,7 +1535,7 @@ struct FactBase {
 template <int P>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
-                           double *__restrict__ Zc, int64_t ldz, int pz, int rep, double *__restrict__ ab,
+                           double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
                            const dv4 *aacc, double *sred, int ps);
 template <int P>
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
@@ -1650,8 +1659,14 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
     }
+    // the last chunk's rows past T (the H.Z GEMM's zero k-padding of B)
+    {
+      const int64_t zrs = zrm_stride(T, pz);
+      const int npad = ((T + 15) & ~15) - T;
+      for (int e = tid; e < npad * pz; e += 256) Zc[zrm_ix(rep, T + e / pz, e % pz, pz, zrs)] = 0.0;
+    }
     __syncthreads();   // so / set visible
-    zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, ldz, pz, rep, ab, aacc, sred, ps);
+    zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, pz, rep, ab, aacc, sred, ps);
   }
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
@@ -1673,6 +1688,9 @@ hipError_t launch_gemm(bool a_trans, const double *A, int64_t lda, const double 
                        double *C, int64_t ldc, int M, int Nc, int K, hipStream_t st,
                        const int *col_done = nullptr, int col_group = 1, bool b_padded = false,
                        const int *clist = nullptr, const int *ccount = nullptr);
+hipError_t launch_gemm_zrm(const double *A, int64_t lda, const double *Z, int pz, int64_t zrs, double *C,
+                           int64_t ldc, int M, int Nc, int K, hipStream_t st, const int *col_done, const int *clist,
+                           const int *ccount);
 
 // Z (the GEMM's B operand) has round_up(T, 16) rows, the pad rows zero, so
 // the H.Z GEMM streams it with running DMA pointers and no k-tail clamp
@@ -2021,8 +2039,9 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
 template <int P>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
-                           double *__restrict__ Zc, int64_t ldz, int pz, int rep, double *__restrict__ ab,
+                           double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
                            const dv4 *aacc, double *sred, int ps) {
+  const int64_t zrs = zrm_stride(T, pz);
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
   dv4 cacc[NT];
@@ -2077,7 +2096,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
       const double ea = (v && li < r) ? fb.EL[(int64_t)s * r + li] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        if (v && 16 * ct + li < pz) Zc[(int64_t)s * ldz + (int64_t)rep * pz + 16 * ct + li] = z[g][ct];
+        if (v && 16 * ct + li < pz) Zc[zrm_ix(rep, s, 16 * ct + li, pz, zrs)] = z[g][ct];
         cacc[ct] = mfma16(ea, z[g][ct], cacc[ct]);
       }
     }
@@ -2293,7 +2312,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
   const double *Qn = init ? Qr : Yr;
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, ldz, pz, rep, ab, aacc, sred, ps);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, pz, rep, ab, aacc, sred, ps);
 }
 
 // One Horner step of the degree-d Chebyshev filter of the factored solver.
@@ -2412,7 +2431,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
   }
   __syncthreads();   // every wave's Qn rows visible to the CSR gather
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, ldz, pz, rep, ab, aacc, sred, ps);
+  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, pz, rep, ab, aacc, sred, ps);
 }
 
 // The middle Horner steps in row-local form.  With W = G* S_{i+1} = F bB +
@@ -2511,7 +2530,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
     double za[KP];
 #pragma unroll
     for (int kk = 0; kk < KP; ++kk)
-      za[kk] = (t0 + li < T && 4 * kk + lk < pz) ? Zc[(int64_t)ta * ldz + (int64_t)rep * pz + 4 * kk + lk] : 0.0;
+      za[kk] = (t0 + li < T && 4 * kk + lk < pz) ? Zc[zrm_ix(rep, ta, 4 * kk + lk, pz, zrm_stride(T, pz))] : 0.0;
     dv4 v[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) v[ct] = dv4{0.0, 0.0, 0.0, 0.0};
@@ -2647,7 +2666,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
         if (c >= p || !v) z = 0.0;
         uv[ct][g] = v ? u : 0.0;
         zv[ct][g] = z;
-        if (v && c < pz) Zc[(int64_t)s * ldz + (int64_t)rep * pz + c] = z;
+        if (v && c < pz) Zc[zrm_ix(rep, s, c, pz, zrm_stride(T, pz))] = z;
       }
     }
 #pragma unroll
@@ -2787,7 +2806,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // left the GEMM's time unchanged and slowed the gathering passes 2-4 % with
   // an even or an odd number of lines per row: C3 15.09 -> 15.27-15.38 ms)
   const int ncz = nb * pz;
-  const int64_t ldz = ncz;
+  const int64_t ldz = ncz;           // HZ: T x nb pz, column-interleaved (rows gathered by idx)
+  const int64_t zrs = z_rows(m) * pz;   // Z: replicate-major 16-row chunks (zrm_ix), nb zrs <= z_rows ldz
   // the per-replicate T-row buffers (Q, Y, V0 in U, PV in S, the warm start
   // Q0) hold compact rows of ps = pz columns (columns >= p are zero, so the
   // register layouts' columns ps..P-1 load as zero and are never stored):
@@ -2808,7 +2828,6 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     zs.p[0] = w.active; zs.n[0] = maxit + 2;
     zs.p[1] = w.iters; zs.n[1] = nb;
     zs.p[2] = w.done; zs.n[2] = nb;
-    if (z_rows(m) > m) { zs.p[3] = (int *)(Zc + (size_t)m * ldz); zs.n[3] = (int64_t)(z_rows(m) - m) * ldz * 2; }
     if (launch_zero_spans(zs, st) != hipSuccess) return 1001;
   }
   const uint64_t seed = 0x5eed0000ull + (uint64_t)m * 131 + k;
@@ -2871,8 +2890,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const double *ca = it == 0 ? ca0 : ca1;
     const double bb = it == 0 ? beta0 : 0.0;
     if (tf) tf(tctx, DFM_KC_GEMM, 1);
-    hipError_t e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, ncz, m, st, w.done, pz, true,
-                               cl_on ? alist : nullptr, cl_on ? acount : nullptr);
+    hipError_t e = launch_gemm_zrm(fb.H, fb.ldH, Zc, pz, zrs, HZ, ldz, m, ncz, m, st, w.done,
+                                   cl_on ? alist : nullptr, cl_on ? acount : nullptr);
     if (tf) tf(tctx, DFM_KC_GEMM, 0);
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
@@ -2927,8 +2946,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
       // basis S_0 goes back into cur (Q), Y stays in alt
       for (int sp = 2; sp <= dg; ++sp) {
         if (tf) tf(tctx, DFM_KC_GEMM, 1);
-        e = launch_gemm(false, fb.H, fb.ldH, Zc, ldz, HZ, ldz, m, ncz, m, st, w.done, pz, true,
-                        cl_on ? alist : nullptr, cl_on ? acount : nullptr);
+        e = launch_gemm_zrm(fb.H, fb.ldH, Zc, pz, zrs, HZ, ldz, m, ncz, m, st, w.done,
+                            cl_on ? alist : nullptr, cl_on ? acount : nullptr);
         if (tf) tf(tctx, DFM_KC_GEMM, 0);
         if (e != hipSuccess) return 1000 + (int)e;
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);

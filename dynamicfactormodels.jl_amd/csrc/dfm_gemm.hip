@@ -384,6 +384,147 @@ __global__ __launch_bounds__(256, MINB) void gemmh_kernel_t(const double *__rest
 #define gemmh_kernel gemmh_kernel_t<4, 2>
 
 // ---------------------------------------------------------------------------
+// gemmh_zrm_kernel: the factored solver's H.Z with Z replicate-major (round 6).
+// Z holds replicate rep's T x pz block as 16-row chunks, each chunk column-
+// major: element (s, c) at rep zrs + (s >> 4) 16 pz + 16 c + (s & 15)
+// (zrs = round_up(T, 16) pz, the chunk rows past T zero).  A 16-deep k stage
+// of one B column is then ONE 128-B line, so the B operand is staged like A
+// (and like gram_dma_kernel's second operand): an [a][k] LDS image, 8 columns
+// per DMA instruction, each column's 16 k values one line — a 64-column tile
+// spanning 5.33 replicates reads whole lines, where the column-interleaved
+// T x nb pz layout read one 512-B k-row segment and a replicate-major
+// [rep][T][pz] layout six 96-B pieces per k-row (round 5: +5.6 % GEMM).
+// The passes that write Z (zscatter_tail, boot_cheb_mid_kernel) then write
+// each replicate's 16-row tile as one contiguous 16 pz x 8-B chunk.  The
+// fragments hold the same elements as gemmh_kernel_t's, so HZ is
+// bit-identical; C (HZ) keeps the column-interleaved layout (its rows are
+// gathered by idx).  A = H as gemmh_kernel_t<3, 3, true> (lda >= round_up(K,
+// 16), zero k-padding); 3-deep ring at 3 workgroups per CU; column
+// compaction by clist as gemmh_kernel_t.
+__global__ __launch_bounds__(256, 3) void gemmh_zrm_kernel(const double *__restrict__ A, int64_t lda,
+                                                          const double *__restrict__ Z, int pz, int64_t zrs,
+                                                          double *__restrict__ C, int64_t ldc, int M, int Nc, int K,
+                                                          int nrb, int ncb, const int *__restrict__ col_done,
+                                                          const int *__restrict__ clist, const int *__restrict__ ccount_p) {
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(16))) double lds[NBUF * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int bid = blockIdx.x, xcd = bid & 7, j = bid >> 3;
+  const int rb = j % nrb, cb = (j / nrb) * 8 + xcd;
+  if (cb >= ncb) return;
+  const int abase = rb * GT, bbase = cb * GT, col_group = pz;
+  const int ccount = clist ? *ccount_p : 0;
+  const bool compact = clist && (int64_t)ccount * 8 < Nc / col_group;
+  clist = compact ? clist : nullptr;
+  if (compact) {
+    if (bbase >= ccount * col_group) return;
+    if (col_done) {
+      bool all = true;
+      const int s0 = bbase / col_group, s1 = min(ccount - 1, (bbase + GT - 1) / col_group);
+      for (int q = s0; q <= s1; ++q) all = all && col_done[clist[q]];
+      if (all) return;
+    }
+  } else if (col_done) {
+    bool all = true;
+    const int r0 = bbase / col_group, r1 = min(Nc - 1, bbase + GT - 1) / col_group;
+    for (int q = r0; q <= r1; ++q) all = all && col_done[q];
+    if (all) return;
+  }
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[i][q] = 0.0;
+  const int fi = lane & 3, fkc = 4 * (lane >> 4) + ((lane >> 2) & 3);
+  const int nst = (K + G2_KS - 1) / G2_KS;
+  // per-lane DMA sources: rows a of the A block and columns a of the B block,
+  // 16 k per row in 8 lane pairs (the [a][k] images' XOR swizzle on the source k)
+  const double *pa[2], *pb[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 2 * wave + h;
+    const int a = 8 * c + (lane >> 3);
+    const int ka = (2 * (lane & 7)) ^ (((a >> 1) & 1) << 3);
+    pa[h] = A + (int64_t)min(abase + a, M - 1) * lda + ka;
+    const int x = bbase + a;
+    int rep, cc;
+    if (clist) {   // compact column x: replicate clist[x / pz] (past the list: finite, discarded)
+      const int slot = min(x / pz, ccount - 1);
+      rep = clist[slot];
+      cc = x - (x / pz) * pz;
+    } else {
+      const int xc = min(x, Nc - 1);   // past Nc: finite data, discarded outputs
+      rep = xc / pz;
+      cc = xc - rep * pz;
+    }
+    pb[h] = Z + (int64_t)rep * zrs + 16 * cc + ka;
+  }
+  const int64_t bstep = (int64_t)G2_KS * pz;
+  const int c0 = (2 * wave) * 128, c1 = c0 + 128;
+  auto issue = [&](int s) {
+    double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa[0], (lds_void_t *)(la + c0), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb[0], (lds_void_t *)(lb + c0), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pa[1], (lds_void_t *)(la + c1), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t *)pb[1], (lds_void_t *)(lb + c1), 16, 0, 0);
+    pa[0] += G2_KS; pa[1] += G2_KS; pb[0] += bstep; pb[1] += bstep;
+  };
+  for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    const int ahead = min(NBUF - 2, nst - 1 - s);
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NBUF - 1 < nst) issue(s + NBUF - 1);
+    const double *la = lds + (s % NBUF) * G2_STAGE, *lb = la + GT * G2_KS;
+    double af[8], bf[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      af[f] = la[g2_offA(wr * 32 + 4 * f + fi, fkc)];
+      bf[f] = lb[g2_offA(wc * 32 + 4 * f + fi, fkc)];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[i][q] = mfma4(af[i], bf[q], acc[i][q]);
+  }
+  const int b1 = (lane >> 2) & 1, b2 = (lane >> 3) & 1, blk = (lane >> 2) & 3;
+  const int oi = lane >> 4, oj = lane & 3;
+#pragma unroll
+  for (int fa = 0; fa < 8; ++fa)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double a0 = acc[fa][4 * q], a1 = acc[fa][4 * q + 1], a2 = acc[fa][4 * q + 2],
+                   a3 = acc[fa][4 * q + 3];
+      double k01 = (b1 ? a1 : a0) + __shfl_xor(b1 ? a0 : a1, 4);
+      double k23 = (b1 ? a3 : a2) + __shfl_xor(b1 ? a2 : a3, 4);
+      const double v = (b2 ? k23 : k01) + __shfl_xor(b2 ? k01 : k23, 8);
+      const int row = abase + wr * 32 + 4 * fa + oi;
+      const int col = bbase + wc * 32 + 16 * q + 4 * blk + oj;
+      if (clist) {
+        if (row < M && col < ccount * col_group) C[(int64_t)row * ldc + g2_phys_col(col, clist, ccount, col_group)] = v;
+      } else if (row < M && col < Nc) {
+        C[(int64_t)row * ldc + col] = v;
+      }
+    }
+}
+
+// H (M x K, lda >= round_up(K, 16), zero k-padding) times the replicate-major
+// chunked Z of nb = Nc / pz replicates (gemmh_zrm_kernel) -> C (M x Nc, ldc)
+hipError_t launch_gemm_zrm(const double *A, int64_t lda, const double *Z, int pz, int64_t zrs, double *C,
+                           int64_t ldc, int M, int Nc, int K, hipStream_t st, const int *col_done, const int *clist,
+                           const int *ccount) {
+  if (lda < (K + G2_KS - 1) / G2_KS * G2_KS || pz < 2 || (pz & 1) || Nc % pz) return hipErrorInvalidValue;
+  const int nrb = (M + GT - 1) / GT, ncb = (Nc + GT - 1) / GT;
+  const int ncb8 = (ncb + 7) / 8 * 8;
+  hipLaunchKernelGGL(gemmh_zrm_kernel, dim3(nrb * ncb8), dim3(256), 0, st, A, lda, Z, pz, zrs, C, ldc, M, Nc, K, nrb,
+                     ncb, col_done, clist, ccount);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Loadings GEMM of the factored bootstrap:
 //   L*[rep][n][j] = ( [E' | L] [ZF ; M1] )[n][rep rp + j] / T
 // (src/DynamicFactorModel.jl:90 for every replicate: L* = X*' F* / T with
