@@ -473,15 +473,15 @@ def main():
         flop_total = 2.0 * T * T * PZ * eig["gemm_products"]
         per_launch_ms = gemm_ms / gemm_n
         achieved = flop_total / (gemm_ms * 1e-3) / 1e12
-        roof = {"kernel": "gemmh_kernel_t<3,3,RUN> (batched eigen-iteration H.Z: LDS-DMA 3-deep ring, running "
-                          "source pointers over the zero-padded Z, 3 workgroups/CU, v_mfma_f64_4x4x4_4b)",
+        roof = {"kernel": "gemmh_zrm_kernel (batched eigen-iteration H.Z: LDS-DMA 3-deep ring, running source "
+                          "pointers over the replicate-major chunked Z, 3 workgroups/CU, v_mfma_f64_4x4x4_4b)",
                 "bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F64_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F64_TFLOPS, 4),
-                "traffic": pmc_traffic("gemmh_kernel_t<3, 3, true>"),
+                "traffic": pmc_traffic("gemmh_zrm_kernel"),
                 "avg_launch_ms": round(per_launch_ms, 4),
                 "flop_per_launch": round(flop_total / gemm_n), "launches": gemm_n,
                 "flop_per_replicate_product": 2 * T * T * PZ, "block_columns": PZ}
-        rp_ms, rp_src = rocprof_avg_ms("dfm::gemmh_kernel_t<3, 3, true>")
+        rp_ms, rp_src = rocprof_avg_ms("dfm::gemmh_zrm_kernel")
         if rp_ms:   # the same algorithmic flop per launch over rocprof's average duration
             roof["rocprof"] = {"avg_launch_ms": round(rp_ms, 4), "source": f"profiles/{rp_src}",
                                "frac": round(flop_total / gemm_n / (rp_ms * 1e-3) / 1e12 / PEAK_F64_TFLOPS, 4)}

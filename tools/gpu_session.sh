@@ -60,10 +60,10 @@ for step in "$@"; do
         --no-cpu-baseline --no-all-fields ${TRACE_ARGS} > "$OUT/trace.json" 2> "$OUT/trace.err" || fail trace $? "$OUT/trace.err"
       line "$OUT/trace.json" bench_under_trace ;;
     pmc)
-      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemmh_kernel|boot_" -f csv -d "$OUT/pmc_f" \
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gemmh_|boot_" -f csv -d "$OUT/pmc_f" \
         -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/pmc_f.out" 2> "$OUT/pmc_f.err" \
         || fail pmc_f $? "$OUT/pmc_f.err"
-      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemmh_kernel|boot_" -f csv -d "$OUT/pmc_w" \
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gemmh_|boot_" -f csv -d "$OUT/pmc_w" \
         -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/pmc_w.out" 2> "$OUT/pmc_w.err" \
         || fail pmc_w $? "$OUT/pmc_w.err"
       python3 tools/pmc_traffic.py "$OUT/pmc_f" "$OUT/pmc_w" > "$OUT/pmc_traffic.json" && head -c 1200 "$OUT/pmc_traffic.json"; echo ;;
