@@ -182,13 +182,17 @@ struct dfm_ctx {
 static const PollBuf *ctx_poll(const dfm_ctx *c) { return c->pollbuf.host ? &c->pollbuf : nullptr; }
 
 // stream -> the owning context's pool (stream_malloc); guarded: contexts are
-// created, re-streamed and destroyed from any host thread
+// created, re-streamed and destroyed from any host thread.  One entry per
+// context (a context re-registers after dfm_ctx_set_stream).  A stream that
+// several contexts are bound to (dfm_ctx_set_stream with a shared external
+// stream) is served by the device's default pool instead of either context's
+// own: a context's pool then never holds blocks another context allocated,
+// so destroying one context (hipMemPoolDestroy) cannot free memory still in
+// flight on the other's calls.
 static std::mutex g_pool_mu;
 static std::vector<std::pair<hipStream_t, hipMemPool_t>> g_pools;
 static void pool_register(hipStream_t st, hipMemPool_t pool) {
   std::lock_guard<std::mutex> g(g_pool_mu);
-  for (auto &e : g_pools)
-    if (e.first == st) { e.second = pool; return; }
   g_pools.emplace_back(st, pool);
 }
 static void pool_unregister(hipMemPool_t pool) {
@@ -201,8 +205,10 @@ hipError_t stream_malloc(void **p, size_t bytes, hipStream_t st) {
   hipMemPool_t pool = nullptr;
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
+    int owners = 0;
     for (auto &e : g_pools)
-      if (e.first == st) { pool = e.second; break; }
+      if (e.first == st) { pool = e.second; ++owners; }
+    if (owners > 1) pool = nullptr;   // a shared stream: the default pool
   }
   const hipError_t e = pool ? hipMallocFromPoolAsync(p, bytes, pool, st) : hipMallocAsync(p, bytes, st);
   if (e == hipSuccess) DFM_POISON_ASYNC(*p, bytes, st);
@@ -1873,6 +1879,9 @@ int dfm_bootstrap(dfm_model *M, int kind, int64_t B, const int32_t *idx, const d
   if (B == 0) return 0;
   for (int64_t i = 0; i < B * M->T; ++i)
     if (idx[i] < 0 || idx[i] >= M->T) return fail(ctx, -8, "resample index out of range at %lld", (long long)i);
+  // the whole call under the device gate — the uploads and the result copy
+  // too, not only dfm_bootstrap_dev's kernels (nested: that share is this one)
+  DeviceShare gate(ctx->device);
   hipSetDevice(ctx->device);
   hipStream_t st = ctx->stream;
   const int64_t width = dfm_stats_width(M, stats, ns);

@@ -330,3 +330,29 @@ def test_bench_gpus2_launches_two_ranks(tmp_path):
     assert "over 2 rank(s)" in two["collective"] and two["outputs_finite"]
     assert rows1.shape == rows2.shape == (9999, rows1.shape[1])
     assert np.array_equal(rows1, rows2)
+
+
+def test_two_contexts_on_one_external_stream(dfm, oracle):
+    """two contexts bound to the same external stream
+    (dfm_ctx_set_stream) draw their stream-ordered scratch from the device's
+    default pool, not from whichever context registered last — so one of
+    them can be destroyed while the other keeps running jobs on the stream.
+    Every row equals a private context's row (src/bootstrap.jl:41-51)."""
+    import torch
+    y, x, w = panel(oracle, 200, 400, 4, 611)
+    idx, eta = dfm.draw_wild_fast(612, 40, 200)
+    stats = [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.t_stat(2)]
+    ref = dfm.wild_bootstrap(dfm.DynamicFactorModel(y, w, x, 4, "ICp2", ctx=dfm.Context(0)), 40, stats, idx=idx, eta=eta)
+    s = torch.cuda.Stream()
+    a, b = dfm.Context(0), dfm.Context(0)
+    a.set_stream(s.cuda_stream)
+    b.set_stream(s.cuda_stream)
+    ga = dfm.DynamicFactorModel(y, w, x, 4, "ICp2", ctx=a)
+    gb = dfm.DynamicFactorModel(y, w, x, 4, "ICp2", ctx=b)
+    assert np.array_equal(dfm.wild_bootstrap(ga, 40, stats, idx=idx, eta=eta), ref)
+    assert np.array_equal(dfm.wild_bootstrap(gb, 40, stats, idx=idx, eta=eta), ref)
+    del ga
+    a.close()
+    for _ in range(3):
+        assert np.array_equal(dfm.wild_bootstrap(gb, 40, stats, idx=idx, eta=eta), ref)
+    torch.cuda.synchronize()
