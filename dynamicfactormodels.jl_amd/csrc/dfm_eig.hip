@@ -1331,7 +1331,10 @@ static int eig_run_t(const double *G, int64_t ldg, int64_t strideG, int m, int n
       ChebCo cc;
       shifted_cheb(kChebDirectStrict, cc.c4);
       shifted_cheb(2, cc.c2);
-      const size_t lds = (size_t)2 * ((m + 15) & ~15) * P * sizeof(double);
+      size_t lds = (size_t)2 * ((m + 15) & ~15) * P * sizeof(double);
+#ifdef DFM_FUSED_PAD   // (A/B builds: extra dynamic LDS -> fewer resident workgroups per CU)
+      lds += DFM_FUSED_PAD;
+#endif
       // DFM_EIG_PROF=1: phase profile of replicate 0 of every fused solve -> stderr
       static const bool want_prof = [] { const char *e = getenv("DFM_EIG_PROF"); return e && atoi(e) != 0; }();
       long long *prof = nullptr;
