@@ -2860,10 +2860,18 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(eig_init_kernel<P>, grid, dim3(256), 0, st, Q0, m, p, warm, kw, w.done, seed, (int64_t)0, ps);
     // the CSR, trace, PF / e2 and the first product's Z0 and ab (the init
     // pass boot_ap2_kernel<init = 1> ran separately before round 6)
-    hipLaunchKernelGGL(boot_prep_kernel<P>, dim3(nb), dim3(256), (size_t)((4 * m + 3) & ~1) * 4 + (size_t)m * 8, st,
+    const size_t prep_lds = (size_t)((4 * m + 3) & ~1) * 4 + (size_t)m * 8;
+    if (prep_lds > 65536)   // T > 2730 (up to F2_T_MAX: 96 KB): above the default dynamic-LDS cap
+      hipFuncSetAttribute((const void *)boot_prep_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)prep_lds);
+    hipLaunchKernelGGL(boot_prep_kernel<P>, dim3(nb), dim3(256), prep_lds, st,
                        fb, idx, eta, off, lst, w.trace, mid ? PFb : nullptr, E2b, Q0, ps, Zc, ldz, pz, ab);
   }
   if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
+  {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
+    const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
+    if (cheb_lds > 65536)
+      hipFuncSetAttribute((const void *)boot_cheb_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cheb_lds);
+  }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
   const double beta0 = warm_started ? warm_beta() : 0.0;
   double ca0[kChebDMax + 1], ca1[kChebDMax + 1];
