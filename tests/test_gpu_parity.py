@@ -519,6 +519,22 @@ def test_direct_and_factored_agree(dfm, oracle):
     assert rel(b[:, 4:], a[:, 4:]) < STAT_RTOL
 
 
+def test_direct_and_factored_agree_at_large_T(dfm, oracle):
+    """T = 3300 (the factored solver's prep and last Horner step then need more
+    than 64 KB of dynamic LDS: 24 T + 8 and 20 T + 4 bytes) against the direct
+    (Gram-forming) path on the same draws (src/bootstrap.jl:41-51)."""
+    y, x, w = panel(oracle, 3300, 3600, 3, 23)
+    g = dfm.DynamicFactorModel(y, w, x, 3, "ICp2")
+    idx, eta = dfm.draw_wild_fast(10, 6, 3300)
+    stats = [dfm.Stat.V(), dfm.Stat.criterion(), dfm.Stat.eigenvalue(1), dfm.Stat.eigenvalue(3)]
+    g.set_bootstrap_mode("direct")
+    a = dfm.wild_bootstrap(g, 6, stats, idx=idx, eta=eta)
+    g.set_bootstrap_mode("factored")
+    assert g.fact_block()[0] > 0
+    b = dfm.wild_bootstrap(g, 6, stats, idx=idx, eta=eta)
+    assert np.all(np.isfinite(b)) and rel(b, a) < STAT_RTOL
+
+
 @pytest.mark.parametrize("T,N,P,crit,kmax", [
     (60, 150, 6, "ICp2", 6), (90, 30, 5, "BIC", 6), (41, 300, 3, "ICp1", 6),
     (60, 150, 6, "PCp2", 6), (200, 160, 4, "PCp1", 6),
