@@ -9,7 +9,8 @@
 #   prof       rocprofv3 --kernel-trace --stats of the headline workload (prof/)
 #   trace      per-dispatch kernel trace of a 3-step C3 run (TRACE_ARGS: extra bench.py flags)
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the C3 GEMM + passes -> pmc_traffic.json
-#   pmc_c2     FETCH_SIZE / WRITE_SIZE of the C2 job's fused solver + Chow -> pmc_traffic_c2.json
+#   pmc_c2     FETCH_SIZE / WRITE_SIZE of the C2 job's fused solver + Chow, one lane
+#              (DFM_NO_LANES=1: per-launch bytes cover more replicates than a lane launch) -> pmc_traffic_c2.json
 #   sq_c2      SQ counter passes of the C2 kernels (one lane: DFM_NO_LANES=1)
 #   shards     C3 at 1250 / 2500 / 5000 / 9999 replicates (shards.jsonl)
 #   configs    tools/bench_configs.py c1,c2,c4,c5 (configs.jsonl)
