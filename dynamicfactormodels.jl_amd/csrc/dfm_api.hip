@@ -98,10 +98,11 @@ hipError_t launch_chow(int orient, const PanelSrc &src, int T, int N, int r, int
                        int64_t out_stride, char *ws, size_t ws_bytes, hipStream_t st, int nblk = 1,
                        const int *brow = nullptr, int64_t lbs = 0);
 size_t chow_workspace_bytes(int T, int N, int r, int nb);
-struct FactBase {
+struct FactBase {   // layout shared with dfm_eig.hip's definition
   int T, r;
   int64_t ldH;
   const double *F, *EL, *S, *H, *cF, *hd;
+  const double *FtF = nullptr;
 };
 __global__ void eig_trace_kernel(const double *__restrict__ G, int64_t ldg, int64_t strideG, int m,
                                  double *__restrict__ trace);
@@ -133,6 +134,7 @@ hipError_t launch_predict(const double *Xp, int64_t ld, int T, int N, const doub
                           double *work, double *F_out, double *yhat, hipStream_t st);
 int fact_precompute(const double *Ep, int64_t ld, int T, int N, int r, const double *Lb, const double *Fb,
                     const double *H, int64_t ldH, double *EL, double *S, double *cF, double *hd, hipStream_t st);
+hipError_t launch_fact_ftf(const FactBase &fb, double *FtF, hipStream_t st);
 hipError_t launch_targeted(int mode, const double *y, const double *w, int q, const double *Xp,
                            int64_t ld, int T, int N, double cv, double *tstat, uint8_t *mask,
                            char *ws, size_t ws_bytes, hipStream_t st, int *bad);
@@ -349,6 +351,7 @@ struct dfm_model {
   bool fact_ready = false;
   int64_t ldH = 0;
   double *H = nullptr, *EL = nullptr, *S = nullptr, *cF = nullptr, *hd = nullptr;
+  double *FtF = nullptr;   // F'F (16 x 16): the factored solver's middle Horner steps
   double *FSF = nullptr;   // F S F' (T x ldH): the direct path's identity-based replicate Grams
   // T >= N bootstrap Grams by one weighted-outer-product GEMM (gram_wk_*):
   // K = [E_s' E_s] lower-triangle pairs (Tp x ldk) and A0 = C'C (N x N)
@@ -844,7 +847,7 @@ int dfm_model_destroy(dfm_model *m) {
   hipSetDevice(m->ctx->device);
   hipStreamSynchronize(m->ctx->stream);
   for (double *p : {m->Xp, m->Cp, m->Ep, m->y, m->w, m->F, m->Lall, m->Ub, m->colssr, m->H, m->EL, m->S,
-                    m->cF, m->hd, m->FSF, m->Kwk, m->A0wk})
+                    m->cF, m->hd, m->FtF, m->FSF, m->Kwk, m->A0wk})
     hipFree(p);
   for (size_t j = 1; j < m->Ubs.size(); ++j) hipFree(m->Ubs[j]);
   hipFree(m->ws);
@@ -1596,6 +1599,9 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
     }
     int rc0 = fact_precompute(M->Ep, M->ld, T, N, r, M->L, M->F, M->H, M->ldH, M->EL, M->S, M->cF, M->hd, st);
     if (rc0) return fail(ctx, rc0, "factored precompute failed");
+    // F'F once per model (it was one launch per solve on every lane's stream)
+    HIPCHK(ctx, dalloc(&M->FtF, 256));
+    HIPCHK(ctx, launch_fact_ftf(FactBase{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd}, M->FtF, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     M->fact_ready = true;
   }
@@ -1691,7 +1697,7 @@ static int bootstrap_one(dfm_model *M, int kind, int64_t B, const int32_t *idx, 
     HIPCHK(ctx, dalloc(&pSig.p, (size_t)nb));
     if (spectrum_work(m, (int)nb) > 0) HIPCHK(ctx, dalloc(&pWk.p, (size_t)spectrum_work(m, (int)nb)));
   }
-  FactBase fb{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd};
+  FactBase fb{T, r, M->ldH, M->F, M->EL, M->S, M->H, M->cF, M->hd, M->FtF};
   for (int64_t b0 = 0; b0 < B; b0 += nb) {
     const int n = (int)std::min<int64_t>(nb, B - b0);
     PanelSrc src{M->Cp, M->Ep, idx + b0 * T, kind == DFM_BOOT_WILD ? eta + b0 * T : nullptr, M->ld, T};

@@ -1515,6 +1515,7 @@ struct FactBase {
   int T, r;
   int64_t ldH;
   const double *F, *EL, *S, *H, *cF, *hd;   // T x r, T x r, r x r, T x ldH, T, T
+  const double *FtF = nullptr;   // F'F (16 x 16) when the model holds it (else computed per solve)
 };
 
 // Z, the H.Z GEMM's B operand, replicate-major in 16-row chunks (round 6,
@@ -2866,7 +2867,8 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     hipLaunchKernelGGL(boot_prep_kernel<P>, dim3(nb), dim3(256), prep_lds, st,
                        fb, idx, eta, off, lst, w.trace, mid ? PFb : nullptr, E2b, Q0, ps, Zc, ldz, pz, ab);
   }
-  if (mid) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
+  if (mid && !fb.FtF) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
+  const double *ftf = fb.FtF ? fb.FtF : FtF;
   {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
     const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
     if (cheb_lds > 65536)
@@ -2964,7 +2966,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
         if (mid && it == 0 && sp < dg)
           hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
-                             ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, FtF, Zc, ps);
+                             ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, ftf, Zc, ps);
         else
           hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
                              st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, pz, ab, ca[dg - sp], bb, k, cur, Zc, ps);
@@ -3241,6 +3243,11 @@ hipError_t launch_gram_fact(const FactBase &fb, const double *FSF, const int32_t
     hipLaunchKernelGGL(gram_fact_kernel<8>, grid, dim3(256), lds, st, fb, FSF, idx, eta, R, G, ldg, strideG);
   else
     hipLaunchKernelGGL(gram_fact_kernel<16>, grid, dim3(256), lds, st, fb, FSF, idx, eta, R, G, ldg, strideG);
+  return hipGetLastError();
+}
+
+hipError_t launch_fact_ftf(const FactBase &fb, double *FtF, hipStream_t st) {
+  hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   return hipGetLastError();
 }
 
