@@ -12,6 +12,7 @@
 #   pmc_c2     FETCH_SIZE / WRITE_SIZE of the C2 job's fused solver + Chow, one lane
 #              (DFM_NO_LANES=1: per-launch bytes cover more replicates than a lane launch) -> pmc_traffic_c2.json
 #   sq_c2      SQ counter passes of the C2 kernels (one lane: DFM_NO_LANES=1)
+#   sq_c3      SQ / TA / TCP counter passes of the C3 per-replicate passes (KRE: kernel regex)
 #   shards     C3 at 1250 / 2500 / 5000 / 9999 replicates (shards.jsonl)
 #   configs    tools/bench_configs.py c1,c2,c4,c5 (configs.jsonl)
 #   c2         C2 only, 5 reps (c2.jsonl)
@@ -78,6 +79,16 @@ for step in "$@"; do
         || fail pmc2_w $? "$OUT/pmc2_w.err"
       unset DFM_NO_LANES
       python3 tools/pmc_traffic.py "$OUT/pmc2_f" "$OUT/pmc2_w" > "$OUT/pmc_traffic_c2.json" && head -c 1200 "$OUT/pmc_traffic_c2.json"; echo ;;
+    sq_c3)   # SQ / TA / TCP counter passes of the C3 passes (KRE: kernel regex, default the per-replicate passes)
+      KRE=${KRE:-boot_}
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-include-regex "$KRE" -f csv -d "$OUT/sq3a" -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/sq3a.out" 2> "$OUT/sq3a.err" \
+        || fail sq3a $? "$OUT/sq3a.err"
+      timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY TA_FLAT_READ_WAVEFRONTS TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ \
+        GRBM_GUI_ACTIVE --kernel-include-regex "$KRE" -f csv -d "$OUT/sq3b" -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/sq3b.out" 2> "$OUT/sq3b.err" \
+        || fail sq3b $? "$OUT/sq3b.err" ;;
     sq_c2)
       export DFM_NO_LANES=1
       timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
