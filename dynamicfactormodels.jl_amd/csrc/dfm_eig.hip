@@ -2595,6 +2595,13 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
   const int li = lane & 15, lk = lane >> 4;
   __shared__ double sa[16 * P], sb[16 * P];
   __shared__ double sred[NT * 256];
+  // per-wave staging (round 6: this pass is bound by the texture-address unit,
+  // TA_TA_BUSY 0.95 of its cycles): the tile's PF and EL rows arrive as ONE
+  // contiguous 16-row range each (16 r doubles) instead of two differently
+  // shaped gathers of the same rows, and the tile's Z chunk (16 rows x pz,
+  // contiguous in the replicate-major layout) leaves as whole 16-B pieces
+  // instead of one 128-B-strided element per lane
+  __shared__ double stg[BW][2][16 * 17];
   double *abr = ab + (int64_t)rep * 32 * P;
   for (int e = tid; e < 16 * P; e += 64 * BW) sa[e] = abr[e];
   __syncthreads();
@@ -2618,31 +2625,57 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) { aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0}; cacc[ct] = aacc[ct]; }
   const int ntile = (T + 15) >> 4;
+  const int RS = r | 1;   // staged row stride (odd: the 16-row reads spread over the banks)
+  double *sP = stg[wave][0], *sE = stg[wave][1];
+  const int64_t zrs = zrm_stride(T, pz);
   for (int tile = wave; tile < ntile; tile += BW) {
     const int t0 = tile * 16;
-    const int ta = min(t0 + li, T - 1);
-    double pA[4], eA[4], hz[NT][4], pv[NT][4], e2v[4], pfa[4], ea[4];
+    const int nr = min(16, T - t0) * r;   // valid doubles of the tile's contiguous PF / EL range
+    double hz[NT][4], pv[NT][4], e2v[4];
+    double pst[4], est[4];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int j = 4 * kk + lk;
-      const bool ok = kk < KR && j < r && t0 + li < T;
-      pA[kk] = ok ? pfr[(int64_t)ta * r + j] : 0.0;
-      eA[kk] = ok ? fb.EL[(int64_t)ta * r + j] : 0.0;
+    for (int u = 0; u < 4; ++u) {   // 16 r <= 256 doubles: four rounds of 64 lanes
+      const int e = u * 64 + lane;
+      pst[u] = e < nr ? pfr[(int64_t)t0 * r + e] : 0.0;
+      est[u] = e < nr ? fb.EL[(int64_t)t0 * r + e] : 0.0;
     }
+    const double e2l = t0 + li < T ? e2r[t0 + li] : 0.0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int s = t0 + 4 * g + lk;
-      const bool v = s < T;
       const int sc = min(s, T - 1);
-      e2v[g] = v ? e2r[sc] : 0.0;
-      pfa[g] = (v && li < r) ? pfr[(int64_t)sc * r + li] : 0.0;
-      ea[g] = (v && li < r) ? fb.EL[(int64_t)sc * r + li] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
         const int c = 16 * ct + li;
         hz[ct][g] = c < pz ? HZ[(int64_t)sc * ldz + (int64_t)rep * pz + c] : 0.0;
         pv[ct][g] = c < ps ? pvr[(int64_t)sc * ps + c] : 0.0;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = u * 64 + lane;
+      if (e < 16 * r) {
+        const int row = e / r, j = e - row * r;
+        sP[row * RS + j] = pst[u];
+        sE[row * RS + j] = est[u];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's writes land before its reads
+    double pA[4], eA[4], pfa[4], ea[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int j = 4 * kk + lk;
+      const bool ok = kk < KR && j < r && t0 + li < T;
+      pA[kk] = ok ? sP[li * RS + j] : 0.0;
+      eA[kk] = ok ? sE[li * RS + j] : 0.0;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int s = t0 + 4 * g + lk;
+      const bool v = s < T;
+      e2v[g] = v ? __shfl(e2l, 4 * g + lk, 16) : 0.0;
+      pfa[g] = (v && li < r) ? sP[(4 * g + lk) * RS + li] : 0.0;
+      ea[g] = (v && li < r) ? sE[(4 * g + lk) * RS + li] : 0.0;
     }
     dv4 yP[NT], yE[NT];
 #pragma unroll
@@ -2670,8 +2703,23 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
         if (c >= p || !v) z = 0.0;
         uv[ct][g] = v ? u : 0.0;
         zv[ct][g] = z;
-        if (v && c < pz) Zc[zrm_ix(rep, s, c, pz, zrm_stride(T, pz))] = z;
       }
+    }
+    // the Z chunk through the PF staging (its reads above are complete in
+    // this wave's LDS order): chunk element 16 c + (s & 15); rows past T hold
+    // z = 0, the value boot_prep_kernel left in the chunk's pad rows
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const int c = 16 * ct + li;
+        if (c < pz) sP[16 * c + 4 * g + lk] = zv[ct][g];
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    {
+      double2 *zc2 = reinterpret_cast<double2 *>(Zc + (int64_t)rep * zrs + (int64_t)tile * 16 * pz);
+      for (int e = lane; e < 8 * pz; e += 64) zc2[e] = double2{sP[2 * e], sP[2 * e + 1]};
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g)
