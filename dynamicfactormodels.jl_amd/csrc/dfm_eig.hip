@@ -1536,11 +1536,11 @@ DFM_DEV int64_t zrm_ix(int rep, int s, int c, int pz, int64_t zrs) {
 // the init pass of boot_ap2_kernel before, the same arithmetic in the same
 // order (its tile loop and zscatter_tail), without that pass's launch and
 // its reload of the CSR this kernel already holds in LDS.
-template <int P>
+template <int P, bool STG>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
                            double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
-                           const dv4 *aacc, double *sred, int ps);
+                           const dv4 *aacc, double *sred, int ps, double *zst);
 template <int P>
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta, int *__restrict__ off,
@@ -1552,6 +1552,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   static_assert(BW * 64 == 256, "prep runs the factored passes' wave layout");
   constexpr int NT = P / 16;
   __shared__ double sred[NT * 256];
+  __shared__ double zst[BW][16 * P];   // per-wave Z chunk staging (zscatter_tail)
   extern __shared__ int sh[];   // cnt[T+1], six[T], sorted list L[T] (+ so[T+1], eta[T]: Zc)
   __shared__ double red[256];
   __shared__ int scan[256];
@@ -1670,7 +1671,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       for (int e = tid; e < npad * pz; e += 256) Zc[zrm_ix(rep, T + e / pz, e % pz, pz, zrs)] = 0.0;
     }
     __syncthreads();   // so / set visible
-    zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, pz, rep, ab, aacc, sred, ps);
+    zscatter_tail<P, true>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, pz, rep, ab, aacc, sred, ps, zst[wave]);
   }
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
@@ -2039,12 +2040,17 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
 
 // Shared tail of ap2 and the Chebyshev step: Z = P' D Qn by CSR gather
 // (bucket s lists t ascending), cc = EL' Z, and the fixed-order wave sums of
-// a = F' Qn (aacc, accumulated by the caller) and cc into ab[rep].
-template <int P>
+// a = F' Qn (aacc, accumulated by the caller) and cc into ab[rep].  STG (the
+// prep pass): zst is this wave's LDS staging (16 pz doubles) and a tile's Z
+// chunk (16 rows x pz, contiguous in the replicate-major layout) leaves as
+// 16-B pieces instead of one 128-B-strided element per lane — prep -3 %; in
+// ap2 / the last Horner step the same staging measured +0.3 % (round 6, item
+// 13 of profiles/r06_c3_ab.txt), so they store directly.
+template <int P, bool STG>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
                            double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
-                           const dv4 *aacc, double *sred, int ps) {
+                           const dv4 *aacc, double *sred, int ps, double *zst) {
   const int64_t zrs = zrm_stride(T, pz);
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
@@ -2093,6 +2099,18 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
           z[g][ct] = fma(e, 16 * ct + li < ps ? Qn[(int64_t)t * ps + 16 * ct + li] : 0.0, z[g][ct]);
       }
     }
+    if constexpr (STG) {
+      // (rows past T: 0, the chunk's pad-row value the H.Z GEMM's k-padding needs)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous tile's staged reads are done
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ct = 0; ct < NT; ++ct)
+          if (16 * ct + li < pz) zst[16 * (16 * ct + li) + 4 * g + lk] = s0 + 4 * g + lk < T ? z[g][ct] : 0.0;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      double2 *zc2 = reinterpret_cast<double2 *>(Zc + (int64_t)rep * zrs + (int64_t)tile * 16 * pz);
+      for (int e = lane; e < 8 * pz; e += 64) zc2[e] = double2{zst[2 * e], zst[2 * e + 1]};
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int s = s0 + 4 * g + lk;
@@ -2100,7 +2118,7 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
       const double ea = (v && li < r) ? fb.EL[(int64_t)s * r + li] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
-        if (v && 16 * ct + li < pz) Zc[zrm_ix(rep, s, 16 * ct + li, pz, zrs)] = z[g][ct];
+        if (!STG && v && 16 * ct + li < pz) Zc[zrm_ix(rep, s, 16 * ct + li, pz, zrs)] = z[g][ct];
         cacc[ct] = mfma16(ea, z[g][ct], cacc[ct]);
       }
     }
@@ -2316,7 +2334,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   }
   // Z = P' D Qn by CSR gather (bucket s lists t ascending), cc = EL' Z
   const double *Qn = init ? Qr : Yr;
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, pz, rep, ab, aacc, sred, ps);
+  zscatter_tail<P, false>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qn, Zc, pz, rep, ab, aacc, sred, ps, nullptr);
 }
 
 // One Horner step of the degree-d Chebyshev filter of the factored solver.
@@ -2435,7 +2453,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
   }
   __syncthreads();   // every wave's Qn rows visible to the CSR gather
-  zscatter_tail<P>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, pz, rep, ab, aacc, sred, ps);
+  zscatter_tail<P, false>(fb, T, r, ntile, tid, wave, lane, set, so, sl, Qr, Zc, pz, rep, ab, aacc, sred, ps, nullptr);
 }
 
 // The middle Horner steps in row-local form.  With W = G* S_{i+1} = F bB +
