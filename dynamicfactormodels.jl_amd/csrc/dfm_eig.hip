@@ -2079,8 +2079,11 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
         const bool ok = q < qn1[g];
         const int t = sl[ok ? q : 0];
         ev[g][u] = ok ? set[t] : 0.0;
+        // (lanes past their bucket issue no load: most second / third entries
+        // are empty, and these passes are bound by the texture-address unit)
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) val[g][u][ct] = 16 * ct + li < ps ? Qn[(int64_t)t * ps + 16 * ct + li] : 0.0;
+        for (int ct = 0; ct < NT; ++ct)
+          val[g][u][ct] = (ok && 16 * ct + li < ps) ? Qn[(int64_t)t * ps + 16 * ct + li] : 0.0;
       }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {

@@ -13,6 +13,7 @@
 #              (DFM_NO_LANES=1: per-launch bytes cover more replicates than a lane launch) -> pmc_traffic_c2.json
 #   sq_c2      SQ counter passes of the C2 kernels (one lane: DFM_NO_LANES=1)
 #   sq_c3      SQ / TA / TCP counter passes of the C3 per-replicate passes (KRE: kernel regex)
+#   ta_c2      TA / TCP counters of every C2 kernel (one lane)
 #   shards     C3 at 1250 / 2500 / 5000 / 9999 replicates (shards.jsonl)
 #   configs    tools/bench_configs.py c1,c2,c4,c5 (configs.jsonl)
 #   c2         C2 only, 5 reps (c2.jsonl)
@@ -89,6 +90,12 @@ for step in "$@"; do
         GRBM_GUI_ACTIVE --kernel-include-regex "$KRE" -f csv -d "$OUT/sq3b" -o run -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-all-fields > "$OUT/sq3b.out" 2> "$OUT/sq3b.err" \
         || fail sq3b $? "$OUT/sq3b.err" ;;
+    ta_c2)   # TA / TCP counters of every C2 kernel (one lane)
+      export DFM_NO_LANES=1
+      timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY TA_FLAT_READ_WAVEFRONTS TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ \
+        GRBM_GUI_ACTIVE -f csv -d "$OUT/ta2" -o run -- python3 tools/bench_configs.py --configs c2 --reps 1 \
+        > "$OUT/ta2.out" 2> "$OUT/ta2.err" || fail ta2 $? "$OUT/ta2.err"
+      unset DFM_NO_LANES ;;
     sq_c2)
       export DFM_NO_LANES=1
       timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
