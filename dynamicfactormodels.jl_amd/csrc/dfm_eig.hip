@@ -1651,13 +1651,10 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       for (int g = 0; g < 4; ++g) {
         const int t = t0 + 4 * g + lk;
         const int tc = min(t, T - 1);
-        const double f = r > 0 ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
-        fa[g] = (t < T && li < r) ? f : 0.0;
+        fa[g] = (t < T && li < r) ? fb.F[(int64_t)tc * r + li] : 0.0;
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) {
-          const double q = 16 * ct + li < ps ? Q0[(int64_t)tc * ps + 16 * ct + li] : 0.0;
-          qv[ct][g] = t < T ? q : 0.0;
-        }
+        for (int ct = 0; ct < NT; ++ct)
+          qv[ct][g] = (t < T && 16 * ct + li < ps) ? Q0[(int64_t)tc * ps + 16 * ct + li] : 0.0;
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -2029,10 +2026,9 @@ DFM_DEV void ap2_load_lds(Ap2Tile<P> &L, int tile, int T, int r, int lane, int i
   for (int g = 0; g < 4; ++g) {
     const int t = t0 + 4 * g + lk;
     const int tc = min(t, T - 1);
-    // r = 0 (expanding windows: no base factors): no load at all — the
-    // clamped column would be F[-1], one element before the buffer
-    const double f = r > 0 ? fb.F[(int64_t)tc * r + min(li, r - 1)] : 0.0;
-    L.fa[g] = (t < T && li < r) ? f : 0.0;
+    // only lanes holding a factor column of a row < T load (r = 0, the
+    // expanding windows' case without base factors, loads nothing)
+    L.fa[g] = (t < T && li < r) ? fb.F[(int64_t)tc * r + li] : 0.0;
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) L.q[ct][g] = (init && 16 * ct + li < ps) ? Qr[(int64_t)tc * ps + 16 * ct + li] : 0.0;
   }
