@@ -1802,19 +1802,55 @@ template <int P>
 struct Y2Tile {
   double fA[4], eA[4], hz[P / 16][4], q[P / 16][4];
 };
-template <int P>
+// STG (the last Horner step, r <= 8): stg is this wave's 2 x 16 x 9 doubles
+// of LDS; the tile's F rows arrive as ONE contiguous 16-row range and each
+// EL[idx] row as one contiguous piece per group of r lanes, both transposed
+// to the A layout through LDS, and the caller reads the F rows' accumulator
+// layout (fa) from the same stage instead of a second gather of those rows.
+template <int P, bool STG = false>
 DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, const int *six, const FactBase &fb,
                      const double *__restrict__ HZ, int64_t ldz, int pz, int rep, const double *__restrict__ Qr,
-                     int ps) {
+                     int ps, double *stg = nullptr) {
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
   const int ta = min(t0 + li, T - 1);
-  const int ia = six[ta];
+  if constexpr (STG) {
+    const int RS = r | 1, nr = min(16, T - t0) * r;
+    double *sF = stg, *sE = stg + 16 * 9;
+    double fv[2], ev[2];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const int j = max(0, min(4 * kk + lk, r - 1));   // never index -1 (r = 0: expanding windows)
-    L.fA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.F[(int64_t)ta * r + j] : 0.0;
-    L.eA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.EL[(int64_t)ia * r + j] : 0.0;
+    for (int u = 0; u < 2; ++u) {   // 16 r <= 128 doubles
+      const int e = u * 64 + lane;
+      const int row = r > 0 ? e / r : 0, j = e - row * r;
+      const bool ok = e < nr;
+      fv[u] = ok ? fb.F[(int64_t)t0 * r + e] : 0.0;
+      ev[u] = ok ? fb.EL[(int64_t)six[t0 + row] * r + j] : 0.0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous tile's staged reads are done
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = u * 64 + lane;
+      if (e < 16 * r) {
+        const int row = e / r, j = e - row * r;
+        sF[row * RS + j] = fv[u];
+        sE[row * RS + j] = ev[u];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's writes land before its reads
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bool ok = kk < KR && 4 * kk + lk < r && t0 + li < T;
+      L.fA[kk] = ok ? sF[li * RS + 4 * kk + lk] : 0.0;
+      L.eA[kk] = ok ? sE[li * RS + 4 * kk + lk] : 0.0;
+    }
+  } else {
+    const int ia = six[ta];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int j = max(0, min(4 * kk + lk, r - 1));   // never index -1 (r = 0: expanding windows)
+      L.fA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.F[(int64_t)ta * r + j] : 0.0;
+      L.eA[kk] = (kk < KR && 4 * kk + lk < r && t0 + li < T) ? fb.EL[(int64_t)ia * r + j] : 0.0;
+    }
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -2350,7 +2386,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
 // The filter damps the unwanted spectrum ~T_d(2 lambda_k/b - 1) times
 // relative to the wanted one; the basis is orthonormalised by the next
 // Rayleigh-Ritz step (CholQR folded into eig_small).
-template <int P>
+template <int P, bool STG>
 __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigWork w, int T, int p,
                                                         const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta,
@@ -2366,6 +2402,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int li = lane & 15, lk = lane >> 4;
   __shared__ double sa[16 * P], sb[16 * P];
   __shared__ double sred[NT * 256];
+  __shared__ double stg[STG ? BW : 1][STG ? 2 * 16 * 9 : 1];   // per-wave F / EL[idx] staging (y2_load)
   extern __shared__ double sdyn[];
   double *set = sdyn;                          // eta_t
   int *six = (int *)(sdyn + T);                // idx_t
@@ -2413,7 +2450,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int ntile = (T + 15) >> 4;
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Xr, ps);   // cur.q = V0 rows
+    y2_load<P, STG>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Xr, ps, stg[STG ? wave : 0]);   // cur.q = V0 rows
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -2434,7 +2471,10 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       const int t = t0 + 4 * g + lk;
       const bool v = t < T;
       const int tc = min(t, T - 1);
-      fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, max(r - 1, 0))] : 0.0;   // never F[-1] (r = 0)
+      if constexpr (STG)
+        fa[g] = (v && li < r) ? stg[wave][(4 * g + lk) * (r | 1) + li] : 0.0;
+      else
+        fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, max(r - 1, 0))] : 0.0;   // never F[-1] (r = 0)
       const double e = v ? set[t] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct) {
@@ -2934,10 +2974,12 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   }
   if (mid && !fb.FtF) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   const double *ftf = fb.FtF ? fb.FtF : FtF;
+  // the last Horner step stages F / EL[idx] rows through LDS for r <= 8 (round 6)
+  auto chk = fb.r <= 8 ? boot_cheb_kernel<P, true> : boot_cheb_kernel<P, false>;
   {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
     const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
     if (cheb_lds > 65536)
-      hipFuncSetAttribute((const void *)boot_cheb_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cheb_lds);
+      hipFuncSetAttribute((const void *)chk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cheb_lds);
   }
   if (tf) tf(tctx, DFM_KC_EIG_OTHER, 0);
   const double beta0 = warm_started ? warm_beta() : 0.0;
@@ -3033,7 +3075,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
           hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
                              ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, ftf, Zc, ps);
         else
-          hipLaunchKernelGGL(boot_cheb_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
+          hipLaunchKernelGGL(chk, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
                              st, fb, w, m, p, idx, eta, off, lst, HZ, ldz, pz, ab, ca[dg - sp], bb, k, cur, Zc, ps);
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 0);
       }
