@@ -1601,6 +1601,12 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
   }
   __syncthreads();
   for (int t = tid; t < T; t += 256) lst[(int64_t)rep * T + t] = L[t];
+  // LDS after the sorted list: bucket starts so[0..T] and eta_t (PF below, zscatter_tail)
+  int *so = sh + 3 * T + 1;
+  double *set = reinterpret_cast<double *>(sh + ((4 * T + 2 + 1) & ~1));
+  for (int q = tid; q <= T; q += 256) so[q] = q ? cnt[q - 1] : 0;
+  for (int t = tid; t < T; t += 256) set[t] = et ? et[t] : 1.0;
+  __syncthreads();
   if (PF)   // P'D F (row stride r) and P'D^2 1 of the middle Horner steps (boot_cheb_mid_kernel):
     for (int s = tid; s < T; s += 256) {   // this thread's own sorted buckets, t ascending
       const int b0 = s ? cnt[s - 1] : 0, b1 = cnt[s];
@@ -1609,7 +1615,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       for (int j = 0; j < 16; ++j) a[j] = 0.0;
       for (int q = b0; q < b1; ++q) {
         const int t = L[q];
-        const double h = et ? et[t] : 1.0;
+        const double h = set[t];
         a2 = fma(h, h, a2);
         if ((r & 1) == 0) {   // 16-B loads of the F row (F rows start 16-B aligned)
           const double2 *f2 = reinterpret_cast<const double2 *>(fb.F + (int64_t)t * r);
@@ -1627,17 +1633,18 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
         }
       }
       double *pf = PF + ((int64_t)rep * T + s) * r;
+      if ((r & 1) == 0) {   // 16-B stores (rows start 16-B aligned for even r)
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < r) pf[j] = a[j];
+        for (int j = 0; j < 8; ++j)
+          if (2 * j < r) reinterpret_cast<double2 *>(pf)[j] = double2{a[2 * j], a[2 * j + 1]};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j < r) pf[j] = a[j];
+      }
       E2[(int64_t)rep * T + s] = a2;
     }
   if (Zc) {
-    // LDS for zscatter_tail after the sorted list: bucket starts so[0..T], eta_t
-    int *so = sh + 3 * T + 1;
-    double *set = reinterpret_cast<double *>(sh + ((4 * T + 2 + 1) & ~1));
-    for (int q = tid; q <= T; q += 256) so[q] = q ? cnt[q - 1] : 0;
-    for (int t = tid; t < T; t += 256) set[t] = et ? et[t] : 1.0;
     // a = F'Q0 in boot_ap2_kernel's init order (its tiles, its accumulator layout)
     const int lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
     const int ntile = (T + 15) >> 4;
@@ -1675,7 +1682,19 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
     const int i = ix[t];
     const double e = et ? et[t] : 1.0;
     double fe = 0.0;
-    for (int j = 0; j < r; ++j) fe = fma(fb.F[(int64_t)t * r + j], fb.EL[(int64_t)i * r + j], fe);
+    if ((r & 1) == 0) {   // F and EL rows as 16-B pieces (half the load instructions; same fma order)
+      const double2 *f2 = reinterpret_cast<const double2 *>(fb.F + (int64_t)t * r);
+      const double2 *e2 = reinterpret_cast<const double2 *>(fb.EL + (int64_t)i * r);
+      double2 fv[8], ev[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (2 * j < r) { fv[j] = f2[j]; ev[j] = e2[j]; }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (2 * j < r) { fe = fma(fv[j].x, ev[j].x, fe); fe = fma(fv[j].y, ev[j].y, fe); }
+    } else {
+      for (int j = 0; j < r; ++j) fe = fma(fb.F[(int64_t)t * r + j], fb.EL[(int64_t)i * r + j], fe);
+    }
     acc += fb.cF[t] + 2.0 * e * fe + e * e * fb.hd[i];
   }
   red[tid] = acc;
