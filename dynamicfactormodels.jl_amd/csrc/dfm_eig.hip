@@ -1821,11 +1821,18 @@ template <int P>
 struct Y2Tile {
   double fA[4], eA[4], hz[P / 16][4], q[P / 16][4];
 };
-// STG (the last Horner step, r <= 8): stg is this wave's 2 x 16 x 9 doubles
-// of LDS; the tile's F rows arrive as ONE contiguous 16-row range and each
-// EL[idx] row as one contiguous piece per group of r lanes, both transposed
-// to the A layout through LDS, and the caller reads the F rows' accumulator
-// layout (fa) from the same stage instead of a second gather of those rows.
+// STG (P = 16, even r <= 8, pz <= 16; the last Horner step — in y2 the
+// staged form spills, 128 VGPRs + 52 B of scratch, and y2 runs 60 % slower,
+// profiles/r06_c3_ab.txt item 19): every
+// operand of the tile arrives as 16-B pieces through this wave's LDS stage
+// (stg, Y2_STG doubles) — the F rows as one contiguous range, each EL[idx]
+// and HZ[idx] row as r / 2 and pz / 2 pieces, the Q rows as one contiguous
+// range — and is transposed to its register layout there: half the load
+// requests of one-double-per-lane loads, for passes bound by the texture-
+// address unit (round 6).  Stage layout: F rows [0, 144) (kept for the
+// caller's accumulator-layout read of F, fa), EL rows [144, 288), then HZ
+// and Q rows over [144, 688) once the EL reads are done.
+constexpr int Y2_STG = 16 * 9 + 2 * 16 * 17;
 template <int P, bool STG = false>
 DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, const int *six, const FactBase &fb,
                      const double *__restrict__ HZ, int64_t ldz, int pz, int rep, const double *__restrict__ Qr,
@@ -1834,34 +1841,61 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
   const int li = lane & 15, lk = lane >> 4, t0 = tile * 16;
   const int ta = min(t0 + li, T - 1);
   if constexpr (STG) {
-    const int RS = r | 1, nr = min(16, T - t0) * r;
-    double *sF = stg, *sE = stg + 16 * 9;
-    double fv[2], ev[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {   // 16 r <= 128 doubles
-      const int e = u * 64 + lane;
-      const int row = r > 0 ? e / r : 0, j = e - row * r;
-      const bool ok = e < nr;
-      fv[u] = ok ? fb.F[(int64_t)t0 * r + e] : 0.0;
-      ev[u] = ok ? fb.EL[(int64_t)six[t0 + row] * r + j] : 0.0;
+    static_assert(P == 16, "the staged loader covers one 16-column block");
+    const int nrow = min(16, T - t0), hr = r >> 1, hp = pz >> 1, hq = ps >> 1;
+    // issue every piece first (F, EL: 8 r <= 64 pieces; HZ, Q: 8 pz, 8 ps <= 128)
+    double2 fv, ev, hv[2], qv[2];
+    {
+      const int row = hr ? lane / hr : 0, jp = lane - row * hr;
+      const bool ok = lane < nrow * hr;
+      fv = ok ? reinterpret_cast<const double2 *>(fb.F + (int64_t)t0 * r)[lane] : double2{0.0, 0.0};
+      ev = ok ? reinterpret_cast<const double2 *>(fb.EL + (int64_t)six[t0 + row] * r)[jp] : double2{0.0, 0.0};
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous tile's staged reads are done
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = u * 64 + lane;
-      if (e < 16 * r) {
-        const int row = e / r, j = e - row * r;
-        sF[row * RS + j] = fv[u];
-        sE[row * RS + j] = ev[u];
-      }
+      const int row = e / hp, jp = e - row * hp;
+      const bool okh = e < nrow * hp;
+      hv[u] = okh ? reinterpret_cast<const double2 *>(HZ + (int64_t)six[t0 + row] * ldz + (int64_t)rep * pz)[jp]
+                  : double2{0.0, 0.0};
+      const bool okq = e < nrow * hq;
+      qv[u] = okq ? reinterpret_cast<const double2 *>(Qr + (int64_t)t0 * ps)[e] : double2{0.0, 0.0};
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's writes land before its reads
+    const int RF = r + 1, RH = pz + 1, RQ = ps + 1;
+    double *sF = stg, *sE = stg + 16 * 9;         // (RF <= 9)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous tile's staged reads are done
+    if (lane < 16 * hr) {
+      const int row = lane / hr, j = 2 * (lane - row * hr);
+      sF[row * RF + j] = fv.x; sF[row * RF + j + 1] = fv.y;
+      sE[row * RF + j] = ev.x; sE[row * RF + j + 1] = ev.y;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const bool ok = kk < KR && 4 * kk + lk < r && t0 + li < T;
-      L.fA[kk] = ok ? sF[li * RS + 4 * kk + lk] : 0.0;
-      L.eA[kk] = ok ? sE[li * RS + 4 * kk + lk] : 0.0;
+      L.fA[kk] = ok ? sF[li * RF + 4 * kk + lk] : 0.0;
+      L.eA[kk] = ok ? sE[li * RF + 4 * kk + lk] : 0.0;
     }
+    double *sH = stg + 16 * 9, *sQ = sH + 16 * 17;   // over EL (read above), after F (kept for fa)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = u * 64 + lane;
+      if (e < 16 * hp) {
+        const int row = e / hp, j = 2 * (e - row * hp);
+        sH[row * RH + j] = hv[u].x; sH[row * RH + j + 1] = hv[u].y;
+      }
+      if (e < 16 * hq) {
+        const int row = e / hq, j = 2 * (e - row * hq);
+        sQ[row * RQ + j] = qv[u].x; sQ[row * RQ + j + 1] = qv[u].y;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      L.hz[0][g] = li < pz ? sH[(4 * g + lk) * RH + li] : 0.0;
+      L.q[0][g] = li < ps ? sQ[(4 * g + lk) * RQ + li] : 0.0;
+    }
+    return;
   } else {
     const int ia = six[ta];
 #pragma unroll
@@ -2421,7 +2455,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
   const int li = lane & 15, lk = lane >> 4;
   __shared__ double sa[16 * P], sb[16 * P];
   __shared__ double sred[NT * 256];
-  __shared__ double stg[STG ? BW : 1][STG ? 2 * 16 * 9 : 1];   // per-wave F / EL[idx] staging (y2_load)
+  __shared__ double stg[STG ? BW : 1][STG ? Y2_STG : 1];   // per-wave operand staging (y2_load)
   extern __shared__ double sdyn[];
   double *set = sdyn;                          // eta_t
   int *six = (int *)(sdyn + T);                // idx_t
@@ -2491,7 +2525,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_kernel(FactBase fb, EigW
       const bool v = t < T;
       const int tc = min(t, T - 1);
       if constexpr (STG)
-        fa[g] = (v && li < r) ? stg[wave][(4 * g + lk) * (r | 1) + li] : 0.0;
+        fa[g] = (v && li < r) ? stg[wave][(4 * g + lk) * (r + 1) + li] : 0.0;
       else
         fa[g] = (v && li < r) ? fb.F[(int64_t)tc * r + min(li, max(r - 1, 0))] : 0.0;   // never F[-1] (r = 0)
       const double e = v ? set[t] : 0.0;
@@ -2994,7 +3028,9 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   if (mid && !fb.FtF) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   const double *ftf = fb.FtF ? fb.FtF : FtF;
   // the last Horner step stages F / EL[idx] rows through LDS for r <= 8 (round 6)
-  auto chk = fb.r <= 8 ? boot_cheb_kernel<P, true> : boot_cheb_kernel<P, false>;
+  const bool stg_ok = P == 16 && fb.r <= 8 && (fb.r & 1) == 0 && pz <= 16;
+  auto chk = stg_ok ? boot_cheb_kernel<P, P == 16> : boot_cheb_kernel<P, false>;
+
   {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
     const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
     if (cheb_lds > 65536)
