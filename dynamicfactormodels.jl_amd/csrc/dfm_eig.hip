@@ -1821,9 +1821,10 @@ template <int P>
 struct Y2Tile {
   double fA[4], eA[4], hz[P / 16][4], q[P / 16][4];
 };
-// STG (P = 16, even r <= 8, pz <= 16; the last Horner step — in y2 the
-// staged form spills, 128 VGPRs + 52 B of scratch, and y2 runs 60 % slower,
-// profiles/r06_c3_ab.txt item 19): every
+// STG (P = 16, even r <= 8, pz <= 16; y2 and the last Horner step — y2
+// reads its MFMA B operands from LDS per tile when staged, else the staged
+// form spills: 128 VGPRs + 52 B of scratch, y2 60 % slower, profiles/
+// r06_c3_ab.txt items 19 and 23): every
 // operand of the tile arrives as 16-B pieces through this wave's LDS stage
 // (stg, Y2_STG doubles) — the F rows as one contiguous range, each EL[idx]
 // and HZ[idx] row as r / 2 and pz / 2 pieces, the Q rows as one contiguous
@@ -1919,7 +1920,7 @@ DFM_DEV void y2_load(Y2Tile<P> &L, int tile, int T, int r, int KR, int lane, con
 }
 
 // y2: one workgroup (4 waves) per replicate; wave w takes 16-row tiles w, w+4, ...
-template <int P>
+template <int P, bool STG>
 // 4 workgroups per CU (~113 VGPRs, no spills; a tile is loaded at the top of
 // its own iteration, no register prefetch of the next): these per-replicate
 // passes are HBM-latency-bound, and resident waves buy more bandwidth than
@@ -1938,6 +1939,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   __shared__ double sa[16 * P], sb[16 * P];          // a = F'Q, S a + cc  (rows >= r zero)
   __shared__ double red[3 * NT * NT * 256];
   extern __shared__ double sdyn[];                   // eta (T doubles), idx (T ints)
+  __shared__ double stgy[STG ? BW : 1][STG ? Y2_STG : 1];   // per-wave operand staging (y2_load)
   double *set = sdyn;
   int *six = (int *)(sdyn + T);
   {
@@ -1957,14 +1959,16 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   }
   __syncthreads();
   const int KR = (r + 3) >> 2;
-  double bA[4][NT], bB[4][NT];
+  double bA[4][NT], bB[4][NT];   // (STG: read from LDS per tile instead, to make room for the staged loader)
+  if constexpr (!STG) {
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk)
+    for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) {
-      bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
-      bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
-    }
+      for (int ct = 0; ct < NT; ++ct) {
+        bA[kk][ct] = sa[(4 * kk + lk) * P + 16 * ct + li];
+        bB[kk][ct] = sb[(4 * kk + lk) * P + 16 * ct + li];
+      }
+  }
   dv4 acc[3][NT][NT];
 #pragma unroll
   for (int m3 = 0; m3 < 3; ++m3)
@@ -1978,7 +1982,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
   // each tile's operands load at the top of its iteration (occupancy hides the latency)
   Y2Tile<P> cur;
   for (int tile = wave; tile < ntile; tile += BW) {
-    y2_load<P>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Qr, ps);
+    y2_load<P, STG>(cur, tile, T, r, KR, lane, six, fb, HZ, ldz, pz, rep, Qr, ps, stgy[STG ? wave : 0]);
     const int t0 = tile * 16;
     dv4 yF[NT], yE[NT];
 #pragma unroll
@@ -1988,8 +1992,13 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_y2_kernel(FactBase fb, EigWor
       if (kk < KR) {
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-          yF[ct] = mfma16(cur.fA[kk], bB[kk][ct], yF[ct]);
-          yE[ct] = mfma16(cur.eA[kk], bA[kk][ct], yE[ct]);
+          if constexpr (STG) {
+            yF[ct] = mfma16(cur.fA[kk], sb[(4 * kk + lk) * P + 16 * ct + li], yF[ct]);
+            yE[ct] = mfma16(cur.eA[kk], sa[(4 * kk + lk) * P + 16 * ct + li], yE[ct]);
+          } else {
+            yF[ct] = mfma16(cur.fA[kk], bB[kk][ct], yF[ct]);
+            yE[ct] = mfma16(cur.eA[kk], bA[kk][ct], yE[ct]);
+          }
         }
       }
     }
@@ -3030,6 +3039,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // the last Horner step stages F / EL[idx] rows through LDS for r <= 8 (round 6)
   const bool stg_ok = P == 16 && fb.r <= 8 && (fb.r & 1) == 0 && pz <= 16;
   auto chk = stg_ok ? boot_cheb_kernel<P, P == 16> : boot_cheb_kernel<P, false>;
+  auto y2k = stg_ok ? boot_y2_kernel<P, P == 16> : boot_y2_kernel<P, false>;
 
   {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
     const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
@@ -3071,7 +3081,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     if (e != hipSuccess) return 1000 + (int)e;
     last_gemm = it;
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 1);
-    hipLaunchKernelGGL(boot_y2_kernel<P>, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, pz,
+    hipLaunchKernelGGL(y2k, dim3(nb), dim3(64 * BW), (size_t)m * 12, st, fb, w, m, idx, eta, HZ, ldz, pz,
                        ab, qin, qs, alt, ps);
     if (tf) tf(tctx, DFM_KC_EIG_GQ, 0);
     if (tf) tf(tctx, DFM_KC_EIG_SMALL, 1);
