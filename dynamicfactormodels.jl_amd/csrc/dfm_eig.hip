@@ -2267,6 +2267,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
   __shared__ double sres[BW][P];
   __shared__ double stile[BW][2][16 * (P + 1)];   // per-wave Q / Y tile transposes (ap2_load_lds)
   __shared__ int s_conv;
+  __shared__ double sAm[P * P], sBm[P * P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = fb.r;
   const int li = lane & 15, lk = lane >> 4;
   {
@@ -2277,19 +2278,22 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
     if (tid == 0) so[T] = o[T];
   }
   double *small = w.small + (int64_t)rep * small_stride<P>();
-  double bAm[KP][NT], bBm[KP][NT], th[NT];
+  // the Rayleigh-Ritz step's A and Bm (P x P each) in LDS: the MFMA B
+  // operands are read per tile instead of held in 2 KP NT registers (round 6:
+  // the kernel sat at 128 VGPRs with 32 B of scratch)
+  for (int e = tid; e < P * P; e += 64 * BW) {
+    sAm[e] = init ? 0.0 : small[e];
+    sBm[e] = init ? 0.0 : small[P * P + e];
+  }
+  double th[NT];
   bool dd[NT];
 #pragma unroll
   for (int ct = 0; ct < NT; ++ct) {
     const int c = 16 * ct + li;
     th[ct] = init ? 0.0 : small[2 * P * P + c];
     dd[ct] = init ? false : (small[2 * P * P + P + c] != 0.0);
-#pragma unroll
-    for (int kk = 0; kk < KP; ++kk) {
-      bAm[kk][ct] = init ? 0.0 : small[(4 * kk + lk) * P + c];
-      bBm[kk][ct] = init ? 0.0 : small[P * P + (4 * kk + lk) * P + c];
-    }
   }
+  __syncthreads();
   const double *Qr = Qc + (int64_t)rep * qs;   // qs = 0: the shared warm start (init / first step)
   double *Yr = Yq + (int64_t)rep * T * P;
   // the filter's first Horner term (boot_cheb_kernel): S = (fa1 / b) Y Bm + fa0 Q Bm,
@@ -2320,10 +2324,11 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
       for (int kk = 0; kk < KP; ++kk)
 #pragma unroll
         for (int ct = 0; ct < NT; ++ct) {
-          u[ct] = mfma16(cur.qa[kk], bAm[kk][ct], u[ct]);
-          ya[ct] = mfma16(cur.yo[kk], bAm[kk][ct], ya[ct]);
-          qn[ct] = mfma16(cur.yo[kk], bBm[kk][ct], qn[ct]);
-          if (cheb) qb[ct] = mfma16(cur.qa[kk], bBm[kk][ct], qb[ct]);
+          const double am = sAm[(4 * kk + lk) * P + 16 * ct + li], bm = sBm[(4 * kk + lk) * P + 16 * ct + li];
+          u[ct] = mfma16(cur.qa[kk], am, u[ct]);
+          ya[ct] = mfma16(cur.yo[kk], am, ya[ct]);
+          qn[ct] = mfma16(cur.yo[kk], bm, qn[ct]);
+          if (cheb) qb[ct] = mfma16(cur.qa[kk], bm, qb[ct]);
         }
       if (cheb) {   // V0 = Q Bm for the filter's later steps (boot_cheb_kernel), kept in w.U
         double *Xr = w.U + (int64_t)rep * T * P;
@@ -2418,7 +2423,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_ap2_kernel(FactBase fb, EigWo
 #pragma unroll
       for (int kk = 0; kk < KP; ++kk)
 #pragma unroll
-        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa[kk], bAm[kk][ct], u[ct]);
+        for (int ct = 0; ct < NT; ++ct) u[ct] = mfma16(qa[kk], sAm[(4 * kk + lk) * P + 16 * ct + li], u[ct]);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int t = t0 + 4 * g + lk;
