@@ -1540,7 +1540,56 @@ template <int P, bool STG>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
                            double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
-                           const dv4 *aacc, double *sred, int ps, double *zst);
+                           const dv4 *aacc, double *sred, int ps, double *zst, const double *apre = nullptr);
+// a = F'Q0 of the first product for the whole batch: F and the warm start Q0
+// are shared by every replicate, so boot_prep_kernel's per-workgroup tile
+// loop and fixed-order wave sums are run ONCE, in the same order (one
+// workgroup of the same shape: bit-identical), into apre in ab's layout
+// (round 6; before, every replicate's workgroup formed the same 16 x P block).
+template <int P>
+__global__ __launch_bounds__(256) void prep_a_kernel(FactBase fb, const double *__restrict__ Q0, int ps,
+                                                     double *__restrict__ apre) {
+  constexpr int NT = P / 16;
+  __shared__ double sred[NT * 256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4, T = fb.T, r = fb.r;
+  const int ntile = (T + 15) >> 4;
+  dv4 aacc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
+  for (int tile = wave; tile < ntile; tile += BW) {
+    const int t0 = tile * 16;
+    double fa[4], qv[NT][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int t = t0 + 4 * g + lk;
+      const int tc = min(t, T - 1);
+      fa[g] = (t < T && li < r) ? fb.F[(int64_t)tc * r + li] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+        qv[ct][g] = (t < T && 16 * ct + li < ps) ? Q0[(int64_t)tc * ps + 16 * ct + li] : 0.0;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) aacc[ct] = mfma16(fa[g], qv[ct][g], aacc[ct]);
+  }
+  for (int wv = 0; wv < BW; ++wv) {
+    if (wave == wv)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int e = (ct * 4 + g) * 64 + lane;
+          sred[e] = (wv ? sred[e] : 0.0) + aacc[ct][g];
+        }
+    __syncthreads();
+  }
+  for (int e = tid; e < NT * 256; e += 64 * BW) {
+    const int l = e & 63, g = (e >> 6) & 3, ct = e >> 8;
+    apre[(4 * g + (l >> 4)) * P + 16 * ct + (l & 15)] = sred[e];
+  }
+}
+
 template <int P>
 __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32_t *__restrict__ idx,
                                                         const double *__restrict__ eta, int *__restrict__ off,
@@ -1548,7 +1597,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
                                                         double *__restrict__ PF, double *__restrict__ E2,
                                                         const double *__restrict__ Q0, int ps,
                                                         double *__restrict__ Zc, int64_t ldz, int pz,
-                                                        double *__restrict__ ab) {
+                                                        double *__restrict__ ab, const double *__restrict__ apre) {
   static_assert(BW * 64 == 256, "prep runs the factored passes' wave layout");
   constexpr int NT = P / 16;
   __shared__ double sred[NT * 256];
@@ -1651,7 +1700,7 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
     dv4 aacc[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct) aacc[ct] = dv4{0.0, 0.0, 0.0, 0.0};
-    for (int tile = wave; tile < ntile; tile += BW) {
+    for (int tile = wave; tile < (apre ? 0 : ntile); tile += BW) {   // (apre: a = F'Q0 formed once per batch)
       const int t0 = tile * 16;
       double fa[4], qv[NT][4];
 #pragma unroll
@@ -1675,7 +1724,8 @@ __global__ __launch_bounds__(256) void boot_prep_kernel(FactBase fb, const int32
       for (int e = tid; e < npad * pz; e += 256) Zc[zrm_ix(rep, T + e / pz, e % pz, pz, zrs)] = 0.0;
     }
     __syncthreads();   // so / set visible
-    zscatter_tail<P, true>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, pz, rep, ab, aacc, sred, ps, zst[wave]);
+    zscatter_tail<P, true>(fb, T, r, ntile, tid, wave, lane, set, so, L, Q0, Zc, pz, rep, ab, aacc, sred, ps, zst[wave],
+                           apre);
   }
   double acc = 0.0;
   for (int t = tid; t < T; t += 256) {
@@ -2144,7 +2194,7 @@ template <int P, bool STG>
 DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid, int wave, int lane,
                            const double *set, const int *so, const int *sl, const double *Qn,
                            double *__restrict__ Zc, int pz, int rep, double *__restrict__ ab,
-                           const dv4 *aacc, double *sred, int ps, double *zst) {
+                           const dv4 *aacc, double *sred, int ps, double *zst, const double *apre) {
   const int64_t zrs = zrm_stride(T, pz);
   constexpr int NT = P / 16;
   const int li = lane & 15, lk = lane >> 4;
@@ -2221,8 +2271,11 @@ DFM_DEV void zscatter_tail(const FactBase &fb, int T, int r, int ntile, int tid,
     }
   }
   // a and cc: fixed-order sums over the waves -> ab[rep] = [a (16 x P); cc (16 x P)]
+  // (apre: a was formed once for the whole batch, prep_a_kernel — the same sums)
   double *abr = ab + (int64_t)rep * 32 * P;
-  for (int pass = 0; pass < 2; ++pass) {
+  if (apre)
+    for (int e = tid; e < 16 * P; e += 64 * BW) abr[e] = apre[e];
+  for (int pass = apre ? 1 : 0; pass < 2; ++pass) {
     for (int wv = 0; wv < BW; ++wv) {
       if (wave == wv)
 #pragma unroll
@@ -3013,11 +3066,13 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   // read with replicate stride 0 by the init pass and the first step's y2 /
   // ap2 (L2-resident) instead of nb materialised copies
   double *Q0 = nullptr;
-  if (stream_malloc((void **)&Q0, (size_t)m * P * 8 + (size_t)(nb + 4) * 4, st) != hipSuccess) return 1002;
+  if (stream_malloc((void **)&Q0, (size_t)m * P * 8 + (size_t)16 * P * 8 + (size_t)(nb + 4) * 4, st) != hipSuccess)
+    return 1002;
+  double *apre = Q0 + (size_t)m * P;   // a = F'Q0, the same for every replicate (prep_a_kernel)
   // straggler phase (< 1/8 of the batch active at a poll): the GEMMs tile only
   // the listed replicates' column groups (list built once, a superset of the
   // later active sets; replicates retired since are computed and ignored)
-  int *alist = (int *)(Q0 + (size_t)m * P), *acount = alist + nb;
+  int *alist = (int *)(apre + 16 * P), *acount = alist + nb;
   bool cl_on = false;
   struct Q0Free { double *q; hipStream_t s; ~Q0Free() { hipFreeAsync(q, s); } } q0free{Q0, st};
   const double *qin = Q0;
@@ -3036,8 +3091,9 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
     const size_t prep_lds = (size_t)((4 * m + 3) & ~1) * 4 + (size_t)m * 8;
     if (prep_lds > 65536)   // T > 2730 (up to F2_T_MAX: 96 KB): above the default dynamic-LDS cap
       hipFuncSetAttribute((const void *)boot_prep_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)prep_lds);
+    hipLaunchKernelGGL(prep_a_kernel<P>, dim3(1), dim3(256), 0, st, fb, Q0, ps, apre);
     hipLaunchKernelGGL(boot_prep_kernel<P>, dim3(nb), dim3(256), prep_lds, st,
-                       fb, idx, eta, off, lst, w.trace, mid ? PFb : nullptr, E2b, Q0, ps, Zc, ldz, pz, ab);
+                       fb, idx, eta, off, lst, w.trace, mid ? PFb : nullptr, E2b, Q0, ps, Zc, ldz, pz, ab, apre);
   }
   if (mid && !fb.FtF) hipLaunchKernelGGL(ftf_kernel, dim3(1), dim3(1024), 0, st, fb, FtF);
   const double *ftf = fb.FtF ? fb.FtF : FtF;
