@@ -2755,7 +2755,7 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_pv_kernel(FactBase fb, EigWor
   }
 }
 
-template <int P>
+template <int P, bool FAST>
 __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, EigWork w, int T, int p,
                                                             const double *__restrict__ HZ, int64_t ldz, int pz,
                                                             double *__restrict__ ab, double fai, double bbeta, int k,
@@ -2810,11 +2810,18 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
     const int nr = min(16, T - t0) * r;   // valid doubles of the tile's contiguous PF / EL range
     double hz[NT][4], pv[NT][4], e2v[4];
     double pst[4], est[4];
+    double2 pst2 = double2{0.0, 0.0}, est2 = double2{0.0, 0.0};
+    if constexpr (FAST) {   // even r <= 8: the 8 r <= 64 pieces of 16 B, one round
+      const bool ok = 2 * lane < nr;
+      pst2 = ok ? reinterpret_cast<const double2 *>(pfr + (int64_t)t0 * r)[lane] : double2{0.0, 0.0};
+      est2 = ok ? reinterpret_cast<const double2 *>(fb.EL + (int64_t)t0 * r)[lane] : double2{0.0, 0.0};
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {   // 16 r <= 256 doubles: four rounds of 64 lanes
-      const int e = u * 64 + lane;
-      pst[u] = e < nr ? pfr[(int64_t)t0 * r + e] : 0.0;
-      est[u] = e < nr ? fb.EL[(int64_t)t0 * r + e] : 0.0;
+      for (int u = 0; u < 4; ++u) {   // 16 r <= 256 doubles: four rounds of 64 lanes
+        const int e = u * 64 + lane;
+        pst[u] = e < nr ? pfr[(int64_t)t0 * r + e] : 0.0;
+        est[u] = e < nr ? fb.EL[(int64_t)t0 * r + e] : 0.0;
+      }
     }
     const double e2l = t0 + li < T ? e2r[t0 + li] : 0.0;
 #pragma unroll
@@ -2828,13 +2835,21 @@ __global__ __launch_bounds__(64 * BW, 4) void boot_cheb_mid_kernel(FactBase fb, 
         pv[ct][g] = c < ps ? pvr[(int64_t)sc * ps + c] : 0.0;
       }
     }
+    if constexpr (FAST) {
+      if (2 * lane < 16 * r) {
+        const int e = 2 * lane, row = e / r, j = e - row * r;
+        sP[row * RS + j] = pst2.x; sP[row * RS + j + 1] = pst2.y;
+        sE[row * RS + j] = est2.x; sE[row * RS + j + 1] = est2.y;
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = u * 64 + lane;
-      if (e < 16 * r) {
-        const int row = e / r, j = e - row * r;
-        sP[row * RS + j] = pst[u];
-        sE[row * RS + j] = est[u];
+      for (int u = 0; u < 4; ++u) {
+        const int e = u * 64 + lane;
+        if (e < 16 * r) {
+          const int row = e / r, j = e - row * r;
+          sP[row * RS + j] = pst[u];
+          sE[row * RS + j] = est[u];
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's writes land before its reads
@@ -3101,6 +3116,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
   const bool stg_ok = P == 16 && fb.r <= 8 && (fb.r & 1) == 0 && pz <= 16;
   auto chk = stg_ok ? boot_cheb_kernel<P, P == 16> : boot_cheb_kernel<P, false>;
   auto y2k = stg_ok ? boot_y2_kernel<P, P == 16> : boot_y2_kernel<P, false>;
+  auto cmk = stg_ok ? boot_cheb_mid_kernel<P, true> : boot_cheb_mid_kernel<P, false>;
 
   {   // the last Horner step's dynamic LDS (eta, idx, CSR: 20 T bytes) past 64 KB for T > 3276
     const size_t cheb_lds = (size_t)m * 8 + (size_t)(3 * m + 1) * 4;
@@ -3198,7 +3214,7 @@ static int eig_run_fact2_t(const FactBase &fb, const int32_t *idx, const double 
         if (e != hipSuccess) return 1000 + (int)e;
         if (tf) tf(tctx, DFM_KC_EIG_APPLY, 1);
         if (mid && it == 0 && sp < dg)
-          hipLaunchKernelGGL(boot_cheb_mid_kernel<P>, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
+          hipLaunchKernelGGL(cmk, dim3(nb), dim3(64 * BW), 0, st, fb, w, m, p, HZ, ldz, pz, ab,
                              ca[dg - sp], bb, k, PFb, E2b, w.S, FVb, ftf, Zc, ps);
         else
           hipLaunchKernelGGL(chk, dim3(nb), dim3(64 * BW), (size_t)m * 8 + (size_t)(3 * m + 1) * 4,
